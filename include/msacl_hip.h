@@ -1,0 +1,201 @@
+/*
+ * msacl_hip.h — C ABI of the MI355X (gfx950) MSACL rollout + update engine.
+ *
+ * The reference (adamyindh/Multi-Step-Actor-Critic-...; Python only) has no FFI: its hot-path
+ * boundary is the duck-typed plugin API behind create_envs / create_sampler / create_buffer.
+ * Each entry point below states which reference interface it replaces (file:line relative to
+ * the reference's repository root). The Python host layer binds these through ctypes
+ *  and mirrors the reference's plugin API on top of them.
+ *
+ * Conventions
+ *   - every data pointer is a DEVICE pointer owned by the caller (torch tensors in the Python
+ *     layer); the library only allocates its own per-handle state;
+ *   - all work is enqueued asynchronously on `stream` (a hipStream_t; NULL = default stream);
+ *     no call synchronises, allocates or copies to the host on the hot path, so the calls
+ *     can be captured into a hipGraph;
+ *   - functions return 0 on success or a negative MH_E* code; mh_last_error() gives text.
+ *     No C++ exception crosses the ABI. A handle is not thread-safe (one host thread/stream).
+ *   - layouts: row-major AoS for every tensor exchanged with the caller ([E][obs_dim] etc.),
+ *     exactly the shapes the reference's numpy arrays / torch tensors have.
+ */
+#ifndef MSACL_HIP_H
+#define MSACL_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MH_ABI_VERSION 1
+
+/* error codes */
+#define MH_OK 0
+#define MH_EINVAL (-1)   /* bad argument (null handle, unknown env id, size mismatch)   */
+#define MH_EHIP (-2)     /* a HIP runtime call failed                                   */
+#define MH_ENOMEM (-3)   /* device allocation failed                                    */
+#define MH_ESTATE (-4)   /* call order violated (e.g. rollout before mh_nstep_attach)   */
+
+/* env ids — the six ids accepted by RL/env/make_env.py:16-29 */
+#define MH_ENV_VANDERPOL 0
+#define MH_ENV_PENDULUM 1
+#define MH_ENV_DUCTEDFAN 2
+#define MH_ENV_TWOLINK 3
+#define MH_ENV_SINGLETRACKCAR 4
+#define MH_ENV_QUADTRACKING 5
+
+typedef struct mh_env_s* mh_env_t;
+
+/* Static description of one env (what gymnasium's single_observation_space /
+ * single_action_space expose to RL/utils/init_args.py:33-46). Host-only, needs no GPU. */
+typedef struct {
+  int32_t obs_dim, act_dim;
+  int32_t state_dim;      /* float32 persistent state per env (Quad: x v R W = 18)      */
+  int32_t xstate_dim;     /* float64 persistent state per env (Quad: Rd_last = 9)        */
+  int32_t reset_dim;      /* floats of one injected reset state (= state_dim)           */
+  int32_t control_step;   /* Euler substeps per env step                                */
+  int32_t max_step;       /* truncation horizon (1000)                                  */
+  int32_t record_floats;  /* floats of one n-step ring record (2*obs+act+4, padded to 4) */
+  float obs_low[16], obs_high[16];
+  float act_low[4], act_high[4];
+} mh_env_info_t;
+
+int mh_env_info(int32_t env_id, mh_env_info_t* out);
+
+/* Replaces create_envs (RL/create_pkg/create_envs.py:9-35): a batch of `num_envs` envs of one
+ * id, stepped in lockstep on the device. `seed` keys the in-kernel Philox stream used for
+ * throughput-mode resets and action noise. */
+int mh_env_create(int32_t env_id, int64_t num_envs, uint64_t seed, mh_env_t* out);
+int mh_env_destroy(mh_env_t h);
+
+/* Replaces SyncVectorEnv.reset (called at RL/trainer/sampler/base.py:98): reset every env.
+ * reset_states: [E][reset_dim] injected initial states (parity mode) or NULL (device draws
+ * from the reset distribution of RL/env/<Env>.py reset()). obs: [E][obs_dim] output.
+ * Also clears the n-step rings if attached. */
+int mh_env_reset(mh_env_t h, const float* reset_states, float* obs, void* stream);
+
+/* Replaces envs.step(actions_clip) (RL/trainer/sampler/base.py:148 -> gymnasium 0.28.1
+ * SyncVectorEnv.step -> RL/env/<Env>.py step()), including the vector env's autoreset:
+ *   act            [E][act_dim]  actions as passed to env.step (not clipped here)
+ *   reset_states   [E][reset_dim] state used if env i finishes this step, or NULL (draws)
+ *   next_obs       [E][obs_dim]  observation after autoreset (what step() returns)
+ *   real_next_obs  [E][obs_dim]  pre-reset observation (infos["final_observation"] rows)
+ *   reward         [E] float32 env reward (the vector env's float64 buffer holds exactly it)
+ *   terminated/truncated [E] uint8
+ * Any output pointer may be NULL. */
+int mh_env_step(mh_env_t h, const float* act, const float* reset_states, float* next_obs,
+                float* real_next_obs, float* reward, uint8_t* terminated, uint8_t* truncated,
+                void* stream);
+
+/* Persistent per-env state, for checkpoints and parity tests. state [E][state_dim],
+ * xstate [E][xstate_dim] (may be NULL when xstate_dim == 0), steps [E] (steps since reset). */
+int mh_env_get_state(mh_env_t h, float* state, double* xstate, int32_t* steps, void* stream);
+int mh_env_set_state(mh_env_t h, const float* state, const double* xstate, const int32_t* steps,
+                     void* stream);
+
+/* Device window store = the storage of RL/trainer/buffer/nstep_replay_buffer.py:52-70 laid out
+ * exactly as the reference's numpy arrays: obs/obs2 [capacity][n][obs_dim], act
+ * [capacity][n][act_dim], rew/cost/done/logp [capacity][n]. cursor is a DEVICE int64[4]:
+ * {ptr, size, total_emitted, last_emitted} with ptr/size following store() (:106-119). */
+typedef struct {
+  float* obs;
+  float* act;
+  float* rew;
+  float* cost;
+  float* obs2;
+  float* done;
+  float* logp;
+  int64_t capacity;
+  int64_t* cursor;
+} mh_window_store_t;
+
+/* Attach per-env n-step deques (RL/trainer/sampler/base.py:95: deque(maxlen=n) per env) and
+ * the reward/cost scales of RL/utils/rew_plus_cost.py:18-21. */
+int mh_nstep_attach(mh_env_t h, int32_t n_step, float reward_scale, float cost_scale);
+
+/* One lockstep step of BaseSampler._n_step (RL/trainer/sampler/base.py:118-222) minus the
+ * policy MLP: TanhGauss sample from `logits` (act_distribution_cls.py:45-57) with in-kernel
+ * Philox noise, clip (base.py:140-143), env step + autoreset, rew_plus_cost, deque push, and
+ * emission of every full window into `store` in env-index order (base.py:178-217,
+ * nstep_replay_buffer.py:122-125).
+ *   logits    [E][2*act_dim] StochaPolicy output (mean | std), or NULL when injecting
+ *   act_in    [E][act_dim] already-clipped actions to use instead of sampling (parity mode)
+ *   logp_in   [E] their log-probabilities (parity mode; NULL -> 0)
+ *   reset_states [E][reset_dim] or NULL
+ *   obs       [E][obs_dim] in: current observation (policy input); out: next observation
+ *   store     window store receiving the emitted windows (NULL: deques only)
+ *   act_out/logp_out  optional [E][act_dim] / [E] copies of the actions taken */
+int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const float* logp_in,
+                    const float* reset_states, float* obs, const mh_window_store_t* store,
+                    float* act_out, float* logp_out, void* stream);
+
+/* NstepReplayBuffer.sample_batch gather (RL/trainer/buffer/nstep_replay_buffer.py:128-150):
+ * out_X[b] = store.X[idx[b]] for the 7 arrays (any out pointer may be NULL). */
+int mh_replay_gather(const mh_window_store_t* store, int32_t n_step, int32_t obs_dim,
+                     int32_t act_dim, const int64_t* idx, int64_t batch, float* out_obs,
+                     float* out_act, float* out_rew, float* out_cost, float* out_obs2,
+                     float* out_done, float* out_logp, void* stream);
+
+/* Device uniform indices in [0, size) from the store cursor (np.random.randint at
+ * nstep_replay_buffer.py:138), keyed by (seed, draw counter). */
+int mh_replay_sample_indices(const mh_window_store_t* store, uint64_t seed, uint64_t counter,
+                             int64_t batch, int64_t* idx_out, void* stream);
+
+/* ---- MSACL target / certificate kernels (RL/algorithm/msacl.py), all [B][n] float32 ---- */
+
+/* _q_update backup + twin MSE (msacl.py:242-257):
+ *   backup = rew + (1-done) * gamma * (min(q1t, q2t) - alpha * next_logp)
+ *   loss = mean((q1-backup)^2) + mean((q2-backup)^2)
+ * Writes backup [B*n], dq1/dq2 = dloss/dq (gradients for autograd), loss_out [1], and
+ * abs_td [B] = mean_k |min(q1,q2) - backup| per window (PER priority source). */
+int mh_msacl_q_target(const float* q1, const float* q2, const float* q1t, const float* q2t,
+                      const float* next_logp, const float* rew, const float* done,
+                      const float* log_alpha, float gamma, int32_t B, int32_t n,
+                      float* backup, float* dq1, float* dq2, float* loss_out, float* abs_td,
+                      void* stream);
+
+/* _lyapunov_update certificate (msacl.py:279-332). Inputs: logp (policy log-prob of the
+ * stored actions), old_logp, V(obs) lya_obs, V(obs2) lya_obs2, obs/obs2 [B][n][D].
+ * Coefficients c (start_obs_norm_coef), w (lya_diff_coef), s (start_lya_coef) are [n].
+ * Writes is_clip [B*n], esl [B*n], lya_diff [B], loss_out [1] (= bound*pos_scale +
+ * mean(lya_diff)*diff_scale) and gradients d_lya_obs [B*n], d_lya_obs2 [B*n]. */
+int mh_msacl_lyapunov(const float* logp, const float* old_logp, const float* lya_obs,
+                      const float* lya_obs2, const float* obs, const float* obs2, const float* c,
+                      const float* w, const float* s, float alpha1, float alpha2,
+                      float pos_scale, float diff_scale, int32_t B, int32_t n, int32_t D,
+                      float* is_clip, float* esl, float* lya_diff, float* loss_out,
+                      float* d_lya_obs, float* d_lya_obs2, void* stream);
+
+/* _policy_update stability advantage (msacl.py:383-400):
+ *   adv_raw[b] = sum_k w_k (s_k V(obs_b0) - V(obs2_bk)); stats_out = {sum, sumsq} (float64)
+ * Normalisation is a second call so the (sum, sumsq, count) triple can be all-reduced
+ * across ranks in between. */
+int mh_msacl_stability_adv(const float* lya_obs0, const float* lya_obs2, const float* w,
+                           const float* s, int32_t B, int32_t n, float* adv_raw,
+                           double* stats_out, void* stream);
+/* PPO-clipped surrogate on the normalised advantage (msacl.py:400-405):
+ *   adv = (adv_raw - mean) / (std + 1e-8) with mean/std from stats (count = n_total);
+ *   loss = mean(min(r*adv, clip(r, 1-eps, 1+eps)*adv)); d_ratio = dloss/dr. */
+int mh_msacl_ppo_clip(const float* ratio, const float* adv_raw, const double* stats,
+                      double n_total, float clip_eps, int32_t B, float* adv, float* loss_out,
+                      float* d_ratio, void* stream);
+
+/* ---- prioritized replay (new: the reference trainer expects buffer.update_batch(idx, prio),
+ * RL/trainer/nstep_off_serial_trainer.py:93-95, but ships no prioritized buffer) ---- */
+/* sum-tree over `capacity` leaves (tree: float64 [2*pow2]); leaf i priority p_i. */
+int mh_per_update(double* tree, int64_t pow2, const int64_t* idx, const float* prio,
+                  int64_t count, float alpha, float eps, double* max_prio, void* stream);
+int mh_per_set_new(double* tree, int64_t pow2, const int64_t* cursor_before, const int64_t* cursor_after,
+                   int64_t capacity, const double* max_prio, void* stream);
+int mh_per_sample(const double* tree, int64_t pow2, const int64_t* cursor, uint64_t seed,
+                  uint64_t counter, int64_t batch, float beta, int64_t* idx_out,
+                  float* weight_out, void* stream);
+
+const char* mh_last_error(void);
+int mh_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MSACL_HIP_H */

@@ -1,0 +1,316 @@
+// capi.hip — C ABI (include/msacl_hip.h): env handles, lockstep rollout, window store, gather.
+#include <string>
+#include <cstring>
+
+#include "msacl_hip.h"
+#include "rollout.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define MH_HIP(call)                                                                  \
+  do {                                                                                \
+    hipError_t _e = (call);                                                           \
+    if (_e != hipSuccess)                                                             \
+      return fail(MH_EHIP, std::string(#call) + ": " + hipGetErrorString(_e));        \
+  } while (0)
+
+template <class Env>
+void fill_info(mh_env_info_t* o) {
+  std::memset(o, 0, sizeof(*o));
+  o->obs_dim = Env::D;
+  o->act_dim = Env::A;
+  o->state_dim = Env::S;
+  o->xstate_dim = Env::XS;
+  o->reset_dim = Env::RS;
+  o->control_step = Env::K;
+  o->max_step = mh::MAX_STEP;
+  o->record_floats = mh::rec_floats(Env::D, Env::A);
+  for (int i = 0; i < Env::D; ++i) {
+    o->obs_low[i] = Env::obs_lo(i);
+    o->obs_high[i] = Env::obs_hi(i);
+  }
+  for (int i = 0; i < Env::A; ++i) {
+    o->act_low[i] = Env::act_lo(i);
+    o->act_high[i] = Env::act_hi(i);
+  }
+}
+
+}  // namespace
+
+struct mh_env_s {
+  int env_id = -1;
+  int64_t E = 0;
+  uint64_t seed = 0;
+  mh_env_info_t info{};
+  float* state = nullptr;
+  double* xstate = nullptr;
+  int32_t* steps = nullptr;
+  double* tab = nullptr;
+  int64_t* meta = nullptr;
+  // n-step
+  int n = 0;
+  float reward_scale = 1.0f, cost_scale = 1.0f;
+  float* ring = nullptr;
+  int32_t* ring_len = nullptr;
+  int32_t* ring_pos = nullptr;
+  int32_t* emit_rank = nullptr;
+  int32_t* block_count = nullptr;
+  int32_t* block_offset = nullptr;
+
+  int grid() const { return (int)((E + mh::BLK - 1) / mh::BLK); }
+  mh::StepArgs base_args() const {
+    mh::StepArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.E = E;
+    a.state = state;
+    a.xstate = xstate;
+    a.steps = steps;
+    a.tab = tab;
+    a.meta = meta;
+    a.seed = seed;
+    a.n = n;
+    a.reward_scale = reward_scale;
+    a.cost_scale = cost_scale;
+    return a;
+  }
+};
+
+static void free_handle(mh_env_s* h) {
+  if (!h) return;
+  void* ptrs[] = {h->state, h->xstate, h->steps, h->tab, h->meta, h->ring, h->ring_len,
+                  h->ring_pos, h->emit_rank, h->block_count, h->block_offset};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  delete h;
+}
+
+extern "C" {
+
+int mh_abi_version(void) { return MH_ABI_VERSION; }
+
+const char* mh_last_error(void) { return g_err.c_str(); }
+
+int mh_env_info(int32_t env_id, mh_env_info_t* out) {
+  if (!out) return fail(MH_EINVAL, "mh_env_info: null out");
+  switch (env_id) {
+    case MH_ENV_VANDERPOL: fill_info<mh::VanderPol>(out); return MH_OK;
+    case MH_ENV_PENDULUM: fill_info<mh::Pendulum>(out); return MH_OK;
+    case MH_ENV_DUCTEDFAN: fill_info<mh::DuctedFan>(out); return MH_OK;
+    case MH_ENV_TWOLINK: fill_info<mh::TwoLink>(out); return MH_OK;
+    case MH_ENV_SINGLETRACKCAR: fill_info<mh::SingleTrackCar>(out); return MH_OK;
+    case MH_ENV_QUADTRACKING: fill_info<mh::QuadTracking>(out); return MH_OK;
+  }
+  return fail(MH_EINVAL, "mh_env_info: unknown env id " + std::to_string(env_id));
+}
+
+int mh_env_create(int32_t env_id, int64_t num_envs, uint64_t seed, mh_env_t* out) {
+  if (!out) return fail(MH_EINVAL, "mh_env_create: null out");
+  *out = nullptr;
+  if (num_envs <= 0 || num_envs > (int64_t)1 << 31)
+    return fail(MH_EINVAL, "mh_env_create: num_envs out of range");
+  mh_env_s* h = new mh_env_s();
+  int rc = mh_env_info(env_id, &h->info);
+  if (rc != MH_OK) {
+    delete h;
+    return rc;
+  }
+  h->env_id = env_id;
+  h->E = num_envs;
+  h->seed = seed;
+  const int64_t E = num_envs;
+  hipError_t e = hipSuccess;
+  e = hipMalloc(&h->state, sizeof(float) * E * h->info.state_dim);
+  if (e == hipSuccess && h->info.xstate_dim > 0) e = hipMalloc(&h->xstate, sizeof(double) * E * h->info.xstate_dim);
+  if (e == hipSuccess) e = hipMalloc(&h->steps, sizeof(int32_t) * E);
+  if (e == hipSuccess) e = hipMalloc(&h->meta, sizeof(int64_t) * 8);
+  if (e == hipSuccess) e = hipMemset(h->meta, 0, sizeof(int64_t) * 8);
+  if (e == hipSuccess) e = hipMemset(h->steps, 0, sizeof(int32_t) * E);
+  if (e == hipSuccess) e = hipMemset(h->state, 0, sizeof(float) * E * h->info.state_dim);
+  if (e == hipSuccess && env_id == MH_ENV_QUADTRACKING) {
+    const int rows = mh::MAX_STEP + 1;
+    double* host = new double[(size_t)rows * mh::QT_ROW];
+    mh::quad_fill_table(host, rows);
+    e = hipMalloc(&h->tab, sizeof(double) * rows * mh::QT_ROW);
+    if (e == hipSuccess) e = hipMemcpy(h->tab, host, sizeof(double) * rows * mh::QT_ROW, hipMemcpyHostToDevice);
+    delete[] host;
+  }
+  if (e != hipSuccess) {
+    free_handle(h);
+    return fail(e == hipErrorOutOfMemory ? MH_ENOMEM : MH_EHIP,
+                std::string("mh_env_create: ") + hipGetErrorString(e));
+  }
+  *out = h;
+  return MH_OK;
+}
+
+int mh_env_destroy(mh_env_t h) {
+  free_handle(h);
+  return MH_OK;
+}
+
+int mh_nstep_attach(mh_env_t h, int32_t n_step, float reward_scale, float cost_scale) {
+  if (!h) return fail(MH_EINVAL, "mh_nstep_attach: null handle");
+  if (n_step <= 0 || n_step > 4096) return fail(MH_EINVAL, "mh_nstep_attach: n_step out of range");
+  if (h->ring) {
+    (void)hipFree(h->ring); (void)hipFree(h->ring_len); (void)hipFree(h->ring_pos);
+    (void)hipFree(h->emit_rank); (void)hipFree(h->block_count); (void)hipFree(h->block_offset);
+    h->ring = nullptr;
+  }
+  h->n = n_step;
+  h->reward_scale = reward_scale;
+  h->cost_scale = cost_scale;
+  const int64_t E = h->E;
+  const int F = h->info.record_floats;
+  MH_HIP(hipMalloc(&h->ring, sizeof(float) * E * n_step * F));
+  MH_HIP(hipMalloc(&h->ring_len, sizeof(int32_t) * E));
+  MH_HIP(hipMalloc(&h->ring_pos, sizeof(int32_t) * E));
+  MH_HIP(hipMalloc(&h->emit_rank, sizeof(int32_t) * E));
+  MH_HIP(hipMalloc(&h->block_count, sizeof(int32_t) * h->grid()));
+  MH_HIP(hipMalloc(&h->block_offset, sizeof(int32_t) * h->grid()));
+  MH_HIP(hipMemset(h->ring_len, 0, sizeof(int32_t) * E));
+  MH_HIP(hipMemset(h->ring_pos, 0, sizeof(int32_t) * E));
+  MH_HIP(hipMemset(h->ring, 0, sizeof(float) * E * n_step * F));
+  return MH_OK;
+}
+
+int mh_env_reset(mh_env_t h, const float* reset_states, float* obs, void* stream) {
+  if (!h) return fail(MH_EINVAL, "mh_env_reset: null handle");
+  hipStream_t st = (hipStream_t)stream;
+  mh::StepArgs a = h->base_args();
+  a.reset_in = reset_states;
+  a.obs = obs;
+  a.ring = h->ring;
+  a.ring_len = h->ring_len;
+  a.ring_pos = h->ring_pos;
+  MH_HIP(mh::launch_reset(h->env_id, a, st));
+  MH_HIP(mh::launch_finalize(h->block_count, 0, h->block_offset, h->meta, nullptr, 1, st));
+  return MH_OK;
+}
+
+int mh_env_step(mh_env_t h, const float* act, const float* reset_states, float* next_obs,
+                float* real_next_obs, float* reward, uint8_t* terminated, uint8_t* truncated,
+                void* stream) {
+  if (!h) return fail(MH_EINVAL, "mh_env_step: null handle");
+  if (!act) return fail(MH_EINVAL, "mh_env_step: null actions");
+  hipStream_t st = (hipStream_t)stream;
+  mh::StepArgs a = h->base_args();
+  a.act_in = act;
+  a.reset_in = reset_states;
+  a.obs = next_obs;
+  a.real_next_obs = real_next_obs;
+  a.reward_out = reward;
+  a.term_out = terminated;
+  a.trunc_out = truncated;
+  a.reward_scale = 1.0f;
+  a.cost_scale = 1.0f;
+  MH_HIP(mh::launch_rollout(h->env_id, a, st));
+  MH_HIP(mh::launch_finalize(h->block_count, 0, h->block_offset, h->meta, nullptr, 1, st));
+  return MH_OK;
+}
+
+int mh_env_get_state(mh_env_t h, float* state, double* xstate, int32_t* steps, void* stream) {
+  if (!h) return fail(MH_EINVAL, "mh_env_get_state: null handle");
+  hipStream_t st = (hipStream_t)stream;
+  if (state) MH_HIP(mh::launch_transpose_f32(h->state, state, h->info.state_dim, h->E, true, st));
+  if (xstate && h->info.xstate_dim > 0)
+    MH_HIP(mh::launch_transpose_f64(h->xstate, xstate, h->info.xstate_dim, h->E, true, st));
+  if (steps) MH_HIP(hipMemcpyAsync(steps, h->steps, sizeof(int32_t) * h->E, hipMemcpyDeviceToDevice, st));
+  return MH_OK;
+}
+
+int mh_env_set_state(mh_env_t h, const float* state, const double* xstate, const int32_t* steps,
+                     void* stream) {
+  if (!h) return fail(MH_EINVAL, "mh_env_set_state: null handle");
+  hipStream_t st = (hipStream_t)stream;
+  if (state) MH_HIP(mh::launch_transpose_f32(state, h->state, h->info.state_dim, h->E, false, st));
+  if (xstate && h->info.xstate_dim > 0)
+    MH_HIP(mh::launch_transpose_f64(xstate, h->xstate, h->info.xstate_dim, h->E, false, st));
+  if (steps) MH_HIP(hipMemcpyAsync(h->steps, steps, sizeof(int32_t) * h->E, hipMemcpyDeviceToDevice, st));
+  return MH_OK;
+}
+
+int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const float* logp_in,
+                    const float* reset_states, float* obs, const mh_window_store_t* store,
+                    float* act_out, float* logp_out, void* stream) {
+  if (!h) return fail(MH_EINVAL, "mh_rollout_step: null handle");
+  if (!h->ring) return fail(MH_ESTATE, "mh_rollout_step: call mh_nstep_attach first");
+  if (!obs) return fail(MH_EINVAL, "mh_rollout_step: null obs");
+  if (!logits && !act_in) return fail(MH_EINVAL, "mh_rollout_step: need logits or act_in");
+  if (store && (store->capacity <= 0 || !store->cursor || !store->obs || !store->act || !store->rew ||
+                !store->cost || !store->obs2 || !store->done || !store->logp))
+    return fail(MH_EINVAL, "mh_rollout_step: incomplete window store");
+  hipStream_t st = (hipStream_t)stream;
+  mh::StepArgs a = h->base_args();
+  a.logits = logits;
+  a.act_in = act_in;
+  a.logp_in = logp_in;
+  a.reset_in = reset_states;
+  a.obs = obs;
+  a.act_out = act_out;
+  a.logp_out = logp_out;
+  a.ring = h->ring;
+  a.ring_len = h->ring_len;
+  a.ring_pos = h->ring_pos;
+  a.emit_rank = h->emit_rank;
+  a.block_count = h->block_count;
+  MH_HIP(mh::launch_rollout(h->env_id, a, st));
+  MH_HIP(mh::launch_finalize(h->block_count, store ? h->grid() : 0, h->block_offset, h->meta,
+                             store ? store->cursor : nullptr, store ? store->capacity : 1, st));
+  if (store) {
+    mh::EmitArgs ea;
+    ea.E = h->E;
+    ea.ring = h->ring;
+    ea.ring_pos = h->ring_pos;
+    ea.emit_rank = h->emit_rank;
+    ea.block_offset = h->block_offset;
+    ea.meta = h->meta;
+    ea.capacity = store->capacity;
+    ea.n = h->n;
+    ea.F = h->info.record_floats;
+    ea.D = h->info.obs_dim;
+    ea.A = h->info.act_dim;
+    ea.obs = store->obs;
+    ea.act = store->act;
+    ea.rew = store->rew;
+    ea.cost = store->cost;
+    ea.obs2 = store->obs2;
+    ea.done = store->done;
+    ea.logp = store->logp;
+    MH_HIP(mh::launch_emit(ea, st));
+  }
+  return MH_OK;
+}
+
+int mh_replay_gather(const mh_window_store_t* store, int32_t n_step, int32_t obs_dim, int32_t act_dim,
+                     const int64_t* idx, int64_t batch, float* out_obs, float* out_act, float* out_rew,
+                     float* out_cost, float* out_obs2, float* out_done, float* out_logp, void* stream) {
+  if (!store || !idx) return fail(MH_EINVAL, "mh_replay_gather: null store/idx");
+  mh::GatherArgs g;
+  g.idx = idx;
+  g.batch = batch;
+  g.n = n_step;
+  g.D = obs_dim;
+  g.A = act_dim;
+  g.s_obs = store->obs; g.s_act = store->act; g.s_rew = store->rew; g.s_cost = store->cost;
+  g.s_obs2 = store->obs2; g.s_done = store->done; g.s_logp = store->logp;
+  g.o_obs = out_obs; g.o_act = out_act; g.o_rew = out_rew; g.o_cost = out_cost;
+  g.o_obs2 = out_obs2; g.o_done = out_done; g.o_logp = out_logp;
+  MH_HIP(mh::launch_gather(g, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_replay_sample_indices(const mh_window_store_t* store, uint64_t seed, uint64_t counter,
+                             int64_t batch, int64_t* idx_out, void* stream) {
+  if (!store || !store->cursor || !idx_out) return fail(MH_EINVAL, "mh_replay_sample_indices: null arg");
+  MH_HIP(mh::launch_sample_idx(store->cursor, seed, counter, batch, idx_out, (hipStream_t)stream));
+  return MH_OK;
+}
+
+}  // extern "C"

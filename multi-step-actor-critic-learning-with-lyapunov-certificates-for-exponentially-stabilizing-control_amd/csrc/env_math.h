@@ -1,0 +1,752 @@
+// env_math.h — per-env physics of the six MSACL control environments, written once as
+// __host__ __device__ functions so the same source runs inside the gfx950 rollout kernel
+// and in the host-side check build used by the CPU test-suite.
+//
+// Precision flow mirrors the reference's NumPy-2 (NEP 50) dtype semantics exactly:
+//   * a Python float constant times a float32 value is a float32 op with the constant
+//     rounded to float32 (weak scalar);
+//   * float32 arrays combined with float64 arrays promote to float64, and an in-place
+//     `f32_array += f64_array` is evaluated in float64 and rounded once.
+// No FMA contraction (see #pragma below) so every op rounds where NumPy rounds.
+// float32 transcendentals are evaluated in float64 and rounded once (correctly rounded in
+// practice; NumPy's SIMD float32 sin/cos are within 1.5 ulp of this).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#pragma clang fp contract(off)
+
+#define MH_HD __host__ __device__ __forceinline__
+
+namespace mh {
+
+enum EnvId : int {
+  ENV_VANDERPOL = 0,
+  ENV_PENDULUM = 1,
+  ENV_DUCTEDFAN = 2,
+  ENV_TWOLINK = 3,
+  ENV_SINGLETRACKCAR = 4,
+  ENV_QUADTRACKING = 5,
+  ENV_COUNT = 6
+};
+
+constexpr int MAX_STEP = 1000;  // every env: truncated = current_step >= 1000
+
+// ---------------------------------------------------------------- f32 helpers
+MH_HD float sin32(float x) { return (float)sin((double)x); }
+MH_HD float cos32(float x) { return (float)cos((double)x); }
+MH_HD float tan32(float x) { return (float)tan((double)x); }
+
+// `s ** 2` on a NumPy float32 SCALAR calls the C library's powf (glibc 2.35 e_powf.c, the
+// ARM optimized-routines algorithm: 16-entry log2 table + degree-5 poly, 32-entry exp2 table +
+// degree-3 poly, all in double), which differs from s*s in ~0.09% of inputs. Arrays use
+// s*s. The reference squares scalars in VanderPol._dynamics and SingleTrackCar._f/_g, so those
+// sites use this bit-exact restatement (verified against libm on 9.3M random floats).
+MH_HD double mh_asdouble(uint64_t u) {
+  union { uint64_t u; double d; } c;
+  c.u = u;
+  return c.d;
+}
+MH_HD uint64_t mh_asuint64(double d) {
+  union { uint64_t u; double d; } c;
+  c.d = d;
+  return c.u;
+}
+MH_HD float mh_asfloat(uint32_t u) {
+  union { uint32_t u; float f; } c;
+  c.u = u;
+  return c.f;
+}
+MH_HD uint32_t mh_asuint(float f) {
+  union { uint32_t u; float f; } c;
+  c.f = f;
+  return c.u;
+}
+MH_HD float powf2(float x) {
+  constexpr double LOG_INVC[16] = {
+      0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010bp+0,  0x1.3c995b0b80385p+0,
+      0x1.30d190c8864a5p+0, 0x1.25e227b0b8eap+0,  0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0,
+      0x1.0953f419900a7p+0, 0x1p+0,               0x1.e608cfd9a47acp-1, 0x1.ca4b31f026aap-1,
+      0x1.b2036576afce6p-1, 0x1.9c2d163a1aa2dp-1, 0x1.886e6037841edp-1, 0x1.767dcf5534862p-1};
+  constexpr double LOG_C[16] = {
+      -0x1.efec65b963019p-2, -0x1.b0b6832d4fca4p-2, -0x1.7418b0a1fb77bp-2, -0x1.39de91a6dcf7bp-2,
+      -0x1.01d9bf3f2b631p-2, -0x1.97c1d1b3b7afp-3,  -0x1.2f9e393af3c9fp-3, -0x1.960cbbf788d5cp-4,
+      -0x1.a6f9db6475fcep-5, 0x0p+0,                0x1.338ca9f24f53dp-4,  0x1.476a9543891bap-3,
+      0x1.e840b4ac4e4d2p-3,  0x1.40645f0c6651cp-2,  0x1.88e9c2c1b9ff8p-2,  0x1.ce0a44eb17bccp-2};
+  constexpr uint64_t EXP_T[32] = {
+      0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+      0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+      0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+      0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+      0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+      0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+      0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+      0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
+  constexpr double A0 = 0x1.27616c9496e0bp-2, A1 = -0x1.71969a075c67ap-2, A2 = 0x1.ec70a6ca7baddp-2,
+                   A3 = -0x1.7154748bef6c8p-1, A4 = 0x1.71547652ab82bp0;
+  constexpr double C0 = 0x1.c6af84b912394p-5, C1 = 0x1.ebfce50fac4f3p-3, C2 = 0x1.62e42ff0c52d6p-1;
+  uint32_t ix = mh_asuint(x) & 0x7fffffffu;  // y = 2 is even: sign drops
+  if (ix == 0u) return 0.0f;
+  if (ix >= 0x7f800000u) return x * x;
+  if (ix < 0x00800000u) {  // subnormal: normalise
+    ix = mh_asuint(mh_asfloat(ix) * 0x1p23f) & 0x7fffffffu;
+    ix -= 23u << 23;
+  }
+  const uint32_t tmp = ix - 0x3f330000u;
+  const int i = (int)((tmp >> 19) % 16u);
+  const uint32_t top = tmp & 0xff800000u;
+  const uint32_t iz = ix - top;
+  const int k = (int32_t)top >> 23;
+  const double z = (double)mh_asfloat(iz);
+  const double r = z * LOG_INVC[i] - 1.0;
+  const double y0 = LOG_C[i] + (double)k;
+  const double r2 = r * r;
+  double y = A0 * r + A1;
+  const double p = A2 * r + A3;
+  const double r4 = r2 * r2;
+  double q = A4 * r + y0;
+  q = p * r2 + q;
+  y = y * r4 + q;
+  const double ylogx = 2.0 * y;
+  if (((mh_asuint64(ylogx) >> 47) & 0xffffu) >= (mh_asuint64(126.0) >> 47)) return x * x;  // |2 log2 x| >= 126
+  const double SHIFT = 0x1.8p+52 / 32;
+  double kd = ylogx + SHIFT;
+  const uint64_t ki = mh_asuint64(kd);
+  kd -= SHIFT;
+  const double rr = ylogx - kd;
+  uint64_t t = EXP_T[ki % 32];
+  t += ki << (52 - 5);
+  const double s = mh_asdouble(t);
+  const double zz = C0 * rr + C1;
+  const double rr2 = rr * rr;
+  double yy = C2 * rr + 1.0;
+  yy = zz * rr2 + yy;
+  yy = yy * s;
+  return (float)yy;
+}
+
+// NumPy float32 add.reduce order (pairwise_sum: <8 sequential from -0.0, else 8 lanes).
+template <int N>
+MH_HD float np_sum(const float* a) {
+  if constexpr (N < 8) {
+    float r = -0.0f;
+#pragma unroll
+    for (int i = 0; i < N; ++i) r = r + a[i];
+    return r;
+  } else {
+    float r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int i = 8;
+#pragma unroll
+    for (; i < N - (N % 8); i += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) r[j] = r[j] + a[i + j];
+    }
+    float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+    for (; i < N; ++i) res = res + a[i];
+    return res;
+  }
+}
+
+// f32 state updated by a float64 derivative: `obs += deriv * dt` with deriv float64.
+MH_HD float upd64(float s, double d, double dt) { return (float)((double)s + d * dt); }
+
+// Shared quadratic reward of the five regulation envs (e.g. VanderPol.py:108-115):
+// reward = -(sum(Q*obs^2) + sum(R*u^2)) + 1[all |obs| <= 0.01]
+template <int D, int A>
+MH_HD float quad_reward(const float* s, const float* Q, const float* u, const float* R) {
+  float a[D], b[A];
+#pragma unroll
+  for (int i = 0; i < D; ++i) a[i] = Q[i] * (s[i] * s[i]);
+#pragma unroll
+  for (int i = 0; i < A; ++i) b[i] = R[i] * (u[i] * u[i]);
+  float cost = np_sum<D>(a) + np_sum<A>(b);
+  float r = -cost;
+  bool near = true;
+#pragma unroll
+  for (int i = 0; i < D; ++i) near = near && (fabsf(s[i]) <= 0.01f);
+  if (near) r = r + 1.0f;
+  return r;
+}
+
+// ---------------------------------------------------------------- VanderPol
+// RL/env/VanderPol.py:23-129. x'' = mu (1 - x^2) x' - x + u, mu = 1, K = 5, dt = 0.01.
+struct VanderPol {
+  static constexpr int D = 2, A = 1, S = 2, XS = 0, RS = 2, K = 5;
+  MH_HD static float obs_lo(int i) { (void)i; return -10.0f; }
+  MH_HD static float obs_hi(int i) { (void)i; return 10.0f; }
+  MH_HD static float act_lo(int i) { (void)i; return -5.0f; }
+  MH_HD static float act_hi(int i) { (void)i; return 5.0f; }
+  MH_HD static float reset_noise() { return 5.0f; }
+  MH_HD static void step(float* s, double*, int, const float* u, const double*, float* obs, float* rew) {
+    for (int k = 0; k < K; ++k) {
+      float x = s[0], xd = s[1];
+      float acc = ((1.0f * (1.0f - powf2(x))) * xd - x) + u[0];  // VanderPol.py:95 (scalar x**2)
+      s[0] = s[0] + xd * 0.01f;
+      s[1] = s[1] + acc * 0.01f;
+    }
+    const float Q[2] = {2.0f, 1.0f}, R[1] = {0.1f};
+    *rew = quad_reward<2, 1>(s, Q, u, R);
+    obs[0] = s[0]; obs[1] = s[1];
+  }
+  MH_HD static void reset_from(const float* rs, float* s, double*, const double*, float* obs) {
+    s[0] = obs[0] = rs[0];
+    s[1] = obs[1] = rs[1];
+  }
+};
+
+// ---------------------------------------------------------------- Pendulum
+// RL/env/Pendulum.py:22-137. theta'' = (m g L sin th - b th' + u) / (m L^2).
+struct Pendulum {
+  static constexpr int D = 2, A = 1, S = 2, XS = 0, RS = 2, K = 5;
+  MH_HD static float obs_lo(int i) { return i == 0 ? -3.14159274101257324f : -10.0f; }
+  MH_HD static float obs_hi(int i) { return i == 0 ? 3.14159274101257324f : 10.0f; }
+  MH_HD static float act_lo(int i) { (void)i; return -5.0f; }
+  MH_HD static float act_hi(int i) { (void)i; return 5.0f; }
+  MH_HD static void step(float* s, double*, int, const float* u, const double*, float* obs, float* rew) {
+    const float mgL = (float)((0.15 * 9.81) * 0.5);   // Pendulum.py:102 python-float prefix
+    const float mL2 = (float)(0.15 * (0.5 * 0.5));
+    const float b = 0.1f;
+    for (int k = 0; k < K; ++k) {
+      float th = s[0], thd = s[1];
+      float acc = ((mgL * sin32(th) - b * thd) + u[0]) / mL2;
+      s[0] = s[0] + thd * 0.01f;
+      s[1] = s[1] + acc * 0.01f;
+    }
+    const float Q[2] = {2.0f, 1.0f}, R[1] = {0.1f};
+    *rew = quad_reward<2, 1>(s, Q, u, R);
+    obs[0] = s[0]; obs[1] = s[1];
+  }
+  MH_HD static void reset_from(const float* rs, float* s, double*, const double*, float* obs) {
+    s[0] = obs[0] = rs[0];
+    s[1] = obs[1] = rs[1];
+  }
+};
+
+// ---------------------------------------------------------------- DuctedFan
+// RL/env/DuctedFan.py:24-147, planar ducted fan, m=8.5 g=9.81 r=0.26 d=0.95 J=0.048.
+struct DuctedFan {
+  static constexpr int D = 6, A = 2, S = 6, XS = 0, RS = 6, K = 5;
+  MH_HD static float obs_lo(int i) { return i == 2 ? -1.57079637050628662f : -5.0f; }
+  MH_HD static float obs_hi(int i) { return i == 2 ? 1.57079637050628662f : 5.0f; }
+  MH_HD static float act_lo(int i) { (void)i; return -5.0f; }
+  MH_HD static float act_hi(int i) { (void)i; return 5.0f; }
+  MH_HD static void step(float* s, double*, int, const float* u, const double*, float* obs, float* rew) {
+    const float nmg = (float)(-8.5 * 9.81), mg = (float)(8.5 * 9.81);
+    const float d = 0.95f, m = 8.5f, r = 0.26f, J = 0.048f;
+    for (int k = 0; k < K; ++k) {
+      float th = s[2], vx = s[3], vy = s[4], om = s[5];
+      float st = sin32(th), ct = cos32(th);
+      float ax = (((nmg * st - d * vx) + u[0] * ct) - u[1] * st) / m;            // DuctedFan.py:107
+      float ay = (((mg * (ct - 1.0f) - d * vy) + u[0] * st) + u[1] * ct) / m;    // DuctedFan.py:108
+      float aw = (r * u[0]) / J;                                                  // DuctedFan.py:109
+      s[0] = s[0] + vx * 0.01f;
+      s[1] = s[1] + vy * 0.01f;
+      s[2] = s[2] + om * 0.01f;
+      s[3] = s[3] + ax * 0.01f;
+      s[4] = s[4] + ay * 0.01f;
+      s[5] = s[5] + aw * 0.01f;
+    }
+    const float Q[6] = {2.0f, 2.0f, 2.0f, 1.0f, 1.0f, 1.0f}, R[2] = {0.1f, 0.1f};
+    *rew = quad_reward<6, 2>(s, Q, u, R);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) obs[i] = s[i];
+  }
+  MH_HD static void reset_from(const float* rs, float* s, double*, const double*, float* obs) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) s[i] = obs[i] = rs[i];
+  }
+};
+
+// ---------------------------------------------------------------- TwoLink
+// RL/env/TwoLink.py:22-177. M(q) q'' = u - C(q,q') q' - G(q); derivative in float64
+// (M and C are float64 arrays, G float32), LU solve with partial pivoting (LAPACK getrf/getrs).
+struct TwoLink {
+  static constexpr int D = 4, A = 2, S = 4, XS = 0, RS = 4, K = 5;
+  MH_HD static float obs_lo(int i) { return i < 2 ? -1.57079637050628662f : -20.0f; }
+  MH_HD static float obs_hi(int i) { return i < 2 ? 1.57079637050628662f : 20.0f; }
+  MH_HD static float act_lo(int i) { (void)i; return -20.0f; }
+  MH_HD static float act_hi(int i) { (void)i; return 20.0f; }
+  MH_HD static void deriv(const float* s, const float* u, double* out) {
+    const double I1 = (1.0 / 12.0) * 1.0 * (1.0 * 1.0);
+    const double I2 = I1;
+    const float q1 = s[0], q2 = s[1], dq1 = s[2], dq2 = s[3];
+    // mass matrix (TwoLink.py:100-107)
+    float c2 = cos32(q2);
+    float in11 = (float)(1.0 * 1.0 + 0.5 * 0.5) + ((float)((2.0 * 1.0) * 0.5) * c2);
+    float M11f = (float)((I1 + I2) + 1.0 * (0.5 * 0.5)) + (1.0f * in11);
+    float in12 = (float)(0.5 * 0.5) + ((float)(1.0 * 0.5) * c2);
+    float M12f = (float)I2 + (1.0f * in12);
+    double M11 = M11f, M12 = M12f, M21 = M12f, M22 = I2 + 1.0 * (0.5 * 0.5);
+    // coriolis (TwoLink.py:109-119)
+    float s2 = sin32(q2);
+    float h = (float)((-1.0 * 1.0) * 0.5) * s2;
+    float C11 = h * dq2, C12 = h * dq2 + h * dq1, C21 = (-h) * dq1;
+    // gravity (TwoLink.py:121-129)
+    float g1a = (float)((-(1.0 * 0.5 + 1.0 * 1.0)) * 9.81) * sin32(q1);
+    float sq12 = sin32(q1 + q2);
+    float g1b = (float)((1.0 * 0.5) * 9.81) * sq12;
+    float G1 = g1a - g1b;
+    float G2 = (float)((-1.0 * 0.5) * 9.81) * sq12;
+    // rhs = (u - C @ dq) - G   (float64)
+    double Cq1 = (double)C11 * (double)dq1 + (double)C12 * (double)dq2;
+    double Cq2 = (double)C21 * (double)dq1 + 0.0 * (double)dq2;
+    double b1 = ((double)u[0] - Cq1) - (double)G1;
+    double b2 = ((double)u[1] - Cq2) - (double)G2;
+    // LU with partial pivoting on the first column (getrf), then forward/back substitution
+    double a11 = M11, a12 = M12, a21 = M21, a22 = M22;
+    if (fabs(a21) > fabs(a11)) {
+      double t;
+      t = a11; a11 = a21; a21 = t;
+      t = a12; a12 = a22; a22 = t;
+      t = b1; b1 = b2; b2 = t;
+    }
+    double l21 = a21 * (1.0 / a11);
+    double u22 = a22 - l21 * a12;
+    double y2 = b2 - l21 * b1;
+    double x2 = y2 * (1.0 / u22);
+    double x1 = (b1 - a12 * x2) * (1.0 / a11);
+    out[0] = dq1; out[1] = dq2; out[2] = x1; out[3] = x2;
+  }
+  MH_HD static void step(float* s, double*, int, const float* u, const double*, float* obs, float* rew) {
+    for (int k = 0; k < K; ++k) {
+      double d[4];
+      deriv(s, u, d);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s[i] = upd64(s[i], d[i], 0.01);
+    }
+    const float Q[4] = {2.0f, 2.0f, 1.0f, 1.0f}, R[2] = {0.1f, 0.1f};
+    *rew = quad_reward<4, 2>(s, Q, u, R);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) obs[i] = s[i];
+  }
+  MH_HD static void reset_from(const float* rs, float* s, double*, const double*, float* obs) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s[i] = obs[i] = rs[i];
+  }
+};
+
+// ---------------------------------------------------------------- SingleTrackCar
+// RL/env/SingleTrackCar.py:41-320. x' = f(x) + g(x) u in float64 containers whose entries are
+// float32 expressions; dynamic model when |v| >= 0.1 (v = ve + v_ref), kinematic otherwise.
+struct CarConst {
+  // Python-float constant folds, evaluated in the reference's left-to-right order.
+  static constexpr double lf = 0.3048 * 3.793293;
+  static constexpr double lr = 0.3048 * 4.667707;
+  static constexpr double h = 0.3048 * 2.01355;
+  static constexpr double m = 4.4482216152605 / 0.3048 * (74.91452);
+  static constexpr double Iz = 4.4482216152605 * 0.3048 * (1321.416);
+  static constexpr double mu = 0.1 * 1.0489;
+  static constexpr double CS = 21.92 / 1.0489;  // -tire_p_ky1 / tire_p_dy1
+  static constexpr double g = 9.81;
+  static constexpr double lsum = lr + lf;
+  static constexpr double P1 = mu * m;
+  static constexpr double Q2 = mu * m / (Iz * (lr + lf));
+  static constexpr double K1 = lf * lf * CS * g * lr + lr * lr * CS * g * lf;
+  static constexpr double K2 = lr * CS * g * lf - lf * CS * g * lr;
+  static constexpr double K3 = lf * CS * g * lr;
+  static constexpr double K4 = CS * g * lf * lr - CS * g * lr * lf;
+  static constexpr double K5 = CS * g * lf + CS * g * lr;
+  static constexpr double K6 = CS * g * lr;
+  static constexpr double K7 = -(lf * lf) * CS * h + lr * lr * CS * h;
+  static constexpr double K8 = lr * CS * h + lf * CS * h;
+  static constexpr double K9 = lf * CS * h;
+  static constexpr double K10 = CS * h * lr + CS * h * lf;
+  static constexpr double K11 = CS * h - CS * h;
+  static constexpr double lwb = lf + lr;
+  static constexpr double ilwb = 1.0 / (lf + lr);
+};
+
+struct SingleTrackCar {
+  static constexpr int D = 7, A = 2, S = 7, XS = 0, RS = 7, K = 5;
+  MH_HD static float obs_lo(int i) {
+    const float lo[7] = {-1.0f, -1.0f, -1.06599998474121094f, -1.0f, -1.57079637050628662f,
+                         -1.57079637050628662f, -1.04719758033752441f};
+    return lo[i];
+  }
+  MH_HD static float obs_hi(int i) { return -obs_lo(i); }
+  MH_HD static float act_lo(int i) { (void)i; return -5.0f; }
+  MH_HD static float act_hi(int i) { (void)i; return 5.0f; }
+  MH_HD static void deriv(const float* x, const float* u, double* out) {
+    using C = CarConst;
+    const float sxe = x[0], sye = x[1], delta = x[2], ve = x[3], pe = x[4], ped = x[5], beta = x[6];
+    float v = ve + 1.0f;        // v_ref = 1.0
+    float psid = ped + 0.0f;    // omega_ref = 0.0
+    double f[7], g5[2] = {0.0, 0.0}, g6[2] = {0.0, 0.0}, g2 = 0.0, g3 = 0.0;
+    float pb = pe + beta;
+    f[0] = (double)(((v * cos32(pb)) - 1.0f) + (0.0f * sye));   // SingleTrackCar.py:165
+    f[1] = (double)((v * sin32(pb)) - (0.0f * sxe));            // SingleTrackCar.py:166
+    f[3] = -0.0;                                               // -a_ref
+    f[2] = 0.0;
+    const float lsum = (float)C::lsum;
+    if (!(fabsf(v) < 0.1f)) {
+      // dynamic model (SingleTrackCar.py:178-196, 243-256)
+      float X = (float)C::P1 / ((v * (float)C::Iz) * lsum);
+      float t1 = ((-X) * (float)C::K1) * psid;
+      float t2 = (float)(C::Q2 * C::K2) * beta;
+      float t3 = (float)(C::Q2 * C::K3) * delta;
+      f[4] = (double)ped;
+      f[5] = (double)((t1 + t2) + t3);
+      float Y1 = (float)C::mu / (powf2(v) * lsum);
+      float Y2 = (float)C::mu / (v * lsum);
+      float b1 = ((Y1 * (float)C::K4) - 1.0f) * psid;
+      float b2 = (Y2 * (float)C::K5) * beta;
+      float b3 = (Y2 * (float)C::K6) * delta;
+      f[6] = (double)((b1 - b2) + b3);
+      g2 = 1.0;  // g[DELTA, VDELTA]
+      g3 = 1.0;  // g[VE, ALONG]
+      float gt1 = ((-X) * (float)C::K7) * psid;
+      float gt2 = (float)(C::Q2 * C::K8) * beta;
+      float gt3 = (float)(C::Q2 * C::K9) * delta;
+      g5[1] = (double)((gt1 + gt2) - gt3);
+      float hb1 = (Y1 * (float)C::K10) * psid;
+      float hb2 = (Y2 * (float)C::K11) * beta;
+      float hb3 = ((Y2 * (float)C::CS) * (float)C::h) * delta;
+      g6[1] = (double)((hb1 - hb2) - hb3);
+    } else {
+      // kinematic model (SingleTrackCar.py:199-204, 259-277)
+      const float lwb = (float)C::lwb, lr = (float)C::lr, ilwb = (float)C::ilwb;
+      float td = tan32(delta), cd = cos32(delta), cb = cos32(beta), sb = sin32(beta);
+      f[4] = (double)((((v * cb) / lwb) * td) - 0.0f);
+      f[5] = 0.0;
+      f[6] = 0.0;
+      float tt = (td * lr) / lwb;
+      float bdot = ((1.0f / (1.0f + powf2(tt))) * lr) / (lwb * powf2(cd));
+      g5[1] = (double)(ilwb * (cb * td));
+      float inner = ((((-v) * sb) * td) * bdot) + ((v * cb) / powf2(cd));
+      g5[0] = (double)(ilwb * inner);
+      g6[0] = (double)bdot;
+    }
+    // f + g @ u   (float64)
+    const double u0 = (double)u[0], u1 = (double)u[1];
+    out[0] = f[0] + (0.0 * u0 + 0.0 * u1);
+    out[1] = f[1] + (0.0 * u0 + 0.0 * u1);
+    out[2] = f[2] + (g2 * u0 + 0.0 * u1);
+    out[3] = f[3] + (0.0 * u0 + g3 * u1);
+    out[4] = f[4] + (0.0 * u0 + 0.0 * u1);
+    out[5] = f[5] + (g5[0] * u0 + g5[1] * u1);
+    out[6] = f[6] + (g6[0] * u0 + g6[1] * u1);
+  }
+  MH_HD static void step(float* s, double*, int, const float* u, const double*, float* obs, float* rew) {
+    for (int k = 0; k < K; ++k) {
+      double d[7];
+      deriv(s, u, d);
+#pragma unroll
+      for (int i = 0; i < 7; ++i) s[i] = upd64(s[i], d[i], 0.01);
+    }
+    const float Q[7] = {2.0f, 2.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f}, R[2] = {0.1f, 0.1f};
+    *rew = quad_reward<7, 2>(s, Q, u, R);
+#pragma unroll
+    for (int i = 0; i < 7; ++i) obs[i] = s[i];
+  }
+  MH_HD static void reset_from(const float* rs, float* s, double*, const double*, float* obs) {
+#pragma unroll
+    for (int i = 0; i < 7; ++i) s[i] = obs[i] = rs[i];
+  }
+};
+
+// ---------------------------------------------------------------- QuadTracking
+// RL/env/QuadTracking.py:20-424. Persistent f32 state x[3] v[3] R[9] (row-major) W[3];
+// float64 Rd_last[9]; desired trajectory rows are a host table indexed by steps-since-reset.
+constexpr int QT_ROW = 16;  // T, DT, XD[3], B1[3], VD[3] (f32 values), AD[3] (f32 values), pad[2]
+
+struct QuadConst {
+  static constexpr double m = 4.34;
+  static constexpr double g3 = 9.8;
+  static constexpr double J0 = 0.0820, J1 = 0.0845, J2 = 0.1377;
+  static constexpr double kx = 69.44, kv = 24.304;
+  static constexpr double mg = 4.34 * 9.8;  // model.m * g[2]
+};
+
+// Orthogonal polar factor of a float32 3x3 via float64 Newton iteration X <- (X + X^-T)/2,
+// with the det<0 column flip of NormalizeOrientMatrix (QuadTracking.py:308-315).
+MH_HD void polar3(const float* Rin, float* Rout) {
+  double X[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) X[i] = (double)Rin[i];
+  double det0 = X[0] * (X[4] * X[8] - X[5] * X[7]) - X[1] * (X[3] * X[8] - X[5] * X[6]) +
+                X[2] * (X[3] * X[7] - X[4] * X[6]);
+  for (int it = 0; it < 60; ++it) {
+    double C[9];
+    C[0] = X[4] * X[8] - X[5] * X[7];
+    C[1] = X[5] * X[6] - X[3] * X[8];
+    C[2] = X[3] * X[7] - X[4] * X[6];
+    C[3] = X[2] * X[7] - X[1] * X[8];
+    C[4] = X[0] * X[8] - X[2] * X[6];
+    C[5] = X[1] * X[6] - X[0] * X[7];
+    C[6] = X[1] * X[5] - X[2] * X[4];
+    C[7] = X[2] * X[3] - X[0] * X[5];
+    C[8] = X[0] * X[4] - X[1] * X[3];
+    double det = X[0] * C[0] + X[1] * C[1] + X[2] * C[2];
+    double idet = 1.0 / det;
+    double diff = 0.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      double xn = 0.5 * (X[i] + C[i] * idet);
+      diff = fmax(diff, fabs(xn - X[i]));
+      X[i] = xn;
+    }
+    if (diff <= 4e-16) break;
+  }
+  if (det0 < 0.0) {
+    // R = U diag(1,1,-1) Vh = X (I - 2 v3 v3^T), v3 = eigenvector of H = X^T A (smallest eig).
+    double H[9];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        double acc = 0.0;
+        for (int k = 0; k < 3; ++k) acc += X[k * 3 + i] * (double)Rin[k * 3 + j];
+        H[i * 3 + j] = acc;
+      }
+    for (int i = 0; i < 3; ++i)
+      for (int j = i + 1; j < 3; ++j) {
+        double a = 0.5 * (H[i * 3 + j] + H[j * 3 + i]);
+        H[i * 3 + j] = H[j * 3 + i] = a;
+      }
+    double V[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    for (int sweep = 0; sweep < 30; ++sweep) {
+      double off = fabs(H[1]) + fabs(H[2]) + fabs(H[5]);
+      if (off < 1e-300) break;
+      for (int p = 0; p < 2; ++p)
+        for (int q = p + 1; q < 3; ++q) {
+          double apq = H[p * 3 + q];
+          if (fabs(apq) < 1e-300) continue;
+          double app = H[p * 3 + p], aqq = H[q * 3 + q];
+          double theta = 0.5 * (aqq - app) / apq;
+          double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+          double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+          for (int k = 0; k < 3; ++k) {  // H <- J^T H J
+            double hkp = H[k * 3 + p], hkq = H[k * 3 + q];
+            H[k * 3 + p] = c * hkp - s * hkq;
+            H[k * 3 + q] = s * hkp + c * hkq;
+          }
+          for (int k = 0; k < 3; ++k) {
+            double hpk = H[p * 3 + k], hqk = H[q * 3 + k];
+            H[p * 3 + k] = c * hpk - s * hqk;
+            H[q * 3 + k] = s * hpk + c * hqk;
+          }
+          for (int k = 0; k < 3; ++k) {
+            double vkp = V[k * 3 + p], vkq = V[k * 3 + q];
+            V[k * 3 + p] = c * vkp - s * vkq;
+            V[k * 3 + q] = s * vkp + c * vkq;
+          }
+        }
+    }
+    int mi = 0;
+    for (int i = 1; i < 3; ++i)
+      if (H[i * 3 + i] < H[mi * 3 + mi]) mi = i;
+    double v3[3] = {V[0 * 3 + mi], V[1 * 3 + mi], V[2 * 3 + mi]};
+    double Y[9];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        double acc = 0.0;
+        for (int k = 0; k < 3; ++k) {
+          double hk = (k == j ? 1.0 : 0.0) - 2.0 * v3[k] * v3[j];
+          acc += X[i * 3 + k] * hk;
+        }
+        Y[i * 3 + j] = acc;
+      }
+    for (int i = 0; i < 9; ++i) X[i] = Y[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Rout[i] = (float)X[i];
+}
+
+MH_HD void cross64(const double* a, const double* b, double* c) {
+  c[0] = a[1] * b[2] - a[2] * b[1];
+  c[1] = a[2] * b[0] - a[0] * b[2];
+  c[2] = a[0] * b[1] - a[1] * b[0];
+}
+MH_HD double norm3(const double* a) { return sqrt((a[0] * a[0] + a[1] * a[1]) + a[2] * a[2]); }
+
+struct QuadTracking {
+  // state floats: x[0:3] v[3:6] R[6:15] W[15:18]; xstate doubles: Rd_last[9]
+  static constexpr int D = 12, A = 4, S = 18, XS = 9, RS = 18, K = 4;
+  MH_HD static float obs_lo(int i) { (void)i; return -10.0f; }
+  MH_HD static float obs_hi(int i) { (void)i; return 10.0f; }
+  MH_HD static float act_lo(int i) { return i == 0 ? 0.0f : -10.0f; }
+  MH_HD static float act_hi(int i) { return i == 0 ? (float)(2.0 * QuadConst::mg) : 10.0f; }
+
+  // _get_desired_states (QuadTracking.py:122-149) + error observation (QuadTracking.py:241-246).
+  MH_HD static void desired_and_obs(const float* s, const double* row, bool have_last,
+                                    const double* Rdl, double* Rd, float* obs) {
+    using Q = QuadConst;
+    const float* x = s;
+    const float* v = s + 3;
+    const float* R = s + 6;
+    const float* W = s + 15;
+    const double* xd = row + 2;
+    const double* b1 = row + 5;
+    float vd[3] = {(float)row[8], (float)row[9], (float)row[10]};
+    float ad[3] = {(float)row[11], (float)row[12], (float)row[13]};
+    float ex[3], ev[3];
+    double fd[3];
+    const float nkx = (float)(-Q::kx), kv = (float)Q::kv, mf = (float)Q::m;
+    const double mg[3] = {Q::m * 0.0, Q::m * 0.0, Q::m * Q::g3};
+    for (int i = 0; i < 3; ++i) {
+      ex[i] = (float)((double)x[i] - xd[i]);       // cal_ex
+      ev[i] = v[i] - vd[i];                         // cal_ev (f32 - f32)
+      float t = nkx * ex[i] - kv * ev[i];           // f32
+      double u = (double)t - mg[i];                 // f32 - f64 -> f64
+      double w = u + (double)(mf * ad[i]);          // + f32
+      fd[i] = -w;
+    }
+    double nfd = norm3(fd);
+    double b3[3] = {fd[0] / nfd, fd[1] / nfd, fd[2] / nfd};
+    double c[3];
+    cross64(b3, b1, c);
+    double nc = norm3(c);
+    double b2[3] = {c[0] / nc, c[1] / nc, c[2] / nc};
+    double b1n[3];
+    cross64(b2, b3, b1n);
+    for (int i = 0; i < 3; ++i) {
+      Rd[i * 3 + 0] = b1n[i];
+      Rd[i * 3 + 1] = b2[i];
+      Rd[i * 3 + 2] = b3[i];
+    }
+    float Od[3] = {0.0f, 0.0f, 0.0f};
+    double Odd[3] = {0.0, 0.0, 0.0};
+    if (have_last) {
+      double dt = row[1];
+      float Rdot[9];
+      for (int i = 0; i < 9; ++i) Rdot[i] = (float)((Rd[i] - Rdl[i]) / dt);   // RDerive
+      // getOmega: So3ToVec(Rd^T @ Rdot) -> f32
+      double M21 = 0.0, M02 = 0.0, M10 = 0.0;
+      for (int k = 0; k < 3; ++k) {
+        M21 += Rd[k * 3 + 2] * (double)Rdot[k * 3 + 1];
+        M02 += Rd[k * 3 + 0] * (double)Rdot[k * 3 + 2];
+        M10 += Rd[k * 3 + 1] * (double)Rdot[k * 3 + 0];
+      }
+      Od[0] = (float)M21; Od[1] = (float)M02; Od[2] = (float)M10;
+      Odd[0] = Od[0]; Odd[1] = Od[1]; Odd[2] = Od[2];
+    }
+    // e_R = So3ToVec(Rd^T R - R^T Rd) * 0.5 ; P = R^T Rd
+    double A_[9], P[9];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        double a = 0.0, p = 0.0;
+        for (int k = 0; k < 3; ++k) {
+          a += Rd[k * 3 + i] * (double)R[k * 3 + j];
+          p += (double)R[k * 3 + i] * Rd[k * 3 + j];
+        }
+        A_[i * 3 + j] = a;
+        P[i * 3 + j] = p;
+      }
+    float eR0 = (float)(A_[7] - P[7]);  // [2,1]
+    float eR1 = (float)(A_[2] - P[2]);  // [0,2]
+    float eR2 = (float)(A_[3] - P[3]);  // [1,0]
+    // e_W = W - (R^T Rd) @ Omega_d
+    for (int i = 0; i < 3; ++i) {
+      double q = (P[i * 3 + 0] * Odd[0] + P[i * 3 + 1] * Odd[1]) + P[i * 3 + 2] * Odd[2];
+      obs[9 + i] = (float)((double)W[i] - q);
+    }
+    for (int i = 0; i < 3; ++i) {
+      obs[i] = ex[i];
+      obs[3 + i] = ev[i];
+    }
+    obs[6] = eR0 * 0.5f;
+    obs[7] = eR1 * 0.5f;
+    obs[8] = eR2 * 0.5f;
+  }
+
+  // One env.step (QuadTracking.py:205-285); k = steps since reset before this step.
+  MH_HD static void step(float* s, double* xs, int k, const float* a, const double* tab,
+                         float* obs, float* rew) {
+    using Q = QuadConst;
+    const float f = a[0];
+    const float* M = a + 1;
+    const float mf = (float)Q::m;
+    for (int it = 0; it < K; ++it) {
+      float* x = s;
+      float* v = s + 3;
+      float* R = s + 6;
+      float* W = s + 15;
+      double dv[3];
+      for (int i = 0; i < 3; ++i) dv[i] = (i == 2 ? Q::g3 : 0.0) - (double)((f * R[i * 3 + 2]) / mf);
+      // dR = R @ hat(W)   (float32)
+      float Hh[9] = {0.0f, -W[2], W[1], W[2], 0.0f, -W[0], -W[1], W[0], 0.0f};
+      float dR[9];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+          dR[i * 3 + j] = (R[i * 3 + 0] * Hh[0 * 3 + j] + R[i * 3 + 1] * Hh[1 * 3 + j]) + R[i * 3 + 2] * Hh[2 * 3 + j];
+      // dW = J^-1 (M - W x (J W))   (float64)
+      double Wd[3] = {(double)W[0], (double)W[1], (double)W[2]};
+      double JW[3] = {Q::J0 * Wd[0], Q::J1 * Wd[1], Q::J2 * Wd[2]};
+      double cr[3];
+      cross64(Wd, JW, cr);
+      double dW[3] = {(1.0 / Q::J0) * ((double)M[0] - cr[0]), (1.0 / Q::J1) * ((double)M[1] - cr[1]),
+                      (1.0 / Q::J2) * ((double)M[2] - cr[2])};
+      for (int i = 0; i < 3; ++i) x[i] = x[i] + v[i] * 0.01f;
+      for (int i = 0; i < 3; ++i) v[i] = upd64(v[i], dv[i], 0.01);
+      for (int i = 0; i < 9; ++i) R[i] = R[i] + dR[i] * 0.01f;
+      for (int i = 0; i < 3; ++i) W[i] = upd64(W[i], dW[i], 0.01);
+      float Rn[9];
+      polar3(R, Rn);
+      for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+    }
+    const double* row = tab + (size_t)(k + 1) * QT_ROW;
+    double Rd[9];
+    desired_and_obs(s, row, true, xs, Rd, obs);
+    for (int i = 0; i < 9; ++i) xs[i] = Rd[i];
+    // reward (QuadTracking.py:250-273), reward type 1 (linear bonus)
+    float sx[3], sv[3], sr[3], sw[3], su[4];
+    for (int i = 0; i < 3; ++i) {
+      sx[i] = 1.0f * (obs[i] * obs[i]);
+      sv[i] = 1.0f * (obs[3 + i] * obs[3 + i]);
+      sr[i] = 1.0f * (obs[6 + i] * obs[6 + i]);
+      sw[i] = 1.0f * (obs[9 + i] * obs[9 + i]);
+    }
+    const float Ract[4] = {0.0001f, 0.01f, 0.01f, 0.01f};
+    for (int i = 0; i < 4; ++i) su[i] = Ract[i] * (a[i] * a[i]);
+    float tot = (((np_sum<3>(sx) + np_sum<3>(sv)) + np_sum<3>(sr)) + np_sum<3>(sw)) + np_sum<4>(su);
+    float r = -tot;
+    float dist = 0.0f;
+    for (int i = 0; i < 12; ++i) dist = fmaxf(dist, fabsf(obs[i]));
+    if (dist <= 0.1f) r = r + 10.0f * (1.0f - dist / 0.1f);
+    *rew = r;
+  }
+
+  // reset tail (QuadTracking.py:188-202) from drawn x, v, R, W
+  MH_HD static void reset_from(const float* rs, float* s, double* xs, const double* tab, float* obs) {
+    for (int i = 0; i < 18; ++i) s[i] = rs[i];
+    double Rd[9];
+    desired_and_obs(s, tab, false, nullptr, Rd, obs);
+    for (int i = 0; i < 9; ++i) xs[i] = Rd[i];
+  }
+};
+
+// Host-side fill of the desired-trajectory table (QuadTracking.py:29-36, 229):
+// current_time accumulates += dt * control_step in float64; row k is the time after k steps.
+inline void quad_fill_table(double* tab, int rows) {
+  const double inc = 0.01 * 4;
+  double t = 0.0, tprev = 0.0;
+  for (int k = 0; k < rows; ++k) {
+    if (k > 0) {
+      tprev = t;
+      t = t + inc;
+    }
+    double* r = tab + (size_t)k * QT_ROW;
+    double dt = t - tprev;
+    if (dt < 1e-6) dt = 1e-6;  // safe_time_diff
+    r[0] = t;
+    r[1] = dt;
+    r[2] = 0.4 * t;
+    r[3] = 0.4 * sin(t);
+    r[4] = 0.6 * cos(t);
+    r[5] = cos(t);
+    r[6] = sin(t);
+    r[7] = 0.0;
+    r[8] = (double)(float)0.4;
+    r[9] = (double)(float)(0.4 * cos(t));
+    r[10] = (double)(float)(-0.6 * sin(t));
+    r[11] = (double)(float)0.0;
+    r[12] = (double)(float)(-0.4 * sin(t));
+    r[13] = (double)(float)(-0.6 * cos(t));
+    r[14] = 0.0;
+    r[15] = 0.0;
+  }
+}
+
+}  // namespace mh

@@ -1,0 +1,274 @@
+// msacl_kernels.hip — fused MSACL target / certificate math (RL/algorithm/msacl.py).
+//
+// The replay batch is [B][n] (B = 256, n = 20 at the reference config: 5,120 elements, 20 KB
+// per tensor). Each op below replaces a chain of 8-20 tiny PyTorch launches with ONE
+// single-workgroup kernel: one wavefront per window row keeps the n-step scan (cumprod,
+// lambda-weighted sums) in registers/LDS, and the batch-global means are reduced in float64
+// inside the workgroup in a fixed order, so results are bitwise reproducible run to run.
+// Each kernel also emits the analytic gradient w.r.t. its network-produced inputs, which the
+// Python layer feeds to autograd (custom autograd.Function), so the MLP backward stays PyTorch.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "msacl_hip.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int TPB = 1024;  // one workgroup; 16 wavefronts
+
+// torch.maximum / torch.minimum backward: ties split the gradient in half.
+__device__ __forceinline__ float relu_grad(float a) { return a > 0.0f ? 1.0f : (a == 0.0f ? 0.5f : 0.0f); }
+
+__device__ double block_sum(double v, double* sh) {
+  const int t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (int off = TPB / 2; off > 0; off >>= 1) {
+    if (t < off) sh[t] += sh[t + off];
+    __syncthreads();
+  }
+  double r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+// ------------------------------------------------------------------ Q backup (msacl.py:242-257)
+__global__ __launch_bounds__(TPB) void k_q_target(const float* q1, const float* q2, const float* q1t,
+                                                  const float* q2t, const float* nlogp, const float* rew,
+                                                  const float* done, const float* log_alpha, float gamma,
+                                                  int B, int n, float* backup, float* dq1, float* dq2,
+                                                  float* loss_out, float* abs_td) {
+  __shared__ double sh[TPB];
+  const float alpha = expf(*log_alpha);
+  const int64_t N = (int64_t)B * n;
+  const float inv = (float)(1.0 / (double)N);
+  double acc1 = 0.0, acc2 = 0.0;
+  for (int64_t i = threadIdx.x; i < N; i += TPB) {
+    const float nq = fminf(q1t[i], q2t[i]);
+    const float bk = rew[i] + ((1.0f - done[i]) * gamma) * (nq - alpha * nlogp[i]);
+    backup[i] = bk;
+    const float e1 = q1[i] - bk, e2 = q2[i] - bk;
+    acc1 += (double)e1 * (double)e1;
+    acc2 += (double)e2 * (double)e2;
+    if (dq1) dq1[i] = 2.0f * e1 * inv;
+    if (dq2) dq2[i] = 2.0f * e2 * inv;
+  }
+  const double s1 = block_sum(acc1, sh), s2 = block_sum(acc2, sh);
+  if (threadIdx.x == 0 && loss_out) loss_out[0] = (float)(s1 / (double)N) + (float)(s2 / (double)N);
+  if (abs_td) {
+    __syncthreads();
+    for (int b = threadIdx.x; b < B; b += TPB) {
+      double a = 0.0;
+      for (int k = 0; k < n; ++k) {
+        const int64_t i = (int64_t)b * n + k;
+        a += 0.5 * (fabs((double)q1[i] - (double)backup[i]) + fabs((double)q2[i] - (double)backup[i]));
+      }
+      abs_td[b] = (float)(a / n);
+    }
+  }
+}
+
+// --------------------------------------------------- Lyapunov certificate (msacl.py:279-332)
+// One wavefront per window row b: lanes own the n steps; cumprod of the clipped IS ratio is a
+// wave-level inclusive product scan (n <= 64 per pass, chained across passes).
+__global__ __launch_bounds__(TPB) void k_lyapunov(const float* logp, const float* old_logp, const float* V,
+                                                  const float* V2, const float* obs, const float* obs2,
+                                                  const float* c, const float* w, const float* s, float alpha1,
+                                                  float alpha2, float pos_scale, float diff_scale, int B, int n,
+                                                  int D, float* is_clip, float* esl, float* lya_diff,
+                                                  float* loss_out, float* dV, float* dV2) {
+  __shared__ double sh[TPB];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = TPB / 64;
+  const int64_t N = (int64_t)B * n;
+  const float invN = (float)(1.0 / (double)N);
+  const float invB = (float)(1.0 / (double)B);
+  double bound_acc = 0.0, diff_acc = 0.0;
+  for (int b = wave; b < B; b += nw) {
+    // ||obs[b, 0, :]||
+    float so = 0.0f;
+    for (int d = 0; d < D; ++d) {
+      const float x = obs[((int64_t)b * n) * D + d];
+      so = so + x * x;
+    }
+    const float start_norm = sqrtf(so);
+    const float V0 = V[(int64_t)b * n];
+    float carry = 1.0f;       // running cumprod across 64-lane passes
+    float dV0_acc = 0.0f;     // d loss3 / d V(obs[b,0]) contributions
+    float rowsum = 0.0f;
+    for (int k0 = 0; k0 < n; k0 += 64) {
+      const int k = k0 + lane;
+      const bool ok = k < n;
+      const int64_t i = (int64_t)b * n + (ok ? k : 0);
+      float cr = 1.0f;
+      if (ok) {
+        const float ratio = expf(logp[i] - old_logp[i]);
+        cr = fminf(fmaxf(ratio, 0.0f), 1.0f);   // torch.clamp(ratio, 0, 1)
+      }
+      // inclusive product scan over the wave (Hillis-Steele with shuffles)
+      float p = cr;
+      for (int off = 1; off < 64; off <<= 1) {
+        const float o = __shfl_up(p, off, 64);
+        if (lane >= off) p = p * o;
+      }
+      p = p * carry;
+      carry = __shfl(p, 63, 64);
+      if (ok) {
+        is_clip[i] = p;
+        // bound terms (loss_lya2): relu(a1*|x|^2 - V) + relu(V - a2*|x|^2)
+        float pw = 0.0f;
+        float o2 = 0.0f;
+        for (int d = 0; d < D; ++d) {
+          const float x = obs[i * D + d];
+          pw = pw + x * x;
+          const float y = obs2[i * D + d];
+          o2 = o2 + y * y;
+        }
+        const float Vi = V[i];
+        const float l1 = alpha1 * pw - Vi, l2 = Vi - alpha2 * pw;
+        bound_acc += (double)fmaxf(l1, 0.0f) + (double)fmaxf(l2, 0.0f);
+        float g = pos_scale * invN * (-relu_grad(l1) + relu_grad(l2));
+        // exponential stability label (msacl.py:307-314)
+        const float diff = start_norm * c[k] - sqrtf(o2);
+        const float E_ = diff >= 0.0f ? 1.0f : -1.0f;
+        esl[i] = E_;
+        const float t = E_ * (V2[i] - V0 * s[k]);
+        const float term = p * fmaxf(t, 0.0f);
+        rowsum = rowsum + w[k] * term;
+        const float gt = diff_scale * invB * w[k] * p * relu_grad(t);
+        dV2[i] = gt * E_;
+        dV0_acc = dV0_acc + gt * E_ * (-s[k]);
+        dV[i] = g;  // the k = 0 entry also receives dV0 below
+      }
+    }
+    // wave reductions: lambda-weighted row sum and the V(obs_b0) gradient
+    for (int off = 32; off > 0; off >>= 1) {
+      rowsum = rowsum + __shfl_xor(rowsum, off, 64);
+      dV0_acc = dV0_acc + __shfl_xor(dV0_acc, off, 64);
+    }
+    if (lane == 0) {
+      lya_diff[b] = rowsum;
+      dV[(int64_t)b * n] = dV[(int64_t)b * n] + dV0_acc;
+      diff_acc += (double)rowsum;
+    }
+  }
+  const double sb = block_sum(bound_acc, sh);
+  const double sd = block_sum(diff_acc, sh);
+  if (threadIdx.x == 0 && loss_out)
+    loss_out[0] = (float)(sb / (double)N) * pos_scale + (float)(sd / (double)B) * diff_scale;
+}
+
+// ------------------------------------------------ stability advantage (msacl.py:383-399)
+__global__ __launch_bounds__(TPB) void k_stab_adv(const float* V0, const float* V2, const float* w,
+                                                  const float* s, int B, int n, float* adv, double* stats) {
+  __shared__ double sh[TPB];
+  double a1 = 0.0, a2 = 0.0;
+  for (int b = threadIdx.x; b < B; b += TPB) {
+    float acc = 0.0f;
+    const float v0 = V0[b];
+    for (int k = 0; k < n; ++k) acc = acc + w[k] * ((v0 * s[k]) - V2[(int64_t)b * n + k]);
+    adv[b] = acc;
+    a1 += (double)acc;
+    a2 += (double)acc * (double)acc;
+  }
+  const double t1 = block_sum(a1, sh), t2 = block_sum(a2, sh);
+  if (threadIdx.x == 0) {
+    stats[0] = t1;
+    stats[1] = t2;
+  }
+}
+
+// --------------------------------------------------- PPO clip on the advantage (msacl.py:400-405)
+__global__ __launch_bounds__(TPB) void k_ppo_clip(const float* ratio, const float* adv_raw, const double* stats,
+                                                  double n_total, float eps, int B, float* adv, float* loss_out,
+                                                  float* d_ratio) {
+  __shared__ double sh[TPB];
+  const double mean = stats[0] / n_total;
+  double var = (stats[1] - n_total * mean * mean) / (n_total - 1.0);
+  var = var > 0.0 ? var : 0.0;
+  const float meanf = (float)mean, stdf = (float)sqrt(var);
+  const float lo = 1.0f - eps, hi = 1.0f + eps;
+  const float invB = (float)(1.0 / (double)B);
+  double acc = 0.0;
+  for (int b = threadIdx.x; b < B; b += TPB) {
+    const float A = (adv_raw[b] - meanf) / (stdf + 1e-8f);
+    adv[b] = A;
+    const float r = ratio[b];
+    const float rc = fminf(fmaxf(r, lo), hi);
+    const float s1 = r * A, s2 = rc * A;
+    acc += (double)fminf(s1, s2);
+    const float gclip = (r >= lo && r <= hi) ? 1.0f : 0.0f;
+    float g;
+    if (s1 < s2)
+      g = A;
+    else if (s1 > s2)
+      g = gclip * A;
+    else
+      g = 0.5f * A + 0.5f * gclip * A;
+    d_ratio[b] = g * invB;
+  }
+  const double t = block_sum(acc, sh);
+  if (threadIdx.x == 0) loss_out[0] = (float)(t / (double)B);
+}
+
+thread_local std::string g_merr;
+
+}  // namespace
+
+#define MH_CHECK_LAUNCH(name)                                    \
+  do {                                                           \
+    hipError_t _e = hipGetLastError();                           \
+    if (_e != hipSuccess) return MH_EHIP;                        \
+  } while (0)
+
+extern "C" {
+
+int mh_msacl_q_target(const float* q1, const float* q2, const float* q1t, const float* q2t,
+                      const float* next_logp, const float* rew, const float* done, const float* log_alpha,
+                      float gamma, int32_t B, int32_t n, float* backup, float* dq1, float* dq2,
+                      float* loss_out, float* abs_td, void* stream) {
+  if (!q1 || !q2 || !q1t || !q2t || !next_logp || !rew || !done || !log_alpha || !backup || B <= 0 || n <= 0)
+    return MH_EINVAL;
+  k_q_target<<<1, TPB, 0, (hipStream_t)stream>>>(q1, q2, q1t, q2t, next_logp, rew, done, log_alpha, gamma, B, n,
+                                                 backup, dq1, dq2, loss_out, abs_td);
+  MH_CHECK_LAUNCH("q_target");
+  return MH_OK;
+}
+
+int mh_msacl_lyapunov(const float* logp, const float* old_logp, const float* lya_obs, const float* lya_obs2,
+                      const float* obs, const float* obs2, const float* c, const float* w, const float* s,
+                      float alpha1, float alpha2, float pos_scale, float diff_scale, int32_t B, int32_t n,
+                      int32_t D, float* is_clip, float* esl, float* lya_diff, float* loss_out, float* d_lya_obs,
+                      float* d_lya_obs2, void* stream) {
+  if (!logp || !old_logp || !lya_obs || !lya_obs2 || !obs || !obs2 || !c || !w || !s || !is_clip || !esl ||
+      !lya_diff || !d_lya_obs || !d_lya_obs2 || B <= 0 || n <= 0 || D <= 0)
+    return MH_EINVAL;
+  k_lyapunov<<<1, TPB, 0, (hipStream_t)stream>>>(logp, old_logp, lya_obs, lya_obs2, obs, obs2, c, w, s, alpha1,
+                                                 alpha2, pos_scale, diff_scale, B, n, D, is_clip, esl, lya_diff,
+                                                 loss_out, d_lya_obs, d_lya_obs2);
+  MH_CHECK_LAUNCH("lyapunov");
+  return MH_OK;
+}
+
+int mh_msacl_stability_adv(const float* lya_obs0, const float* lya_obs2, const float* w, const float* s,
+                           int32_t B, int32_t n, float* adv_raw, double* stats_out, void* stream) {
+  if (!lya_obs0 || !lya_obs2 || !w || !s || !adv_raw || !stats_out || B <= 0 || n <= 0) return MH_EINVAL;
+  k_stab_adv<<<1, TPB, 0, (hipStream_t)stream>>>(lya_obs0, lya_obs2, w, s, B, n, adv_raw, stats_out);
+  MH_CHECK_LAUNCH("stab_adv");
+  return MH_OK;
+}
+
+int mh_msacl_ppo_clip(const float* ratio, const float* adv_raw, const double* stats, double n_total,
+                      float clip_eps, int32_t B, float* adv, float* loss_out, float* d_ratio, void* stream) {
+  if (!ratio || !adv_raw || !stats || !adv || !loss_out || !d_ratio || B <= 0 || n_total < 2.0) return MH_EINVAL;
+  k_ppo_clip<<<1, TPB, 0, (hipStream_t)stream>>>(ratio, adv_raw, stats, n_total, clip_eps, B, adv, loss_out,
+                                                 d_ratio);
+  MH_CHECK_LAUNCH("ppo_clip");
+  return MH_OK;
+}
+
+}  // extern "C"

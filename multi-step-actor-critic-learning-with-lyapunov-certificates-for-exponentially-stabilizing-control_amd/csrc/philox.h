@@ -1,0 +1,56 @@
+// philox.h — counter-based Philox4x32-10 for in-kernel action noise and reset draws.
+// Stateless: the counter is (env index, stream id, lockstep tick) so a hipGraph replay only
+// needs the device-resident tick to advance, never a host-side RNG state.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mh {
+
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+__host__ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)M0 * c.x;
+    uint64_t p1 = (uint64_t)M1 * c.z;
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+// uniform in [0, 1) with 32 random bits, as double
+__host__ __device__ __forceinline__ double u01(uint32_t v) { return (double)v * 2.3283064365386963e-10; }
+
+struct Rng {
+  uint32_t k0, k1;
+  uint32_t env_lo, env_hi, tick_lo, tick_hi;
+  __host__ __device__ __forceinline__ u32x4 draw(uint32_t stream) const {
+    return philox4x32_10(u32x4{env_lo, env_hi ^ (stream << 16), tick_lo, tick_hi}, k0, k1);
+  }
+  // 4 standard normals via Box-Muller (float64 internally)
+  __host__ __device__ __forceinline__ void normal4(uint32_t stream, double* out) const {
+    u32x4 r = draw(stream);
+    double u1 = 1.0 - u01(r.x), u2 = u01(r.y), u3 = 1.0 - u01(r.z), u4 = u01(r.w);
+    double a = sqrt(-2.0 * log(u1)), b = sqrt(-2.0 * log(u3));
+    const double tp = 6.283185307179586;
+    out[0] = a * cos(tp * u2);
+    out[1] = a * sin(tp * u2);
+    out[2] = b * cos(tp * u4);
+    out[3] = b * sin(tp * u4);
+  }
+};
+
+__host__ __device__ __forceinline__ Rng make_rng(uint64_t seed, uint64_t env, uint64_t tick) {
+  return Rng{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)env, (uint32_t)(env >> 32),
+             (uint32_t)tick, (uint32_t)(tick >> 32)};
+}
+
+}  // namespace mh

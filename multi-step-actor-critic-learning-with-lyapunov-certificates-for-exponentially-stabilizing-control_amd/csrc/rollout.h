@@ -1,0 +1,77 @@
+// rollout.h — argument blocks and launchers shared by rollout.hip and capi.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "env_math.h"
+#include "philox.h"
+
+namespace mh {
+
+constexpr int BLK = 256;  // envs per step-kernel block (4 wavefronts)
+
+// floats of one n-step ring record: obs[D] act[A] obs2[D] rew cost done logp, padded to 16 B
+__host__ __device__ constexpr int rec_floats(int D, int A) { return ((2 * D + A + 4) + 3) / 4 * 4; }
+
+struct StepArgs {
+  int64_t E;
+  float* state;      // [S][E]
+  double* xstate;    // [XS][E]
+  int32_t* steps;    // [E]
+  const double* tab; // QuadTracking desired-trajectory table (device) or null
+  int64_t* meta;     // device int64[8]: tick, emit base row, last emitted total
+  uint64_t seed;
+  // io (AoS)
+  float* obs;                 // [E][D] in: pre-step obs (ring), out: next obs
+  const float* logits;        // [E][2A]
+  const float* act_in;        // [E][A]
+  const float* logp_in;       // [E]
+  const float* reset_in;      // [E][RS]
+  float* act_out;
+  float* logp_out;
+  float* real_next_obs;
+  float* reward_out;
+  uint8_t* term_out;
+  uint8_t* trunc_out;
+  // n-step ring
+  float* ring;                // [E][n][F]
+  int32_t* ring_len;
+  int32_t* ring_pos;
+  int32_t* emit_rank;         // [E]
+  int32_t* block_count;       // [grid]
+  int n;
+  float reward_scale, cost_scale;
+};
+
+struct EmitArgs {
+  int64_t E;
+  const float* ring;
+  const int32_t* ring_pos;
+  const int32_t* emit_rank;
+  const int32_t* block_offset;
+  const int64_t* meta;
+  int64_t capacity;
+  int n, F, D, A;
+  float *obs, *act, *rew, *cost, *obs2, *done, *logp;
+};
+
+struct GatherArgs {
+  const int64_t* idx;
+  int64_t batch;
+  int n, D, A;
+  const float *s_obs, *s_act, *s_rew, *s_cost, *s_obs2, *s_done, *s_logp;
+  float *o_obs, *o_act, *o_rew, *o_cost, *o_obs2, *o_done, *o_logp;
+};
+
+hipError_t launch_rollout(int env_id, const StepArgs& a, hipStream_t st);
+hipError_t launch_reset(int env_id, const StepArgs& a, hipStream_t st);
+hipError_t launch_finalize(const int32_t* block_count, int32_t nb, int32_t* block_offset, int64_t* meta,
+                           int64_t* cursor, int64_t capacity, hipStream_t st);
+hipError_t launch_emit(const EmitArgs& a, hipStream_t st);
+hipError_t launch_gather(const GatherArgs& a, hipStream_t st);
+hipError_t launch_sample_idx(const int64_t* cursor, uint64_t seed, uint64_t counter, int64_t batch,
+                             int64_t* idx, hipStream_t st);
+hipError_t launch_transpose_f32(const float* src, float* dst, int W, int64_t E, bool to_aos, hipStream_t st);
+hipError_t launch_transpose_f64(const double* src, double* dst, int W, int64_t E, bool to_aos, hipStream_t st);
+
+}  // namespace mh

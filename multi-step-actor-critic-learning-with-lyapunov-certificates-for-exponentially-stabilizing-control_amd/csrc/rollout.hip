@@ -1,0 +1,483 @@
+// rollout.hip — lockstep rollout kernels for the six MSACL envs on gfx950.
+//
+// One thread owns one env for a whole lockstep step: persistent state is float32 SoA
+// ([dim][E], coalesced across the wavefront), caller-facing tensors are row-major AoS
+// ([E][dim], what torch/numpy hold). The fused step kernel does, per env:
+//   TanhGauss sample (or injected action) -> clip -> K Euler substeps -> reward ->
+//   termination/truncation -> rew_plus_cost -> autoreset -> n-step deque push,
+// and writes the block-local rank of every env whose deque became full. A single-block
+// finalize kernel scans the per-block counts (env-index-order emission, base.py:178) and
+// advances the store cursor; the emit kernel then copies each full deque into its window row,
+// staging the env's ring record block through LDS so both sides are wide/coalesced.
+#include "rollout.h"
+
+namespace mh {
+
+// --------------------------------------------------------------- reset distributions
+// Uniform draws evaluated like Generator.uniform(low, high) -> float64 -> astype(float32).
+__device__ __forceinline__ float uni(double u, float lo, float hi) {
+  return (float)((double)lo + ((double)hi - (double)lo) * u);
+}
+
+template <class Env>
+struct ResetDraw;
+
+template <>
+struct ResetDraw<VanderPol> {  // VanderPol.py:79-82, U(-5, 5)^2
+  __device__ static void draw(const Rng& r, float* rs) {
+    u32x4 q = r.draw(1);
+    rs[0] = uni(u01(q.x), -5.0f, 5.0f);
+    rs[1] = uni(u01(q.y), -5.0f, 5.0f);
+  }
+};
+template <>
+struct ResetDraw<Pendulum> {  // Pendulum.py:83-86, uniform over the observation box
+  __device__ static void draw(const Rng& r, float* rs) {
+    u32x4 q = r.draw(1);
+    rs[0] = uni(u01(q.x), Pendulum::obs_lo(0), Pendulum::obs_hi(0));
+    rs[1] = uni(u01(q.y), Pendulum::obs_lo(1), Pendulum::obs_hi(1));
+  }
+};
+template <int N>
+__device__ __forceinline__ void draw_box(const Rng& r, float* rs, float half) {
+  for (int i = 0; i < N; i += 4) {
+    u32x4 q = r.draw(1 + i / 4);
+    uint32_t v[4] = {q.x, q.y, q.z, q.w};
+    for (int j = 0; j < 4 && i + j < N; ++j) rs[i + j] = uni(u01(v[j]), -half, half);
+  }
+}
+template <>
+struct ResetDraw<DuctedFan> {  // DuctedFan.py:89-92
+  __device__ static void draw(const Rng& r, float* rs) { draw_box<6>(r, rs, 0.5f); }
+};
+template <>
+struct ResetDraw<TwoLink> {  // TwoLink.py:81-84
+  __device__ static void draw(const Rng& r, float* rs) { draw_box<4>(r, rs, 0.5f); }
+};
+template <>
+struct ResetDraw<SingleTrackCar> {  // SingleTrackCar.py:121-124
+  __device__ static void draw(const Rng& r, float* rs) { draw_box<7>(r, rs, 0.5f); }
+};
+template <>
+struct ResetDraw<QuadTracking> {  // QuadTracking.py:169-186
+  __device__ static void draw(const Rng& r, float* rs) {
+    u32x4 q0 = r.draw(1), q1 = r.draw(2), q2 = r.draw(3);
+    const uint32_t v[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+    for (int i = 0; i < 6; ++i) rs[i] = uni(u01(v[i]), -0.01f, 0.01f);       // x, v
+    for (int i = 0; i < 3; ++i) rs[15 + i] = uni(u01(v[6 + i]), -0.01f, 0.01f);  // Omega
+    double nz[4];
+    r.normal4(4, nz);
+    double rv[3] = {nz[0] * 0.01, nz[1] * 0.01, nz[2] * 0.01};  // rotvec ~ N(0, 0.01^2)
+    double th = sqrt(rv[0] * rv[0] + rv[1] * rv[1] + rv[2] * rv[2]);
+    double sc = th <= 1e-3 ? 0.5 - th * th / 48.0 + th * th * th * th / 3840.0 : sin(0.5 * th) / th;
+    double x = sc * rv[0], y = sc * rv[1], z = sc * rv[2], w = cos(0.5 * th);
+    double Rm[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w),     2 * (x * z + y * w),
+                    2 * (x * y + z * w),     1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
+                    2 * (x * z - y * w),     2 * (y * z + x * w),     1 - 2 * (x * x + y * y)};
+    for (int i = 0; i < 9; ++i) rs[6 + i] = (float)Rm[i];
+  }
+};
+
+// --------------------------------------------------------------- fused lockstep step
+template <class Env>
+__global__ __launch_bounds__(BLK) void k_rollout(StepArgs a) {
+  constexpr int D = Env::D, A = Env::A, S = Env::S, XS = Env::XS, RS = Env::RS;
+  constexpr int F = rec_floats(D, A);
+  const int64_t E = a.E;
+  const int64_t e = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  const bool live = e < E;
+  bool emit = false;
+  if (live) {
+    float s[S];
+    double xs[XS > 0 ? XS : 1];
+#pragma unroll
+    for (int i = 0; i < S; ++i) s[i] = a.state[(int64_t)i * E + e];
+#pragma unroll
+    for (int i = 0; i < XS; ++i) xs[i] = a.xstate[(int64_t)i * E + e];
+    const int k = a.steps[e];
+    const uint64_t tick = a.meta[0];
+    const Rng rng = make_rng(a.seed, (uint64_t)e, tick);
+
+    float obs0[D];
+    if (a.ring) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) obs0[i] = a.obs[e * D + i];
+    }
+    // ---- action: injected, or TanhGaussDistribution.sample() + clip
+    float u[A];
+    float logp = 0.0f;
+    if (a.act_in) {
+#pragma unroll
+      for (int i = 0; i < A; ++i) u[i] = a.act_in[e * A + i];
+      if (a.logp_in) logp = a.logp_in[e];
+    } else {
+      double nz[4];
+      rng.normal4(0, nz);
+      float lg = -0.0f, lt = -0.0f, ls = -0.0f;
+#pragma unroll
+      for (int i = 0; i < A; ++i) {
+        const float mu = a.logits[e * 2 * A + i];
+        const float sd = a.logits[e * 2 * A + A + i];
+        const float z = mu + sd * (float)nz[i];
+        // Normal.log_prob: -((z-mu)^2)/(2 var) - log(std) - log(sqrt(2 pi))
+        const float df = z - mu;
+        lg = lg + ((-(df * df) / (2.0f * (sd * sd)) - logf(sd)) - 0.918938533204672742f);
+        const float th = tanhf(z);
+        lt = lt + logf(1.000001f - th * th);
+        const float lo = Env::act_lo(i), hi = Env::act_hi(i);
+        const float half = (hi - lo) / 2.0f, mid = (hi + lo) / 2.0f;
+        ls = ls + logf(half);
+        float act = half * th + mid;
+        act = fminf(fmaxf(act, lo), hi);  // actions.clip(low, high)
+        u[i] = act;
+      }
+      logp = (lg - lt) - ls;
+    }
+    if (a.act_out) {
+#pragma unroll
+      for (int i = 0; i < A; ++i) a.act_out[e * A + i] = u[i];
+    }
+    if (a.logp_out) a.logp_out[e] = logp;
+
+    // ---- env.step
+    float obs2[D], r;
+    Env::step(s, xs, k, u, a.tab, obs2, &r);
+    bool term = false;
+#pragma unroll
+    for (int i = 0; i < D; ++i) term = term || (obs2[i] < Env::obs_lo(i)) || (obs2[i] > Env::obs_hi(i));
+    int k1 = k + 1;
+    const bool trunc = k1 >= MAX_STEP;
+    const bool done = term || trunc;
+    // ---- rew_plus_cost (rew_plus_cost.py:18-21)
+    float sq[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) sq[i] = obs2[i] * obs2[i];
+    const float cost = np_sum<D>(sq) * a.cost_scale;
+    const float rew = r * a.reward_scale;
+    // ---- autoreset (gymnasium 0.28.1 SyncVectorEnv.step)
+    float obsn[D];
+    if (done) {
+      float rs[RS];
+      if (a.reset_in) {
+#pragma unroll
+        for (int i = 0; i < RS; ++i) rs[i] = a.reset_in[e * RS + i];
+      } else {
+        ResetDraw<Env>::draw(rng, rs);
+      }
+      Env::reset_from(rs, s, xs, a.tab, obsn);
+      k1 = 0;
+    } else {
+#pragma unroll
+      for (int i = 0; i < D; ++i) obsn[i] = obs2[i];
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i) a.state[(int64_t)i * E + e] = s[i];
+#pragma unroll
+    for (int i = 0; i < XS; ++i) a.xstate[(int64_t)i * E + e] = xs[i];
+    a.steps[e] = k1;
+    if (a.obs) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) a.obs[e * D + i] = obsn[i];
+    }
+    if (a.real_next_obs) {
+#pragma unroll
+      for (int i = 0; i < D; ++i) a.real_next_obs[e * D + i] = obs2[i];
+    }
+    if (a.reward_out) a.reward_out[e] = r;
+    if (a.term_out) a.term_out[e] = term ? 1 : 0;
+    if (a.trunc_out) a.trunc_out[e] = trunc ? 1 : 0;
+
+    // ---- n-step deque push (base.py:180-217)
+    if (a.ring) {
+      float rec[F];
+#pragma unroll
+      for (int i = 0; i < D; ++i) rec[i] = obs0[i];
+#pragma unroll
+      for (int i = 0; i < A; ++i) rec[D + i] = u[i];
+#pragma unroll
+      for (int i = 0; i < D; ++i) rec[D + A + i] = obs2[i];
+      rec[2 * D + A + 0] = rew;
+      rec[2 * D + A + 1] = cost;
+      rec[2 * D + A + 2] = done ? 1.0f : 0.0f;
+      rec[2 * D + A + 3] = logp;
+#pragma unroll
+      for (int i = 2 * D + A + 4; i < F; ++i) rec[i] = 0.0f;
+      const int n = a.n;
+      int len = a.ring_len[e], pos = a.ring_pos[e];
+      float4* dst = reinterpret_cast<float4*>(a.ring + (e * n + pos) * F);
+#pragma unroll
+      for (int i = 0; i < F / 4; ++i) dst[i] = make_float4(rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
+      pos = pos + 1 == n ? 0 : pos + 1;
+      len = len + 1 < n ? len + 1 : n;
+      emit = (len == n);
+      if (done) len = 0;  // deque.clear() when the newest item is done
+      a.ring_len[e] = len;
+      a.ring_pos[e] = pos;
+    }
+  }
+  if (a.ring) {
+    // block-local exclusive rank of emitters (wave ballot + LDS), env-index order
+    __shared__ int wcnt[BLK / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(emit);
+    if (lane == 0) wcnt[wave] = __popcll(m);
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < BLK / 64; ++w) {
+      base += (w < wave) ? wcnt[w] : 0;
+      tot += wcnt[w];
+    }
+    const int rank = emit ? base + __popcll(m & ((1ull << lane) - 1ull)) : -1;
+    if (live) a.emit_rank[e] = rank;
+    if (threadIdx.x == 0) a.block_count[blockIdx.x] = tot;
+  }
+}
+
+// --------------------------------------------------------------- reset kernel
+template <class Env>
+__global__ __launch_bounds__(BLK) void k_reset(StepArgs a) {
+  constexpr int D = Env::D, S = Env::S, XS = Env::XS, RS = Env::RS;
+  const int64_t E = a.E;
+  const int64_t e = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  if (e >= E) return;
+  float rs[RS], s[S], o[D];
+  double xs[XS > 0 ? XS : 1];
+  if (a.reset_in) {
+#pragma unroll
+    for (int i = 0; i < RS; ++i) rs[i] = a.reset_in[e * RS + i];
+  } else {
+    ResetDraw<Env>::draw(make_rng(a.seed, (uint64_t)e, a.meta[0]), rs);
+  }
+  Env::reset_from(rs, s, xs, a.tab, o);
+#pragma unroll
+  for (int i = 0; i < S; ++i) a.state[(int64_t)i * E + e] = s[i];
+#pragma unroll
+  for (int i = 0; i < XS; ++i) a.xstate[(int64_t)i * E + e] = xs[i];
+  a.steps[e] = 0;
+  if (a.obs) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) a.obs[e * D + i] = o[i];
+  }
+  if (a.ring) {
+    a.ring_len[e] = 0;
+    a.ring_pos[e] = 0;
+  }
+}
+
+// --------------------------------------------------------------- finalize (scan + cursor)
+__global__ __launch_bounds__(1024) void k_finalize(const int32_t* block_count, int32_t nb,
+                                                   int32_t* block_offset, int64_t* meta,
+                                                   int64_t* cursor, int64_t capacity) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int per = (nb + 1023) / 1024;
+  const int lo = min(nb, t * per), hi = min(nb, lo + per);
+  int64_t local = 0;
+  for (int i = lo; i < hi; ++i) local += block_count[i];
+  part[t] = local;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    int64_t v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int64_t run = t > 0 ? part[t - 1] : 0;
+  for (int i = lo; i < hi; ++i) {
+    block_offset[i] = (int32_t)run;
+    run += block_count[i];
+  }
+  if (t == 0) {
+    const int64_t total = part[1023];
+    meta[0] += 1;  // lockstep tick (RNG counter)
+    meta[2] = total;
+    if (cursor) {
+      const int64_t base = cursor[0];
+      meta[1] = base;
+      int64_t keep = total < capacity ? total : capacity;
+      (void)keep;
+      cursor[0] = (base + total) % capacity;
+      const int64_t sz = cursor[1] + total;
+      cursor[1] = sz < capacity ? sz : capacity;
+      cursor[2] += total;
+      cursor[3] = total;
+    }
+  }
+}
+
+// --------------------------------------------------------------- window emission
+__global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
+  extern __shared__ float lds[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t e = (int64_t)blockIdx.x * 4 + wave;
+  if (e >= a.E) return;
+  const int rank = a.emit_rank[e];
+  if (rank < 0) return;
+  const int64_t g = (int64_t)a.block_offset[e / BLK] + rank;
+  const int64_t total = a.meta[2];
+  const int64_t M = a.capacity;
+  if (g < total - M) return;  // overwritten later in this same step (FIFO order)
+  const int64_t row = (a.meta[1] + g) % M;
+  const int n = a.n, F = a.F, D = a.D, A = a.A;
+  float* buf = lds + wave * n * F;
+  const float4* src = reinterpret_cast<const float4*>(a.ring + e * (int64_t)n * F);
+  float4* b4 = reinterpret_cast<float4*>(buf);
+  for (int i = lane; i < (n * F) / 4; i += 64) b4[i] = src[i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int pos = a.ring_pos[e];  // oldest record of a full deque
+  struct Field {
+    float* dst;
+    int off, width;
+  };
+  const Field fields[7] = {{a.obs, 0, D},          {a.act, D, A},          {a.obs2, D + A, D},
+                           {a.rew, 2 * D + A, 1},  {a.cost, 2 * D + A + 1, 1},
+                           {a.done, 2 * D + A + 2, 1}, {a.logp, 2 * D + A + 3, 1}};
+#pragma unroll
+  for (int f = 0; f < 7; ++f) {
+    const int W = fields[f].width, off = fields[f].off;
+    float* dst = fields[f].dst + row * (int64_t)n * W;
+    for (int idx = lane; idx < n * W; idx += 64) {
+      const int j = idx / W, d = idx - j * W;
+      int slot = pos + j;
+      slot = slot >= n ? slot - n : slot;
+      dst[idx] = buf[slot * F + off + d];
+    }
+  }
+}
+
+// --------------------------------------------------------------- replay gather / indices
+__global__ __launch_bounds__(256) void k_gather(GatherArgs a) {
+  const int64_t b = blockIdx.x;
+  if (b >= a.batch) return;
+  const int64_t r = a.idx[b];
+  const int n = a.n;
+  struct Field {
+    const float* src;
+    float* dst;
+    int width;
+  };
+  const Field fields[7] = {{a.s_obs, a.o_obs, a.D},   {a.s_act, a.o_act, a.A},   {a.s_rew, a.o_rew, 1},
+                           {a.s_cost, a.o_cost, 1},   {a.s_obs2, a.o_obs2, a.D}, {a.s_done, a.o_done, 1},
+                           {a.s_logp, a.o_logp, 1}};
+#pragma unroll
+  for (int f = 0; f < 7; ++f) {
+    if (!fields[f].dst) continue;
+    const int64_t len = (int64_t)n * fields[f].width;
+    const float* s = fields[f].src + r * len;
+    float* d = fields[f].dst + b * len;
+    for (int64_t i = threadIdx.x; i < len; i += 256) d[i] = s[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_sample_idx(const int64_t* cursor, uint64_t seed, uint64_t counter,
+                                                   int64_t batch, int64_t* idx) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= batch) return;
+  const int64_t size = cursor[1];
+  const Rng r = make_rng(seed, (uint64_t)b, counter);
+  const u32x4 q = r.draw(7);
+  const uint64_t v = ((uint64_t)q.x << 32) | q.y;
+  idx[b] = size > 0 ? (int64_t)(v % (uint64_t)size) : 0;
+}
+
+// --------------------------------------------------------------- state transposes
+template <typename T>
+__global__ __launch_bounds__(256) void k_soa_to_aos(const T* src, T* dst, int W, int64_t E) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= E * W) return;
+  const int64_t e = i / W;
+  const int c = (int)(i - e * W);
+  dst[i] = src[(int64_t)c * E + e];
+}
+template <typename T>
+__global__ __launch_bounds__(256) void k_aos_to_soa(const T* src, T* dst, int W, int64_t E) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= E * W) return;
+  const int64_t e = i / W;
+  const int c = (int)(i - e * W);
+  dst[(int64_t)c * E + e] = src[i];
+}
+
+// --------------------------------------------------------------- launchers
+template <class Env>
+hipError_t launch_rollout_t(const StepArgs& a, hipStream_t st) {
+  const int grid = (int)((a.E + BLK - 1) / BLK);
+  k_rollout<Env><<<grid, BLK, 0, st>>>(a);
+  return hipGetLastError();
+}
+template <class Env>
+hipError_t launch_reset_t(const StepArgs& a, hipStream_t st) {
+  const int grid = (int)((a.E + BLK - 1) / BLK);
+  k_reset<Env><<<grid, BLK, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_rollout(int env_id, const StepArgs& a, hipStream_t st) {
+  switch (env_id) {
+    case ENV_VANDERPOL: return launch_rollout_t<VanderPol>(a, st);
+    case ENV_PENDULUM: return launch_rollout_t<Pendulum>(a, st);
+    case ENV_DUCTEDFAN: return launch_rollout_t<DuctedFan>(a, st);
+    case ENV_TWOLINK: return launch_rollout_t<TwoLink>(a, st);
+    case ENV_SINGLETRACKCAR: return launch_rollout_t<SingleTrackCar>(a, st);
+    case ENV_QUADTRACKING: return launch_rollout_t<QuadTracking>(a, st);
+  }
+  return hipErrorInvalidValue;
+}
+hipError_t launch_reset(int env_id, const StepArgs& a, hipStream_t st) {
+  switch (env_id) {
+    case ENV_VANDERPOL: return launch_reset_t<VanderPol>(a, st);
+    case ENV_PENDULUM: return launch_reset_t<Pendulum>(a, st);
+    case ENV_DUCTEDFAN: return launch_reset_t<DuctedFan>(a, st);
+    case ENV_TWOLINK: return launch_reset_t<TwoLink>(a, st);
+    case ENV_SINGLETRACKCAR: return launch_reset_t<SingleTrackCar>(a, st);
+    case ENV_QUADTRACKING: return launch_reset_t<QuadTracking>(a, st);
+  }
+  return hipErrorInvalidValue;
+}
+hipError_t launch_finalize(const int32_t* block_count, int32_t nb, int32_t* block_offset, int64_t* meta,
+                           int64_t* cursor, int64_t capacity, hipStream_t st) {
+  k_finalize<<<1, 1024, 0, st>>>(block_count, nb, block_offset, meta, cursor, capacity);
+  return hipGetLastError();
+}
+hipError_t launch_emit(const EmitArgs& a, hipStream_t st) {
+  const int grid = (int)((a.E + 3) / 4);
+  const size_t shm = (size_t)4 * a.n * a.F * sizeof(float);
+  k_emit<<<grid, 256, shm, st>>>(a);
+  return hipGetLastError();
+}
+hipError_t launch_gather(const GatherArgs& a, hipStream_t st) {
+  if (a.batch <= 0) return hipSuccess;
+  k_gather<<<(int)a.batch, 256, 0, st>>>(a);
+  return hipGetLastError();
+}
+hipError_t launch_sample_idx(const int64_t* cursor, uint64_t seed, uint64_t counter, int64_t batch,
+                             int64_t* idx, hipStream_t st) {
+  if (batch <= 0) return hipSuccess;
+  k_sample_idx<<<(int)((batch + 255) / 256), 256, 0, st>>>(cursor, seed, counter, batch, idx);
+  return hipGetLastError();
+}
+hipError_t launch_transpose_f32(const float* src, float* dst, int W, int64_t E, bool to_aos, hipStream_t st) {
+  const int64_t n = E * W;
+  if (n == 0) return hipSuccess;
+  const int grid = (int)((n + 255) / 256);
+  if (to_aos)
+    k_soa_to_aos<float><<<grid, 256, 0, st>>>(src, dst, W, E);
+  else
+    k_aos_to_soa<float><<<grid, 256, 0, st>>>(src, dst, W, E);
+  return hipGetLastError();
+}
+hipError_t launch_transpose_f64(const double* src, double* dst, int W, int64_t E, bool to_aos, hipStream_t st) {
+  const int64_t n = E * W;
+  if (n == 0) return hipSuccess;
+  const int grid = (int)((n + 255) / 256);
+  if (to_aos)
+    k_soa_to_aos<double><<<grid, 256, 0, st>>>(src, dst, W, E);
+  else
+    k_aos_to_soa<double><<<grid, 256, 0, st>>>(src, dst, W, E);
+  return hipGetLastError();
+}
+
+}  // namespace mh

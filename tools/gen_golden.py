@@ -1,0 +1,408 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by EXECUTING the reference's own code.
+
+Runs only in the build container (the reference is not on the GPU box); the fixtures it writes
+are data (inputs + reference outputs) and are committed. Nothing here is imported by the
+product package.
+
+  env_<Name>.npz     512 (state, action) -> (obs, reward, terminated, truncated, state') pairs
+                     per env, from the reference env.step (RL/env/<Name>.py) run on injected
+                     states (tools/refload.py: methods compiled from the reference source;
+                     gymnasium absent and not stood in for), incl. near-bound states and
+                     steps 998/999 (truncation).
+  reset_QuadTracking.npz  reset observation from injected (x, v, R, W) via the reference reset
+                     tail (QuadTracking.py:161-202, the RNG draws replaced by the injected state).
+  nstep_<Name>.npz   BaseSampler._n_step (RL/trainer/sampler/base.py:118-222, compiled from the
+                     reference source) over a vector env of reference env objects with the
+                     gymnasium 0.28.1 SyncVectorEnv autoreset restated, the reference
+                     StochaPolicy/TanhGaussDistribution sampling actions (torch CPU RNG, seeded);
+                     records actions, log-probs, injected resets and every emitted window.
+  msacl_update.npz   two MSACL.model_update calls (RL/algorithm/msacl.py:174-224) on a fixed
+                     batch with fixed weights; the Normal.rsample noise is recorded so the
+                     device implementation can replay it. `.cuda()` is made a no-op in this
+                     process only (no GPU in the build container).
+Usage: python tools/gen_golden.py
+"""
+from __future__ import annotations
+
+import ast
+import os
+import sys
+import types
+from collections import deque
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from oracle import envs as OE  # noqa: E402
+from tools.refload import REF, RefModule, load_env  # noqa: E402
+
+OUT = os.path.join(ROOT, "tests", "golden")
+F32 = np.float32
+
+
+# ---------------------------------------------------------------------- env step pairs
+def _rollout_states(name, n_keep, rng, horizon=60):
+    """Realistic input states: oracle rollouts from reset draws with random in-box actions."""
+    cls = OE.ENVS[name]
+    E = max(n_keep, 64)
+    if name == "QuadTracking":
+        rs = cls.reset_draw(rng, E, gauss=lambda k: rng.standard_normal((k, 3)))
+    else:
+        rs = cls.reset_draw(rng, E)
+    st, xs, _ = OE.env_reset_from(name, rs)
+    steps = np.zeros(E, np.int64)
+    pool = []
+    for t in range(horizon):
+        act = _actions(name, rng, E, gentle=True)
+        s2, xs2, obs, rew, te, tr = OE.env_step(name, st, act, xs, steps)
+        done = te | tr
+        steps = steps + 1
+        st, xs = s2, xs2
+        if done.any():
+            idx = np.nonzero(done)[0]
+            if name == "QuadTracking":
+                r2 = cls.reset_draw(rng, idx.size, gauss=lambda k: rng.standard_normal((k, 3)))
+            else:
+                r2 = cls.reset_draw(rng, idx.size)
+            a, b, _ = OE.env_reset_from(name, r2)
+            st[idx] = a
+            if xs is not None:
+                xs[idx] = b
+            steps[idx] = 0
+        pool.append((st.copy(), None if xs is None else xs.copy(), steps.copy()))
+    S = np.concatenate([p[0] for p in pool])
+    X = None if pool[0][1] is None else np.concatenate([p[1] for p in pool])
+    K = np.concatenate([p[2] for p in pool])
+    pick = rng.choice(S.shape[0], n_keep, replace=False)
+    return S[pick], (None if X is None else X[pick]), K[pick]
+
+
+def _actions(name, rng, n, gentle=False):
+    cls = OE.ENVS[name]
+    lo, hi = cls.act_low.astype(np.float64), cls.act_high.astype(np.float64)
+    if name == "QuadTracking" and gentle:
+        mg = 4.34 * 9.8
+        a = np.stack([rng.normal(mg, 3.0, n), rng.normal(0, 0.3, n), rng.normal(0, 0.3, n), rng.normal(0, 0.3, n)], 1)
+        return np.clip(a, lo, hi).astype(F32)
+    if gentle:
+        return rng.uniform(lo * 0.3, hi * 0.3, size=(n, lo.size)).astype(F32)
+    return rng.uniform(lo, hi, size=(n, lo.size)).astype(F32)
+
+
+def gen_env_pairs(name, N=512, seed=0):
+    rng = np.random.default_rng(1000 + seed + OE.ENV_IDS[name])
+    mod = load_env(name)
+    env = mod.make()
+    cls = OE.ENVS[name]
+    S, X, K = _rollout_states(name, N, rng)
+    A = np.concatenate([_actions(name, rng, N // 2, gentle=True), _actions(name, rng, N - N // 2)])
+    # edge cases: truncation boundary and near-bound states
+    K[0:8] = 999
+    K[8:16] = 998
+    if name != "QuadTracking":
+        lo, hi = cls.obs_low.astype(np.float64), cls.obs_high.astype(np.float64)
+        for j in range(16, 48):
+            d = j % cls.obs_dim
+            S[j, d] = F32((hi[d] if j % 2 else lo[d]) * (1.0 - 1e-4 * (j % 5)))
+    else:
+        S[16:24, 0:3] += F32(9.5)  # position error near the +-10 bound
+    obs_out = np.zeros((N, cls.obs_dim), F32)
+    state_out = np.zeros_like(S)
+    xstate_out = None if X is None else np.zeros_like(X)
+    rew = np.zeros(N, np.float64)
+    term = np.zeros(N, bool)
+    trunc = np.zeros(N, bool)
+    T = OE.QuadTracking.T
+    for i in range(N):
+        k = int(K[i])
+        if name == "QuadTracking":
+            env.x = S[i, 0:3].copy()
+            env.v = S[i, 3:6].copy()
+            env.R = S[i, 6:15].reshape(3, 3).copy()
+            env.Omega = S[i, 15:18].copy()
+            env.Rd_last = X[i].reshape(3, 3).astype(np.float64).copy()
+            env.Omega_d_last = np.zeros(3, F32)
+            env.current_step = k
+            env.current_time = float(T[k])
+            env.t_last = np.array([T[k], T[k - 1] if k > 0 else 0.0])
+        else:
+            env.obs = S[i].copy()
+            env.current_step = k
+        o, r, te, tr, _ = env.step(A[i].copy())
+        obs_out[i] = o
+        rew[i] = r
+        term[i] = bool(te)
+        trunc[i] = bool(tr)
+        if name == "QuadTracking":
+            state_out[i] = np.concatenate([env.x, env.v, env.R.reshape(9), env.Omega])
+            xstate_out[i] = env.Rd_last.reshape(9)
+        else:
+            state_out[i] = env.obs
+    d = dict(state=S, steps=K.astype(np.int32), act=A, obs=obs_out, reward=rew, terminated=term,
+             truncated=trunc, state_out=state_out)
+    if X is not None:
+        d["xstate"] = X.astype(np.float64)
+        d["xstate_out"] = xstate_out
+    np.savez_compressed(os.path.join(OUT, f"env_{name}.npz"), **d)
+    print(f"env_{name}: {N} pairs, term={term.sum()} trunc={trunc.sum()}")
+
+
+# ---------------------------------------------------------------------- reset helpers
+_RESET_SKIP = ("seed", "np_random", "super()", "random_rot_vec")
+
+
+def ref_reset(mod, env, name, rs):
+    """Reference reset() with its RNG draws replaced by the injected state rs."""
+    if name == "QuadTracking":
+        env.x = rs[0:3].copy()
+        env.v = rs[3:6].copy()
+        env.R = rs[6:15].reshape(3, 3).copy()
+        env.Omega = rs[15:18].copy()
+    else:
+        env.obs = rs.astype(F32).copy()
+    out = mod.run_statements("reset", env, lambda s: any(t in s for t in _RESET_SKIP))
+    return np.asarray(out[0], F32).copy()
+
+
+def gen_quad_reset(N=256, seed=7):
+    rng = np.random.default_rng(seed)
+    mod = load_env("QuadTracking")
+    env = mod.make()
+    rs = OE.QuadTracking.reset_draw(rng, N, gauss=lambda k: rng.standard_normal((k, 3)))
+    rs[: N // 4, 0:6] *= 300.0  # larger position/velocity offsets as well
+    obs, rdl = [], []
+    for i in range(N):
+        obs.append(ref_reset(mod, env, "QuadTracking", rs[i]))
+        rdl.append(np.asarray(env.Rd_last, np.float64).reshape(9).copy())
+    np.savez_compressed(os.path.join(OUT, "reset_QuadTracking.npz"), reset_state=rs, obs=np.stack(obs),
+                        rd_last=np.stack(rdl))
+    print(f"reset_QuadTracking: {N}")
+
+
+# ---------------------------------------------------------------------- n-step sampler traces
+class RefVectorEnv:
+    """gymnasium 0.28.1 SyncVectorEnv.step autoreset (restated) over reference env objects."""
+
+    def __init__(self, mod, name, E, init_resets, init_steps, reset_pool):
+        self.mod, self.name, self.E = mod, name, E
+        self.envs = [mod.make() for _ in range(E)]
+        cls = OE.ENVS[name]
+        self.action_space = types.SimpleNamespace(low=np.tile(cls.act_low, (E, 1)), high=np.tile(cls.act_high, (E, 1)))
+        self.pool = reset_pool
+        self.pool_i = 0
+        self.obs0 = np.stack([ref_reset(mod, e, name, init_resets[i]) for i, e in enumerate(self.envs)])
+        for i, e in enumerate(self.envs):
+            e.current_step = int(init_steps[i])
+        self.log_actions, self.log_resets = [], []
+
+    def step(self, actions):
+        self.log_actions.append(np.asarray(actions, F32).copy())
+        rs_used = np.zeros((self.E, self.pool.shape[1]), F32)
+        obs, finals = [], np.empty(self.E, dtype=object)
+        rewards = np.zeros(self.E, np.float64)
+        terms = np.zeros(self.E, bool)
+        truncs = np.zeros(self.E, bool)
+        for i, env in enumerate(self.envs):
+            o, r, te, tr, info = env.step(actions[i])
+            rewards[i], terms[i], truncs[i] = r, te, tr
+            o = np.asarray(o, F32).copy()
+            if te or tr:
+                finals[i] = o
+                rs = self.pool[self.pool_i]
+                self.pool_i += 1
+                rs_used[i] = rs
+                o = ref_reset(self.mod, env, self.name, rs)
+            obs.append(o)
+        self.log_resets.append(rs_used)
+        return np.stack(obs).astype(F32), rewards, terms, truncs, {"final_observation": finals}
+
+
+def load_n_step():
+    """Compile BaseSampler._n_step and nStepExperience from RL/trainer/sampler/base.py."""
+    path = f"{REF}/RL/trainer/sampler/base.py"
+    tree = ast.parse(open(path).read())
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    ns = {"__name__": "ref_base"}
+    fn = None
+    for node in tree.body:
+        if isinstance(node, ast.ImportFrom) and node.module == "RL.create_pkg.create_envs":
+            continue  # imports gymnasium (absent)
+        if isinstance(node, ast.ClassDef) and node.name == "BaseSampler":
+            for item in node.body:
+                if isinstance(item, ast.FunctionDef) and item.name == "_n_step":
+                    fn = item
+            continue
+        exec(compile(ast.Module(body=[node], type_ignores=[]), path, "exec"), ns)
+    exec(compile(ast.Module(body=[fn], type_ignores=[]), path, "exec"), ns)
+    return ns["_n_step"]
+
+
+def gen_nstep_trace(name, E=24, T=40, n_step=5, seed=3, tag=""):
+    import torch
+    from RL.apprfunc.mlp import StochaPolicy
+    from RL.utils.act_distribution_cls import TanhGaussDistribution
+
+    rng = np.random.default_rng(seed + 17 * OE.ENV_IDS[name])
+    torch.manual_seed(seed)
+    mod = load_env(name)
+    cls = OE.ENVS[name]
+
+    def draw(k):
+        if name == "QuadTracking":
+            return cls.reset_draw(rng, k, gauss=lambda m: rng.standard_normal((m, 3)))
+        return cls.reset_draw(rng, k)
+
+    init_resets = draw(E)
+    init_steps = np.zeros(E, np.int64)
+    if name != "QuadTracking":
+        init_steps[: E // 4] = 1000 - 7  # exercise truncation (and deque clears) inside the trace
+    pool = draw(E * T)
+    venv = RefVectorEnv(mod, name, E, init_resets, init_steps, pool)
+    policy = StochaPolicy(obs_dim=cls.obs_dim, act_dim=cls.act_dim, hidden_sizes=[64, 64], hidden_activation="relu",
+                          output_activation="linear", min_log_std=-20, max_log_std=1,
+                          act_high_lim=cls.act_high.copy(), act_low_lim=cls.act_low.copy(),
+                          action_distribution_cls=TanhGaussDistribution)
+    if name == "QuadTracking":  # keep quads airborne for a while: near-hover mean, small std
+        with torch.no_grad():
+            last = policy.policy[-2]
+            last.weight.mul_(0.01)
+            last.bias.zero_()
+            last.bias[cls.act_dim:] = -1.5
+    logps = []
+
+    class Net:
+        def __init__(self):
+            self.policy = policy
+
+        def create_action_distributions(self, logits):
+            dist = policy.get_act_dist_cls(logits)
+            orig = dist.sample
+
+            def sample():
+                a, lp = orig()
+                logps.append(lp.detach().numpy().astype(F32).copy())
+                return a, lp
+            dist.sample = sample
+            return dist
+
+    smp = types.SimpleNamespace(env_id=name, num_envs=E, envs=venv, networks=Net(), noise_params=None,
+                                action_type="continu", reward_scale=100.0, cost_scale=100.0, target_value=0.0,
+                                n_step=n_step, n_step_buffers=[deque(maxlen=n_step) for _ in range(E)],
+                                obs=venv.obs0.astype(F32).copy())
+    _n_step = types.MethodType(load_n_step(), smp)
+    counts, windows = [], {k: [] for k in ("obs", "act", "rew", "cost", "obs2", "done", "logp")}
+    obs_trace = [smp.obs.copy()]
+    with torch.no_grad():
+        for t in range(T):
+            exps = _n_step()
+            counts.append(len(exps))
+            for ex in exps:
+                for k, v in zip(windows.keys(), ex):
+                    windows[k].append(np.asarray(v, F32))
+            obs_trace.append(np.asarray(smp.obs, F32).copy())
+    d = dict(init_reset=init_resets, init_steps=init_steps.astype(np.int32), actions=np.stack(venv.log_actions),
+             logp=np.stack(logps), resets=np.stack(venv.log_resets), counts=np.array(counts, np.int64),
+             obs_trace=np.stack(obs_trace), n_step=np.int64(n_step))
+    for k, v in windows.items():
+        d["w_" + k] = np.stack(v) if v else np.zeros((0,), F32)
+    fn = f"nstep_{name}{tag}.npz"
+    np.savez_compressed(os.path.join(OUT, fn), **d)
+    print(f"{fn}: E={E} T={T} n={n_step} windows={sum(counts)} resets={int((np.abs(d['resets']).sum(-1) > 0).sum())}")
+
+
+# ---------------------------------------------------------------------- MSACL update
+def gen_msacl(B=64, n=20, seed=11):
+    import torch
+    import torch.distributions.normal as tdn
+
+    torch.Tensor.cuda = lambda self, *a, **k: self   # build container has no GPU (this process only)
+    torch.nn.Module.cuda = lambda self, *a, **k: self
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    from RL.algorithm.msacl import MSACL
+
+    torch.manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    cls = OE.QuadTracking
+    D, A = cls.obs_dim, cls.act_dim
+    kw = dict(env_name="QuadTracking", obs_dim=D, act_dim=A, action_type="continu",
+              action_high_limit=cls.act_high.copy(), action_low_limit=cls.act_low.copy(),
+              value_func_name="ActionValue", value_func_type="MLP", value_hidden_sizes=[64, 64],
+              value_hidden_activation="relu", value_output_activation="linear",
+              lyapunov_func_name="LyapunovValue", lyapunov_func_type="MLP", lyapunov_hidden_sizes=[64, 64],
+              lyapunov_hidden_activation="tanh", lyapunov_output_dim=32, lyapunov_output_activation="linear",
+              lyapunov_single_input_dim=False, policy_func_name="StochaPolicy", policy_func_type="MLP",
+              policy_act_distribution="TanhGaussDistribution", policy_hidden_sizes=[64, 64],
+              policy_hidden_activation="relu", policy_min_log_std=-20, policy_max_log_std=1,
+              q_learning_rate=1e-3, lyapunov_learning_rate=1e-3, policy_learning_rate=3e-4, alpha_learning_rate=1e-3,
+              lya_diff_scale=10.0, lya_zero_scale=1.0, lya_positive_scale=1.0, gamma=0.99, retrace_lambda=0.95,
+              tau=0.005, disable_auto_alpha=False, alpha=1.0, set_alpha_bound=False, alpha_bound=2.0, n_step=n,
+              policy_frequency=2, target_network_frequency=1, anneal_lr=False, alpha1=1, alpha2=2, lya_eta=0.15,
+              clip_coef=0.1, replay_batch_size=B, max_iteration=1000)
+    alg = MSACL(**kw)
+    init_sd = {k: v.detach().numpy().copy() for k, v in alg.networks.state_dict().items()}
+    # a synthetic but well-formed batch: old log-probs from the current policy plus noise
+    obs = (rng.standard_normal((B, n, D)) * 0.3).astype(F32)
+    obs2 = (obs + rng.standard_normal((B, n, D)).astype(F32) * 0.05).astype(F32)
+    lo, hi = cls.act_low, cls.act_high
+    act = (lo + (hi - lo) * rng.uniform(0.05, 0.95, size=(B, n, A))).astype(F32)
+    with torch.no_grad():
+        dist = alg.networks.create_action_distributions(alg.networks.policy(torch.from_numpy(obs)))
+        lp = dist.log_prob(torch.from_numpy(act)).numpy()
+    logp = (lp + rng.normal(0, 0.5, size=lp.shape)).astype(F32)
+    rew = (rng.standard_normal((B, n)) * 10).astype(F32)
+    cost = (rng.uniform(0, 5, size=(B, n))).astype(F32)
+    done = np.zeros((B, n), F32)
+    done[rng.choice(B, B // 8, replace=False), n - 1] = 1.0
+    data_np = dict(obs=obs, act=act, rew=rew, cost=cost, obs2=obs2, done=done, logp=logp)
+    eps_log = []
+    orig = tdn._standard_normal
+
+    def rec(shape, dtype, device):
+        e = orig(shape, dtype=dtype, device=device)
+        eps_log.append(e.detach().numpy().copy())
+        return e
+    tdn._standard_normal = rec
+    outs = []
+    for it in range(2):
+        data = {k: torch.from_numpy(v.copy()) for k, v in data_np.items()}
+        tb = alg.model_update(data, it)
+        outs.append(tb)
+        sd = {k: v.detach().numpy().copy() for k, v in alg.networks.state_dict().items()}
+        if it == 0:
+            sd0 = sd
+    tdn._standard_normal = orig
+    tb0 = outs[0]
+    d = {"in_" + k: v for k, v in data_np.items()}
+    for k, v in init_sd.items():
+        d["init/" + k] = v
+    for k, v in sd0.items():
+        d["after0/" + k] = v
+    for k, v in sd.items():
+        d["after1/" + k] = v
+    for i, e in enumerate(eps_log):
+        d[f"eps{i}"] = e
+    d["tb_keys"] = np.array(list(tb0.keys()))
+    d["tb_vals"] = np.array([float(v) for v in tb0.values()])
+    d["cfg_B"], d["cfg_n"] = np.int64(B), np.int64(n)
+    np.savez_compressed(os.path.join(OUT, "msacl_update.npz"), **d)
+    print("msacl_update:", {k: round(float(v), 6) for k, v in tb0.items()}, "eps draws:", len(eps_log))
+
+
+if __name__ == "__main__":
+    os.makedirs(OUT, exist_ok=True)
+    which = sys.argv[1:] or ["env", "reset", "nstep", "msacl"]
+    if "env" in which:
+        for nm in OE.ENVS:
+            gen_env_pairs(nm)
+    if "reset" in which:
+        gen_quad_reset()
+    if "nstep" in which:
+        for nm in OE.ENVS:
+            gen_nstep_trace(nm)
+        gen_nstep_trace("VanderPol", E=16, T=60, n_step=20, seed=5, tag="_n20")
+    if "msacl" in which:
+        gen_msacl()
