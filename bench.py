@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""Headline benchmark: env steps/sec (whole node), QuadrotorTracking, 65,536 envs per GPU.
+
+A "step" is one NstepOffSerialTrainer.step() of the MSACL pipeline built exactly like
+example/msacl_train.py (create_envs -> init_args -> create_alg/sampler/buffer/trainer):
+sample() = 20 lockstep steps of all envs (policy MLP + fused HIP rollout/n-step emission),
+add_batch, replay sample_batch(256) and the full MSACL model_update (twin-Q, Lyapunov, 2x
+policy + alpha on even iterations). Env-steps per step = envs x horizon (20).
+
+Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run
+(one rank per GPU, RCCL). Rank 0 prints ONE JSON line.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--env", default="QuadTracking")
+    p.add_argument("--envs", type=int, default=65536, help="parallel envs per GPU")
+    p.add_argument("--policy", choices=["init", "hover"], default="init",
+                   help="init: PyTorch default init (SURVEY 8d); hover: action mean [mg,0,0,0], long episodes")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def set_hover_policy(policy, mg):
+    """SURVEY 8d second variant: mean = [mg, 0, 0, 0] (tanh-squashed centre of the box is mg
+    for the thrust), std = (2, 0.5, 0.5, 0.5) in pre-tanh units scaled to the box."""
+    import math
+    import torch
+    last = policy.policy[-2]
+    with torch.no_grad():
+        last.weight.zero_()
+        last.bias.zero_()
+        A = last.bias.numel() // 2
+        stds = [2.0 / mg, 0.5 / 10.0, 0.5 / 10.0, 0.5 / 10.0][:A]
+        for i, s in enumerate(stds):
+            last.bias[A + i] = math.log(s)
+
+
+def cpu_baseline(env_name, policy_net, seconds):
+    """Oracle restatement of the reference sampler (per-env Python loop, NumPy policy), 1 thread."""
+    import numpy as np
+    from threadpoolctl import threadpool_limits
+    from oracle.sampler import CpuPolicy, PerEnvCpuSampler
+    lin = [m for m in policy_net.policy if hasattr(m, "weight")]
+    pol = CpuPolicy([(m.weight.detach().cpu().numpy(), m.bias.detach().cpu().numpy()) for m in lin])
+    n_envs = 64
+    with threadpool_limits(limits=1):
+        import torch
+        torch.set_num_threads(1)
+        smp = PerEnvCpuSampler(env_name, n_envs, 20, pol, seed=0)
+        steps = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            smp.step()
+            steps += n_envs
+        dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env_steps/s", "cores": 1, "kind": "port",
+            "sample": f"{env_name}, {n_envs} envs x {steps // n_envs} lockstep steps ({dt:.1f} s): oracle restatement of "
+                      "BaseSampler._n_step + SyncVectorEnv (per-env Python loop, NumPy MLP policy 256x256, 1 thread)"}
+
+
+def main():
+    a = parse()
+    import torch
+    import msacl_amd  # noqa: F401
+    import msacl_amd._native as N
+    from msacl_amd.utils import dist as D
+    from msacl_amd.utils.config import build_pipeline, default_msacl_args
+
+    D.init_from_env()
+    rank, world = D.rank(), D.world_size()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    horizon = 20
+    tmp = tempfile.mkdtemp(prefix=f"msacl_bench_r{rank}_")
+    cfg = default_msacl_args(env_name=a.env, env_num=a.envs, env_seed=1 + rank * 1000003, seed=rank * 1000000,
+                             sample_batch_size=horizon, n_step=20, replay_batch_size=256, buffer_max_size=int(1e6),
+                             buffer_warm_size=5000, max_iteration=10 ** 9, eval_interval=10 ** 9,
+                             log_save_interval=10 ** 9, apprfunc_save_interval=10 ** 9, save_folder=tmp,
+                             num_eval_episode=1, sampler_sync_timing=False, device=dev)
+    if a.policy == "hover":
+        cfg["buffer_warm_size"] = 0
+    args, alg, sampler, buffer, evaluator, trainer = build_pipeline(cfg)
+    if a.policy == "hover":
+        set_hover_policy(alg.networks.policy, float(sampler.envs.single_action_space.high[0]) / 2)
+
+    def one_step():
+        trainer.step()
+        trainer.iteration += 1
+
+    for _ in range(a.warmup):
+        one_step()
+    h = sampler.envs.handle()
+    N.check(N.lib().mh_env_set_timing(h, 1), "timing")
+    ms0 = (ctypes.c_double * 3)()
+    l0 = ctypes.c_int64()
+    N.lib().mh_env_read_timing(h, ms0, ctypes.byref(l0), 1)
+    win0 = int(buffer.cursor[2].item())
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t1 = time.perf_counter()
+    N.check(N.lib().mh_env_set_timing(h, 0), "timing")
+    ms = (ctypes.c_double * 3)()
+    launches = ctypes.c_int64()
+    N.check(N.lib().mh_env_read_timing(h, ms, ctypes.byref(launches), 1), "read timing")
+    windows = int(buffer.cursor[2].item()) - win0
+    elapsed = D.max_over_ranks(t1 - t0)
+    env_steps_total = world * a.envs * horizon * a.steps
+    value = env_steps_total / elapsed
+
+    # ---- live roofline of the engine's kernels over the timed region (HIP events)
+    info = sampler.envs.info
+    S, XS, D_, A_, F = info.state_dim, info.xstate_dim, info.obs_dim, info.act_dim, info.record_floats
+    n = sampler.n_step
+    bytes_step_kernel = a.envs * ((S * 4 + XS * 8 + 4 + 2 * A_ * 4 + D_ * 4 + 8)
+                                  + (S * 4 + XS * 8 + 4 + D_ * 4 + F * 4 + 8 + 4))
+    L = max(1, launches.value)
+    t_step = ms[0] / L * 1e-3
+    t_emit = ms[2] / L * 1e-3
+    bytes_emit = (windows / L) * (n * F * 4 + n * (2 * D_ + A_ + 4) * 4)
+    kernels = {
+        "rollout_step": {"avg_us": t_step * 1e6, "bytes": bytes_step_kernel,
+                         "GBps": bytes_step_kernel / t_step / 1e9 if t_step > 0 else 0.0},
+        "window_scan": {"avg_us": ms[1] / L * 1e3},
+        "window_emit": {"avg_us": t_emit * 1e6, "bytes": bytes_emit,
+                        "GBps": bytes_emit / t_emit / 1e9 if t_emit > 0 else 0.0},
+    }
+    dom = "rollout_step" if ms[0] >= ms[2] else "window_emit"
+    ach = kernels[dom]["GBps"]
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(dom, {}).get("bytes_per_launch")
+        except Exception:
+            traffic = None
+    roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic}
+
+    out = {
+        "metric": "env steps/sec (whole node), QuadrotorTracking 65536 envs, 1/2/4/8 MI355X",
+        "value": round(value, 1), "unit": "env_steps/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"{a.env} MSACL NstepOffSerialTrainer.step: {a.envs} envs/GPU x horizon {horizon}, "
+                               f"n-step {n} windows, replay batch 256, full MSACL update",
+                   "env": a.env, "envs_per_gpu": a.envs, "horizon": horizon, "n_step": n, "replay_batch": 256,
+                   "policy": a.policy, "parallelism": f"dp{world}"},
+        "roofline": roof,
+        "kernels": kernels,
+        "windows_per_step": round(windows / a.steps, 1),
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(a.env, alg.networks.policy, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -129,6 +129,12 @@ int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const 
                     const float* reset_states, float* obs, const mh_window_store_t* store,
                     float* act_out, float* logp_out, void* stream);
 
+/* Per-kernel HIP-event timing of mh_rollout_step (profiling aid; do not enable inside a
+ * captured hipGraph). read_timing drains the pending events (host sync) and returns the summed
+ * milliseconds of {step kernel, window scan, window emission} and the number of timed calls. */
+int mh_env_set_timing(mh_env_t h, int32_t enable);
+int mh_env_read_timing(mh_env_t h, double* ms_out, int64_t* launches_out, int32_t reset);
+
 /* NstepReplayBuffer.sample_batch gather (RL/trainer/buffer/nstep_replay_buffer.py:128-150):
  * out_X[b] = store.X[idx[b]] for the 7 arrays (any out pointer may be NULL). */
 int mh_replay_gather(const mh_window_store_t* store, int32_t n_step, int32_t obs_dim,
@@ -147,12 +153,14 @@ int mh_replay_sample_indices(const mh_window_store_t* store, uint64_t seed, uint
  *   backup = rew + (1-done) * gamma * (min(q1t, q2t) - alpha * next_logp)
  *   loss = mean((q1-backup)^2) + mean((q2-backup)^2)
  * Writes backup [B*n], dq1/dq2 = dloss/dq (gradients for autograd), loss_out [1], and
- * abs_td [B] = mean_k |min(q1,q2) - backup| per window (PER priority source). */
+ * abs_td [B] = mean_k (|q1-backup| + |q2-backup|)/2 per window (PER priority source).
+ * weight [B] (nullable): per-window importance weights (prioritized replay); with weights the
+ * loss is mean_b,k w_b (q - backup)^2. NULL reproduces the reference loss exactly. */
 int mh_msacl_q_target(const float* q1, const float* q2, const float* q1t, const float* q2t,
                       const float* next_logp, const float* rew, const float* done,
-                      const float* log_alpha, float gamma, int32_t B, int32_t n,
-                      float* backup, float* dq1, float* dq2, float* loss_out, float* abs_td,
-                      void* stream);
+                      const float* log_alpha, const float* weight, float gamma, int32_t B,
+                      int32_t n, float* backup, float* dq1, float* dq2, float* loss_out,
+                      float* abs_td, void* stream);
 
 /* _lyapunov_update certificate (msacl.py:279-332). Inputs: logp (policy log-prob of the
  * stored actions), old_logp, V(obs) lya_obs, V(obs2) lya_obs2, obs/obs2 [B][n][D].

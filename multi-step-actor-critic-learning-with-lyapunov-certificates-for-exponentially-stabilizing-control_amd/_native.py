@@ -1,0 +1,144 @@
+"""ctypes binding of include/msacl_hip.h (the engine's C ABI).
+
+The library is built in-tree by `make -C csrc` (or __graft_entry__.build()) into
+csrc/build/libmsacl_hip.so. There is no CPU fallback anywhere in the product path: if the
+library is missing or a call fails, this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MSACL_HIP_LIB", os.path.join(_HERE, "csrc", "build", "libmsacl_hip.so"))
+
+ENV_IDS = {
+    "VanderPol": 0,
+    "Pendulum": 1,
+    "DuctedFan": 2,
+    "TwoLink": 3,
+    "SingleTrackCar": 4,
+    "QuadTracking": 5,
+}
+
+c_vp = ctypes.c_void_p
+c_i32 = ctypes.c_int32
+c_i64 = ctypes.c_int64
+c_u64 = ctypes.c_uint64
+c_f32 = ctypes.c_float
+c_f64 = ctypes.c_double
+
+
+class EnvInfo(ctypes.Structure):
+    _fields_ = [
+        ("obs_dim", c_i32), ("act_dim", c_i32), ("state_dim", c_i32), ("xstate_dim", c_i32),
+        ("reset_dim", c_i32), ("control_step", c_i32), ("max_step", c_i32), ("record_floats", c_i32),
+        ("obs_low", c_f32 * 16), ("obs_high", c_f32 * 16), ("act_low", c_f32 * 4), ("act_high", c_f32 * 4),
+    ]
+
+
+class WindowStore(ctypes.Structure):
+    _fields_ = [
+        ("obs", c_vp), ("act", c_vp), ("rew", c_vp), ("cost", c_vp), ("obs2", c_vp), ("done", c_vp),
+        ("logp", c_vp), ("capacity", c_i64), ("cursor", c_vp),
+    ]
+
+
+# name -> (restype, argtypes)
+_PROTOS = {
+    "mh_abi_version": (ctypes.c_int, []),
+    "mh_last_error": (ctypes.c_char_p, []),
+    "mh_env_info": (ctypes.c_int, [c_i32, ctypes.POINTER(EnvInfo)]),
+    "mh_env_create": (ctypes.c_int, [c_i32, c_i64, c_u64, ctypes.POINTER(c_vp)]),
+    "mh_env_destroy": (ctypes.c_int, [c_vp]),
+    "mh_env_reset": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
+    "mh_env_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mh_env_get_state": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mh_env_set_state": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mh_nstep_attach": (ctypes.c_int, [c_vp, c_i32, c_f32, c_f32]),
+    "mh_rollout_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(WindowStore), c_vp, c_vp, c_vp]),
+    "mh_env_set_timing": (ctypes.c_int, [c_vp, c_i32]),
+    "mh_env_read_timing": (ctypes.c_int, [c_vp, ctypes.POINTER(c_f64), ctypes.POINTER(c_i64), c_i32]),
+    "mh_replay_gather": (ctypes.c_int, [ctypes.POINTER(WindowStore), c_i32, c_i32, c_i32, c_vp, c_i64,
+                                        c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mh_replay_sample_indices": (ctypes.c_int, [ctypes.POINTER(WindowStore), c_u64, c_u64, c_i64, c_vp, c_vp]),
+    "mh_msacl_q_target": (ctypes.c_int, [c_vp] * 9 + [c_f32, c_i32, c_i32] + [c_vp] * 5 + [c_vp]),
+    "mh_msacl_lyapunov": (ctypes.c_int, [c_vp] * 9 + [c_f32] * 4 + [c_i32] * 3 + [c_vp] * 6 + [c_vp]),
+    "mh_msacl_stability_adv": (ctypes.c_int, [c_vp] * 4 + [c_i32, c_i32, c_vp, c_vp, c_vp]),
+    "mh_msacl_ppo_clip": (ctypes.c_int, [c_vp, c_vp, c_vp, c_f64, c_f32, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "mh_per_update": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_f32, c_f32, c_vp, c_vp]),
+    "mh_per_set_new": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "mh_per_sample": (ctypes.c_int, [c_vp, c_i64, c_vp, c_u64, c_u64, c_i64, c_f32, c_vp, c_vp, c_vp]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load the engine library (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"MSACL HIP engine library not found at {LIB_PATH}; build it with "
+                f"`make -C {os.path.join(_HERE, 'csrc')}` (or __graft_entry__.build()). "
+                "There is no CPU fallback.")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _PROTOS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.mh_abi_version() != 1:
+            raise RuntimeError("libmsacl_hip ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_PROTOS)
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().mh_last_error()
+        raise RuntimeError(f"{what} failed (code {rc}): {msg.decode() if msg else ''}")
+
+
+def env_info(name_or_id):
+    eid = ENV_IDS[name_or_id] if isinstance(name_or_id, str) else int(name_or_id)
+    info = EnvInfo()
+    check(lib().mh_env_info(eid, ctypes.byref(info)), "mh_env_info")
+    return info
+
+
+# ------------------------------------------------------------------ torch plumbing helpers
+def ptr(t):
+    """Device pointer of a contiguous tensor (None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        raise ValueError("tensor passed to the HIP engine must be contiguous")
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(device=None):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(t, name, dtype=None, numel=None, device=None):
+    """Host-side shape/dtype/device checks before any kernel touches `t`."""
+    import torch
+    if t is None:
+        return
+    if t.device.type != "cuda":
+        raise ValueError(f"{name} must be a device tensor (got {t.device})")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name} is on {t.device}, expected {device}")
+    if dtype is not None and t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype} (got {t.dtype})")
+    if numel is not None and t.numel() != numel:
+        raise ValueError(f"{name} must have {numel} elements (got {t.numel()})")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    _ = torch

@@ -1,0 +1,281 @@
+"""MSACL (RL/algorithm/msacl.py:23-460) on MI355X.
+
+Networks, optimisers and autograd stay PyTorch-ROCm (the north star keeps the MLPs in
+PyTorch). The element-wise/scan target math between the network evaluations runs in fused
+gfx950 kernels (csrc/msacl_kernels.hip) that also return the analytic gradient w.r.t. the
+network outputs, which is handed to autograd:
+  * Q backup + twin MSE                          msacl.py:242-257   -> mh_msacl_q_target
+  * IS cumprod, bound hinges, ESL, lambda-weighted
+    Lyapunov decrease                            msacl.py:279-332   -> mh_msacl_lyapunov
+  * stability advantage + batch normalisation +
+    PPO clip                                     msacl.py:383-405   -> mh_msacl_stability_adv / _ppo_clip
+Data-parallel (one rank per GPU): every optimiser step all-reduces its gradients as one flat
+bucket over RCCL, and the advantage normalisation all-reduces its (sum, sumsq) so the batch
+statistic is the global batch's (msacl.py:400).
+"""
+__all__ = ["ApproxContainer", "MSACL"]
+
+import math
+import time
+from copy import deepcopy
+from typing import Any, Dict, Optional
+
+import torch
+import torch.nn as nn
+from torch.optim import Adam
+
+from .. import _native as N
+from ..create_pkg.create_apprfunc import create_apprfunc
+from ..utils import dist as D
+from ..utils.common_utils import get_apprfunc_dict
+from ..utils.tensorboard_setup import tb_tags
+
+
+def _adam(params, lr):
+    try:
+        return Adam(params, lr=lr, fused=True)
+    except (RuntimeError, TypeError):
+        return Adam(params, lr=lr)
+
+
+class ApproxContainer(nn.Module):
+    """q1, q2 (+ frozen Polyak targets), Lyapunov V, policy, log_alpha and their Adams."""
+
+    def __init__(self, **kwargs):
+        super().__init__()
+        q_args = get_apprfunc_dict("value", **kwargs)
+        self.q1: nn.Module = create_apprfunc(**q_args)
+        self.q2: nn.Module = create_apprfunc(**q_args)
+        self.q1_target = deepcopy(self.q1)
+        self.q2_target = deepcopy(self.q2)
+        for p in list(self.q1_target.parameters()) + list(self.q2_target.parameters()):
+            p.requires_grad = False
+        self.lyapunov: nn.Module = create_apprfunc(**get_apprfunc_dict("lyapunov", **kwargs))
+        self.policy: nn.Module = create_apprfunc(**get_apprfunc_dict("policy", **kwargs))
+        self.log_alpha = nn.Parameter(torch.tensor(1.0, dtype=torch.float32))
+        self._lrs = dict(q=kwargs["q_learning_rate"], lya=kwargs["lyapunov_learning_rate"],
+                         pi=kwargs["policy_learning_rate"], alpha=kwargs["alpha_learning_rate"])
+        self._make_optimizers()
+
+    def _make_optimizers(self):
+        self.q1_optimizer = _adam(self.q1.parameters(), self._lrs["q"])
+        self.q2_optimizer = _adam(self.q2.parameters(), self._lrs["q"])
+        self.lyapunov_optimizer = _adam(self.lyapunov.parameters(), self._lrs["lya"])
+        self.policy_optimizer = _adam(self.policy.parameters(), self._lrs["pi"])
+        self.alpha_optimizer = _adam([self.log_alpha], self._lrs["alpha"])
+
+    def create_action_distributions(self, logits):
+        return self.policy.get_act_dist_cls(logits)
+
+
+class _Scratch:
+    """Per-shape device work buffers for the fused kernels (allocated once per batch shape)."""
+
+    def __init__(self, B, n, device):
+        f = lambda *s: torch.empty(*s, dtype=torch.float32, device=device)  # noqa: E731
+        self.backup, self.dq1, self.dq2 = f(B, n), f(B, n), f(B, n)
+        self.abs_td, self.loss_q = f(B), f(1)
+        self.is_clip, self.esl, self.lya_diff, self.loss_lya = f(B, n), f(B, n), f(B), f(1)
+        self.dV, self.dV2 = f(B, n), f(B, n)
+        self.adv_raw, self.adv, self.loss_ppo, self.d_ratio = f(B), f(B), f(1), f(B)
+        self.stats = torch.empty(2, dtype=torch.float64, device=device)
+
+
+class MSACL:
+    def __init__(self, gamma: float = 0.99, retrace_lambda: float = 0.95, lya_eta: float = 0.15,
+                 tau: float = 0.005, alpha: float = math.e, auto_alpha: bool = True,
+                 target_entropy: Optional[float] = None, policy_frequency: int = 2,
+                 target_network_frequency: int = 1, lya_diff_scale: float = 1.0, lya_zero_scale: float = 1.0,
+                 lya_positive_scale: float = 1.0, **kwargs: Any):
+        dev = kwargs.get("device")
+        if dev is None:
+            dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
+        if dev is None:
+            raise RuntimeError("MSACL's fused target kernels need a HIP device; no CPU fallback exists")
+        self.device = torch.device(dev)
+        self.networks = ApproxContainer(**kwargs).to(self.device)
+        self.gamma, self.retrace_lambda, self.lya_eta, self.tau = gamma, retrace_lambda, lya_eta, tau
+        self.q_learning_rate = kwargs["q_learning_rate"]
+        self.lyapunov_learning_rate = kwargs["lyapunov_learning_rate"]
+        self.policy_learning_rate = kwargs["policy_learning_rate"]
+        self.alpha_learning_rate = kwargs["alpha_learning_rate"]
+        self.policy_frequency = policy_frequency
+        self.target_network_frequency = target_network_frequency
+        self.n_step = int(kwargs["n_step"])
+        self.batch_size = kwargs["replay_batch_size"]
+        self.anneal_lr = kwargs.get("anneal_lr", False)
+        self.max_iteration = kwargs["max_iteration"]
+        self.disable_auto_alpha = kwargs.get("disable_auto_alpha", False)
+        self.auto_alpha = not self.disable_auto_alpha
+        self.set_alpha_bound = kwargs.get("set_alpha_bound", False)
+        self.alpha_bound = kwargs.get("alpha_bound", 2.0)
+        self.per_flag = kwargs.get("buffer_name") == "prioritized_replay_buffer"
+        with torch.no_grad():
+            self.networks.log_alpha.fill_(math.log(alpha))
+        if target_entropy is None:
+            target_entropy = -kwargs["act_dim"] - (1 if kwargs["env_name"] == "QuadTracking" else 0)
+        self.target_entropy = target_entropy
+        self.lya_diff_scale, self.lya_zero_scale, self.lya_positive_scale = lya_diff_scale, lya_zero_scale, lya_positive_scale
+        self.alpha1 = kwargs.get("alpha1", 1.0)
+        self.alpha2 = kwargs.get("alpha2", 2.0)
+        self.clip_coef = kwargs.get("clip_coef", 0.1)
+        n = self.n_step
+        # coefficient vectors (msacl.py:153-164), same torch expressions, on this device
+        self.start_obs_norm_coef = ((torch.tensor(1 - self.lya_eta) ** torch.arange(1, n + 1)
+                                     * torch.tensor(self.alpha2 / self.alpha1)) ** 0.5).to(self.device).contiguous()
+        w = torch.pow(self.retrace_lambda, torch.arange(n))
+        self.lya_diff_coef = (w / torch.sum(w)).to(self.device).contiguous()
+        self.start_lya_coef = torch.pow((1 - self.lya_eta), torch.arange(n) + 1).to(self.device).contiguous()
+        self._scratch = {}
+        self.last_priority = None
+
+    @property
+    def adjustable_parameters(self):
+        return ("gamma", "tau", "auto_alpha", "alpha", "target_entropy", "policy_frequency", "target_network_frequency")
+
+    def _buf(self, B, n):
+        key = (B, n)
+        if key not in self._scratch:
+            self._scratch[key] = _Scratch(B, n, self.device)
+        return self._scratch[key]
+
+    def _get_alpha(self, requires_grad: bool = False):
+        alpha = self.networks.log_alpha.exp()
+        return alpha if requires_grad else alpha.item()
+
+    # ------------------------------------------------------------------ update
+    def model_update(self, data: Dict[str, torch.Tensor], global_iteration: int):
+        start = time.time()
+        if self.anneal_lr:
+            frac = max(0.0, 1.0 - global_iteration / self.max_iteration)
+            for opt, lr in ((self.networks.q1_optimizer, self.q_learning_rate), (self.networks.q2_optimizer, self.q_learning_rate),
+                            (self.networks.lyapunov_optimizer, self.lyapunov_learning_rate),
+                            (self.networks.policy_optimizer, self.policy_learning_rate),
+                            (self.networks.alpha_optimizer, self.alpha_learning_rate)):
+                opt.param_groups[0]["lr"] = lr * frac
+        data = {k: (v.to(self.device).contiguous() if torch.is_tensor(v) else v) for k, v in data.items()}
+        loss_q, q1_mean, q2_mean = self._q_update(data)
+        if global_iteration % self.target_network_frequency == 0:
+            self._target_update()
+        loss_lya = self._lyapunov_update(data)
+        tb_info = None
+        if global_iteration % self.policy_frequency == 0:
+            for _ in range(self.policy_frequency):
+                loss_policy, entropy = self._policy_update(data=data)
+                if self.auto_alpha:
+                    self._alpha_update(entropy=entropy)
+            tb_info = {
+                "MSACL/entropy-RL iter": entropy.item(),
+                "MSACL/alpha-RL iter": self._get_alpha(),
+                "MSACL/q1_mean-RL iter": q1_mean.item(),
+                "MSACL/q2_mean-RL iter": q2_mean.item(),
+                tb_tags["loss_critic"]: loss_q.item(),
+                tb_tags["loss_lyapunov"]: loss_lya.item(),
+                tb_tags["loss_actor"]: loss_policy.item(),
+                tb_tags["alg_time"]: (time.time() - start) * 1000,
+            }
+        if self.per_flag:
+            return tb_info, data.get("idx"), self.last_priority
+        return tb_info
+
+    def _q_update(self, data):
+        obs, act, rew, obs2, done = data["obs"], data["act"], data["rew"], data["obs2"], data["done"]
+        B, n = rew.shape
+        s = self._buf(B, n)
+        q1 = self.networks.q1(obs, act)
+        q2 = self.networks.q2(obs, act)
+        with torch.no_grad():
+            dist = self.networks.create_action_distributions(self.networks.policy(obs2))
+            next_act, next_logp = dist.rsample()
+            q1t = self.networks.q1_target(obs2, next_act).contiguous()
+            q2t = self.networks.q2_target(obs2, next_act).contiguous()
+        weight = data.get("weight") if self.per_flag else None
+        N.check(N.lib().mh_msacl_q_target(
+            N.ptr(q1.detach().contiguous()), N.ptr(q2.detach().contiguous()), N.ptr(q1t), N.ptr(q2t),
+            N.ptr(next_logp.contiguous()), N.ptr(rew), N.ptr(done), N.ptr(self.networks.log_alpha.detach()),
+            N.ptr(weight.contiguous() if weight is not None else None), float(self.gamma), B, n, N.ptr(s.backup),
+            N.ptr(s.dq1), N.ptr(s.dq2), N.ptr(s.loss_q), N.ptr(s.abs_td), N.stream_of(self.device)), "mh_msacl_q_target")
+        self.networks.q1_optimizer.zero_grad()
+        self.networks.q2_optimizer.zero_grad()
+        torch.autograd.backward([q1, q2], [s.dq1, s.dq2])
+        D.allreduce_grads(list(self.networks.q1.parameters()) + list(self.networks.q2.parameters()))
+        self.networks.q1_optimizer.step()
+        self.networks.q2_optimizer.step()
+        self.last_priority = s.abs_td.clone()
+        return s.loss_q[0].clone(), q1.detach().mean(), q2.detach().mean()
+
+    def _lyapunov_update(self, data):
+        obs, obs2, act, old_logp = data["obs"], data["obs2"], data["act"], data["logp"]
+        B, n = old_logp.shape
+        s = self._buf(B, n)
+        with torch.no_grad():
+            dist = self.networks.create_action_distributions(self.networks.policy(obs))
+            logp = dist.log_prob(act).contiguous()
+        V = self.networks.lyapunov(obs)
+        V2 = self.networks.lyapunov(obs2)
+        N.check(N.lib().mh_msacl_lyapunov(
+            N.ptr(logp), N.ptr(old_logp), N.ptr(V.detach().contiguous()), N.ptr(V2.detach().contiguous()), N.ptr(obs),
+            N.ptr(obs2), N.ptr(self.start_obs_norm_coef), N.ptr(self.lya_diff_coef), N.ptr(self.start_lya_coef),
+            float(self.alpha1), float(self.alpha2), float(self.lya_positive_scale), float(self.lya_diff_scale), B, n,
+            obs.shape[-1], N.ptr(s.is_clip), N.ptr(s.esl), N.ptr(s.lya_diff), N.ptr(s.loss_lya), N.ptr(s.dV),
+            N.ptr(s.dV2), N.stream_of(self.device)), "mh_msacl_lyapunov")
+        self.networks.lyapunov_optimizer.zero_grad()
+        torch.autograd.backward([V, V2], [s.dV, s.dV2])
+        D.allreduce_grads(list(self.networks.lyapunov.parameters()))
+        self.networks.lyapunov_optimizer.step()
+        return s.loss_lya[0].clone()
+
+    def _policy_update(self, data):
+        obs, old_act, obs2, old_logp = data["obs"], data["act"], data["obs2"], data["logp"]
+        B, n = old_logp.shape
+        s = self._buf(B, n)
+        for p in list(self.networks.q1.parameters()) + list(self.networks.q2.parameters()):
+            p.requires_grad = False
+        dist = self.networks.create_action_distributions(self.networks.policy(obs))
+        new_act, new_act_logp = dist.rsample()
+        q1 = self.networks.q1(obs, new_act)
+        q2 = self.networks.q2(obs, new_act)
+        loss_policy_q = (torch.min(q1, q2) - self._get_alpha() * new_act_logp).mean()
+        ratio = torch.exp(dist.log_prob(old_act) - old_logp)
+        is_ratio = ratio[:, 0]
+        with torch.no_grad():
+            V0 = self.networks.lyapunov(obs[:, 0]).contiguous()
+            V2 = self.networks.lyapunov(obs2).contiguous()
+        N.check(N.lib().mh_msacl_stability_adv(N.ptr(V0), N.ptr(V2), N.ptr(self.lya_diff_coef), N.ptr(self.start_lya_coef),
+                                               B, n, N.ptr(s.adv_raw), N.ptr(s.stats), N.stream_of(self.device)),
+                "mh_msacl_stability_adv")
+        D.allreduce_(s.stats)
+        n_total = float(B * D.world_size())
+        r_det = is_ratio.detach().contiguous()
+        N.check(N.lib().mh_msacl_ppo_clip(N.ptr(r_det), N.ptr(s.adv_raw), N.ptr(s.stats), n_total, float(self.clip_coef), B,
+                                          N.ptr(s.adv), N.ptr(s.loss_ppo), N.ptr(s.d_ratio), N.stream_of(self.device)),
+                "mh_msacl_ppo_clip")
+        loss_policy = -loss_policy_q.detach() - s.loss_ppo[0]
+        self.networks.policy_optimizer.zero_grad()
+        torch.autograd.backward([loss_policy_q, is_ratio], [torch.tensor(-1.0, device=self.device), -s.d_ratio])
+        D.allreduce_grads(list(self.networks.policy.parameters()))
+        self.networks.policy_optimizer.step()
+        entropy = -new_act_logp.mean().detach()
+        for p in list(self.networks.q1.parameters()) + list(self.networks.q2.parameters()):
+            p.requires_grad = True
+        return loss_policy.detach(), entropy
+
+    def _alpha_update(self, entropy):
+        alpha = self._get_alpha(requires_grad=True)
+        loss_alpha = alpha * (entropy - self.target_entropy)
+        self.networks.alpha_optimizer.zero_grad()
+        loss_alpha.backward()
+        D.allreduce_grads([self.networks.log_alpha])
+        self.networks.alpha_optimizer.step()
+        if self.set_alpha_bound:
+            with torch.no_grad():
+                self.networks.log_alpha.clamp_(max=math.log(self.alpha_bound))
+
+    def _target_update(self):
+        """Polyak averaging (msacl.py:445-460) as two multi-tensor ops per net."""
+        with torch.no_grad():
+            polyak = 1 - self.tau
+            for net, targ in ((self.networks.q1, self.networks.q1_target), (self.networks.q2, self.networks.q2_target)):
+                tp = [p.data for p in targ.parameters()]
+                torch._foreach_mul_(tp, polyak)
+                torch._foreach_add_(tp, torch._foreach_mul([p.data for p in net.parameters()], 1 - polyak))

@@ -1,6 +1,7 @@
 // capi.hip — C ABI (include/msacl_hip.h): env handles, lockstep rollout, window store, gather.
 #include <string>
 #include <cstring>
+#include <vector>
 
 #include "msacl_hip.h"
 #include "rollout.h"
@@ -64,6 +65,23 @@ struct mh_env_s {
   int32_t* block_count = nullptr;
   int32_t* block_offset = nullptr;
 
+  // optional per-kernel HIP-event timing of mh_rollout_step (bench.py's live roofline)
+  bool timing = false;
+  std::vector<hipEvent_t> ev_free;
+  std::vector<hipEvent_t> ev_pending;  // groups of 4: before rollout / finalize / emit / end
+  double t_ms[3] = {0.0, 0.0, 0.0};
+  int64_t t_launches = 0;
+
+  hipEvent_t take_event() {
+    if (!ev_free.empty()) {
+      hipEvent_t e = ev_free.back();
+      ev_free.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+  }
   int grid() const { return (int)((E + mh::BLK - 1) / mh::BLK); }
   mh::StepArgs base_args() const {
     mh::StepArgs a;
@@ -84,6 +102,8 @@ struct mh_env_s {
 
 static void free_handle(mh_env_s* h) {
   if (!h) return;
+  for (hipEvent_t e : h->ev_free) (void)hipEventDestroy(e);
+  for (hipEvent_t e : h->ev_pending) (void)hipEventDestroy(e);
   void* ptrs[] = {h->state, h->xstate, h->steps, h->tab, h->meta, h->ring, h->ring_len,
                   h->ring_pos, h->emit_rank, h->block_count, h->block_offset};
   for (void* p : ptrs)
@@ -260,9 +280,15 @@ int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const 
   a.ring_pos = h->ring_pos;
   a.emit_rank = h->emit_rank;
   a.block_count = h->block_count;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  if (h->timing)
+    for (int i = 0; i < 4; ++i) ev[i] = h->take_event();
+  if (ev[0]) MH_HIP(hipEventRecord(ev[0], st));
   MH_HIP(mh::launch_rollout(h->env_id, a, st));
+  if (ev[1]) MH_HIP(hipEventRecord(ev[1], st));
   MH_HIP(mh::launch_finalize(h->block_count, store ? h->grid() : 0, h->block_offset, h->meta,
                              store ? store->cursor : nullptr, store ? store->capacity : 1, st));
+  if (ev[2]) MH_HIP(hipEventRecord(ev[2], st));
   if (store) {
     mh::EmitArgs ea;
     ea.E = h->E;
@@ -284,6 +310,39 @@ int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const 
     ea.done = store->done;
     ea.logp = store->logp;
     MH_HIP(mh::launch_emit(ea, st));
+  }
+  if (ev[3]) {
+    MH_HIP(hipEventRecord(ev[3], st));
+    for (int i = 0; i < 4; ++i) h->ev_pending.push_back(ev[i]);
+  }
+  return MH_OK;
+}
+
+int mh_env_set_timing(mh_env_t h, int32_t enable) {
+  if (!h) return fail(MH_EINVAL, "mh_env_set_timing: null handle");
+  h->timing = enable != 0;
+  return MH_OK;
+}
+
+int mh_env_read_timing(mh_env_t h, double* ms_out, int64_t* launches_out, int32_t reset) {
+  if (!h || !ms_out || !launches_out) return fail(MH_EINVAL, "mh_env_read_timing: null arg");
+  for (size_t g = 0; g + 3 < h->ev_pending.size(); g += 4) {
+    hipEvent_t* e = &h->ev_pending[g];
+    MH_HIP(hipEventSynchronize(e[3]));
+    for (int k = 0; k < 3; ++k) {
+      float ms = 0.0f;
+      MH_HIP(hipEventElapsedTime(&ms, e[k], e[k + 1]));
+      h->t_ms[k] += ms;
+    }
+    h->t_launches += 1;
+    for (int k = 0; k < 4; ++k) h->ev_free.push_back(e[k]);
+  }
+  h->ev_pending.clear();
+  for (int k = 0; k < 3; ++k) ms_out[k] = h->t_ms[k];
+  *launches_out = h->t_launches;
+  if (reset) {
+    h->t_ms[0] = h->t_ms[1] = h->t_ms[2] = 0.0;
+    h->t_launches = 0;
   }
   return MH_OK;
 }

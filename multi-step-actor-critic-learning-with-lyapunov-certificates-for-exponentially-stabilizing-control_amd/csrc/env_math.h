@@ -559,7 +559,8 @@ MH_HD void cross64(const double* a, const double* b, double* c) {
   c[1] = a[2] * b[0] - a[0] * b[2];
   c[2] = a[0] * b[1] - a[1] * b[0];
 }
-MH_HD double norm3(const double* a) { return sqrt((a[0] * a[0] + a[1] * a[1]) + a[2] * a[2]); }
+// np.linalg.norm of a 3-vector = sqrt(ddot) and OpenBLAS's ddot accumulates with FMA
+MH_HD double norm3(const double* a) { return sqrt(fma(a[2], a[2], fma(a[1], a[1], a[0] * a[0]))); }
 
 struct QuadTracking {
   // state floats: x[0:3] v[3:6] R[6:15] W[15:18]; xstate doubles: Rd_last[9]

@@ -40,9 +40,9 @@ __device__ double block_sum(double v, double* sh) {
 // ------------------------------------------------------------------ Q backup (msacl.py:242-257)
 __global__ __launch_bounds__(TPB) void k_q_target(const float* q1, const float* q2, const float* q1t,
                                                   const float* q2t, const float* nlogp, const float* rew,
-                                                  const float* done, const float* log_alpha, float gamma,
-                                                  int B, int n, float* backup, float* dq1, float* dq2,
-                                                  float* loss_out, float* abs_td) {
+                                                  const float* done, const float* log_alpha, const float* weight,
+                                                  float gamma, int B, int n, float* backup, float* dq1,
+                                                  float* dq2, float* loss_out, float* abs_td) {
   __shared__ double sh[TPB];
   const float alpha = expf(*log_alpha);
   const int64_t N = (int64_t)B * n;
@@ -53,10 +53,11 @@ __global__ __launch_bounds__(TPB) void k_q_target(const float* q1, const float* 
     const float bk = rew[i] + ((1.0f - done[i]) * gamma) * (nq - alpha * nlogp[i]);
     backup[i] = bk;
     const float e1 = q1[i] - bk, e2 = q2[i] - bk;
-    acc1 += (double)e1 * (double)e1;
-    acc2 += (double)e2 * (double)e2;
-    if (dq1) dq1[i] = 2.0f * e1 * inv;
-    if (dq2) dq2[i] = 2.0f * e2 * inv;
+    const float wb = weight ? weight[i / n] : 1.0f;
+    acc1 += (double)wb * (double)e1 * (double)e1;
+    acc2 += (double)wb * (double)e2 * (double)e2;
+    if (dq1) dq1[i] = 2.0f * e1 * inv * wb;
+    if (dq2) dq2[i] = 2.0f * e2 * inv * wb;
   }
   const double s1 = block_sum(acc1, sh), s2 = block_sum(acc2, sh);
   if (threadIdx.x == 0 && loss_out) loss_out[0] = (float)(s1 / (double)N) + (float)(s2 / (double)N);
@@ -229,12 +230,12 @@ extern "C" {
 
 int mh_msacl_q_target(const float* q1, const float* q2, const float* q1t, const float* q2t,
                       const float* next_logp, const float* rew, const float* done, const float* log_alpha,
-                      float gamma, int32_t B, int32_t n, float* backup, float* dq1, float* dq2,
-                      float* loss_out, float* abs_td, void* stream) {
+                      const float* weight, float gamma, int32_t B, int32_t n, float* backup, float* dq1,
+                      float* dq2, float* loss_out, float* abs_td, void* stream) {
   if (!q1 || !q2 || !q1t || !q2t || !next_logp || !rew || !done || !log_alpha || !backup || B <= 0 || n <= 0)
     return MH_EINVAL;
-  k_q_target<<<1, TPB, 0, (hipStream_t)stream>>>(q1, q2, q1t, q2t, next_logp, rew, done, log_alpha, gamma, B, n,
-                                                 backup, dq1, dq2, loss_out, abs_td);
+  k_q_target<<<1, TPB, 0, (hipStream_t)stream>>>(q1, q2, q1t, q2t, next_logp, rew, done, log_alpha, weight, gamma,
+                                                 B, n, backup, dq1, dq2, loss_out, abs_td);
   MH_CHECK_LAUNCH("q_target");
   return MH_OK;
 }

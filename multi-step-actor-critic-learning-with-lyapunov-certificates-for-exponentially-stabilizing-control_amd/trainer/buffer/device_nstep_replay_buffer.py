@@ -1,0 +1,146 @@
+"""HBM-resident n-step replay buffer (drop-in for RL/trainer/buffer/nstep_replay_buffer.py).
+
+Storage is the reference's dict of seven float32 arrays `[max_size, n_step, ...]`, held as
+device tensors and written directly by the rollout kernel's window-emission stage (the HIP
+sampler binds to this store on the first add_batch, after which add_batch is bookkeeping only:
+no host copy, no per-window Python loop). The FIFO cursor {ptr, size, total, last} lives on
+the device so the whole rollout can run without a host sync.
+
+API: add_batch(samples), sample_batch(batch_size) -> dict of [B, n, ...] tensors, .size,
+__len__, __get_RAM__(), store(...) (single window, host path). The uniform index draw of
+`np.random.randint(0, size, B)` (nstep_replay_buffer.py:138) is a device Philox draw.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from ... import _native as N
+
+KEYS = ("obs", "act", "rew", "cost", "obs2", "done", "logp")
+
+
+class DeviceWindowBatch:
+    """What the HIP sampler's sample() returns: windows already emitted into `store_owner`
+    (when bound) or into the sampler's staging store. `count` is a device int64 scalar."""
+
+    def __init__(self, sampler, store_owner, count, first_total=None):
+        self.sampler = sampler
+        self.store_owner = store_owner
+        self.count = count
+        self.first_total = first_total
+
+    def __len__(self):
+        return int(self.count.item())
+
+
+class DeviceNstepReplayBuffer:
+    def __init__(self, **kwargs):
+        self.obsv_dim = int(kwargs["obs_dim"])
+        self.act_dim = int(kwargs["act_dim"])
+        self.max_size = int(kwargs["buffer_max_size"])
+        self.n_step = int(kwargs["n_step"])
+        dev = kwargs.get("device")
+        self.device = torch.device(dev) if dev is not None else torch.device("cuda", torch.cuda.current_device())
+        self.seed = int(kwargs.get("buffer_seed", kwargs.get("seed", 0) or 0)) & ((1 << 63) - 1)
+        M, n, D, A = self.max_size, self.n_step, self.obsv_dim, self.act_dim
+        z = lambda *s: torch.zeros(*s, dtype=torch.float32, device=self.device)  # noqa: E731
+        self.n_step_buf = {"obs": z(M, n, D), "act": z(M, n, A), "rew": z(M, n), "cost": z(M, n),
+                           "obs2": z(M, n, D), "done": z(M, n), "logp": z(M, n)}
+        self.cursor = torch.zeros(4, dtype=torch.int64, device=self.device)  # ptr, size, total, last
+        self.ws = N.WindowStore(*[ctypes.c_void_p(self.n_step_buf[k].data_ptr()) for k in KEYS],
+                                M, ctypes.c_void_p(self.cursor.data_ptr()))
+        self._draws = 0
+        self._idx = None
+
+    # ------------------------------------------------------------------ size / memory
+    @property
+    def ptr(self):
+        return int(self.cursor[0].item())
+
+    @property
+    def size(self):
+        return int(self.cursor[1].item())
+
+    def __len__(self):
+        return self.size
+
+    def __get_RAM__(self):
+        """MB held by valid windows (nstep_replay_buffer.py:76-88 semantics)."""
+        size = self.size
+        if size == 0:
+            return 0.0
+        per_row = sum(v[0].numel() * v.element_size() for v in self.n_step_buf.values())
+        return round(per_row * size / (1024 * 1024), 2)
+
+    # ------------------------------------------------------------------ writes
+    def store(self, obs, act, rew, cost, next_obs, done, logp):
+        """Single window from host data (reference store(), :91-119) — compatibility path."""
+        p = self.ptr
+        for k, v in zip(KEYS, (obs, act, rew, cost, next_obs, done, logp)):
+            self.n_step_buf[k][p].copy_(torch.as_tensor(np.asarray(v, np.float32)))
+        c = self.cursor.cpu()
+        c[0] = (p + 1) % self.max_size
+        c[1] = min(int(c[1]) + 1, self.max_size)
+        c[2] += 1
+        c[3] = 1
+        self.cursor.copy_(c)
+
+    def add_batch(self, samples):
+        if isinstance(samples, DeviceWindowBatch):
+            if samples.store_owner is self:
+                self._on_windows_added()
+                return
+            samples.sampler.bind_store(self)
+            self._absorb_staged(samples)
+            self._on_windows_added()
+            return
+        for s in samples:
+            self.store(*s)
+        self._on_windows_added()
+
+    def _absorb_staged(self, batch):
+        """First batch of an unbound sampler: copy its staged windows in emission order."""
+        staged = batch.store_owner
+        cnt = int(staged.cursor[1].item())
+        if cnt == 0:
+            return
+        keep = min(cnt, self.max_size)  # FIFO: only the newest max_size windows survive
+        src = torch.arange(cnt - keep, cnt, device=self.device)
+        c = self.cursor.cpu()
+        ptr = int(c[0]) + (cnt - keep)
+        dst = (ptr + torch.arange(keep, device=self.device)) % self.max_size
+        for k in KEYS:
+            self.n_step_buf[k][dst] = staged.n_step_buf[k][src]
+        c[0] = (int(c[0]) + cnt) % self.max_size
+        c[1] = min(int(c[1]) + cnt, self.max_size)
+        c[2] += cnt
+        c[3] = cnt
+        self.cursor.copy_(c)
+
+    def _on_windows_added(self):
+        pass
+
+    # ------------------------------------------------------------------ reads
+    def sample_indices(self, batch_size):
+        idx = torch.empty(batch_size, dtype=torch.int64, device=self.device)
+        N.check(N.lib().mh_replay_sample_indices(ctypes.byref(self.ws), self.seed, self._draws, batch_size,
+                                                 N.ptr(idx), N.stream_of(self.device)), "mh_replay_sample_indices")
+        self._draws += 1
+        return idx
+
+    def gather(self, idx):
+        B = int(idx.numel())
+        n, D, A = self.n_step, self.obsv_dim, self.act_dim
+        e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
+        out = {"obs": e(B, n, D), "act": e(B, n, A), "rew": e(B, n), "cost": e(B, n), "obs2": e(B, n, D),
+               "done": e(B, n), "logp": e(B, n)}
+        idx = idx.to(self.device, torch.int64).contiguous()
+        N.check(N.lib().mh_replay_gather(ctypes.byref(self.ws), n, D, A, N.ptr(idx), B,
+                                         *[N.ptr(out[k]) for k in KEYS], N.stream_of(self.device)), "mh_replay_gather")
+        return out
+
+    def sample_batch(self, batch_size: int) -> dict:
+        return self.gather(self.sample_indices(batch_size))

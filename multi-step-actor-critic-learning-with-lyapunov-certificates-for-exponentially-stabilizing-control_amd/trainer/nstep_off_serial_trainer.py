@@ -1,0 +1,130 @@
+"""n-step off-policy serial trainer (RL/trainer/nstep_off_serial_trainer.py:22-163).
+
+Same loop: warm-up fill, then per iteration sample -> add_batch -> sample_batch ->
+model_update -> log / save / evaluate. Differences, all at the device boundary:
+  * the reference moves every network to CPU around sampler.sample() (:78); here the sampler
+    declares its device (`sampler.device`) and the networks stay on it;
+  * replay batches are already device tensors (no `.cuda()` H2D copy, :87-89);
+  * the HIP sampler is bound to the device buffer at construction so windows are emitted in
+    place;
+  * tensorboard is optional (in-memory writer when absent).
+"""
+__all__ = ["NstepOffSerialTrainer"]
+
+import os
+import time
+from math import inf
+
+import torch
+
+from ..utils import dist as D
+from ..utils.common_utils import ModuleOnDevice
+from ..utils.log_data import LogData
+from ..utils.tensorboard_setup import add_scalars, make_writer, tb_tags
+
+
+class NstepOffSerialTrainer:
+    def __init__(self, alg, sampler, buffer, evaluator, **kwargs):
+        self.alg = alg
+        self.sampler = sampler
+        self.buffer = buffer
+        self.evaluator = evaluator
+        self.per_flag = kwargs["buffer_name"] == "prioritized_replay_buffer"
+        self.networks = self.alg.networks
+        self.sampler.networks = self.networks
+        if self.evaluator is not None:
+            self.evaluator.networks = self.networks
+        if kwargs.get("ini_network_dir") is not None:
+            self.networks.load_state_dict(torch.load(kwargs["ini_network_dir"], weights_only=True))
+        D.broadcast_module(self.networks)
+        self.replay_batch_size = kwargs["replay_batch_size"]
+        self.max_iteration = kwargs["max_iteration"]
+        self.policy_frequency = kwargs["policy_frequency"]
+        self.sample_interval = kwargs.get("sample_interval", 1)
+        self.log_save_interval = kwargs["log_save_interval"]
+        self.apprfunc_save_interval = kwargs["apprfunc_save_interval"]
+        self.save_folder = kwargs["save_folder"]
+        self.eval_interval = kwargs["eval_interval"]
+        self.best_tar = -inf
+        self.iteration = 0
+        self.is_main = D.rank() == 0
+        self.writer = make_writer(self.save_folder, flush_secs=20)
+        add_scalars({tb_tags["alg_time"]: 0, tb_tags["sampler_time"]: 0}, self.writer, 0)
+        self.writer.flush()
+        if hasattr(self.sampler, "bind_store") and hasattr(self.buffer, "ws"):
+            self.sampler.bind_store(self.buffer)
+        self.sample_device = getattr(self.sampler, "device", "cpu")
+        warm_calls = 0
+        while self.buffer.size < kwargs["buffer_warm_size"]:
+            with ModuleOnDevice(self.networks, self.sample_device):
+                samples, _ = self.sampler.sample()
+            self.buffer.add_batch(samples)
+            warm_calls += 1
+            if warm_calls > int(kwargs.get("buffer_warm_max_samples", 100000)):
+                raise RuntimeError("buffer warm-up did not reach buffer_warm_size: episodes never reach n_step")
+        self.sampler_tb_dict = LogData()
+        self.use_gpu = kwargs.get("use_gpu", torch.cuda.is_available())
+        self.start_time = time.time()
+
+    def step(self):
+        if self.iteration % self.sample_interval == 0:
+            with ModuleOnDevice(self.networks, self.sample_device):
+                sampler_samples, sampler_tb_dict = self.sampler.sample()
+            self.buffer.add_batch(sampler_samples)
+            self.sampler_tb_dict.add_average(sampler_tb_dict)
+        replay_samples = self.buffer.sample_batch(self.replay_batch_size)
+        self.networks.train()
+        if self.per_flag:
+            alg_tb_dict, idx, new_priority = self.alg.model_update(replay_samples, self.iteration)
+            self.buffer.update_batch(idx, new_priority)
+            if alg_tb_dict is not None and self.iteration % self.log_save_interval == 0 and self.is_main:
+                add_scalars(alg_tb_dict, self.writer, step=self.iteration)
+        elif self.iteration % self.policy_frequency == 0:
+            alg_tb_dict = self.alg.model_update(replay_samples, self.iteration)
+            if self.iteration % self.log_save_interval == 0 and self.is_main:
+                print("Iter = ", self.iteration, "save training data!")
+                add_scalars(alg_tb_dict, self.writer, step=self.iteration)
+        else:
+            self.alg.model_update(replay_samples, self.iteration)
+        self.networks.eval()
+        if self.iteration % self.log_save_interval == 0 and self.is_main:
+            print("Iter = ", self.iteration, "save average sampling time!")
+            add_scalars(self.sampler_tb_dict.pop(), self.writer, step=self.iteration)
+        if self.iteration % self.apprfunc_save_interval == 0 and self.is_main:
+            self.save_apprfunc()
+        if self.evaluator is not None and self.iteration % self.eval_interval == 0 and self.iteration > 0:
+            self._evaluate()
+
+    def _evaluate(self):
+        with ModuleOnDevice(self.networks, getattr(self.evaluator, "device", self.sample_device)):
+            ret_mean, ret_std, cost_mean, cost_std = self.evaluator.run_evaluation(self.iteration)
+        if not self.is_main:
+            return
+        apf = os.path.join(self.save_folder, "apprfunc")
+        if ret_mean >= self.best_tar and self.iteration >= self.max_iteration / 5:
+            self.best_tar = ret_mean
+            print("Eval_Iter: {}, Highest total average return = {}! Current total average cost = {}".format(
+                self.iteration, self.best_tar, cost_mean))
+            for fn in os.listdir(apf):
+                if fn.endswith("_opt.pkl"):
+                    os.remove(os.path.join(apf, fn))
+            torch.save(self.networks.state_dict(), os.path.join(apf, "apprfunc_{}_opt.pkl".format(self.iteration)))
+        self.writer.add_scalar(tb_tags["Buffer RAM of RL iteration"], self.buffer.__get_RAM__(), self.iteration)
+        self.writer.add_scalar(tb_tags["TRM of RL iteration"], ret_mean, self.iteration)
+        self.writer.add_scalar(tb_tags["TRS of RL iteration"], ret_std, self.iteration)
+        self.writer.add_scalar(tb_tags["TRM of total time"], ret_mean, int(time.time() - self.start_time))
+        self.writer.add_scalar(tb_tags["TCM of RL iteration"], cost_mean, self.iteration)
+        self.writer.add_scalar(tb_tags["TCS of RL iteration"], cost_std, self.iteration)
+        self.writer.add_scalar(tb_tags["TCM of total time"], cost_mean, int(time.time() - self.start_time))
+
+    def train(self):
+        while self.iteration <= self.max_iteration:
+            self.step()
+            self.iteration += 1
+        if self.is_main:
+            self.save_apprfunc()
+        self.writer.flush()
+
+    def save_apprfunc(self):
+        torch.save(self.networks.state_dict(),
+                   os.path.join(self.save_folder, "apprfunc", "apprfunc_{}.pkl".format(self.iteration)))

@@ -1,0 +1,129 @@
+"""Device n-step off-policy sampler (drop-in for RL/trainer/sampler/nstep_off_sampler.py +
+BaseSampler._n_step, RL/trainer/sampler/base.py:118-222).
+
+Per lockstep step: the policy MLP runs in PyTorch-ROCm on the [E, obs_dim] observation tensor,
+then ONE fused gfx950 kernel samples the TanhGauss action, clips it, integrates the env,
+computes reward/cost, autoresets, pushes the n-step deque and flags full windows; a scan and an
+emission kernel then write every full window straight into the bound replay store (env-index
+order, like base.py:178-213). `sample()` runs `horizon = sample_batch_size` such steps and
+returns a DeviceWindowBatch; the buffer's add_batch() binds the store so subsequent windows are
+emitted in place (no host round trip, no per-window Python).
+"""
+from __future__ import annotations
+
+import ctypes
+import time
+
+import torch
+
+from ... import _native as N
+from ...create_pkg.create_alg import create_approx_contrainer
+from ...env.hip_vector_env import HipVectorEnv
+from ...utils.tensorboard_setup import tb_tags
+from ..buffer.device_nstep_replay_buffer import DeviceNstepReplayBuffer, DeviceWindowBatch
+
+
+class HipNstepOffSampler:
+    def __init__(self, **kwargs):
+        self.env_id = kwargs["env_name"]
+        self.num_envs = int(kwargs["env_num"])
+        dev = kwargs.get("device")
+        self.device = torch.device(dev) if dev is not None else torch.device("cuda", torch.cuda.current_device())
+        self.envs = HipVectorEnv(self.env_id, self.num_envs, seed=int(kwargs.get("env_seed") or 0) +
+                                 int(kwargs.get("sampler_seed_offset", 0)), device=self.device)
+        self.obs_dim = self.envs.single_observation_space.shape
+        self.act_dim = self.envs.single_action_space.shape
+        self.networks = create_approx_contrainer(**kwargs).to(self.device)
+        self.sample_batch_size = int(kwargs["sample_batch_size"]) * self.num_envs
+        self.action_type = kwargs["action_type"]
+        self.reward_scale = float(kwargs["reward_scale"])
+        self.cost_scale = float(kwargs["cost_scale"])
+        self.noise_params = kwargs.get("noise_params")
+        if self.noise_params is not None:
+            raise NotImplementedError("noise_params: additive action noise is not supported by the HIP sampler yet")
+        if self.action_type != "continu":
+            raise RuntimeError("Only continuous action space is supported!")
+        self.target_value = kwargs.get("target_value", 0.0)
+        self.total_sample_number = 0
+        self.horizon = self.sample_batch_size // self.num_envs
+        self.n_step = int(kwargs.get("n_step", 1))
+        self.gamma = kwargs.get("gamma", 0.99)
+        self.td_lambda = kwargs.get("retrace_lambda", 0.95)
+        self.sync_timing = bool(kwargs.get("sampler_sync_timing", True))
+        self._h = self.envs.handle()
+        N.check(N.lib().mh_nstep_attach(self._h, self.n_step, self.reward_scale, self.cost_scale), "mh_nstep_attach")
+        self.obs, _ = self.envs.reset(seed=None)
+        self._bound = None
+        self._staging = None
+        self._graph = None
+
+    # ------------------------------------------------------------------ reference API
+    def get_total_sample_num(self) -> int:
+        return self.total_sample_number
+
+    def get_total_sample_number(self) -> int:
+        return self.total_sample_number
+
+    def load_state_dict(self, state_dict):
+        self.networks.load_state_dict(state_dict)
+
+    def bind_store(self, buffer: DeviceNstepReplayBuffer):
+        """Emit windows directly into `buffer` from now on."""
+        if buffer.n_step != self.n_step or buffer.obsv_dim != self.envs.obs_dim or buffer.act_dim != self.envs.act_dim:
+            raise ValueError("replay buffer shape does not match the sampler (n_step / obs_dim / act_dim)")
+        if buffer.device != self.device:
+            raise ValueError("replay buffer lives on a different device than the sampler")
+        self._bound = buffer
+        self._graph = None
+
+    def _target(self):
+        if self._bound is not None:
+            return self._bound
+        if self._staging is None:
+            self._staging = DeviceNstepReplayBuffer(obs_dim=self.envs.obs_dim, act_dim=self.envs.act_dim,
+                                                    buffer_max_size=max(1, self.horizon * self.num_envs),
+                                                    n_step=self.n_step, device=self.device)
+        self._staging.cursor.zero_()
+        return self._staging
+
+    # ------------------------------------------------------------------ one lockstep step
+    def _lockstep(self, store, logits=None, act_in=None, logp_in=None, reset_states=None, act_out=None,
+                  logp_out=None):
+        N.check(N.lib().mh_rollout_step(self._h, N.ptr(logits), N.ptr(act_in), N.ptr(logp_in), N.ptr(reset_states),
+                                        N.ptr(self.obs), ctypes.byref(store.ws) if store is not None else None,
+                                        N.ptr(act_out), N.ptr(logp_out), N.stream_of(self.device)),
+                "mh_rollout_step")
+
+    def _policy_logits(self):
+        return self.networks.policy(self.obs).contiguous()
+
+    def _sample(self):
+        store = self._target()
+        before = store.cursor[2].clone()
+        with torch.no_grad():
+            for _ in range(self.horizon):
+                self._lockstep(store, logits=self._policy_logits())
+        return DeviceWindowBatch(self, store, store.cursor[2] - before)
+
+    def sample(self):
+        """-> (DeviceWindowBatch, {sampler_time ms}) (base.py:308-323)."""
+        self.total_sample_number += self.sample_batch_size
+        t0 = time.perf_counter()
+        data = self._sample()
+        if self.sync_timing:
+            torch.cuda.synchronize(self.device)
+        tb = {tb_tags["sampler_time"]: (time.perf_counter() - t0) * 1000}
+        return data, tb
+
+    # ------------------------------------------------------------------ parity mode
+    def step_injected(self, actions, logp, reset_states=None, store=None):
+        """One lockstep step with injected (already clipped) actions and log-probs."""
+        act = torch.as_tensor(actions, dtype=torch.float32, device=self.device).contiguous()
+        lp = torch.as_tensor(logp, dtype=torch.float32, device=self.device).contiguous()
+        N.require_device(act, "actions", torch.float32, self.num_envs * self.envs.act_dim, self.device)
+        N.require_device(lp, "logp", torch.float32, self.num_envs, self.device)
+        rs = None
+        if reset_states is not None:
+            rs = torch.as_tensor(reset_states, dtype=torch.float32, device=self.device).contiguous()
+            N.require_device(rs, "reset_states", torch.float32, self.num_envs * self.envs.reset_dim, self.device)
+        self._lockstep(store if store is not None else self._bound, act_in=act, logp_in=lp, reset_states=rs)

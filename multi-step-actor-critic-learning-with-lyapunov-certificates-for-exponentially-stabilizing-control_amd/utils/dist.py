@@ -1,0 +1,93 @@
+"""Data-parallel plumbing: one process per GPU, torch.distributed with the "nccl" backend
+(= RCCL over xGMI on ROCm), or "gloo" for the CPU tests.
+
+The reference is single-process (no torch.distributed anywhere); the only exchange this engine
+adds is the gradient all-reduce of each optimiser step plus the 2-float (sum, sumsq) all-reduce
+of the stability-advantage normalisation. Gradients of one optimiser step go out as ONE flat
+bucket (at the reference config 0.54-0.56 MB for Q/Lyapunov, 0.28 MB for the policy): at these
+sizes a ring all-reduce over xGMI is latency-bound, so one call per step beats per-tensor calls.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def is_initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def world_size() -> int:
+    return dist.get_world_size() if is_initialized() else 1
+
+
+def rank() -> int:
+    return dist.get_rank() if is_initialized() else 0
+
+
+def init_from_env(backend=None):
+    """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, MASTER_ADDR/PORT)."""
+    if is_initialized() or int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return False
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    kw = {}
+    if backend == "nccl":
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        kw["device_id"] = torch.device("cuda", local)
+    dist.init_process_group(backend=backend, **kw)
+    return True
+
+
+def allreduce_(t: torch.Tensor, average: bool = False) -> torch.Tensor:
+    if world_size() > 1:
+        dist.all_reduce(t)
+        if average:
+            t.div_(world_size())
+    return t
+
+
+def allreduce_grads(params) -> None:
+    """Average the .grad of `params` across ranks with a single flat all-reduce."""
+    if world_size() <= 1:
+        return
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return
+    flat = torch._utils._flatten_dense_tensors(grads)
+    dist.all_reduce(flat)
+    flat.div_(world_size())
+    for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+        g.copy_(f)
+
+
+def broadcast_module(module: torch.nn.Module, src: int = 0) -> None:
+    """Make every rank start from rank `src`'s parameters and buffers."""
+    if world_size() <= 1:
+        return
+    tensors = [p.data for p in module.parameters()] + [b for b in module.buffers()]
+    flat = torch._utils._flatten_dense_tensors(tensors)
+    dist.broadcast(flat, src)
+    for t, f in zip(tensors, torch._utils._unflatten_dense_tensors(flat, tensors)):
+        t.copy_(f)
+
+
+def max_over_ranks(x: float) -> float:
+    if world_size() <= 1:
+        return float(x)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: float) -> float:
+    if world_size() <= 1:
+        return float(x)
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t)
+    return float(t.item())

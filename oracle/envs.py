@@ -231,6 +231,12 @@ class SingleTrackCar:
 
 
 # ------------------------------------------------------------------------------ QuadTracking
+def _rownorm(v):
+    """np.linalg.norm per row (BLAS ddot: sqrt(fma(z,z,fma(y,y,x*x))), bit-exact to the
+    reference's per-env call at QuadTracking.py:131,137)."""
+    return np.array([np.linalg.norm(r) for r in v], dtype=F64)
+
+
 QUAD_ROWS = MAX_STEP + 1
 
 
@@ -286,9 +292,9 @@ class QuadTracking:
         ex = (x - xd).astype(F32)
         ev = (v - vd).astype(F32)
         fd = -(-cls.kx * ex - cls.kv * ev - cls.m * cls.g + cls.m * ad)
-        b3 = fd / np.sqrt(np.einsum("ni,ni->n", fd, fd))[:, None]
+        b3 = fd / _rownorm(fd)[:, None]
         c = np.cross(b3, b1)
-        b2 = c / np.sqrt(np.einsum("ni,ni->n", c, c))[:, None]
+        b2 = c / _rownorm(c)[:, None]
         b1n = np.cross(b2, b3)
         Rd = np.stack([b1n, b2, b3], axis=2)  # columns
         if Rd_last is None:

@@ -1,0 +1,105 @@
+"""GPU parity of the n-step window path: fused rollout step (injected actions) + scan +
+emission into the device store vs the reference's own _n_step traces (tests/golden/nstep_*),
+FIFO wrap of the store, and the replay gather."""
+import ctypes
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import msacl_amd  # noqa: F401
+import msacl_amd._native as N
+from msacl_amd.env.hip_vector_env import HipVectorEnv
+from msacl_amd.trainer.buffer.device_nstep_replay_buffer import KEYS, DeviceNstepReplayBuffer
+from oracle import envs as OE
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+G = os.path.join(ROOT, "tests", "golden")
+TOL = dict(rtol=1e-5, atol=1e-5)
+TRACES = sorted(glob.glob(os.path.join(G, "nstep_*.npz")))
+
+
+def _run_trace(path, capacity=None, tile=1):
+    g = np.load(path)
+    name = os.path.basename(path)[6:-4].replace("_n20", "")
+    E0, T, n = g["init_reset"].shape[0], g["actions"].shape[0], int(g["n_step"])
+    E = E0 * tile
+    tl = lambda a: np.concatenate([a] * tile, axis=0)  # noqa: E731
+    env = HipVectorEnv(name, E, seed=1)
+    h = env.handle()
+    N.check(N.lib().mh_nstep_attach(h, n, 100.0, 100.0), "attach")
+    obs, _ = env.reset(reset_states=tl(g["init_reset"]))
+    env.set_state(None, None, tl(g["init_steps"]))
+    total = int(g["counts"].sum()) * tile
+    buf = DeviceNstepReplayBuffer(obs_dim=env.obs_dim, act_dim=env.act_dim, buffer_max_size=capacity or total + 7,
+                                  n_step=n)
+    dev = obs.device
+    for t in range(T):
+        act = torch.as_tensor(tl(g["actions"][t]), device=dev).contiguous()
+        lp = torch.as_tensor(tl(g["logp"][t]), device=dev).contiguous()
+        rs = torch.as_tensor(tl(g["resets"][t]), device=dev).contiguous()
+        N.check(N.lib().mh_rollout_step(h, None, N.ptr(act), N.ptr(lp), N.ptr(rs), N.ptr(obs), ctypes.byref(buf.ws),
+                                        None, None, N.stream_of(dev)), "rollout")
+        if tile == 1:
+            np.testing.assert_allclose(obs.cpu().numpy(), g["obs_trace"][t + 1], **TOL)
+    torch.cuda.synchronize()
+    return g, buf, total, tile
+
+
+def _expected_windows(g, tile):
+    """Window order of a tiled trace: per step, env-index order over the tiled envs."""
+    if tile == 1:
+        return {k: g["w_" + k] for k in KEYS}
+    out = {k: [] for k in KEYS}
+    off = 0
+    for c in g["counts"]:
+        for _ in range(tile):
+            for k in KEYS:
+                out[k].append(g["w_" + k][off:off + c])
+        off += c
+    return {k: np.concatenate(v) for k, v in out.items()}
+
+
+@pytest.mark.parametrize("path", TRACES, ids=os.path.basename)
+def test_windows_match_reference_sampler(path):
+    g, buf, total, _ = _run_trace(path)
+    assert buf.size == total and int(buf.cursor[2]) == total
+    for k in KEYS:
+        np.testing.assert_allclose(buf.n_step_buf[k][:total].cpu().numpy(), g["w_" + k], **TOL, err_msg=k)
+    assert not buf.n_step_buf["done"][:total, :-1].any()
+
+
+@pytest.mark.parametrize("path", TRACES[:2], ids=os.path.basename)
+def test_windows_tiled_to_many_envs(path):
+    g, buf, total, tile = _run_trace(path, tile=256)
+    exp = _expected_windows(g, tile)
+    for k in KEYS:
+        np.testing.assert_allclose(buf.n_step_buf[k][:total].cpu().numpy(), exp[k], **TOL, err_msg=k)
+
+
+@pytest.mark.parametrize("cap", [37, 100])
+def test_store_fifo_wrap(cap):
+    path = os.path.join(G, "nstep_VanderPol.npz")
+    g, buf, total, _ = _run_trace(path, capacity=cap)
+    assert buf.size == cap and buf.ptr == total % cap
+    rows = (np.arange(total - cap, total)) % cap
+    for k in KEYS:
+        np.testing.assert_allclose(buf.n_step_buf[k].cpu().numpy()[rows], g["w_" + k][total - cap:], **TOL)
+
+
+def test_replay_gather_and_indices():
+    path = os.path.join(G, "nstep_DuctedFan.npz")
+    g, buf, total, _ = _run_trace(path)
+    idx = torch.tensor([0, 5, total - 1, 3, 3], device="cuda")
+    out = buf.gather(idx)
+    for k in KEYS:
+        np.testing.assert_allclose(out[k].cpu().numpy(), g["w_" + k][idx.cpu().numpy()], **TOL)
+    draws = buf.sample_indices(100000).cpu().numpy()
+    assert draws.min() >= 0 and draws.max() < total
+    counts = np.bincount(draws, minlength=total)
+    assert counts.min() > 0.5 * 100000 / total  # roughly uniform
+    batch = buf.sample_batch(256)
+    assert batch["obs"].shape == (256, int(g["n_step"]), 6) and batch["rew"].shape == (256, int(g["n_step"]))
