@@ -50,8 +50,8 @@ class Registry:
                 continue
             self.register(stem, ep, extra_fn(mod) if extra_fn else None)
 
-    def build(self, name, *args, **kwargs):
-        spec = self.get(name)
+    def build(self, key, /, *args, **kwargs):
+        spec = self.get(key)
         merged = dict(spec.kwargs)
         merged.update(kwargs)
         if not callable(spec.entry_point):

@@ -17,8 +17,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 G = os.path.join(ROOT, "tests", "golden")
 
 
+_KEEP = []
+
+
 def dev(a, dtype=torch.float32):
-    return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device="cuda").contiguous()
+    """Device copy kept alive for the test's duration (a pointer into a freed temporary would
+    let the caching allocator hand the same block to the next input)."""
+    t = torch.as_tensor(np.ascontiguousarray(a), dtype=dtype, device="cuda").contiguous()
+    _KEEP.append(t)
+    return t
 
 
 @pytest.mark.parametrize("B,n", [(256, 20), (64, 5), (7, 70)])

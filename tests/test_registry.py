@@ -46,3 +46,26 @@ def test_create_envs_and_init_args_without_gpu(tmp_path):
     assert (tmp_path / "config.json").exists()
     with pytest.raises(ValueError):
         create_envs.create_envs(env_name="CartPole", env_num=1, env_seed=0)
+
+
+def test_approx_container_builds_on_cpu():
+    """The networks (PyTorch) build through create_apprfunc with the reference's kwargs; the
+    state_dict keys equal the reference ApproxContainer's (checkpoint compatibility)."""
+    import torch
+    from msacl_amd.algorithm.msacl import ApproxContainer
+    from msacl_amd.utils.config import default_msacl_args
+    a = default_msacl_args(obs_dim=12, act_dim=4, action_type="continu",
+                           action_high_limit=np.array([85.064, 10, 10, 10], np.float32),
+                           action_low_limit=np.array([0, -10, -10, -10], np.float32))
+    net = ApproxContainer(**a)
+    obs = torch.randn(5, 12)
+    logits = net.policy(obs)
+    assert logits.shape == (5, 8) and (logits[:, 4:] > 0).all()
+    d = net.create_action_distributions(logits)
+    act, lp = d.sample()
+    assert act.shape == (5, 4) and lp.shape == (5,)
+    assert torch.allclose(d.log_prob(act), lp, atol=1e-2)
+    assert net.q1(obs, act).shape == (5,) and net.lyapunov(obs).shape == (5,)
+    keys = set(net.state_dict())
+    assert {"log_alpha", "policy.act_high_lim", "q1.q.0.weight", "q2_target.q.4.bias", "lyapunov.lya.4.weight",
+            "policy.policy.4.weight"} <= keys
