@@ -107,11 +107,6 @@ def main():
 
     for _ in range(a.warmup):
         one_step()
-    h = sampler.envs.handle()
-    N.check(N.lib().mh_env_set_timing(h, 1), "timing")
-    ms0 = (ctypes.c_double * 3)()
-    l0 = ctypes.c_int64()
-    N.lib().mh_env_read_timing(h, ms0, ctypes.byref(l0), 1)
     win0 = int(buffer.cursor[2].item())
     if world > 1:
         torch.distributed.barrier()
@@ -123,14 +118,43 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     t1 = time.perf_counter()
-    N.check(N.lib().mh_env_set_timing(h, 0), "timing")
-    ms = (ctypes.c_double * 3)()
-    launches = ctypes.c_int64()
-    N.check(N.lib().mh_env_read_timing(h, ms, ctypes.byref(launches), 1), "read timing")
-    windows = int(buffer.cursor[2].item()) - win0
+    windows_timed = int(buffer.cursor[2].item()) - win0
     elapsed = D.max_over_ranks(t1 - t0)
     env_steps_total = world * a.envs * horizon * a.steps
     value = env_steps_total / elapsed
+
+    # ---- phase split (diagnostic, after the timed region): sample() vs replay sample + update
+    ph_s = ph_u = 0.0
+    for _ in range(2):
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        samples, _ = sampler.sample()
+        buffer.add_batch(samples)
+        torch.cuda.synchronize()
+        tb_ = time.perf_counter()
+        rs = buffer.sample_batch(trainer.replay_batch_size)
+        alg.model_update(rs, trainer.iteration)
+        trainer.iteration += 1
+        torch.cuda.synchronize()
+        ph_s += tb_ - ta
+        ph_u += time.perf_counter() - tb_
+    phases = {"sample_ms": round(ph_s / 2 * 1e3, 3), "replay_and_update_ms": round(ph_u / 2 * 1e3, 3)}
+
+    # ---- per-kernel durations: HIP events recorded on the launch stream around each engine
+    # kernel, over 2 more trainer steps run right after the timed region (graph replays carry
+    # no per-kernel events, so this phase launches the same kernels eagerly)
+    h = sampler.envs.handle()
+    ms = (ctypes.c_double * 3)()
+    launches = ctypes.c_int64()
+    N.lib().mh_env_read_timing(h, ms, ctypes.byref(launches), 1)
+    sampler.set_kernel_timing(True)
+    win1 = int(buffer.cursor[2].item())
+    for _ in range(2):
+        one_step()
+    torch.cuda.synchronize()
+    sampler.set_kernel_timing(False)
+    N.check(N.lib().mh_env_read_timing(h, ms, ctypes.byref(launches), 1), "read timing")
+    windows = int(buffer.cursor[2].item()) - win1
 
     # ---- live roofline of the engine's kernels over the timed region (HIP events)
     info = sampler.envs.info
@@ -172,7 +196,8 @@ def main():
                    "policy": a.policy, "parallelism": f"dp{world}"},
         "roofline": roof,
         "kernels": kernels,
-        "windows_per_step": round(windows / a.steps, 1),
+        "windows_per_step": round(windows_timed / a.steps, 1),
+        "phases": phases,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(a.env, alg.networks.policy, a.cpu_seconds)

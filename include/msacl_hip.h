@@ -135,6 +135,11 @@ int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const 
 int mh_env_set_timing(mh_env_t h, int32_t enable);
 int mh_env_read_timing(mh_env_t h, double* ms_out, int64_t* launches_out, int32_t reset);
 
+/* Let mh_rollout_step take the policy head's RAW output (mean | log_std) and apply
+ * StochaPolicy's std = exp(clamp(log_std, lo, hi)) (RL/apprfunc/mlp.py:132-136) in-kernel,
+ * saving the chunk/clamp/exp/cat launches of the PyTorch forward. */
+int mh_nstep_set_log_std_clamp(mh_env_t h, int32_t enable, float lo, float hi);
+
 /* NstepReplayBuffer.sample_batch gather (RL/trainer/buffer/nstep_replay_buffer.py:128-150):
  * out_X[b] = store.X[idx[b]] for the 7 arrays (any out pointer may be NULL). */
 int mh_replay_gather(const mh_window_store_t* store, int32_t n_step, int32_t obs_dim,

@@ -57,6 +57,7 @@ _PROTOS = {
     "mh_env_set_state": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mh_nstep_attach": (ctypes.c_int, [c_vp, c_i32, c_f32, c_f32]),
     "mh_rollout_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(WindowStore), c_vp, c_vp, c_vp]),
+    "mh_nstep_set_log_std_clamp": (ctypes.c_int, [c_vp, c_i32, c_f32, c_f32]),
     "mh_env_set_timing": (ctypes.c_int, [c_vp, c_i32]),
     "mh_env_read_timing": (ctypes.c_int, [c_vp, ctypes.POINTER(c_f64), ctypes.POINTER(c_i64), c_i32]),
     "mh_replay_gather": (ctypes.c_int, [ctypes.POINTER(WindowStore), c_i32, c_i32, c_i32, c_vp, c_i64,

@@ -32,9 +32,12 @@ from ..utils.tensorboard_setup import tb_tags
 
 
 def _adam(params, lr):
+    """Fused single-kernel Adam, capturable (step counter on device) so the whole update can
+    be replayed as a HIP graph."""
+    params = list(params)
     try:
-        return Adam(params, lr=lr, fused=True)
-    except (RuntimeError, TypeError):
+        return Adam(params, lr=lr, fused=True, capturable=True)
+    except (RuntimeError, TypeError, ValueError):
         return Adam(params, lr=lr)
 
 
@@ -128,6 +131,12 @@ class MSACL:
         self.start_lya_coef = torch.pow((1 - self.lya_eta), torch.arange(n) + 1).to(self.device).contiguous()
         self._scratch = {}
         self.last_priority = None
+        self._neg_one = torch.tensor(-1.0, device=self.device)
+        self.use_graph = bool(kwargs.get("alg_use_graph", True))
+        self._static = None
+        self._static_shapes = None
+        self._graphs = {}
+        self._warm = set()
 
     @property
     def adjustable_parameters(self):
@@ -154,29 +163,75 @@ class MSACL:
                             (self.networks.alpha_optimizer, self.alpha_learning_rate)):
                 opt.param_groups[0]["lr"] = lr * frac
         data = {k: (v.to(self.device).contiguous() if torch.is_tensor(v) else v) for k, v in data.items()}
-        loss_q, q1_mean, q2_mean = self._q_update(data)
-        if global_iteration % self.target_network_frequency == 0:
-            self._target_update()
-        loss_lya = self._lyapunov_update(data)
+        flags = (global_iteration % self.target_network_frequency == 0, global_iteration % self.policy_frequency == 0)
+        if self._graphable():
+            outs = self._graph_update(data, flags)
+        else:
+            outs = self._update_body(data, *flags)
         tb_info = None
-        if global_iteration % self.policy_frequency == 0:
-            for _ in range(self.policy_frequency):
-                loss_policy, entropy = self._policy_update(data=data)
-                if self.auto_alpha:
-                    self._alpha_update(entropy=entropy)
+        if flags[1]:
+            loss_q, q1_mean, q2_mean, loss_lya, loss_policy, entropy = outs
+            vals = torch.stack([entropy, self.networks.log_alpha.detach().exp(), q1_mean, q2_mean, loss_q, loss_lya,
+                                loss_policy]).tolist()  # one device->host transfer instead of seven
             tb_info = {
-                "MSACL/entropy-RL iter": entropy.item(),
-                "MSACL/alpha-RL iter": self._get_alpha(),
-                "MSACL/q1_mean-RL iter": q1_mean.item(),
-                "MSACL/q2_mean-RL iter": q2_mean.item(),
-                tb_tags["loss_critic"]: loss_q.item(),
-                tb_tags["loss_lyapunov"]: loss_lya.item(),
-                tb_tags["loss_actor"]: loss_policy.item(),
+                "MSACL/entropy-RL iter": vals[0],
+                "MSACL/alpha-RL iter": vals[1],
+                "MSACL/q1_mean-RL iter": vals[2],
+                "MSACL/q2_mean-RL iter": vals[3],
+                tb_tags["loss_critic"]: vals[4],
+                tb_tags["loss_lyapunov"]: vals[5],
+                tb_tags["loss_actor"]: vals[6],
                 tb_tags["alg_time"]: (time.time() - start) * 1000,
             }
         if self.per_flag:
             return tb_info, data.get("idx"), self.last_priority
         return tb_info
+
+    def _update_body(self, data, do_target, do_policy):
+        """One model_update's device work (msacl.py:193-210); returns device tensors only."""
+        loss_q, q1_mean, q2_mean = self._q_update(data)
+        if do_target:
+            self._target_update()
+        loss_lya = self._lyapunov_update(data)
+        loss_policy = entropy = None
+        if do_policy:
+            for _ in range(self.policy_frequency):
+                loss_policy, entropy = self._policy_update(data=data)
+                if self.auto_alpha:
+                    self._alpha_update(entropy=entropy)
+        return loss_q, q1_mean, q2_mean, loss_lya, loss_policy, entropy
+
+    # ------------------------------------------------------------------ HIP-graph replay
+    def _graphable(self):
+        return (self.use_graph and not self.anneal_lr and D.world_size() == 1 and torch.cuda.is_available()
+                and not torch.cuda.is_current_stream_capturing())
+
+    def _graph_update(self, data, flags):
+        """Replay the whole update (~350 launches) as one HIP graph. The first call per branch
+        (even/odd iteration) runs eagerly on the static inputs (lazy hipBLASLt / Adam state
+        init), the second captures, later calls only copy the new replay batch in and replay."""
+        shapes = tuple((k, tuple(v.shape)) for k, v in sorted(data.items()) if torch.is_tensor(v))
+        if self._static is None or self._static_shapes != shapes:
+            self._static = {k: v.clone() for k, v in data.items() if torch.is_tensor(v)}
+            self._static_shapes = shapes
+            self._graphs = {}
+            self._warm = set()
+        for k, v in self._static.items():
+            if data[k].data_ptr() != v.data_ptr():
+                v.copy_(data[k])
+        if flags not in self._warm:
+            self._warm.add(flags)
+            return self._update_body(self._static, *flags)
+        if flags not in self._graphs:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                outs = self._update_body(self._static, *flags)
+                prio = self.last_priority
+            self._graphs[flags] = (g, outs, prio)
+        g, outs, prio = self._graphs[flags]
+        g.replay()
+        self.last_priority = prio
+        return outs
 
     def _q_update(self, data):
         obs, act, rew, obs2, done = data["obs"], data["act"], data["rew"], data["obs2"], data["done"]
@@ -235,7 +290,9 @@ class MSACL:
         new_act, new_act_logp = dist.rsample()
         q1 = self.networks.q1(obs, new_act)
         q2 = self.networks.q2(obs, new_act)
-        loss_policy_q = (torch.min(q1, q2) - self._get_alpha() * new_act_logp).mean()
+        # alpha as a 0-d device tensor (the reference's alpha.item() float has the same f32 value)
+        alpha = self.networks.log_alpha.detach().exp()
+        loss_policy_q = (torch.min(q1, q2) - alpha * new_act_logp).mean()
         ratio = torch.exp(dist.log_prob(old_act) - old_logp)
         is_ratio = ratio[:, 0]
         with torch.no_grad():
@@ -252,7 +309,7 @@ class MSACL:
                 "mh_msacl_ppo_clip")
         loss_policy = -loss_policy_q.detach() - s.loss_ppo[0]
         self.networks.policy_optimizer.zero_grad()
-        torch.autograd.backward([loss_policy_q, is_ratio], [torch.tensor(-1.0, device=self.device), -s.d_ratio])
+        torch.autograd.backward([loss_policy_q, is_ratio], [self._neg_one, -s.d_ratio])
         D.allreduce_grads(list(self.networks.policy.parameters()))
         self.networks.policy_optimizer.step()
         entropy = -new_act_logp.mean().detach()

@@ -58,6 +58,8 @@ struct mh_env_s {
   // n-step
   int n = 0;
   float reward_scale = 1.0f, cost_scale = 1.0f;
+  int raw_log_std = 0;
+  float log_std_lo = -20.0f, log_std_hi = 1.0f;
   float* ring = nullptr;
   int32_t* ring_len = nullptr;
   int32_t* ring_pos = nullptr;
@@ -96,6 +98,9 @@ struct mh_env_s {
     a.n = n;
     a.reward_scale = reward_scale;
     a.cost_scale = cost_scale;
+    a.raw_log_std = raw_log_std;
+    a.log_std_lo = log_std_lo;
+    a.log_std_hi = log_std_hi;
     return a;
   }
 };
@@ -315,6 +320,15 @@ int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const 
     MH_HIP(hipEventRecord(ev[3], st));
     for (int i = 0; i < 4; ++i) h->ev_pending.push_back(ev[i]);
   }
+  return MH_OK;
+}
+
+int mh_nstep_set_log_std_clamp(mh_env_t h, int32_t enable, float lo, float hi) {
+  if (!h) return fail(MH_EINVAL, "mh_nstep_set_log_std_clamp: null handle");
+  if (enable && !(lo <= hi)) return fail(MH_EINVAL, "mh_nstep_set_log_std_clamp: lo > hi");
+  h->raw_log_std = enable != 0;
+  h->log_std_lo = lo;
+  h->log_std_hi = hi;
   return MH_OK;
 }
 

@@ -41,6 +41,8 @@ struct StepArgs {
   int32_t* block_count;       // [grid]
   int n;
   float reward_scale, cost_scale;
+  int raw_log_std;               // logits second half is log_std: std = exp(clamp(., lo, hi))
+  float log_std_lo, log_std_hi;  // StochaPolicy min/max_log_std (mlp.py:125-136)
 };
 
 struct EmitArgs {

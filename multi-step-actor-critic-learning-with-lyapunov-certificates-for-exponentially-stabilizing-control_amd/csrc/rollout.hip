@@ -117,7 +117,8 @@ __global__ __launch_bounds__(BLK) void k_rollout(StepArgs a) {
 #pragma unroll
       for (int i = 0; i < A; ++i) {
         const float mu = a.logits[e * 2 * A + i];
-        const float sd = a.logits[e * 2 * A + A + i];
+        float sd = a.logits[e * 2 * A + A + i];
+        if (a.raw_log_std) sd = expf(fminf(fmaxf(sd, a.log_std_lo), a.log_std_hi));  // clamp(.).exp()
         const float z = mu + sd * (float)nz[i];
         // Normal.log_prob: -((z-mu)^2)/(2 var) - log(std) - log(sqrt(2 pi))
         const float df = z - mu;

@@ -1,13 +1,16 @@
 """Device n-step off-policy sampler (drop-in for RL/trainer/sampler/nstep_off_sampler.py +
 BaseSampler._n_step, RL/trainer/sampler/base.py:118-222).
 
-Per lockstep step: the policy MLP runs in PyTorch-ROCm on the [E, obs_dim] observation tensor,
-then ONE fused gfx950 kernel samples the TanhGauss action, clips it, integrates the env,
-computes reward/cost, autoresets, pushes the n-step deque and flags full windows; a scan and an
-emission kernel then write every full window straight into the bound replay store (env-index
-order, like base.py:178-213). `sample()` runs `horizon = sample_batch_size` such steps and
-returns a DeviceWindowBatch; the buffer's add_batch() binds the store so subsequent windows are
-emitted in place (no host round trip, no per-window Python).
+Per lockstep step: the policy MLP runs in PyTorch-ROCm on the [E, obs_dim] observation tensor
+(hidden layers as hipBLASLt GEMMs with the ReLU fused into the GEMM epilogue; the head's
+clamp(log_std).exp() is folded into the rollout kernel), then ONE fused gfx950 kernel samples
+the TanhGauss action, clips it, integrates the env, computes reward/cost, autoresets, pushes
+the n-step deque and flags full windows; a scan and an emission kernel write every full window
+straight into the bound replay store (env-index order, base.py:178-213).
+`sample()` runs `horizon = sample_batch_size` such steps; after the first (eager) call the
+whole horizon loop is captured once into a HIP graph and replayed (no per-launch host cost).
+It returns a DeviceWindowBatch; the buffer's add_batch() binds the store so subsequent windows
+are emitted in place (no host round trip, no per-window Python).
 """
 from __future__ import annotations
 
@@ -15,10 +18,12 @@ import ctypes
 import time
 
 import torch
+import torch.nn as nn
 
 from ... import _native as N
 from ...create_pkg.create_alg import create_approx_contrainer
 from ...env.hip_vector_env import HipVectorEnv
+from ...utils.act_distribution_cls import TanhGaussDistribution
 from ...utils.tensorboard_setup import tb_tags
 from ..buffer.device_nstep_replay_buffer import DeviceNstepReplayBuffer, DeviceWindowBatch
 
@@ -50,12 +55,15 @@ class HipNstepOffSampler:
         self.gamma = kwargs.get("gamma", 0.99)
         self.td_lambda = kwargs.get("retrace_lambda", 0.95)
         self.sync_timing = bool(kwargs.get("sampler_sync_timing", True))
+        self.use_graph = bool(kwargs.get("sampler_use_graph", True))
         self._h = self.envs.handle()
         N.check(N.lib().mh_nstep_attach(self._h, self.n_step, self.reward_scale, self.cost_scale), "mh_nstep_attach")
         self.obs, _ = self.envs.reset(seed=None)
         self._bound = None
         self._staging = None
         self._graph = None
+        self._graph_key = None
+        self._eager_calls = 0
 
     # ------------------------------------------------------------------ reference API
     def get_total_sample_num(self) -> int:
@@ -74,7 +82,6 @@ class HipNstepOffSampler:
         if buffer.device != self.device:
             raise ValueError("replay buffer lives on a different device than the sampler")
         self._bound = buffer
-        self._graph = None
 
     def _target(self):
         if self._bound is not None:
@@ -86,6 +93,33 @@ class HipNstepOffSampler:
         self._staging.cursor.zero_()
         return self._staging
 
+    # ------------------------------------------------------------------ policy head
+    def _policy_raw(self):
+        """StochaPolicy.forward (mlp.py:132-136) up to the head: returns (logits, raw) where raw
+        means the second half is log_std before clamp/exp (the kernel finishes it)."""
+        pol = self.networks.policy
+        seq = getattr(pol, "policy", None)
+        if getattr(pol, "action_distribution_cls", None) is not TanhGaussDistribution:
+            raise NotImplementedError("the HIP sampler samples TanhGaussDistribution policies")
+        if not isinstance(seq, nn.Sequential):
+            return pol(self.obs).contiguous(), False
+        h = self.obs
+        mods = list(seq)
+        i = 0
+        while i < len(mods):
+            m = mods[i]
+            nxt = mods[i + 1] if i + 1 < len(mods) else None
+            if isinstance(m, nn.Linear) and isinstance(nxt, nn.ReLU):
+                h = torch._addmm_activation(m.bias, h, m.weight.t())  # GEMM + bias + ReLU epilogue
+                i += 2
+            elif isinstance(m, nn.Linear) and (nxt is None or isinstance(nxt, nn.Identity)):
+                h = torch.addmm(m.bias, h, m.weight.t())
+                i += 2
+            else:
+                h = m(h)
+                i += 1
+        return h.contiguous(), True
+
     # ------------------------------------------------------------------ one lockstep step
     def _lockstep(self, store, logits=None, act_in=None, logp_in=None, reset_states=None, act_out=None,
                   logp_out=None):
@@ -94,15 +128,36 @@ class HipNstepOffSampler:
                                         N.ptr(act_out), N.ptr(logp_out), N.stream_of(self.device)),
                 "mh_rollout_step")
 
-    def _policy_logits(self):
-        return self.networks.policy(self.obs).contiguous()
+    def _policy_step(self, store):
+        logits, raw = self._policy_raw()
+        pol = self.networks.policy
+        N.check(N.lib().mh_nstep_set_log_std_clamp(self._h, int(raw), float(getattr(pol, "min_log_std", -20.0)),
+                                                   float(getattr(pol, "max_log_std", 1.0))), "log_std clamp")
+        self._lockstep(store, logits=logits)
+
+    def _horizon(self, store):
+        for _ in range(self.horizon):
+            self._policy_step(store)
+
+    def _graph_for(self, store):
+        key = (id(store), id(self.networks.policy), tuple(p.data_ptr() for p in self.networks.policy.parameters()),
+               self.obs.data_ptr())
+        if self._graph is None or self._graph_key != key:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._horizon(store)
+            self._graph, self._graph_key = g, key
+        return self._graph
 
     def _sample(self):
         store = self._target()
         before = store.cursor[2].clone()
         with torch.no_grad():
-            for _ in range(self.horizon):
-                self._lockstep(store, logits=self._policy_logits())
+            if self.use_graph and self._eager_calls >= 1 and not getattr(self, "_timing", False):
+                self._graph_for(store).replay()
+            else:
+                self._horizon(store)
+                self._eager_calls += 1
         return DeviceWindowBatch(self, store, store.cursor[2] - before)
 
     def sample(self):
@@ -114,6 +169,11 @@ class HipNstepOffSampler:
             torch.cuda.synchronize(self.device)
         tb = {tb_tags["sampler_time"]: (time.perf_counter() - t0) * 1000}
         return data, tb
+
+    def set_kernel_timing(self, enable: bool):
+        """Per-kernel HIP-event timing (runs the horizon eagerly while enabled)."""
+        self._timing = bool(enable)
+        N.check(N.lib().mh_env_set_timing(self._h, int(enable)), "mh_env_set_timing")
 
     # ------------------------------------------------------------------ parity mode
     def step_injected(self, actions, logp, reset_states=None, store=None):

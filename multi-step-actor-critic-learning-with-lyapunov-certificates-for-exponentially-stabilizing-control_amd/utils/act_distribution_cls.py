@@ -21,7 +21,10 @@ class Action_Distribution_Cls:
 
 
 def _independent_normal(mean, std):
-    return torch.distributions.Independent(torch.distributions.Normal(mean, std), reinterpreted_batch_ndims=1)
+    # validate_args=False: argument validation only raises on invalid parameters but costs a
+    # device->host sync per construction (and forbids HIP-graph capture); numerics unchanged.
+    return torch.distributions.Independent(torch.distributions.Normal(mean, std, validate_args=False),
+                                           reinterpreted_batch_ndims=1, validate_args=False)
 
 
 class TanhGaussDistribution:

@@ -151,3 +151,30 @@ def _compare_params(alg, g, prefix):
         worst.append(bad.mean())
         assert bad.mean() < 2e-3, (k, bad.sum(), np.abs(got - ref).max())
     assert worst
+
+
+def test_graph_replayed_update_trains():
+    """The HIP-graph path (warm -> capture -> replay, both even/odd branches) runs, keeps the
+    parameters finite and fits a fixed batch like the eager path."""
+    from msacl_amd.algorithm.msacl import MSACL
+    g = np.load(os.path.join(G, "msacl_update.npz"))
+    B, n = int(g["cfg_B"]), int(g["cfg_n"])
+    data = {k: torch.as_tensor(g["in_" + k], device="cuda") for k in ("obs", "act", "rew", "cost", "obs2", "done", "logp")}
+    losses = {}
+    for mode in (True, False):
+        torch.manual_seed(0)
+        alg = MSACL(**_msacl_kwargs(B, n), alg_use_graph=mode)
+        sd = {k[5:]: torch.as_tensor(g[k]) for k in g.files if k.startswith("init/")}
+        alg.networks.load_state_dict(sd)
+        hist = []
+        for it in range(12):
+            tb = alg.model_update(data, it)
+            if tb is not None:
+                hist.append(tb["Loss/Critic loss-RL iter"])
+        assert all(torch.isfinite(p).all() for p in alg.networks.parameters())
+        if mode:
+            assert len(alg._graphs) == 2
+        losses[mode] = hist
+    for mode, h in losses.items():
+        assert h[-1] < h[0], (mode, h)
+    np.testing.assert_allclose(losses[True][0], losses[False][0], rtol=1e-5)
