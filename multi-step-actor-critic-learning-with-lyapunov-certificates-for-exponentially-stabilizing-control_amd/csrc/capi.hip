@@ -66,6 +66,7 @@ struct mh_env_s {
   int32_t* emit_rank = nullptr;
   int32_t* block_count = nullptr;
   int32_t* block_offset = nullptr;
+  int32_t* emit_list = nullptr;
 
   // optional per-kernel HIP-event timing of mh_rollout_step (bench.py's live roofline)
   bool timing = false;
@@ -110,7 +111,7 @@ static void free_handle(mh_env_s* h) {
   for (hipEvent_t e : h->ev_free) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->ev_pending) (void)hipEventDestroy(e);
   void* ptrs[] = {h->state, h->xstate, h->steps, h->tab, h->meta, h->ring, h->ring_len,
-                  h->ring_pos, h->emit_rank, h->block_count, h->block_offset};
+                  h->ring_pos, h->emit_rank, h->block_count, h->block_offset, h->emit_list};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete h;
@@ -186,6 +187,8 @@ int mh_nstep_attach(mh_env_t h, int32_t n_step, float reward_scale, float cost_s
   if (h->ring) {
     (void)hipFree(h->ring); (void)hipFree(h->ring_len); (void)hipFree(h->ring_pos);
     (void)hipFree(h->emit_rank); (void)hipFree(h->block_count); (void)hipFree(h->block_offset);
+    (void)hipFree(h->emit_list);
+    h->emit_list = nullptr;
     h->ring = nullptr;
   }
   h->n = n_step;
@@ -199,6 +202,7 @@ int mh_nstep_attach(mh_env_t h, int32_t n_step, float reward_scale, float cost_s
   MH_HIP(hipMalloc(&h->emit_rank, sizeof(int32_t) * E));
   MH_HIP(hipMalloc(&h->block_count, sizeof(int32_t) * h->grid()));
   MH_HIP(hipMalloc(&h->block_offset, sizeof(int32_t) * h->grid()));
+  MH_HIP(hipMalloc(&h->emit_list, sizeof(int32_t) * (size_t)h->grid() * mh::BLK));
   MH_HIP(hipMemset(h->ring_len, 0, sizeof(int32_t) * E));
   MH_HIP(hipMemset(h->ring_pos, 0, sizeof(int32_t) * E));
   MH_HIP(hipMemset(h->ring, 0, sizeof(float) * E * n_step * F));
@@ -285,16 +289,50 @@ int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const 
   a.ring_pos = h->ring_pos;
   a.emit_rank = h->emit_rank;
   a.block_count = h->block_count;
+  // fused scan+emission when the block prefix and the staging tiles fit in LDS
+  const size_t fused_lds = (size_t)4 * h->n * h->info.record_floats * sizeof(float) +
+                           (size_t)(h->grid() + 4 + 256) * sizeof(int) + 16;
+  const bool fused = store && h->grid() <= mh::EMIT_FUSED_MAX_NB && fused_lds <= 64 * 1024;
+  if (fused) {
+    a.emit_list = h->emit_list;
+    a.cursor = store->cursor;
+  }
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   if (h->timing)
     for (int i = 0; i < 4; ++i) ev[i] = h->take_event();
   if (ev[0]) MH_HIP(hipEventRecord(ev[0], st));
   MH_HIP(mh::launch_rollout(h->env_id, a, st));
   if (ev[1]) MH_HIP(hipEventRecord(ev[1], st));
-  MH_HIP(mh::launch_finalize(h->block_count, store ? h->grid() : 0, h->block_offset, h->meta,
-                             store ? store->cursor : nullptr, store ? store->capacity : 1, st));
+  if (!fused)
+    MH_HIP(mh::launch_finalize(h->block_count, store ? h->grid() : 0, h->block_offset, h->meta,
+                               store ? store->cursor : nullptr, store ? store->capacity : 1, st));
   if (ev[2]) MH_HIP(hipEventRecord(ev[2], st));
-  if (store) {
+  if (fused) {
+    mh::EmitArgs ea;
+    std::memset(&ea, 0, sizeof(ea));
+    ea.E = h->E;
+    ea.ring = h->ring;
+    ea.ring_pos = h->ring_pos;
+    ea.meta = h->meta;
+    ea.meta_rw = h->meta;
+    ea.capacity = store->capacity;
+    ea.n = h->n;
+    ea.F = h->info.record_floats;
+    ea.D = h->info.obs_dim;
+    ea.A = h->info.act_dim;
+    ea.obs = store->obs;
+    ea.act = store->act;
+    ea.rew = store->rew;
+    ea.cost = store->cost;
+    ea.obs2 = store->obs2;
+    ea.done = store->done;
+    ea.logp = store->logp;
+    ea.block_count = h->block_count;
+    ea.emit_list = h->emit_list;
+    ea.nb = h->grid();
+    ea.cursor = store->cursor;
+    MH_HIP(mh::launch_emit_fused(ea, st));
+  } else if (store) {
     mh::EmitArgs ea;
     ea.E = h->E;
     ea.ring = h->ring;

@@ -461,15 +461,90 @@ struct QuadConst {
   static constexpr double mg = 4.34 * 9.8;  // model.m * g[2]
 };
 
-// Orthogonal polar factor of a float32 3x3 via float64 Newton iteration X <- (X + X^-T)/2,
-// with the det<0 column flip of NormalizeOrientMatrix (QuadTracking.py:308-315).
+// max |X^T X - I| of a 3x3 (row-major)
+template <typename T>
+MH_HD T orth_err3(const T* X, T* G) {
+  T e = T(0);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = i; j < 3; ++j) {
+      T acc = X[0 * 3 + i] * X[0 * 3 + j];
+      acc = fma(X[1 * 3 + i], X[1 * 3 + j], acc);
+      acc = fma(X[2 * 3 + i], X[2 * 3 + j], acc);
+      G[i * 3 + j] = G[j * 3 + i] = acc;
+      T d = acc - (i == j ? T(1) : T(0));
+      e = fmax(e, fabs(d));
+    }
+  return e;
+}
+
+// Newton-Schulz step X <- X (3I - G)/2 = X + X (I - G)/2 with G = X^T X formed in float64.
+MH_HD void ns_step3(double* X, const double* G) {
+  double M[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) M[i] = (((i % 4) == 0 ? 1.0 : 0.0) - G[i]) * 0.5;
+  double Y[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      double acc = X[i * 3 + 0] * M[0 * 3 + j];
+      acc = fma(X[i * 3 + 1], M[1 * 3 + j], acc);
+      acc = fma(X[i * 3 + 2], M[2 * 3 + j], acc);
+      Y[i * 3 + j] = X[i * 3 + j] + acc;
+    }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) X[i] = Y[i];
+}
+
+// Same step with the correction X (I - G)/2 formed in float32 and added in float64: once
+// |I - G| < 1e-6 its rounding error (~6e-8 |I - G|) is ~1e-13, far below the result ulp.
+MH_HD void ns_step3_mixed(double* X, const double* G) {
+  float Mf[9], Xf[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    Mf[i] = (float)(((i % 4) == 0 ? 1.0 : 0.0) - G[i]) * 0.5f;
+    Xf[i] = (float)X[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float acc = Xf[i * 3 + 0] * Mf[0 * 3 + j];
+      acc = fmaf(Xf[i * 3 + 1], Mf[1 * 3 + j], acc);
+      acc = fmaf(Xf[i * 3 + 2], Mf[2 * 3 + j], acc);
+      X[i * 3 + j] += (double)acc;
+    }
+}
+
+// Orthogonal polar factor of a float32 3x3, with the det<0 column flip of
+// NormalizeOrientMatrix (QuadTracking.py:308-315; U @ Vh of a float32 SVD).
+// The integrator keeps R within ~(0.01|W|)^2 of SO(3), where Newton-Schulz converges
+// quadratically without a division (2-3 steps to max|X^T X - I| < 1e-12, i.e. the
+// float64-exact polar factor before the final rounding). Inputs farther than 0.25 from
+// orthogonal take the float64 Newton iteration X <- (X + X^-T)/2.
 MH_HD void polar3(const float* Rin, float* Rout) {
-  double X[9];
+  double X[9], G[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) X[i] = (double)Rin[i];
-  double det0 = X[0] * (X[4] * X[8] - X[5] * X[7]) - X[1] * (X[3] * X[8] - X[5] * X[6]) +
-                X[2] * (X[3] * X[7] - X[4] * X[6]);
-  for (int it = 0; it < 60; ++it) {
+  double e = orth_err3<double>(X, G);
+  const bool near = e < 0.25;
+  if (near) {
+    for (int it = 0; it < 8 && e >= 1e-12; ++it) {
+      if (e < 1e-6)
+        ns_step3_mixed(X, G);
+      else
+        ns_step3(X, G);
+      e = orth_err3<double>(X, G);
+    }
+  }
+  double X0[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) X0[i] = (double)Rin[i];
+  double det0 = X0[0] * (X0[4] * X0[8] - X0[5] * X0[7]) - X0[1] * (X0[3] * X0[8] - X0[5] * X0[6]) +
+                X0[2] * (X0[3] * X0[7] - X0[4] * X0[6]);
+  for (int it = 0; it < 60 && !near; ++it) {
     double C[9];
     C[0] = X[4] * X[8] - X[5] * X[7];
     C[1] = X[5] * X[6] - X[3] * X[8];

@@ -35,6 +35,22 @@ struct Rng {
   __host__ __device__ __forceinline__ u32x4 draw(uint32_t stream) const {
     return philox4x32_10(u32x4{env_lo, env_hi ^ (stream << 16), tick_lo, tick_hi}, k0, k1);
   }
+  // 4 standard normals via Box-Muller in float32 (action noise: torch draws float32 normals too)
+  __host__ __device__ __forceinline__ void normal4f(uint32_t stream, float* out) const {
+    u32x4 r = draw(stream);
+    // 24-bit uniforms; u1,u3 in (0, 1] so log() stays finite
+    float u1 = 1.0f - (float)(r.x >> 8) * 5.9604644775390625e-08f, u2 = (float)(r.y >> 8) * 5.9604644775390625e-08f;
+    float u3 = 1.0f - (float)(r.z >> 8) * 5.9604644775390625e-08f, u4 = (float)(r.w >> 8) * 5.9604644775390625e-08f;
+    float a = sqrtf(-2.0f * logf(u1)), b = sqrtf(-2.0f * logf(u3));
+    const float tp = 6.28318530717958648f;
+    float s2, c2, s4, c4;
+    sincosf(tp * u2, &s2, &c2);
+    sincosf(tp * u4, &s4, &c4);
+    out[0] = a * c2;
+    out[1] = a * s2;
+    out[2] = b * c4;
+    out[3] = b * s4;
+  }
   // 4 standard normals via Box-Muller (float64 internally)
   __host__ __device__ __forceinline__ void normal4(uint32_t stream, double* out) const {
     u32x4 r = draw(stream);

@@ -39,6 +39,8 @@ struct StepArgs {
   int32_t* ring_pos;
   int32_t* emit_rank;         // [E]
   int32_t* block_count;       // [grid]
+  int32_t* emit_list;         // [grid*BLK] block-compacted emitter env ids (rank order)
+  const int64_t* cursor;      // store cursor, snapshotted into meta[1], meta[3], meta[4]
   int n;
   float reward_scale, cost_scale;
   int raw_log_std;               // logits second half is log_std: std = exp(clamp(., lo, hi))
@@ -55,7 +57,17 @@ struct EmitArgs {
   int64_t capacity;
   int n, F, D, A;
   float *obs, *act, *rew, *cost, *obs2, *done, *logp;
+  // fused scan + persistent emission (k_emit_fused)
+  const int32_t* block_count;
+  const int32_t* emit_list;
+  int32_t nb;                 // step-kernel blocks
+  int64_t* meta_rw;           // tick / last total written by block 0
+  int64_t* cursor;            // store cursor written by block 0
 };
+
+constexpr int EMIT_FUSED_MAX_NB = 4096;  // block prefix kept in LDS (16 KB) up to 1M envs
+
+hipError_t launch_emit_fused(const EmitArgs& a, hipStream_t st);
 
 struct GatherArgs {
   const int64_t* idx;

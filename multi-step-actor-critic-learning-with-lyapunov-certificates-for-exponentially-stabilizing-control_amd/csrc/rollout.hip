@@ -65,8 +65,8 @@ struct ResetDraw<QuadTracking> {  // QuadTracking.py:169-186
     const uint32_t v[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
     for (int i = 0; i < 6; ++i) rs[i] = uni(u01(v[i]), -0.01f, 0.01f);       // x, v
     for (int i = 0; i < 3; ++i) rs[15 + i] = uni(u01(v[6 + i]), -0.01f, 0.01f);  // Omega
-    double nz[4];
-    r.normal4(4, nz);
+    float nz[4];
+    r.normal4f(4, nz);
     double rv[3] = {nz[0] * 0.01, nz[1] * 0.01, nz[2] * 0.01};  // rotvec ~ N(0, 0.01^2)
     double th = sqrt(rv[0] * rv[0] + rv[1] * rv[1] + rv[2] * rv[2]);
     double sc = th <= 1e-3 ? 0.5 - th * th / 48.0 + th * th * th * th / 3840.0 : sin(0.5 * th) / th;
@@ -111,15 +111,15 @@ __global__ __launch_bounds__(BLK) void k_rollout(StepArgs a) {
       for (int i = 0; i < A; ++i) u[i] = a.act_in[e * A + i];
       if (a.logp_in) logp = a.logp_in[e];
     } else {
-      double nz[4];
-      rng.normal4(0, nz);
+      float nz[4];
+      rng.normal4f(0, nz);
       float lg = -0.0f, lt = -0.0f, ls = -0.0f;
 #pragma unroll
       for (int i = 0; i < A; ++i) {
         const float mu = a.logits[e * 2 * A + i];
         float sd = a.logits[e * 2 * A + A + i];
         if (a.raw_log_std) sd = expf(fminf(fmaxf(sd, a.log_std_lo), a.log_std_hi));  // clamp(.).exp()
-        const float z = mu + sd * (float)nz[i];
+        const float z = mu + sd * nz[i];
         // Normal.log_prob: -((z-mu)^2)/(2 var) - log(std) - log(sqrt(2 pi))
         const float df = z - mu;
         lg = lg + ((-(df * df) / (2.0f * (sd * sd)) - logf(sd)) - 0.918938533204672742f);
@@ -231,7 +231,14 @@ __global__ __launch_bounds__(BLK) void k_rollout(StepArgs a) {
     }
     const int rank = emit ? base + __popcll(m & ((1ull << lane) - 1ull)) : -1;
     if (live) a.emit_rank[e] = rank;
+    if (emit && a.emit_list) a.emit_list[(int64_t)blockIdx.x * BLK + rank] = (int32_t)(e - (int64_t)blockIdx.x * BLK);
     if (threadIdx.x == 0) a.block_count[blockIdx.x] = tot;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && a.cursor) {
+      // snapshot of the store cursor for the emission kernel (which rewrites the cursor)
+      a.meta[1] = a.cursor[0];
+      a.meta[3] = a.cursor[1];
+      a.meta[4] = a.cursor[2];
+    }
   }
 }
 
@@ -349,6 +356,95 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
   }
 }
 
+// --------------------------------------------------------------- fused scan + persistent emission
+// Every workgroup prefix-scans the step kernel's per-block emitter counts in LDS (nb <= 4096
+// ints), so no separate scan launch is needed; workgroup 0 then advances the store cursor
+// from the snapshot the step kernel took. Waves walk the emitted windows g = 0..total-1
+// (grid-stride), map g -> (step block, rank) by binary search over the LDS prefix and the
+// block-compacted emitter list, stage the env's n records through LDS with 16-B loads and
+// write the seven window rows contiguously.
+__global__ __launch_bounds__(256) void k_emit_fused(EmitArgs a) {
+  // dynamic LDS only (16-B aligned base): [4 waves x n x F staging floats][offs: nb ints,
+  // padded to 4][part: 256 ints][total: int64]
+  extern __shared__ float lds[];
+  const int n = a.n, F = a.F, D = a.D, A = a.A, nb = a.nb;
+  int* offs = reinterpret_cast<int*>(lds + 4 * n * F);
+  int* part = offs + ((nb + 3) & ~3);
+  int64_t& s_total = *reinterpret_cast<int64_t*>(part + 256);
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int per = (nb + 255) / 256;
+  const int lo = min(nb, t * per), hi = min(nb, lo + per);
+  int local = 0;
+  for (int i = lo; i < hi; ++i) local += a.block_count[i];
+  part[t] = local;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const int v = t >= off ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = t > 0 ? part[t - 1] : 0;
+  for (int i = lo; i < hi; ++i) {
+    offs[i] = run;
+    run += a.block_count[i];
+  }
+  if (t == 0) s_total = part[255];
+  __syncthreads();
+  const int64_t total = s_total;
+  const int64_t M = a.capacity;
+  const int64_t base = a.meta[1];
+  if (blockIdx.x == 0 && t == 0) {
+    a.meta_rw[0] += 1;  // lockstep tick (RNG counter)
+    a.meta_rw[2] = total;
+    a.cursor[0] = (base + total) % M;
+    const int64_t sz = a.meta[3] + total;
+    a.cursor[1] = sz < M ? sz : M;
+    a.cursor[2] = a.meta[4] + total;
+    a.cursor[3] = total;
+  }
+  float* buf = lds + wave * n * F;
+  const int64_t start = total > M ? total - M : 0;  // older windows are overwritten this step
+  for (int64_t g = start + (int64_t)blockIdx.x * 4 + wave; g < total; g += (int64_t)gridDim.x * 4) {
+    int bl = 0, bh = nb - 1;  // largest b with offs[b] <= g
+    while (bl < bh) {
+      const int mid = (bl + bh + 1) >> 1;
+      if ((int64_t)offs[mid] <= g) bl = mid; else bh = mid - 1;
+    }
+    const int r = (int)(g - offs[bl]);
+    const int64_t e = (int64_t)bl * BLK + a.emit_list[(int64_t)bl * BLK + r];
+    const int64_t row = (base + g) % M;
+    const float4* src = reinterpret_cast<const float4*>(a.ring + e * (int64_t)n * F);
+    float4* b4 = reinterpret_cast<float4*>(buf);
+    for (int i = lane; i < (n * F) / 4; i += 64) b4[i] = src[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int pos = a.ring_pos[e];
+    struct Field {
+      float* dst;
+      int off, width;
+    };
+    const Field fields[7] = {{a.obs, 0, D},          {a.act, D, A},          {a.obs2, D + A, D},
+                             {a.rew, 2 * D + A, 1},  {a.cost, 2 * D + A + 1, 1},
+                             {a.done, 2 * D + A + 2, 1}, {a.logp, 2 * D + A + 3, 1}};
+#pragma unroll
+    for (int f = 0; f < 7; ++f) {
+      const int W = fields[f].width, off = fields[f].off;
+      float* dst = fields[f].dst + row * (int64_t)n * W;
+      for (int idx = lane; idx < n * W; idx += 64) {
+        const int j = idx / W, d = idx - j * W;
+        int slot = pos + j;
+        slot = slot >= n ? slot - n : slot;
+        dst[idx] = buf[slot * F + off + d];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 // --------------------------------------------------------------- replay gather / indices
 __global__ __launch_bounds__(256) void k_gather(GatherArgs a) {
   const int64_t b = blockIdx.x;
@@ -447,6 +543,15 @@ hipError_t launch_emit(const EmitArgs& a, hipStream_t st) {
   const int grid = (int)((a.E + 3) / 4);
   const size_t shm = (size_t)4 * a.n * a.F * sizeof(float);
   k_emit<<<grid, 256, shm, st>>>(a);
+  return hipGetLastError();
+}
+hipError_t launch_emit_fused(const EmitArgs& a, hipStream_t st) {
+  // windows per step <= E; enough waves to cover a full step in ~4 passes, capped at 8 WGs/CU
+  int64_t want = (a.E + 15) / 16;
+  const int grid = (int)(want < 1 ? 1 : (want > 2048 ? 2048 : want));
+  const size_t shm = (size_t)4 * a.n * a.F * sizeof(float) + (size_t)((a.nb + 3) & ~3) * sizeof(int) +
+                     256 * sizeof(int) + 2 * sizeof(int64_t);
+  k_emit_fused<<<grid, 256, shm, st>>>(a);
   return hipGetLastError();
 }
 hipError_t launch_gather(const GatherArgs& a, hipStream_t st) {

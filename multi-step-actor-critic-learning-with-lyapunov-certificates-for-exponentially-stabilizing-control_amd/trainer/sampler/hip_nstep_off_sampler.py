@@ -156,6 +156,10 @@ class HipNstepOffSampler:
             if self.use_graph and self._eager_calls >= 1 and not getattr(self, "_timing", False):
                 self._graph_for(store).replay()
             else:
+                if getattr(self, "_timing", False):
+                    # park the stream on a GPU spin while the host enqueues the whole horizon,
+                    # so the per-kernel events bracket device time, not host launch latency
+                    torch.cuda._sleep(int(getattr(self, "_timing_spin_cycles", 20_000_000)))
                 self._horizon(store)
                 self._eager_calls += 1
         return DeviceWindowBatch(self, store, store.cursor[2] - before)
