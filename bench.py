@@ -138,42 +138,49 @@ def main():
         torch.cuda.synchronize()
         ph_s += tb_ - ta
         ph_u += time.perf_counter() - tb_
-    phases = {"sample_ms": round(ph_s / 2 * 1e3, 3), "replay_and_update_ms": round(ph_u / 2 * 1e3, 3)}
+    phases = {"sample_ms": round(ph_s / 2 * 1e3, 3), "replay_and_update_ms": round(ph_u / 2 * 1e3, 3),
+              "sampler_only_env_steps_per_s": round(a.envs * horizon / (ph_s / 2), 1),
+              "update_to_data_ratio": round(1.0 / (a.envs * horizon), 9)}
 
-    # ---- per-kernel durations: HIP events recorded on the launch stream around each engine
-    # kernel, over 2 more trainer steps run right after the timed region (graph replays carry
-    # no per-kernel events, so this phase launches the same kernels eagerly)
+    # ---- per-kernel durations, right after the timed region: HIP events on the launch stream
+    # around R back-to-back launches of the engine's lockstep kernels on the live pipeline state
+    # (the graph replays carry no per-kernel events). The stream is parked on a GPU spin while
+    # the host enqueues, so the events bracket device time (tools/gputime.py).
+    from tools.gputime import time_launches
     h = sampler.envs.handle()
-    ms = (ctypes.c_double * 3)()
-    launches = ctypes.c_int64()
-    N.lib().mh_env_read_timing(h, ms, ctypes.byref(launches), 1)
-    sampler.set_kernel_timing(True)
-    win1 = int(buffer.cursor[2].item())
-    for _ in range(2):
-        one_step()
-    torch.cuda.synchronize()
-    sampler.set_kernel_timing(False)
-    N.check(N.lib().mh_env_read_timing(h, ms, ctypes.byref(launches), 1), "read timing")
-    windows = int(buffer.cursor[2].item()) - win1
+    st = N.stream_of(dev)
+    with torch.no_grad():
+        logits, _raw = sampler._policy_raw()
+    reps = 20
 
-    # ---- live roofline of the engine's kernels over the timed region (HIP events)
+    def k_roll():  # k_rollout<Env> alone (no store: ring push, no emission)
+        N.lib().mh_rollout_step(h, N.ptr(logits), None, None, None, N.ptr(sampler.obs), None, None, None, st)
+
+    def k_pair():  # k_rollout<Env> + k_emit_fused into the replay store
+        N.lib().mh_rollout_step(h, N.ptr(logits), None, None, None, N.ptr(sampler.obs), ctypes.byref(buffer.ws),
+                                None, None, st)
+
+    t_step = time_launches(k_roll, reps) * 1e-3
+    win1 = int(buffer.cursor[2].item())
+    t_pair = time_launches(k_pair, reps, warm=0) * 1e-3
+    windows = (int(buffer.cursor[2].item()) - win1) / reps
+    t_emit = max(t_pair - t_step, 1e-9)
+
+    # ---- live roofline of the engine's kernels (algorithmic bytes / measured device time)
     info = sampler.envs.info
     S, XS, D_, A_, F = info.state_dim, info.xstate_dim, info.obs_dim, info.act_dim, info.record_floats
     n = sampler.n_step
     bytes_step_kernel = a.envs * ((S * 4 + XS * 8 + 4 + 2 * A_ * 4 + D_ * 4 + 8)
                                   + (S * 4 + XS * 8 + 4 + D_ * 4 + F * 4 + 8 + 4))
-    L = max(1, launches.value)
-    t_step = ms[0] / L * 1e-3
-    t_emit = ms[2] / L * 1e-3
-    bytes_emit = (windows / L) * (n * F * 4 + n * (2 * D_ + A_ + 4) * 4)
+    bytes_emit = windows * (n * F * 4 + n * (2 * D_ + A_ + 4) * 4)
     kernels = {
-        "rollout_step": {"avg_us": t_step * 1e6, "bytes": bytes_step_kernel,
-                         "GBps": bytes_step_kernel / t_step / 1e9 if t_step > 0 else 0.0},
-        "window_scan": {"avg_us": ms[1] / L * 1e3},
-        "window_emit": {"avg_us": t_emit * 1e6, "bytes": bytes_emit,
-                        "GBps": bytes_emit / t_emit / 1e9 if t_emit > 0 else 0.0},
+        "rollout_step": {"avg_us": round(t_step * 1e6, 3), "bytes": bytes_step_kernel,
+                         "GBps": round(bytes_step_kernel / t_step / 1e9, 1)},
+        "window_emit": {"avg_us": round(t_emit * 1e6, 3), "bytes": bytes_emit, "windows": windows,
+                        "GBps": round(bytes_emit / t_emit / 1e9, 1)},
+        "method": f"HIP events around {reps} back-to-back launches after a GPU spin; emit = (rollout+emit) - rollout",
     }
-    dom = "rollout_step" if ms[0] >= ms[2] else "window_emit"
+    dom = "rollout_step" if t_step >= t_emit else "window_emit"
     ach = kernels[dom]["GBps"]
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")

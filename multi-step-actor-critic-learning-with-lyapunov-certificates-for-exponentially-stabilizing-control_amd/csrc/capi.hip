@@ -55,6 +55,7 @@ struct mh_env_s {
   int32_t* steps = nullptr;
   double* tab = nullptr;
   int64_t* meta = nullptr;
+  uint32_t* ctr = nullptr;
   // n-step
   int n = 0;
   float reward_scale = 1.0f, cost_scale = 1.0f;
@@ -95,6 +96,7 @@ struct mh_env_s {
     a.steps = steps;
     a.tab = tab;
     a.meta = meta;
+    a.ctr = ctr;
     a.seed = seed;
     a.n = n;
     a.reward_scale = reward_scale;
@@ -110,7 +112,7 @@ static void free_handle(mh_env_s* h) {
   if (!h) return;
   for (hipEvent_t e : h->ev_free) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->ev_pending) (void)hipEventDestroy(e);
-  void* ptrs[] = {h->state, h->xstate, h->steps, h->tab, h->meta, h->ring, h->ring_len,
+  void* ptrs[] = {h->state, h->xstate, h->steps, h->tab, h->meta, h->ctr, h->ring, h->ring_len,
                   h->ring_pos, h->emit_rank, h->block_count, h->block_offset, h->emit_list};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -158,6 +160,8 @@ int mh_env_create(int32_t env_id, int64_t num_envs, uint64_t seed, mh_env_t* out
   if (e == hipSuccess) e = hipMalloc(&h->meta, sizeof(int64_t) * 8);
   if (e == hipSuccess) e = hipMemset(h->meta, 0, sizeof(int64_t) * 8);
   if (e == hipSuccess) e = hipMemset(h->steps, 0, sizeof(int32_t) * E);
+  if (e == hipSuccess) e = hipMalloc(&h->ctr, sizeof(uint32_t) * E);
+  if (e == hipSuccess) e = hipMemset(h->ctr, 0, sizeof(uint32_t) * E);
   if (e == hipSuccess) e = hipMemset(h->state, 0, sizeof(float) * E * h->info.state_dim);
   if (e == hipSuccess && env_id == MH_ENV_QUADTRACKING) {
     const int rows = mh::MAX_STEP + 1;
@@ -219,7 +223,6 @@ int mh_env_reset(mh_env_t h, const float* reset_states, float* obs, void* stream
   a.ring_len = h->ring_len;
   a.ring_pos = h->ring_pos;
   MH_HIP(mh::launch_reset(h->env_id, a, st));
-  MH_HIP(mh::launch_finalize(h->block_count, 0, h->block_offset, h->meta, nullptr, 1, st));
   return MH_OK;
 }
 
@@ -240,7 +243,6 @@ int mh_env_step(mh_env_t h, const float* act, const float* reset_states, float* 
   a.reward_scale = 1.0f;
   a.cost_scale = 1.0f;
   MH_HIP(mh::launch_rollout(h->env_id, a, st));
-  MH_HIP(mh::launch_finalize(h->block_count, 0, h->block_offset, h->meta, nullptr, 1, st));
   return MH_OK;
 }
 
@@ -303,7 +305,7 @@ int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const 
   if (ev[0]) MH_HIP(hipEventRecord(ev[0], st));
   MH_HIP(mh::launch_rollout(h->env_id, a, st));
   if (ev[1]) MH_HIP(hipEventRecord(ev[1], st));
-  if (!fused)
+  if (store && !fused)
     MH_HIP(mh::launch_finalize(h->block_count, store ? h->grid() : 0, h->block_offset, h->meta,
                                store ? store->cursor : nullptr, store ? store->capacity : 1, st));
   if (ev[2]) MH_HIP(hipEventRecord(ev[2], st));

@@ -1,10 +1,13 @@
 // msacl_kernels.hip — fused MSACL target / certificate math (RL/algorithm/msacl.py).
 //
 // The replay batch is [B][n] (B = 256, n = 20 at the reference config: 5,120 elements, 20 KB
-// per tensor). Each op below replaces a chain of 8-20 tiny PyTorch launches with ONE
-// single-workgroup kernel: one wavefront per window row keeps the n-step scan (cumprod,
-// lambda-weighted sums) in registers/LDS, and the batch-global means are reduced in float64
-// inside the workgroup in a fixed order, so results are bitwise reproducible run to run.
+// per tensor). Each op below replaces a chain of 8-20 tiny PyTorch launches with ONE kernel:
+// one wavefront per window row keeps the n-step scan (cumprod, lambda-weighted sums) in
+// registers (q_target / lyapunov: 4 rows per workgroup, B/4 workgroups; the small advantage
+// ops: one workgroup), and the batch-global means are reduced in float64 in a fixed order, so
+// results are bitwise reproducible run to run. q_target and lyapunov keep their cross-workgroup
+// partials in a library-owned per-device scratch: calls of one of them on one device must be
+// stream-ordered (they are: the MSACL update issues them on one stream).
 // Each kernel also emits the analytic gradient w.r.t. its network-produced inputs, which the
 // Python layer feeds to autograd (custom autograd.Function), so the MLP backward stays PyTorch.
 #include <hip/hip_runtime.h>
@@ -37,59 +40,156 @@ __device__ double block_sum(double v, double* sh) {
   return r;
 }
 
+// Row kernels: one wavefront per window row b (lanes own the n steps), RPB rows per workgroup,
+// ceil(B / RPB) workgroups. Batch-global sums go through per-workgroup float64 partials; the
+// workgroup that finishes last adds them in workgroup order (deterministic) and resets the
+// arrival counter, so no extra launch and no memset are needed.
+constexpr int RPB = 4;             // rows (wavefronts) per workgroup
+constexpr int RTPB = RPB * 64;
+
+struct RowScratch {
+  double* part = nullptr;          // [cap][2] per-workgroup partial sums
+  unsigned int* arrive = nullptr;  // arrival counter (0 between launches)
+  int64_t cap = 0;
+};
+
+// Library-owned per-device scratch, grown outside graph capture (the first, eager call).
+hipError_t row_scratch(int slot, int64_t blocks, RowScratch** out) {
+  static RowScratch per_dev[2][64];  // [kernel slot][device]: each kernel owns its counter
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  RowScratch& r = per_dev[slot][dev];
+  if (r.cap < blocks) {
+    if (r.part) (void)hipFree(r.part);
+    if (r.arrive) (void)hipFree(r.arrive);
+    r.part = nullptr;
+    r.arrive = nullptr;
+    r.cap = 0;
+    const int64_t cap = blocks < 4096 ? 4096 : blocks;
+    e = hipMalloc(&r.part, sizeof(double) * 2 * cap);
+    if (e == hipSuccess) e = hipMalloc(&r.arrive, sizeof(unsigned int));
+    if (e == hipSuccess) e = hipMemset(r.arrive, 0, sizeof(unsigned int));
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) return e;
+    r.cap = cap;
+  }
+  *out = &r;
+  return hipSuccess;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Sum (a, b) over the workgroup, publish the partials, and let the last workgroup total them.
+// Returns true in thread 0 of the last workgroup with the batch sums in *ta, *tb.
+__device__ bool rows_reduce(double a, double b, double* part, unsigned int* arrive, double* ta, double* tb) {
+  __shared__ double sa[RPB], sb[RPB];
+  __shared__ bool last;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  a = wave_sum(a);
+  b = wave_sum(b);
+  if (lane == 0) {
+    sa[wave] = a;
+    sb[wave] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double x = 0.0, y = 0.0;
+    for (int w = 0; w < RPB; ++w) {
+      x += sa[w];
+      y += sb[w];
+    }
+    part[2 * blockIdx.x] = x;
+    part[2 * blockIdx.x + 1] = y;
+    __threadfence();
+    last = atomicAdd(arrive, 1u) == gridDim.x - 1u;
+  }
+  __syncthreads();
+  if (!last) return false;
+  __threadfence();
+  // last workgroup: fixed-order total (lane-strided partials, then wave/LDS tree)
+  const volatile double* vp = part;
+  double x = 0.0, y = 0.0;
+  for (unsigned int g = threadIdx.x; g < gridDim.x; g += RTPB) {
+    x += vp[2 * g];
+    y += vp[2 * g + 1];
+  }
+  x = wave_sum(x);
+  y = wave_sum(y);
+  __syncthreads();
+  if (lane == 0) {
+    sa[wave] = x;
+    sb[wave] = y;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return false;
+  double X = 0.0, Y = 0.0;
+  for (int w = 0; w < RPB; ++w) {
+    X += sa[w];
+    Y += sb[w];
+  }
+  *ta = X;
+  *tb = Y;
+  *arrive = 0u;
+  return true;
+}
+
 // ------------------------------------------------------------------ Q backup (msacl.py:242-257)
-__global__ __launch_bounds__(TPB) void k_q_target(const float* q1, const float* q2, const float* q1t,
-                                                  const float* q2t, const float* nlogp, const float* rew,
-                                                  const float* done, const float* log_alpha, const float* weight,
-                                                  float gamma, int B, int n, float* backup, float* dq1,
-                                                  float* dq2, float* loss_out, float* abs_td) {
-  __shared__ double sh[TPB];
+__global__ __launch_bounds__(RTPB) void k_q_target(const float* q1, const float* q2, const float* q1t,
+                                                   const float* q2t, const float* nlogp, const float* rew,
+                                                   const float* done, const float* log_alpha, const float* weight,
+                                                   float gamma, int B, int n, float* backup, float* dq1,
+                                                   float* dq2, float* loss_out, float* abs_td, double* part,
+                                                   unsigned int* arrive) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * RPB + (threadIdx.x >> 6);
   const float alpha = expf(*log_alpha);
   const int64_t N = (int64_t)B * n;
   const float inv = (float)(1.0 / (double)N);
-  double acc1 = 0.0, acc2 = 0.0;
-  for (int64_t i = threadIdx.x; i < N; i += TPB) {
-    const float nq = fminf(q1t[i], q2t[i]);
-    const float bk = rew[i] + ((1.0f - done[i]) * gamma) * (nq - alpha * nlogp[i]);
-    backup[i] = bk;
-    const float e1 = q1[i] - bk, e2 = q2[i] - bk;
-    const float wb = weight ? weight[i / n] : 1.0f;
-    acc1 += (double)wb * (double)e1 * (double)e1;
-    acc2 += (double)wb * (double)e2 * (double)e2;
-    if (dq1) dq1[i] = 2.0f * e1 * inv * wb;
-    if (dq2) dq2[i] = 2.0f * e2 * inv * wb;
-  }
-  const double s1 = block_sum(acc1, sh), s2 = block_sum(acc2, sh);
-  if (threadIdx.x == 0 && loss_out) loss_out[0] = (float)(s1 / (double)N) + (float)(s2 / (double)N);
-  if (abs_td) {
-    __syncthreads();
-    for (int b = threadIdx.x; b < B; b += TPB) {
-      double a = 0.0;
-      for (int k = 0; k < n; ++k) {
-        const int64_t i = (int64_t)b * n + k;
-        a += 0.5 * (fabs((double)q1[i] - (double)backup[i]) + fabs((double)q2[i] - (double)backup[i]));
-      }
-      abs_td[b] = (float)(a / n);
+  double acc1 = 0.0, acc2 = 0.0, atd = 0.0;
+  if (b < B) {
+    const float wb = weight ? weight[b] : 1.0f;
+    for (int k = lane; k < n; k += 64) {
+      const int64_t i = (int64_t)b * n + k;
+      const float nq = fminf(q1t[i], q2t[i]);
+      const float bk = rew[i] + ((1.0f - done[i]) * gamma) * (nq - alpha * nlogp[i]);
+      backup[i] = bk;
+      const float e1 = q1[i] - bk, e2 = q2[i] - bk;
+      acc1 += (double)wb * (double)e1 * (double)e1;
+      acc2 += (double)wb * (double)e2 * (double)e2;
+      if (dq1) dq1[i] = 2.0f * e1 * inv * wb;
+      if (dq2) dq2[i] = 2.0f * e2 * inv * wb;
+      atd += 0.5 * (fabs((double)q1[i] - (double)bk) + fabs((double)q2[i] - (double)bk));
     }
+    atd = wave_sum(atd);
+    if (abs_td && lane == 0) abs_td[b] = (float)(atd / n);
   }
+  double s1, s2;
+  if (rows_reduce(acc1, acc2, part, arrive, &s1, &s2) && loss_out)
+    loss_out[0] = (float)(s1 / (double)N) + (float)(s2 / (double)N);
 }
 
 // --------------------------------------------------- Lyapunov certificate (msacl.py:279-332)
-// One wavefront per window row b: lanes own the n steps; cumprod of the clipped IS ratio is a
-// wave-level inclusive product scan (n <= 64 per pass, chained across passes).
-__global__ __launch_bounds__(TPB) void k_lyapunov(const float* logp, const float* old_logp, const float* V,
-                                                  const float* V2, const float* obs, const float* obs2,
-                                                  const float* c, const float* w, const float* s, float alpha1,
-                                                  float alpha2, float pos_scale, float diff_scale, int B, int n,
-                                                  int D, float* is_clip, float* esl, float* lya_diff,
-                                                  float* loss_out, float* dV, float* dV2) {
-  __shared__ double sh[TPB];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = TPB / 64;
+// cumprod of the clipped IS ratio is a wave-level inclusive product scan (n <= 64 per pass,
+// chained across passes).
+__global__ __launch_bounds__(RTPB) void k_lyapunov(const float* logp, const float* old_logp, const float* V,
+                                                   const float* V2, const float* obs, const float* obs2,
+                                                   const float* c, const float* w, const float* s, float alpha1,
+                                                   float alpha2, float pos_scale, float diff_scale, int B, int n,
+                                                   int D, float* is_clip, float* esl, float* lya_diff,
+                                                   float* loss_out, float* dV, float* dV2, double* part,
+                                                   unsigned int* arrive) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * RPB + (threadIdx.x >> 6);
   const int64_t N = (int64_t)B * n;
   const float invN = (float)(1.0 / (double)N);
   const float invB = (float)(1.0 / (double)B);
   double bound_acc = 0.0, diff_acc = 0.0;
-  for (int b = wave; b < B; b += nw) {
+  if (b < B) {
     // ||obs[b, 0, :]||
     float so = 0.0f;
     for (int d = 0; d < D; ++d) {
@@ -154,12 +254,11 @@ __global__ __launch_bounds__(TPB) void k_lyapunov(const float* logp, const float
     if (lane == 0) {
       lya_diff[b] = rowsum;
       dV[(int64_t)b * n] = dV[(int64_t)b * n] + dV0_acc;
-      diff_acc += (double)rowsum;
+      diff_acc = (double)rowsum;
     }
   }
-  const double sb = block_sum(bound_acc, sh);
-  const double sd = block_sum(diff_acc, sh);
-  if (threadIdx.x == 0 && loss_out)
+  double sb, sd;
+  if (rows_reduce(bound_acc, diff_acc, part, arrive, &sb, &sd) && loss_out)
     loss_out[0] = (float)(sb / (double)N) * pos_scale + (float)(sd / (double)B) * diff_scale;
 }
 
@@ -234,8 +333,12 @@ int mh_msacl_q_target(const float* q1, const float* q2, const float* q1t, const 
                       float* dq2, float* loss_out, float* abs_td, void* stream) {
   if (!q1 || !q2 || !q1t || !q2t || !next_logp || !rew || !done || !log_alpha || !backup || B <= 0 || n <= 0)
     return MH_EINVAL;
-  k_q_target<<<1, TPB, 0, (hipStream_t)stream>>>(q1, q2, q1t, q2t, next_logp, rew, done, log_alpha, weight, gamma,
-                                                 B, n, backup, dq1, dq2, loss_out, abs_td);
+  const int64_t nb = ((int64_t)B + RPB - 1) / RPB;
+  RowScratch* rs = nullptr;
+  if (row_scratch(0, nb, &rs) != hipSuccess) return MH_EHIP;
+  k_q_target<<<(unsigned)nb, RTPB, 0, (hipStream_t)stream>>>(q1, q2, q1t, q2t, next_logp, rew, done, log_alpha,
+                                                             weight, gamma, B, n, backup, dq1, dq2, loss_out, abs_td,
+                                                             rs->part, rs->arrive);
   MH_CHECK_LAUNCH("q_target");
   return MH_OK;
 }
@@ -248,9 +351,13 @@ int mh_msacl_lyapunov(const float* logp, const float* old_logp, const float* lya
   if (!logp || !old_logp || !lya_obs || !lya_obs2 || !obs || !obs2 || !c || !w || !s || !is_clip || !esl ||
       !lya_diff || !d_lya_obs || !d_lya_obs2 || B <= 0 || n <= 0 || D <= 0)
     return MH_EINVAL;
-  k_lyapunov<<<1, TPB, 0, (hipStream_t)stream>>>(logp, old_logp, lya_obs, lya_obs2, obs, obs2, c, w, s, alpha1,
-                                                 alpha2, pos_scale, diff_scale, B, n, D, is_clip, esl, lya_diff,
-                                                 loss_out, d_lya_obs, d_lya_obs2);
+  const int64_t nb = ((int64_t)B + RPB - 1) / RPB;
+  RowScratch* rs = nullptr;
+  if (row_scratch(1, nb, &rs) != hipSuccess) return MH_EHIP;
+  k_lyapunov<<<(unsigned)nb, RTPB, 0, (hipStream_t)stream>>>(logp, old_logp, lya_obs, lya_obs2, obs, obs2, c, w, s,
+                                                             alpha1, alpha2, pos_scale, diff_scale, B, n, D, is_clip,
+                                                             esl, lya_diff, loss_out, d_lya_obs, d_lya_obs2, rs->part,
+                                                             rs->arrive);
   MH_CHECK_LAUNCH("lyapunov");
   return MH_OK;
 }

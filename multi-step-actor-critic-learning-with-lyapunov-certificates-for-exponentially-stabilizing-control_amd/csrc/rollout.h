@@ -19,7 +19,8 @@ struct StepArgs {
   double* xstate;    // [XS][E]
   int32_t* steps;    // [E]
   const double* tab; // QuadTracking desired-trajectory table (device) or null
-  int64_t* meta;     // device int64[8]: tick, emit base row, last emitted total
+  int64_t* meta;     // device int64[8]: emit base row, last emitted total, cursor snapshots
+  uint32_t* ctr;     // [E] per-env Philox counter (lockstep steps + resets drawn so far)
   uint64_t seed;
   // io (AoS)
   float* obs;                 // [E][D] in: pre-step obs (ring), out: next obs
@@ -47,6 +48,9 @@ struct StepArgs {
   float log_std_lo, log_std_hi;  // StochaPolicy min/max_log_std (mlp.py:125-136)
 };
 
+// meta[] slots (device int64[8])
+constexpr int META_BASE = 1, META_TOTAL = 2, META_SIZE = 3, META_GTOTAL = 4;
+
 struct EmitArgs {
   int64_t E;
   const float* ring;
@@ -61,7 +65,7 @@ struct EmitArgs {
   const int32_t* block_count;
   const int32_t* emit_list;
   int32_t nb;                 // step-kernel blocks
-  int64_t* meta_rw;           // tick / last total written by block 0
+  int64_t* meta_rw;           // last emitted total, written by block 0
   int64_t* cursor;            // store cursor written by block 0
 };
 

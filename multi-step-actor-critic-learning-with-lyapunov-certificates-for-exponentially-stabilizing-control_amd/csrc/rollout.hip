@@ -95,8 +95,8 @@ __global__ __launch_bounds__(BLK) void k_rollout(StepArgs a) {
 #pragma unroll
     for (int i = 0; i < XS; ++i) xs[i] = a.xstate[(int64_t)i * E + e];
     const int k = a.steps[e];
-    const uint64_t tick = a.meta[0];
-    const Rng rng = make_rng(a.seed, (uint64_t)e, tick);
+    const uint32_t ctr = a.ctr[e];  // per-env counter: graph replays need no host RNG state
+    const Rng rng = make_rng(a.seed, (uint64_t)e, ctr);
 
     float obs0[D];
     if (a.ring) {
@@ -176,6 +176,7 @@ __global__ __launch_bounds__(BLK) void k_rollout(StepArgs a) {
 #pragma unroll
     for (int i = 0; i < XS; ++i) a.xstate[(int64_t)i * E + e] = xs[i];
     a.steps[e] = k1;
+    a.ctr[e] = ctr + 1u;
     if (a.obs) {
 #pragma unroll
       for (int i = 0; i < D; ++i) a.obs[e * D + i] = obsn[i];
@@ -230,32 +231,35 @@ __global__ __launch_bounds__(BLK) void k_rollout(StepArgs a) {
       tot += wcnt[w];
     }
     const int rank = emit ? base + __popcll(m & ((1ull << lane) - 1ull)) : -1;
-    if (live) a.emit_rank[e] = rank;
-    if (emit && a.emit_list) a.emit_list[(int64_t)blockIdx.x * BLK + rank] = (int32_t)(e - (int64_t)blockIdx.x * BLK);
+    if (a.emit_list) {
+      if (emit) a.emit_list[(int64_t)blockIdx.x * BLK + rank] = (int32_t)(e - (int64_t)blockIdx.x * BLK);
+    } else if (live) {
+      a.emit_rank[e] = rank;
+    }
     if (threadIdx.x == 0) a.block_count[blockIdx.x] = tot;
     if (blockIdx.x == 0 && threadIdx.x == 0 && a.cursor) {
       // snapshot of the store cursor for the emission kernel (which rewrites the cursor)
-      a.meta[1] = a.cursor[0];
-      a.meta[3] = a.cursor[1];
-      a.meta[4] = a.cursor[2];
+      a.meta[META_BASE] = a.cursor[0];
+      a.meta[META_SIZE] = a.cursor[1];
+      a.meta[META_GTOTAL] = a.cursor[2];
     }
   }
 }
 
 // --------------------------------------------------------------- reset kernel
 template <class Env>
-__global__ __launch_bounds__(BLK) void k_reset(StepArgs a) {
+__device__ __forceinline__ void reset_one(const StepArgs& a, int64_t e) {
   constexpr int D = Env::D, S = Env::S, XS = Env::XS, RS = Env::RS;
   const int64_t E = a.E;
-  const int64_t e = (int64_t)blockIdx.x * BLK + threadIdx.x;
-  if (e >= E) return;
   float rs[RS], s[S], o[D];
   double xs[XS > 0 ? XS : 1];
   if (a.reset_in) {
 #pragma unroll
     for (int i = 0; i < RS; ++i) rs[i] = a.reset_in[e * RS + i];
   } else {
-    ResetDraw<Env>::draw(make_rng(a.seed, (uint64_t)e, a.meta[0]), rs);
+    const uint32_t ctr = a.ctr[e];
+    ResetDraw<Env>::draw(make_rng(a.seed, (uint64_t)e, ctr), rs);
+    a.ctr[e] = ctr + 1u;
   }
   Env::reset_from(rs, s, xs, a.tab, o);
 #pragma unroll
@@ -271,6 +275,12 @@ __global__ __launch_bounds__(BLK) void k_reset(StepArgs a) {
     a.ring_len[e] = 0;
     a.ring_pos[e] = 0;
   }
+}
+
+template <class Env>
+__global__ __launch_bounds__(BLK) void k_reset(StepArgs a) {
+  const int64_t e = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  if (e < a.E) reset_one<Env>(a, e);
 }
 
 // --------------------------------------------------------------- finalize (scan + cursor)
@@ -298,7 +308,6 @@ __global__ __launch_bounds__(1024) void k_finalize(const int32_t* block_count, i
   }
   if (t == 0) {
     const int64_t total = part[1023];
-    meta[0] += 1;  // lockstep tick (RNG counter)
     meta[2] = total;
     if (cursor) {
       const int64_t base = cursor[0];
@@ -395,7 +404,6 @@ __global__ __launch_bounds__(256) void k_emit_fused(EmitArgs a) {
   const int64_t M = a.capacity;
   const int64_t base = a.meta[1];
   if (blockIdx.x == 0 && t == 0) {
-    a.meta_rw[0] += 1;  // lockstep tick (RNG counter)
     a.meta_rw[2] = total;
     a.cursor[0] = (base + total) % M;
     const int64_t sz = a.meta[3] + total;
