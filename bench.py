@@ -183,11 +183,15 @@ def main():
     dom = "rollout_step" if t_step >= t_emit else "window_emit"
     ach = kernels[dom]["GBps"]
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
+    # HBM bytes per launch from the committed rocprofv3 PMC passes of this same command
+    # (tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)
+    import glob
+    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if pmcs and a.env == "QuadTracking" and a.envs == 65536:
         try:
-            traffic = json.load(open(pmc)).get(dom, {}).get("bytes_per_launch")
-        except Exception:
+            traffic = json.load(open(pmcs[-1])).get(dom, {}).get("bytes_per_launch")
+            traffic = None if traffic is None else round(float(traffic), 1)
+        except (OSError, ValueError):
             traffic = None
     roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic}

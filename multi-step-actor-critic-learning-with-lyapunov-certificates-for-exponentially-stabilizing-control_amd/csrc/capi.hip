@@ -291,10 +291,8 @@ int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const 
   a.ring_pos = h->ring_pos;
   a.emit_rank = h->emit_rank;
   a.block_count = h->block_count;
-  // fused scan+emission when the block prefix and the staging tiles fit in LDS
-  const size_t fused_lds = (size_t)4 * h->n * h->info.record_floats * sizeof(float) +
-                           (size_t)(h->grid() + 4 + 256) * sizeof(int) + 16;
-  const bool fused = store && h->grid() <= mh::EMIT_FUSED_MAX_NB && fused_lds <= 64 * 1024;
+  // fused scan+emission when the per-block emitter prefix fits in LDS (E <= 1M envs)
+  const bool fused = store && h->grid() <= mh::EMIT_FUSED_MAX_NB;
   if (fused) {
     a.emit_list = h->emit_list;
     a.cursor = store->cursor;
@@ -333,7 +331,7 @@ int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const 
     ea.emit_list = h->emit_list;
     ea.nb = h->grid();
     ea.cursor = store->cursor;
-    MH_HIP(mh::launch_emit_fused(ea, st));
+    MH_HIP(mh::launch_emit_fused(h->env_id, ea, st));
   } else if (store) {
     mh::EmitArgs ea;
     ea.E = h->E;

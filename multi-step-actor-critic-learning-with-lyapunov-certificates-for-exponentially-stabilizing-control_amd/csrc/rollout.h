@@ -71,7 +71,7 @@ struct EmitArgs {
 
 constexpr int EMIT_FUSED_MAX_NB = 4096;  // block prefix kept in LDS (16 KB) up to 1M envs
 
-hipError_t launch_emit_fused(const EmitArgs& a, hipStream_t st);
+hipError_t launch_emit_fused(int env_id, const EmitArgs& a, hipStream_t st);
 
 struct GatherArgs {
   const int64_t* idx;

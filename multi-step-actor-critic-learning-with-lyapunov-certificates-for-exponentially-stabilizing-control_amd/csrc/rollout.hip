@@ -365,55 +365,79 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
   }
 }
 
-// --------------------------------------------------------------- fused scan + persistent emission
-// Every workgroup prefix-scans the step kernel's per-block emitter counts in LDS (nb <= 4096
-// ints), so no separate scan launch is needed; workgroup 0 then advances the store cursor
-// from the snapshot the step kernel took. Waves walk the emitted windows g = 0..total-1
-// (grid-stride), map g -> (step block, rank) by binary search over the LDS prefix and the
-// block-compacted emitter list, stage the env's n records through LDS with 16-B loads and
-// write the seven window rows contiguously.
+// Fused scan + emission, one thread per (window, slot) record. Every workgroup re-derives the
+// env-order window offsets from the step kernel's per-block emitter counts (nb <= 4096 ints in
+// LDS, wave-shuffle scan), so no separate scan launch is needed; workgroup 0 advances the store
+// cursor. Thread q handles window g = q / n, slot j = q % n: it locates the emitting env with a
+// binary search over the block offsets, reads ring record (pos + j) mod n of that env (F floats,
+// 16-B loads; the n threads of a window read one contiguous ring block) and scatters the record's
+// fields to row (base + g) mod M of the seven store arrays, where consecutive slots are adjacent
+// (vector stores of D / A floats). All threads are independent: no per-window serial chain.
+template <int W>
+__device__ __forceinline__ void store_vec(float* dst, const float* v) {
+  if constexpr (W % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < W; i += 4) *reinterpret_cast<float4*>(dst + i) = make_float4(v[i], v[i + 1], v[i + 2], v[i + 3]);
+  } else if constexpr (W % 2 == 0) {
+#pragma unroll
+    for (int i = 0; i < W; i += 2) *reinterpret_cast<float2*>(dst + i) = make_float2(v[i], v[i + 1]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < W; ++i) dst[i] = v[i];
+  }
+}
+
+template <int D, int A>
 __global__ __launch_bounds__(256) void k_emit_fused(EmitArgs a) {
-  // dynamic LDS only (16-B aligned base): [4 waves x n x F staging floats][offs: nb ints,
-  // padded to 4][part: 256 ints][total: int64]
-  extern __shared__ float lds[];
-  const int n = a.n, F = a.F, D = a.D, A = a.A, nb = a.nb;
-  int* offs = reinterpret_cast<int*>(lds + 4 * n * F);
-  int* part = offs + ((nb + 3) & ~3);
-  int64_t& s_total = *reinterpret_cast<int64_t*>(part + 256);
+  constexpr int F = rec_floats(D, A);
+  extern __shared__ int offs[];  // [nb] block offsets, then [4] wave totals, then int64 total
+  const int n = a.n, nb = a.nb;
+  int* wtot = offs + ((nb + 3) & ~3);
+  int64_t* s_total = reinterpret_cast<int64_t*>(wtot + 4);
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  // ---- exclusive scan of block_count: 256 contiguous chunks, wave shuffle scan + wave totals
   const int per = (nb + 255) / 256;
   const int lo = min(nb, t * per), hi = min(nb, lo + per);
   int local = 0;
   for (int i = lo; i < hi; ++i) local += a.block_count[i];
-  part[t] = local;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {
-    const int v = t >= off ? part[t - off] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
+  int incl = local;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int v = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += v;
   }
-  int run = t > 0 ? part[t - 1] : 0;
+  if (lane == 63) wtot[wave] = incl;
+  __syncthreads();
+  int wbase = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    wbase += (w < wave) ? wtot[w] : 0;
+    all += wtot[w];
+  }
+  int run = wbase + incl - local;
   for (int i = lo; i < hi; ++i) {
     offs[i] = run;
     run += a.block_count[i];
   }
-  if (t == 0) s_total = part[255];
+  if (t == 0) *s_total = all;
   __syncthreads();
-  const int64_t total = s_total;
+  const int64_t total = *s_total;
   const int64_t M = a.capacity;
-  const int64_t base = a.meta[1];
+  const int64_t base = a.meta[META_BASE];
   if (blockIdx.x == 0 && t == 0) {
-    a.meta_rw[2] = total;
+    a.meta_rw[META_TOTAL] = total;
     a.cursor[0] = (base + total) % M;
-    const int64_t sz = a.meta[3] + total;
+    const int64_t sz = a.meta[META_SIZE] + total;
     a.cursor[1] = sz < M ? sz : M;
-    a.cursor[2] = a.meta[4] + total;
+    a.cursor[2] = a.meta[META_GTOTAL] + total;
     a.cursor[3] = total;
   }
-  float* buf = lds + wave * n * F;
   const int64_t start = total > M ? total - M : 0;  // older windows are overwritten this step
-  for (int64_t g = start + (int64_t)blockIdx.x * 4 + wave; g < total; g += (int64_t)gridDim.x * 4) {
+  const int64_t nrec = (total - start) * n;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + t; q < nrec; q += (int64_t)gridDim.x * 256) {
+    const int64_t gl = q / n;
+    const int j = (int)(q - gl * n);
+    const int64_t g = start + gl;
     int bl = 0, bh = nb - 1;  // largest b with offs[b] <= g
     while (bl < bh) {
       const int mid = (bl + bh + 1) >> 1;
@@ -421,35 +445,29 @@ __global__ __launch_bounds__(256) void k_emit_fused(EmitArgs a) {
     }
     const int r = (int)(g - offs[bl]);
     const int64_t e = (int64_t)bl * BLK + a.emit_list[(int64_t)bl * BLK + r];
-    const int64_t row = (base + g) % M;
-    const float4* src = reinterpret_cast<const float4*>(a.ring + e * (int64_t)n * F);
-    float4* b4 = reinterpret_cast<float4*>(buf);
-    for (int i = lane; i < (n * F) / 4; i += 64) b4[i] = src[i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int pos = a.ring_pos[e];
-    struct Field {
-      float* dst;
-      int off, width;
-    };
-    const Field fields[7] = {{a.obs, 0, D},          {a.act, D, A},          {a.obs2, D + A, D},
-                             {a.rew, 2 * D + A, 1},  {a.cost, 2 * D + A + 1, 1},
-                             {a.done, 2 * D + A + 2, 1}, {a.logp, 2 * D + A + 3, 1}};
+    int slot = a.ring_pos[e] + j;
+    slot = slot >= n ? slot - n : slot;
+    float rec[F];
+    const float4* src = reinterpret_cast<const float4*>(a.ring + (e * n + slot) * (int64_t)F);
 #pragma unroll
-    for (int f = 0; f < 7; ++f) {
-      const int W = fields[f].width, off = fields[f].off;
-      float* dst = fields[f].dst + row * (int64_t)n * W;
-      for (int idx = lane; idx < n * W; idx += 64) {
-        const int j = idx / W, d = idx - j * W;
-        int slot = pos + j;
-        slot = slot >= n ? slot - n : slot;
-        dst[idx] = buf[slot * F + off + d];
-      }
+    for (int i = 0; i < F / 4; ++i) {
+      const float4 v = src[i];
+      rec[4 * i] = v.x;
+      rec[4 * i + 1] = v.y;
+      rec[4 * i + 2] = v.z;
+      rec[4 * i + 3] = v.w;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int64_t row = base + g;
+    if (row >= M) row -= M;
+    if (row >= M) row %= M;
+    const int64_t o = row * n + j;
+    store_vec<D>(a.obs + o * D, rec);
+    store_vec<A>(a.act + o * A, rec + D);
+    store_vec<D>(a.obs2 + o * D, rec + D + A);
+    a.rew[o] = rec[2 * D + A];
+    a.cost[o] = rec[2 * D + A + 1];
+    a.done[o] = rec[2 * D + A + 2];
+    a.logp[o] = rec[2 * D + A + 3];
   }
 }
 
@@ -553,14 +571,25 @@ hipError_t launch_emit(const EmitArgs& a, hipStream_t st) {
   k_emit<<<grid, 256, shm, st>>>(a);
   return hipGetLastError();
 }
-hipError_t launch_emit_fused(const EmitArgs& a, hipStream_t st) {
-  // windows per step <= E; enough waves to cover a full step in ~4 passes, capped at 8 WGs/CU
-  int64_t want = (a.E + 15) / 16;
+template <int D, int A>
+hipError_t launch_emit_fused_t(const EmitArgs& a, hipStream_t st) {
+  // one thread per record of a full step (every env emitting); grid-stride beyond 2048 WGs
+  const int64_t want = (a.E * a.n + 255) / 256;
   const int grid = (int)(want < 1 ? 1 : (want > 2048 ? 2048 : want));
-  const size_t shm = (size_t)4 * a.n * a.F * sizeof(float) + (size_t)((a.nb + 3) & ~3) * sizeof(int) +
-                     256 * sizeof(int) + 2 * sizeof(int64_t);
-  k_emit_fused<<<grid, 256, shm, st>>>(a);
+  const size_t shm = (size_t)((a.nb + 3) & ~3) * sizeof(int) + 4 * sizeof(int) + sizeof(int64_t);
+  k_emit_fused<D, A><<<grid, 256, shm, st>>>(a);
   return hipGetLastError();
+}
+hipError_t launch_emit_fused(int env_id, const EmitArgs& a, hipStream_t st) {
+  switch (env_id) {
+    case ENV_VANDERPOL: return launch_emit_fused_t<VanderPol::D, VanderPol::A>(a, st);
+    case ENV_PENDULUM: return launch_emit_fused_t<Pendulum::D, Pendulum::A>(a, st);
+    case ENV_DUCTEDFAN: return launch_emit_fused_t<DuctedFan::D, DuctedFan::A>(a, st);
+    case ENV_TWOLINK: return launch_emit_fused_t<TwoLink::D, TwoLink::A>(a, st);
+    case ENV_SINGLETRACKCAR: return launch_emit_fused_t<SingleTrackCar::D, SingleTrackCar::A>(a, st);
+    case ENV_QUADTRACKING: return launch_emit_fused_t<QuadTracking::D, QuadTracking::A>(a, st);
+  }
+  return hipErrorInvalidValue;
 }
 hipError_t launch_gather(const GatherArgs& a, hipStream_t st) {
   if (a.batch <= 0) return hipSuccess;
