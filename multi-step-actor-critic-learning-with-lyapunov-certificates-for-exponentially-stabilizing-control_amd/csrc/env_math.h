@@ -8,8 +8,8 @@
 //   * float32 arrays combined with float64 arrays promote to float64, and an in-place
 //     `f32_array += f64_array` is evaluated in float64 and rounded once.
 // No FMA contraction (see #pragma below) so every op rounds where NumPy rounds.
-// float32 transcendentals are evaluated in float64 and rounded once (correctly rounded in
-// practice; NumPy's SIMD float32 sin/cos are within 1.5 ulp of this).
+// float32 transcendentals use the f32 OCML/libm functions (NumPy's SIMD float32 sin/cos are
+// not correctly rounded either; both are within ~1.5 ulp), float64 ones the f64 functions.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -34,9 +34,11 @@ enum EnvId : int {
 constexpr int MAX_STEP = 1000;  // every env: truncated = current_step >= 1000
 
 // ---------------------------------------------------------------- f32 helpers
-MH_HD float sin32(float x) { return (float)sin((double)x); }
-MH_HD float cos32(float x) { return (float)cos((double)x); }
-MH_HD float tan32(float x) { return (float)tan((double)x); }
+// NumPy float32 sin/cos/tan (SIMD, not correctly rounded either): the f32 libm/OCML versions
+// stay within 1-2 ulp, far inside the 1e-5 parity tolerance, at a fraction of the f64 cost.
+MH_HD float sin32(float x) { return sinf(x); }
+MH_HD float cos32(float x) { return cosf(x); }
+MH_HD float tan32(float x) { return tanf(x); }
 
 // `s ** 2` on a NumPy float32 SCALAR calls the C library's powf (glibc 2.35 e_powf.c, the
 // ARM optimized-routines algorithm: 16-entry log2 table + degree-5 poly, 32-entry exp2 table +
@@ -63,7 +65,8 @@ MH_HD uint32_t mh_asuint(float f) {
   c.f = f;
   return c.u;
 }
-MH_HD float powf2(float x) {
+// glibc's double-precision result before its final rounding to float.
+MH_HD double powf2_core(float x) {
   constexpr double LOG_INVC[16] = {
       0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010bp+0,  0x1.3c995b0b80385p+0,
       0x1.30d190c8864a5p+0, 0x1.25e227b0b8eap+0,  0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0,
@@ -87,8 +90,8 @@ MH_HD float powf2(float x) {
                    A3 = -0x1.7154748bef6c8p-1, A4 = 0x1.71547652ab82bp0;
   constexpr double C0 = 0x1.c6af84b912394p-5, C1 = 0x1.ebfce50fac4f3p-3, C2 = 0x1.62e42ff0c52d6p-1;
   uint32_t ix = mh_asuint(x) & 0x7fffffffu;  // y = 2 is even: sign drops
-  if (ix == 0u) return 0.0f;
-  if (ix >= 0x7f800000u) return x * x;
+  if (ix == 0u) return 0.0;
+  if (ix >= 0x7f800000u) return (double)(x * x);
   if (ix < 0x00800000u) {  // subnormal: normalise
     ix = mh_asuint(mh_asfloat(ix) * 0x1p23f) & 0x7fffffffu;
     ix -= 23u << 23;
@@ -109,7 +112,10 @@ MH_HD float powf2(float x) {
   q = p * r2 + q;
   y = y * r4 + q;
   const double ylogx = 2.0 * y;
-  if (((mh_asuint64(ylogx) >> 47) & 0xffffu) >= (mh_asuint64(126.0) >> 47)) return x * x;  // |2 log2 x| >= 126
+  if (((mh_asuint64(ylogx) >> 47) & 0xffffu) >= (mh_asuint64(126.0) >> 47)) {  // |2 log2 x| >= 126
+    if (ylogx > 0x1.fffffffd1d571p+6) return (double)INFINITY;  // __math_oflowf
+    if (ylogx <= -150.0) return 0.0;                              // __math_uflowf
+  }
   const double SHIFT = 0x1.8p+52 / 32;
   double kd = ylogx + SHIFT;
   const uint64_t ki = mh_asuint64(kd);
@@ -123,7 +129,28 @@ MH_HD float powf2(float x) {
   double yy = C2 * rr + 1.0;
   yy = zz * rr2 + yy;
   yy = yy * s;
-  return (float)yy;
+  return yy;
+}
+
+// powf(x, 2) bit-exactly, cheaply: glibc's double result differs from the exact square x*x
+// (exact in double) by at most POWF2_MAX_ERR float-ulps over ALL 2^32 inputs (exhaustive scan,
+// tools/powf2_exhaustive.cpp), so whenever the exact square lies farther than that from a
+// float rounding midpoint, glibc returns the correctly rounded square. Only the rare
+// near-midpoint inputs (and zero / subnormal / overflowing squares, powers of two) take the
+// table path. The exhaustive scan also checks this function against libm powf for every input.
+constexpr double POWF2_MAX_ERR = 0x1p-8;  // guard > measured maximum 1.69e-3 ulp (tools/powf2_exhaustive.cpp)
+MH_HD float powf2(float x) {
+  const double xd = (double)x;
+  const double p = xd * xd;  // exact: 24 x 24 significant bits
+  const float r = (float)p;
+  const uint32_t rb = mh_asuint(r);
+  const uint32_t ex = (rb >> 23) & 0xffu, man = rb & 0x7fffffu;
+  if (ex > 23u && ex < 0xfeu && man != 0u) {
+    const double ulp = mh_asdouble((uint64_t)(ex - 23u - 127u + 1023u) << 52);
+    const double d = fabs(p - (double)r);  // exact, <= ulp / 2
+    if (0.5 * ulp - d > POWF2_MAX_ERR * ulp) return r;
+  }
+  return (float)powf2_core(x);
 }
 
 // NumPy float32 add.reduce order (pairwise_sum: <8 sequential from -0.0, else 8 lanes).
@@ -670,11 +697,13 @@ struct QuadTracking {
       fd[i] = -w;
     }
     double nfd = norm3(fd);
-    double b3[3] = {fd[0] / nfd, fd[1] / nfd, fd[2] / nfd};
+    const double infd = 1.0 / nfd;  // one division, three products (<= 1 ulp f64 apart from fd / nfd)
+    double b3[3] = {fd[0] * infd, fd[1] * infd, fd[2] * infd};
     double c[3];
     cross64(b3, b1, c);
     double nc = norm3(c);
-    double b2[3] = {c[0] / nc, c[1] / nc, c[2] / nc};
+    const double inc = 1.0 / nc;
+    double b2[3] = {c[0] * inc, c[1] * inc, c[2] * inc};
     double b1n[3];
     cross64(b2, b3, b1n);
     for (int i = 0; i < 3; ++i) {
@@ -685,9 +714,9 @@ struct QuadTracking {
     float Od[3] = {0.0f, 0.0f, 0.0f};
     double Odd[3] = {0.0, 0.0, 0.0};
     if (have_last) {
-      double dt = row[1];
+      const double idt = 1.0 / row[1];
       float Rdot[9];
-      for (int i = 0; i < 9; ++i) Rdot[i] = (float)((Rd[i] - Rdl[i]) / dt);   // RDerive
+      for (int i = 0; i < 9; ++i) Rdot[i] = (float)((Rd[i] - Rdl[i]) * idt);   // RDerive
       // getOmega: So3ToVec(Rd^T @ Rdot) -> f32
       double M21 = 0.0, M02 = 0.0, M10 = 0.0;
       for (int k = 0; k < 3; ++k) {

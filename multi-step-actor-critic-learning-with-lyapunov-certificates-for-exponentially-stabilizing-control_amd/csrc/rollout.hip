@@ -67,14 +67,18 @@ struct ResetDraw<QuadTracking> {  // QuadTracking.py:169-186
     for (int i = 0; i < 3; ++i) rs[15 + i] = uni(u01(v[6 + i]), -0.01f, 0.01f);  // Omega
     float nz[4];
     r.normal4f(4, nz);
-    double rv[3] = {nz[0] * 0.01, nz[1] * 0.01, nz[2] * 0.01};  // rotvec ~ N(0, 0.01^2)
-    double th = sqrt(rv[0] * rv[0] + rv[1] * rv[1] + rv[2] * rv[2]);
-    double sc = th <= 1e-3 ? 0.5 - th * th / 48.0 + th * th * th * th / 3840.0 : sin(0.5 * th) / th;
-    double x = sc * rv[0], y = sc * rv[1], z = sc * rv[2], w = cos(0.5 * th);
-    double Rm[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w),     2 * (x * z + y * w),
-                    2 * (x * y + z * w),     1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
-                    2 * (x * z - y * w),     2 * (y * z + x * w),     1 - 2 * (x * x + y * y)};
-    for (int i = 0; i < 9; ++i) rs[6 + i] = (float)Rm[i];
+    // scipy Rotation.from_rotvec(rv).as_matrix() via the unit quaternion, in float32 (the reset
+    // draw itself is distribution-matched, not sample-matched, so f32 rounding is immaterial)
+    const float rv[3] = {nz[0] * 0.01f, nz[1] * 0.01f, nz[2] * 0.01f};  // rotvec ~ N(0, 0.01^2)
+    const float th = sqrtf(rv[0] * rv[0] + rv[1] * rv[1] + rv[2] * rv[2]);
+    float sh, ch;
+    sincosf(0.5f * th, &sh, &ch);
+    const float sc = th <= 1e-3f ? 0.5f - th * th / 48.0f : sh / th;
+    const float x = sc * rv[0], y = sc * rv[1], z = sc * rv[2], w = ch;
+    const float Rm[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - z * w),     2 * (x * z + y * w),
+                         2 * (x * y + z * w),     1 - 2 * (x * x + z * z), 2 * (y * z - x * w),
+                         2 * (x * z - y * w),     2 * (y * z + x * w),     1 - 2 * (x * x + y * y)};
+    for (int i = 0; i < 9; ++i) rs[6 + i] = Rm[i];
   }
 };
 

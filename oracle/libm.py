@@ -79,7 +79,11 @@ def powf2(x):
     yy = _C[2] * rr + 1.0
     yy = zz * rr2 + yy
     yy = yy * s
-    res = yy.astype(np.float32)
-    res[big] = (x[ok][big] * x[ok][big]).astype(np.float32)
+    with np.errstate(over="ignore", under="ignore"):
+        res = yy.astype(np.float32)
+    # e_powf.c: only |x^2| overflow (-> inf) and ylogx <= -150 (-> 0) leave the exp2 path;
+    # subnormal results in between come from exp2 (double rounding included)
+    res[big & (ylogx > float.fromhex("0x1.fffffffd1d571p+6"))] = np.float32(np.inf)
+    res[big & (ylogx <= -150.0)] = np.float32(0.0)
     out[ok] = res
     return out.reshape(shape)

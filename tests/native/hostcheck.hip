@@ -36,6 +36,11 @@ void reset_all(int64_t n, const float* rs, float* state, double* xstate, float* 
 }  // namespace
 
 extern "C" {
+// the kernel's powf(x, 2) restatement (fast exact-square path + glibc table path)
+void mhc_powf2(int64_t n, const float* x, float* out) {
+  for (int64_t i = 0; i < n; ++i) out[i] = mh::powf2(x[i]);
+}
+
 int mhc_env_step(int env_id, int64_t n, float* state, double* xstate, const int32_t* steps, const float* act,
                  float* obs, float* rew) {
   switch (env_id) {
