@@ -476,27 +476,43 @@ __global__ __launch_bounds__(256) void k_emit_fused(EmitArgs a) {
 }
 
 // --------------------------------------------------------------- replay gather / indices
-__global__ __launch_bounds__(256) void k_gather(GatherArgs a) {
-  const int64_t b = blockIdx.x;
-  if (b >= a.batch) return;
-  const int64_t r = a.idx[b];
-  const int n = a.n;
-  struct Field {
-    const float* src;
-    float* dst;
-    int width;
-  };
-  const Field fields[7] = {{a.s_obs, a.o_obs, a.D},   {a.s_act, a.o_act, a.A},   {a.s_rew, a.o_rew, 1},
-                           {a.s_cost, a.o_cost, 1},   {a.s_obs2, a.o_obs2, a.D}, {a.s_done, a.o_done, 1},
-                           {a.s_logp, a.o_logp, 1}};
-#pragma unroll
-  for (int f = 0; f < 7; ++f) {
-    if (!fields[f].dst) continue;
-    const int64_t len = (int64_t)n * fields[f].width;
-    const float* s = fields[f].src + r * len;
-    float* d = fields[f].dst + b * len;
-    for (int64_t i = threadIdx.x; i < len; i += 256) d[i] = s[i];
+// Replay gather: blockIdx.y selects one of the 7 arrays; each thread copies 16-B vectors of
+// the sampled rows (a row of one array is n * width contiguous floats), grid-stride over
+// batch x row-vectors, so every lane moves useful bytes regardless of the field width.
+template <typename V>
+__device__ __forceinline__ void gather_rows(const float* src, float* dst, const int64_t* idx, int64_t batch,
+                                            int64_t len) {
+  const int64_t v = len * (int64_t)sizeof(float) / (int64_t)sizeof(V);
+  const V* s = reinterpret_cast<const V*>(src);
+  V* d = reinterpret_cast<V*>(dst);
+  const int64_t total = batch * v;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
+    const int64_t b = q / v, i = q - b * v;
+    d[q] = s[idx[b] * v + i];
   }
+}
+
+__global__ __launch_bounds__(256) void k_gather(GatherArgs a) {
+  const float* src;
+  float* dst;
+  int w;
+  switch (blockIdx.y) {
+    case 0: src = a.s_obs; dst = a.o_obs; w = a.D; break;
+    case 1: src = a.s_act; dst = a.o_act; w = a.A; break;
+    case 2: src = a.s_rew; dst = a.o_rew; w = 1; break;
+    case 3: src = a.s_cost; dst = a.o_cost; w = 1; break;
+    case 4: src = a.s_obs2; dst = a.o_obs2; w = a.D; break;
+    case 5: src = a.s_done; dst = a.o_done; w = 1; break;
+    default: src = a.s_logp; dst = a.o_logp; w = 1; break;
+  }
+  if (!dst) return;
+  const int64_t len = (int64_t)a.n * w;
+  if (len % 4 == 0)
+    gather_rows<float4>(src, dst, a.idx, a.batch, len);
+  else if (len % 2 == 0)
+    gather_rows<float2>(src, dst, a.idx, a.batch, len);
+  else
+    gather_rows<float>(src, dst, a.idx, a.batch, len);
 }
 
 __global__ __launch_bounds__(256) void k_sample_idx(const int64_t* cursor, uint64_t seed, uint64_t counter,
@@ -597,7 +613,9 @@ hipError_t launch_emit_fused(int env_id, const EmitArgs& a, hipStream_t st) {
 }
 hipError_t launch_gather(const GatherArgs& a, hipStream_t st) {
   if (a.batch <= 0) return hipSuccess;
-  k_gather<<<(int)a.batch, 256, 0, st>>>(a);
+  const int64_t vec = (a.batch * (int64_t)a.n * (a.D > a.A ? a.D : a.A) + 1023) / 1024;  // float4s of the widest array
+  const int gx = (int)(vec < 1 ? 1 : (vec > 2048 ? 2048 : vec));
+  k_gather<<<dim3(gx, 7), 256, 0, st>>>(a);
   return hipGetLastError();
 }
 hipError_t launch_sample_idx(const int64_t* cursor, uint64_t seed, uint64_t counter, int64_t batch,
