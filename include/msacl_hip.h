@@ -129,6 +129,49 @@ int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const 
                     const float* reset_states, float* obs, const mh_window_store_t* store,
                     float* act_out, float* logp_out, void* stream);
 
+/* rew_plus_cost scales (RL/utils/rew_plus_cost.py:18-21) used by every sampler step; also set
+ * by mh_nstep_attach. Default 1, 1. */
+int mh_env_set_reward_cost_scale(mh_env_t h, float reward_scale, float cost_scale);
+
+/* Exploration noise of BaseSampler (base.py:136-137 -> GaussNoise.sample, explore_noise.py:9):
+ * `noise` is a DEVICE float[1] holding the one scalar np.random.normal(mean, std) that is added
+ * to every sampled action of a lockstep step, before the clip. The caller refreshes it per step
+ * (a device RNG write, capturable). NULL disables. Ignored for injected actions. */
+int mh_env_set_action_noise(mh_env_t h, const float* noise);
+
+/* On-policy trajectory store = OnSampler's mini-batch arrays (RL/trainer/sampler/
+ * on_sampler.py:22-41), env-major exactly as the reference's numpy arrays:
+ * obs/obs2 [E][horizon][obs_dim], act [E][horizon][act_dim], rew/cost/logp [E][horizon] float32,
+ * done [E][horizon] uint8 (np.bool_). */
+typedef struct {
+  float* obs;
+  float* act;
+  float* rew;
+  float* cost;
+  float* obs2;
+  uint8_t* done;
+  float* logp;
+  int32_t horizon;
+} mh_traj_store_t;
+
+/* One lockstep step of OnSampler._sample (on_sampler.py:49-55 -> BaseSampler._step,
+ * base.py:225-298) minus the policy/value MLPs: TanhGauss sample (or injected actions), clip,
+ * env step + autoreset, rew_plus_cost, and column t of every trajectory array
+ * (_process_experiences, on_sampler.py:131-141). Arguments as mh_rollout_step. */
+int mh_rollout_traj_step(mh_env_t h, const float* logits, const float* act_in, const float* logp_in,
+                         const float* reset_states, float* obs, const mh_traj_store_t* traj, int32_t t,
+                         float* act_out, float* logp_out, void* stream);
+
+/* GAE + discounted returns over a whole trajectory block (OnSampler._process_experiences /
+ * _finish_trajs, on_sampler.py:108-154). All arrays [num_envs][horizon]:
+ *   val   V(obs_t)                 (mb_val)
+ *   val2  V(real_next_obs_t)       (read only where a segment ends: done or t == horizon-1)
+ *   rew, done                      (mb_rew, mb_done)
+ *   adv, ret                       outputs (mb_adv, mb_ret)
+ * Segments end at done or the horizon; bootstrap = val2 * (1 - done). */
+int mh_gae(const float* val, const float* val2, const float* rew, const uint8_t* done, int64_t num_envs,
+           int32_t horizon, double gamma, double gae_lambda, float* adv, float* ret, void* stream);
+
 /* Per-kernel HIP-event timing of mh_rollout_step (profiling aid; do not enable inside a
  * captured hipGraph). read_timing drains the pending events (host sync) and returns the summed
  * milliseconds of {step kernel, window scan, window emission} and the number of timed calls. */

@@ -37,6 +37,13 @@ class EnvInfo(ctypes.Structure):
     ]
 
 
+class TrajStore(ctypes.Structure):
+    _fields_ = [
+        ("obs", c_vp), ("act", c_vp), ("rew", c_vp), ("cost", c_vp), ("obs2", c_vp), ("done", c_vp),
+        ("logp", c_vp), ("horizon", c_i32),
+    ]
+
+
 class WindowStore(ctypes.Structure):
     _fields_ = [
         ("obs", c_vp), ("act", c_vp), ("rew", c_vp), ("cost", c_vp), ("obs2", c_vp), ("done", c_vp),
@@ -58,6 +65,11 @@ _PROTOS = {
     "mh_nstep_attach": (ctypes.c_int, [c_vp, c_i32, c_f32, c_f32]),
     "mh_rollout_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(WindowStore), c_vp, c_vp, c_vp]),
     "mh_nstep_set_log_std_clamp": (ctypes.c_int, [c_vp, c_i32, c_f32, c_f32]),
+    "mh_env_set_reward_cost_scale": (ctypes.c_int, [c_vp, c_f32, c_f32]),
+    "mh_env_set_action_noise": (ctypes.c_int, [c_vp, c_vp]),
+    "mh_rollout_traj_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(TrajStore), c_i32,
+                                            c_vp, c_vp, c_vp]),
+    "mh_gae": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f64, c_f64, c_vp, c_vp, c_vp]),
     "mh_env_set_timing": (ctypes.c_int, [c_vp, c_i32]),
     "mh_env_read_timing": (ctypes.c_int, [c_vp, ctypes.POINTER(c_f64), ctypes.POINTER(c_i64), c_i32]),
     "mh_replay_gather": (ctypes.c_int, [ctypes.POINTER(WindowStore), c_i32, c_i32, c_i32, c_vp, c_i64,

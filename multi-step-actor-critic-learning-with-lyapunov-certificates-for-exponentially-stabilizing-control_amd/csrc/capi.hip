@@ -61,6 +61,7 @@ struct mh_env_s {
   float reward_scale = 1.0f, cost_scale = 1.0f;
   int raw_log_std = 0;
   float log_std_lo = -20.0f, log_std_hi = 1.0f;
+  const float* act_noise = nullptr;
   float* ring = nullptr;
   int32_t* ring_len = nullptr;
   int32_t* ring_pos = nullptr;
@@ -104,6 +105,7 @@ struct mh_env_s {
     a.raw_log_std = raw_log_std;
     a.log_std_lo = log_std_lo;
     a.log_std_hi = log_std_hi;
+    a.act_noise = act_noise;
     return a;
   }
 };
@@ -358,6 +360,59 @@ int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const 
     MH_HIP(hipEventRecord(ev[3], st));
     for (int i = 0; i < 4; ++i) h->ev_pending.push_back(ev[i]);
   }
+  return MH_OK;
+}
+
+int mh_env_set_reward_cost_scale(mh_env_t h, float reward_scale, float cost_scale) {
+  if (!h) return fail(MH_EINVAL, "mh_env_set_reward_cost_scale: null handle");
+  h->reward_scale = reward_scale;
+  h->cost_scale = cost_scale;
+  return MH_OK;
+}
+
+int mh_env_set_action_noise(mh_env_t h, const float* noise) {
+  if (!h) return fail(MH_EINVAL, "mh_env_set_action_noise: null handle");
+  h->act_noise = noise;
+  return MH_OK;
+}
+
+int mh_rollout_traj_step(mh_env_t h, const float* logits, const float* act_in, const float* logp_in,
+                         const float* reset_states, float* obs, const mh_traj_store_t* traj, int32_t t,
+                         float* act_out, float* logp_out, void* stream) {
+  if (!h) return fail(MH_EINVAL, "mh_rollout_traj_step: null handle");
+  if (!obs) return fail(MH_EINVAL, "mh_rollout_traj_step: null obs");
+  if (!logits && !act_in) return fail(MH_EINVAL, "mh_rollout_traj_step: need logits or act_in");
+  if (!traj || !traj->obs || !traj->act || !traj->rew || !traj->cost || !traj->obs2 || !traj->done ||
+      !traj->logp)
+    return fail(MH_EINVAL, "mh_rollout_traj_step: incomplete trajectory store");
+  if (traj->horizon <= 0 || t < 0 || t >= traj->horizon)
+    return fail(MH_EINVAL, "mh_rollout_traj_step: column t outside [0, horizon)");
+  mh::StepArgs a = h->base_args();
+  a.logits = logits;
+  a.act_in = act_in;
+  a.logp_in = logp_in;
+  a.reset_in = reset_states;
+  a.obs = obs;
+  a.act_out = act_out;
+  a.logp_out = logp_out;
+  a.traj_obs = traj->obs;
+  a.traj_act = traj->act;
+  a.traj_rew = traj->rew;
+  a.traj_cost = traj->cost;
+  a.traj_obs2 = traj->obs2;
+  a.traj_done = traj->done;
+  a.traj_logp = traj->logp;
+  a.traj_H = traj->horizon;
+  a.traj_t = t;
+  MH_HIP(mh::launch_rollout(h->env_id, a, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_gae(const float* val, const float* val2, const float* rew, const uint8_t* done, int64_t num_envs,
+           int32_t horizon, double gamma, double gae_lambda, float* adv, float* ret, void* stream) {
+  if (!val || !val2 || !rew || !done || !adv || !ret) return fail(MH_EINVAL, "mh_gae: null array");
+  if (num_envs < 0 || horizon < 0) return fail(MH_EINVAL, "mh_gae: negative size");
+  MH_HIP(mh::launch_gae(val, val2, rew, done, num_envs, horizon, gamma, gae_lambda, adv, ret, (hipStream_t)stream));
   return MH_OK;
 }
 

@@ -46,6 +46,13 @@ struct StepArgs {
   float reward_scale, cost_scale;
   int raw_log_std;               // logits second half is log_std: std = exp(clamp(., lo, hi))
   float log_std_lo, log_std_hi;  // StochaPolicy min/max_log_std (mlp.py:125-136)
+  const float* act_noise;        // device scalar added to every sampled action before the clip
+                                 // (GaussNoise.sample, explore_noise.py:9; base.py:136-137) or null
+  // on-policy trajectory store (OnSampler mb_* arrays, on_sampler.py:22-41): [E][H][.] rows,
+  // this step writes column traj_t (null traj_obs: not recording)
+  float *traj_obs, *traj_act, *traj_rew, *traj_cost, *traj_obs2, *traj_logp;
+  uint8_t* traj_done;
+  int traj_H, traj_t;
 };
 
 // meta[] slots (device int64[8])
@@ -82,6 +89,8 @@ struct GatherArgs {
 };
 
 hipError_t launch_rollout(int env_id, const StepArgs& a, hipStream_t st);
+hipError_t launch_gae(const float* val, const float* val2, const float* rew, const uint8_t* done, int64_t E,
+                      int H, double gamma, double lam, float* adv, float* ret, hipStream_t st);
 hipError_t launch_reset(int env_id, const StepArgs& a, hipStream_t st);
 hipError_t launch_finalize(const int32_t* block_count, int32_t nb, int32_t* block_offset, int64_t* meta,
                            int64_t* cursor, int64_t capacity, hipStream_t st);

@@ -103,7 +103,7 @@ __global__ __launch_bounds__(BLK) void k_rollout(StepArgs a) {
     const Rng rng = make_rng(a.seed, (uint64_t)e, ctr);
 
     float obs0[D];
-    if (a.ring) {
+    if (a.ring || a.traj_obs) {
 #pragma unroll
       for (int i = 0; i < D; ++i) obs0[i] = a.obs[e * D + i];
     }
@@ -133,6 +133,7 @@ __global__ __launch_bounds__(BLK) void k_rollout(StepArgs a) {
         const float half = (hi - lo) / 2.0f, mid = (hi + lo) / 2.0f;
         ls = ls + logf(half);
         float act = half * th + mid;
+        if (a.act_noise) act = act + a.act_noise[0];  // GaussNoise: one scalar per lockstep step
         act = fminf(fmaxf(act, lo), hi);  // actions.clip(low, high)
         u[i] = act;
       }
@@ -192,6 +193,21 @@ __global__ __launch_bounds__(BLK) void k_rollout(StepArgs a) {
     if (a.reward_out) a.reward_out[e] = r;
     if (a.term_out) a.term_out[e] = term ? 1 : 0;
     if (a.trunc_out) a.trunc_out[e] = trunc ? 1 : 0;
+
+    // ---- on-policy trajectory column (on_sampler.py:131-141: mb_obs/act/rew/cost/obs2/done/logp)
+    if (a.traj_obs) {
+      const int64_t c = e * (int64_t)a.traj_H + a.traj_t;
+#pragma unroll
+      for (int i = 0; i < D; ++i) a.traj_obs[c * D + i] = obs0[i];
+#pragma unroll
+      for (int i = 0; i < A; ++i) a.traj_act[c * A + i] = u[i];
+#pragma unroll
+      for (int i = 0; i < D; ++i) a.traj_obs2[c * D + i] = obs2[i];
+      a.traj_rew[c] = rew;
+      a.traj_cost[c] = cost;
+      a.traj_done[c] = done ? 1 : 0;
+      a.traj_logp[c] = logp;
+    }
 
     // ---- n-step deque push (base.py:180-217)
     if (a.ring) {

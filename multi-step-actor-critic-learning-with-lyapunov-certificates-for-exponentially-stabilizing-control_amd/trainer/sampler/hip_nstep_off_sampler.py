@@ -44,8 +44,6 @@ class HipNstepOffSampler:
         self.reward_scale = float(kwargs["reward_scale"])
         self.cost_scale = float(kwargs["cost_scale"])
         self.noise_params = kwargs.get("noise_params")
-        if self.noise_params is not None:
-            raise NotImplementedError("noise_params: additive action noise is not supported by the HIP sampler yet")
         if self.action_type != "continu":
             raise RuntimeError("Only continuous action space is supported!")
         self.target_value = kwargs.get("target_value", 0.0)
@@ -58,6 +56,15 @@ class HipNstepOffSampler:
         self.use_graph = bool(kwargs.get("sampler_use_graph", True))
         self._h = self.envs.handle()
         N.check(N.lib().mh_nstep_attach(self._h, self.n_step, self.reward_scale, self.cost_scale), "mh_nstep_attach")
+        # GaussNoise (explore_noise.py:3-9; base.py:83-88,136-137): ONE scalar
+        # np.random.normal(mean, std) per lockstep step, added to every action before the clip.
+        # Drawn on the device into a 1-float tensor (capturable), read by the rollout kernel.
+        self._noise = None
+        if self.noise_params is not None:
+            self._noise_mean = float(self.noise_params["mean"])
+            self._noise_std = float(self.noise_params["std"])
+            self._noise = torch.zeros(1, dtype=torch.float32, device=self.device)
+            N.check(N.lib().mh_env_set_action_noise(self._h, N.ptr(self._noise)), "mh_env_set_action_noise")
         self.obs, _ = self.envs.reset(seed=None)
         self._bound = None
         self._staging = None
@@ -128,7 +135,12 @@ class HipNstepOffSampler:
                                         N.ptr(act_out), N.ptr(logp_out), N.stream_of(self.device)),
                 "mh_rollout_step")
 
+    def _draw_noise(self):
+        if self._noise is not None:
+            self._noise.normal_(self._noise_mean, self._noise_std)
+
     def _policy_step(self, store):
+        self._draw_noise()
         logits, raw = self._policy_raw()
         pol = self.networks.policy
         N.check(N.lib().mh_nstep_set_log_std_clamp(self._h, int(raw), float(getattr(pol, "min_log_std", -20.0)),

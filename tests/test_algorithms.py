@@ -1,0 +1,135 @@
+"""SAC / LAC / PPO / POLYC model_update against the reference's own updates
+(tests/golden/{sac,lac,ppo,polyc}_update.npz, tools/gen_golden.py:gen_algs): same initial
+weights, same batch, the reference's recorded Normal.rsample noise replayed (SAC/LAC) and the
+same NumPy global seed for the mini-batch shuffles (PPO/POLYC). The algorithms are PyTorch
+modules (the north star keeps the MLPs in PyTorch), so the host check runs on the CPU and the
+same check runs on the MI355X (fused Adam, HIP-graph replay) under -m gpu.
+
+Tolerances: parameters rtol 1e-4 / atol 3e-5 with <0.2 % outliers (fused vs foreach Adam and
+GEMM reduction order move single ulps that Adam's normalisation can amplify), tb scalars
+rtol 2e-4."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import msacl_amd  # noqa: F401
+from oracle import envs as OE
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+G = os.path.join(ROOT, "tests", "golden")
+
+
+def _kw(env, hidden=64):
+    cls = OE.ENVS[env]
+    return dict(env_name=env, obs_dim=cls.obs_dim, act_dim=cls.act_dim, action_type="continu",
+                action_high_limit=cls.act_high.copy(), action_low_limit=cls.act_low.copy(), value_func_type="MLP",
+                value_hidden_sizes=[hidden, hidden], value_hidden_activation="relu", value_output_activation="linear",
+                policy_func_name="StochaPolicy", policy_func_type="MLP", policy_act_distribution="TanhGaussDistribution",
+                policy_hidden_sizes=[hidden, hidden], policy_hidden_activation="relu", policy_min_log_std=-20,
+                policy_max_log_std=1, target_value=0.0)
+
+
+def make_alg(tag, device):
+    from msacl_amd.create_pkg.create_alg import create_alg
+    if tag == "sac":
+        kw = _kw("QuadTracking")
+        kw.update(value_func_name="ActionValue", q_learning_rate=1e-3, policy_learning_rate=3e-4,
+                  alpha_learning_rate=1e-3, gamma=0.99, tau=0.005, alpha=1.0, auto_alpha=True, policy_frequency=2,
+                  target_network_frequency=1)
+    elif tag == "lac":
+        kw = _kw("Pendulum")
+        kw.update(value_func_name="ActionValue", l_learning_rate=1e-3, policy_learning_rate=3e-4,
+                  alpha_learning_rate=1e-3, beta_learning_rate=1e-3, gamma=0.99, tau=0.005, alpha=1.0, beta=1.0,
+                  auto_alpha=True, alpha3=0.01, policy_frequency=2, target_network_frequency=1)
+    else:
+        kw = _kw("DuctedFan")
+        kw.update(value_func_name="StateValue", lyapunov_func_name="LyapunovValue", lyapunov_func_type="MLP",
+                  lyapunov_hidden_sizes=[64, 64], lyapunov_hidden_activation="tanh", lyapunov_output_dim=32,
+                  lyapunov_output_activation="linear", lyapunov_single_input_dim=False, learning_rate=1e-3,
+                  policy_learning_rate=3e-4, loss_coefficient_value=1.0, loss_coefficient_entropy=0.01,
+                  loss_coefficient_kl=0.2, loss_value_clip=True, value_clip=0.5, beta=0.3, gamma=0.99,
+                  schedule_adam="linear", schedule_clip="linear", clip=0.1, max_iteration=100, num_repeat=2,
+                  num_mini_batch=4, mini_batch_size=16, sample_batch_size=64, env_num=2)
+    kw.update(algorithm=tag, device=device, trainer="on_serial_trainer" if tag in ("ppo", "polyc") else "off_serial_trainer")
+    return create_alg(**kw)
+
+
+def _compare_params(alg, g, prefix):
+    mine = alg.networks.state_dict()
+    n = 0
+    for k in g.files:
+        if not k.startswith(prefix):
+            continue
+        ref = g[k]
+        got = mine[k[len(prefix):]].detach().cpu().numpy()
+        bad = ~np.isclose(got, ref, rtol=1e-4, atol=3e-5)
+        assert bad.mean() < 2e-3, (k, int(bad.sum()), float(np.abs(got - ref).max()))
+        n += 1
+    assert n > 0
+
+
+def _compare_tb(tb, g):
+    ref = dict(zip([str(k) for k in g["tb_keys"]], g["tb_vals"]))
+    assert set(tb) == set(ref)
+    for k, v in tb.items():
+        if "time" not in k.lower():
+            np.testing.assert_allclose(v, ref[k], rtol=2e-4, atol=1e-5, err_msg=k)
+
+
+def run_update_parity(tag, device, monkeypatch):
+    import torch.distributions.normal as tdn
+    g = np.load(os.path.join(G, f"{tag}_update.npz"))
+    alg = make_alg(tag, device)
+    alg.networks.load_state_dict({k[5:]: torch.as_tensor(g[k]) for k in g.files if k.startswith("init/")})
+    eps = iter([g[f"eps{i}"] for i in range(int(g["n_eps"]))])
+    monkeypatch.setattr(tdn, "_standard_normal",
+                        lambda shape, dtype, device: torch.as_tensor(next(eps), dtype=dtype, device=device).reshape(shape))
+    keys = [k[3:] for k in g.files if k.startswith("in_")]
+    data = lambda: {k: torch.as_tensor(g["in_" + k], device=device) for k in keys}  # noqa: E731
+    if tag in ("sac", "lac"):
+        tb = alg.model_update(data(), 0)
+        _compare_tb(tb, g)
+        _compare_params(alg, g, "after0/")
+        assert alg.model_update(data(), 1) is None
+        _compare_params(alg, g, "after1/")
+    else:
+        np.random.seed(int(g["np_seed"]))
+        tb, it = alg.model_update(data())
+        assert it == 8
+        np.testing.assert_array_equal(alg.indices, g["indices_after"])
+        _compare_tb(tb, g)
+        _compare_params(alg, g, "after0/")
+
+
+@pytest.mark.parametrize("tag", ["sac", "lac", "ppo", "polyc"])
+def test_update_matches_reference_cpu(tag, monkeypatch):
+    run_update_parity(tag, "cpu", monkeypatch)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", ["sac", "lac", "ppo", "polyc"])
+def test_update_matches_reference_gpu(tag, monkeypatch):
+    run_update_parity(tag, "cuda", monkeypatch)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", ["sac", "lac"])
+def test_graph_replayed_update_trains(tag):
+    """Warm -> capture -> replay of both (update-policy, no-policy) branches: parameters stay
+    finite, both branches got a graph, and the critic fits the fixed batch."""
+    g = np.load(os.path.join(G, f"{tag}_update.npz"))
+    keys = [k[3:] for k in g.files if k.startswith("in_")]
+    data = {k: torch.as_tensor(g["in_" + k], device="cuda") for k in keys}
+    torch.manual_seed(0)
+    alg = make_alg(tag, "cuda")
+    alg.networks.load_state_dict({k[5:]: torch.as_tensor(g[k]) for k in g.files if k.startswith("init/")})
+    hist = []
+    for it in range(16):
+        tb = alg.model_update(data, it)
+        if tb is not None:
+            hist.append(tb["Loss/Critic loss-RL iter"])
+    assert len(alg._graph._graphs) == 2
+    assert all(torch.isfinite(p).all() for p in alg.networks.parameters())
+    assert hist[-1] < hist[0], hist

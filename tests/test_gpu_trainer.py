@@ -41,3 +41,43 @@ def test_evaluator_runs_episodes(tmp_path):
     args, alg, sampler, buffer, evaluator, trainer = build_pipeline(args)
     m, s, cm, cs = evaluator.run_evaluation(0)
     assert np.isfinite([m, s, cm, cs]).all() and cm >= 0
+
+
+@pytest.mark.parametrize("alg_name,env_name", [("sac", "TwoLink"), ("lac", "Pendulum")])
+def test_off_policy_train_loop(tmp_path, alg_name, env_name):
+    """example/{sac,lac}_train.py's pipeline: off_sampler + replay_buffer + off_serial_trainer."""
+    from msacl_amd.utils.config import default_lac_args, default_sac_args
+    mk = default_sac_args if alg_name == "sac" else default_lac_args
+    args = mk(env_name=env_name, env_num=1024, buffer_warm_size=4096, buffer_max_size=100000, max_iteration=6,
+              eval_interval=3, log_save_interval=2, apprfunc_save_interval=3, save_folder=str(tmp_path), seed=0,
+              num_eval_episode=4)
+    args, alg, sampler, buffer, evaluator, trainer = build_pipeline(args)
+    assert type(buffer).__name__ == "ReplayBuffer" and type(sampler).__name__ == "OffSampler"
+    assert buffer.size >= 4096
+    trainer.train()
+    torch.cuda.synchronize()
+    assert trainer.iteration == 7
+    for p in alg.networks.parameters():
+        assert torch.isfinite(p).all()
+    b = buffer.sample_batch(16)
+    assert b["obs"].shape == (16, sampler.envs.obs_dim)
+
+
+@pytest.mark.parametrize("alg_name", ["ppo", "polyc"])
+def test_on_policy_train_loop(tmp_path, alg_name):
+    """example/{ppo,polyc}_train.py's pipeline: on_sampler (+ GAE kernel) + on_serial_trainer."""
+    from msacl_amd.utils.config import default_ppo_args
+    args = default_ppo_args(algorithm=alg_name, env_name="DuctedFan", env_num=512, sample_batch_size=64,
+                            num_mini_batch=4, mini_batch_size=16, max_iteration=16, eval_interval=8,
+                            log_save_interval=8, apprfunc_save_interval=8, save_folder=str(tmp_path), seed=0,
+                            num_eval_episode=4)
+    args, alg, sampler, buffer, evaluator, trainer = build_pipeline(args)
+    assert buffer is None and type(sampler).__name__ == "OnSampler"
+    trainer.train()
+    torch.cuda.synchronize()
+    assert trainer.global_iteration == 16
+    for p in alg.networks.parameters():
+        assert torch.isfinite(p).all()
+    data, _ = sampler.sample()
+    assert data["obs"].shape == (512 * 64, 6) and data["done"].dtype == torch.bool
+    assert torch.isfinite(data["adv"]).all() and torch.isfinite(data["ret"]).all()

@@ -313,6 +313,165 @@ def gen_nstep_trace(name, E=24, T=40, n_step=5, seed=3, tag=""):
     print(f"{fn}: E={E} T={T} n={n_step} windows={sum(counts)} resets={int((np.abs(d['resets']).sum(-1) > 0).sum())}")
 
 
+# ---------------------------------------------------------------------- 1-step / on-policy traces
+def load_ref_methods(relpath, cls_name, names, skip_modules=(), extra_ns=None):
+    """Compile methods `names` of class `cls_name` from a reference source file (module-level
+    statements executed, imports of `skip_modules` skipped)."""
+    path = f"{REF}/{relpath}"
+    tree = ast.parse(open(path).read())
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    ns = {"__name__": "ref_" + cls_name}
+    ns.update(extra_ns or {})
+    found = {}
+    for node in tree.body:
+        if isinstance(node, ast.ImportFrom) and node.module in skip_modules:
+            continue
+        if isinstance(node, ast.ClassDef) and node.name == cls_name:
+            for item in node.body:
+                if isinstance(item, ast.FunctionDef) and item.name in names:
+                    found[item.name] = item
+            continue
+        exec(compile(ast.Module(body=[node], type_ignores=[]), path, "exec"), ns)
+    out = {}
+    for nm in names:
+        exec(compile(ast.Module(body=[found[nm]], type_ignores=[]), path, "exec"), ns)
+        out[nm] = ns.pop(nm)
+    return out, ns
+
+
+def _ref_policy_and_recorder(name, hidden=64):
+    import torch
+    from RL.apprfunc.mlp import StochaPolicy
+    from RL.utils.act_distribution_cls import TanhGaussDistribution
+    cls = OE.ENVS[name]
+    policy = StochaPolicy(obs_dim=cls.obs_dim, act_dim=cls.act_dim, hidden_sizes=[hidden, hidden],
+                          hidden_activation="relu", output_activation="linear", min_log_std=-20, max_log_std=1,
+                          act_high_lim=cls.act_high.copy(), act_low_lim=cls.act_low.copy(),
+                          action_distribution_cls=TanhGaussDistribution)
+    if name == "QuadTracking":
+        with torch.no_grad():
+            last = policy.policy[-2]
+            last.weight.mul_(0.01)
+            last.bias.zero_()
+            last.bias[cls.act_dim:] = -1.5
+    logps = []
+
+    def make_dist(logits):
+        dist = policy.get_act_dist_cls(logits)
+        orig = dist.sample
+
+        def sample():
+            a, lp = orig()
+            logps.append(lp.detach().numpy().astype(F32).copy())
+            return a, lp
+        dist.sample = sample
+        return dist
+    return policy, make_dist, logps
+
+
+def _trace_env(name, E, T, seed, trunc_frac=4):
+    rng = np.random.default_rng(seed + 17 * OE.ENV_IDS[name])
+    mod = load_env(name)
+    cls = OE.ENVS[name]
+
+    def draw(k):
+        if name == "QuadTracking":
+            return cls.reset_draw(rng, k, gauss=lambda m: rng.standard_normal((m, 3)))
+        return cls.reset_draw(rng, k)
+    init_resets = draw(E)
+    init_steps = np.zeros(E, np.int64)
+    if name != "QuadTracking":
+        init_steps[: E // trunc_frac] = 1000 - 7
+    venv = RefVectorEnv(mod, name, E, init_resets, init_steps, draw(E * T))
+    return venv, init_resets, init_steps
+
+
+def gen_step_trace(name, E=24, T=30, seed=4):
+    """BaseSampler._step (base.py:225-298), the OffSampler's per-step path, with recorded
+    actions/resets; every step's Experience list is stored as [T][E] arrays."""
+    import torch
+    torch.manual_seed(seed)
+    base, _ = load_ref_methods("RL/trainer/sampler/base.py", "BaseSampler", ["_step"],
+                               skip_modules=("RL.create_pkg.create_envs",))
+    venv, init_resets, init_steps = _trace_env(name, E, T, seed)
+    policy, make_dist, logps = _ref_policy_and_recorder(name)
+    net = types.SimpleNamespace(policy=policy, create_action_distributions=make_dist)
+    smp = types.SimpleNamespace(env_id=name, num_envs=E, envs=venv, networks=net, noise_params=None,
+                                action_type="continu", reward_scale=100.0, cost_scale=100.0, target_value=0.0,
+                                obs=venv.obs0.astype(F32).copy())
+    _step = types.MethodType(base["_step"], smp)
+    keys = ("obs", "act", "rew", "cost", "obs2", "done", "logp")
+    rec = {k: [] for k in keys}
+    with torch.no_grad():
+        for t in range(T):
+            exps = _step()
+            assert len(exps) == E
+            for k, j in zip(keys, range(7)):
+                rec[k].append(np.stack([np.asarray(ex[j], F32) for ex in exps]))
+    d = dict(init_reset=init_resets, init_steps=init_steps.astype(np.int32), actions=np.stack(venv.log_actions),
+             logp=np.stack(logps), resets=np.stack(venv.log_resets))
+    for k in keys:
+        d["x_" + k] = np.stack(rec[k])
+    np.savez_compressed(os.path.join(OUT, f"step_{name}.npz"), **d)
+    print(f"step_{name}: E={E} T={T} dones={int(d['x_done'].sum())}")
+
+
+def gen_onpolicy_trace(name, E=16, H=40, seed=6):
+    """OnSampler._sample (on_sampler.py:44-79) incl. _process_experiences/_finish_trajs (GAE),
+    compiled from the reference source, over reference envs with a reference StateValue net."""
+    import torch
+    from RL.apprfunc.mlp import StateValue
+    torch.manual_seed(seed)
+    base, bns = load_ref_methods("RL/trainer/sampler/base.py", "BaseSampler", ["_step"],
+                                 skip_modules=("RL.create_pkg.create_envs",))
+    on, _ = load_ref_methods("RL/trainer/sampler/on_sampler.py", "OnSampler",
+                             ["_sample", "_process_experiences", "_finish_trajs"],
+                             skip_modules=("RL.trainer.sampler.base",), extra_ns={"Experience": bns["Experience"]})
+    cls = OE.ENVS[name]
+    venv, init_resets, init_steps = _trace_env(name, E, H, seed, trunc_frac=3)
+    policy, make_dist, logps = _ref_policy_and_recorder(name)
+    value = StateValue(obs_dim=cls.obs_dim, hidden_sizes=[64, 64], hidden_activation="relu",
+                       output_activation="linear")
+    vcalls = []
+
+    def value_fn(x):
+        out = value(x)
+        vcalls.append(out.detach().numpy().astype(F32).copy())
+        return out
+    net = types.SimpleNamespace(policy=policy, value=value_fn, create_action_distributions=make_dist)
+    D, A = cls.obs_dim, cls.act_dim
+    z = lambda *s, dt=F32: np.zeros(s, dtype=dt)  # noqa: E731
+    smp = types.SimpleNamespace(env_id=name, num_envs=E, envs=venv, networks=net, noise_params=None,
+                                action_type="continu", reward_scale=100.0, cost_scale=100.0, target_value=0.0,
+                                obs=venv.obs0.astype(F32).copy(), horizon=H, gamma=0.99, gae_lambda=0.95,
+                                obs_dim=(D,), act_dim=(A,), mb_obs=z(E, H, D), mb_obs2=z(E, H, D), mb_act=z(E, H, A),
+                                mb_rew=z(E, H), mb_cost=z(E, H), mb_logp=z(E, H), mb_done=z(E, H, dt=np.bool_),
+                                mb_val=z(E, H), mb_adv=z(E, H), mb_ret=z(E, H))
+    for nm, fn in list(base.items()) + list(on.items()):
+        setattr(smp, nm, types.MethodType(fn, smp))
+    with torch.no_grad():
+        out = smp._sample()
+    out = {k: v.numpy() for k, v in out.items()}
+    # bootstrap values V(real_next_obs) of the single-row calls, in call order (t-major, env order)
+    done = out["done"].reshape(E, H)
+    v2 = np.full((E, H), np.nan, F32)
+    it = iter(c for c in vcalls if c.shape == (1,))
+    for t in range(H):
+        for i in range(E):
+            if done[i, t] or t == H - 1:
+                v2[i, t] = next(it)[0]
+    d = dict(init_reset=init_resets, init_steps=init_steps.astype(np.int32), actions=np.stack(venv.log_actions),
+             logp_sampled=np.stack(logps), resets=np.stack(venv.log_resets), val2=v2, H=np.int64(H),
+             gamma=np.float64(0.99), gae_lambda=np.float64(0.95))
+    for k, v in out.items():
+        d["mb_" + k] = v
+    for k, v in value.state_dict().items():
+        d["value/" + k] = v.numpy().copy()
+    np.savez_compressed(os.path.join(OUT, f"onpolicy_{name}.npz"), **d)
+    print(f"onpolicy_{name}: E={E} H={H} dones={int(done.sum())}")
+
+
 # ---------------------------------------------------------------------- MSACL update
 def gen_msacl(B=64, n=20, seed=11):
     import torch
@@ -392,9 +551,135 @@ def gen_msacl(B=64, n=20, seed=11):
     print("msacl_update:", {k: round(float(v), 6) for k, v in tb0.items()}, "eps draws:", len(eps_log))
 
 
+# ---------------------------------------------------------------------- SAC / LAC / PPO / POLYC updates
+def _alg_kwargs(env="QuadTracking", hidden=64):
+    cls = OE.ENVS[env]
+    return dict(env_name=env, obs_dim=cls.obs_dim, act_dim=cls.act_dim, action_type="continu",
+                action_high_limit=cls.act_high.copy(), action_low_limit=cls.act_low.copy(),
+                value_func_type="MLP", value_hidden_sizes=[hidden, hidden], value_hidden_activation="relu",
+                value_output_activation="linear", policy_func_name="StochaPolicy", policy_func_type="MLP",
+                policy_act_distribution="TanhGaussDistribution", policy_hidden_sizes=[hidden, hidden],
+                policy_hidden_activation="relu", policy_min_log_std=-20, policy_max_log_std=1, target_value=0.0)
+
+
+def _off_batch(rng, env, B):
+    cls = OE.ENVS[env]
+    D, A = cls.obs_dim, cls.act_dim
+    obs = (rng.standard_normal((B, D)) * 0.3).astype(F32)
+    obs2 = (obs + rng.standard_normal((B, D)).astype(F32) * 0.05).astype(F32)
+    act = (cls.act_low + (cls.act_high - cls.act_low) * rng.uniform(0.05, 0.95, size=(B, A))).astype(F32)
+    done = np.zeros(B, F32)
+    done[rng.choice(B, B // 8, replace=False)] = 1.0
+    return dict(obs=obs, act=act, rew=(rng.standard_normal(B) * 10).astype(F32),
+                cost=rng.uniform(0, 5, size=B).astype(F32), obs2=obs2, done=done,
+                logp=(rng.standard_normal(B)).astype(F32))
+
+
+def _record_updates(alg, data_np, calls, tag, extra_fn=None):
+    """Run `calls` (list of callables taking a fresh torch data dict) with the Normal.rsample
+    noise recorded; store inputs, weights before/after each call, tb values of the first."""
+    import torch
+    import torch.distributions.normal as tdn
+    init_sd = {k: v.detach().numpy().copy() for k, v in alg.networks.state_dict().items()}
+    eps_log = []
+    orig = tdn._standard_normal
+
+    def rec(shape, dtype, device):
+        e = orig(shape, dtype=dtype, device=device)
+        eps_log.append(e.detach().numpy().copy())
+        return e
+    tdn._standard_normal = rec
+    d = {"in_" + k: v for k, v in data_np.items()}
+    for k, v in init_sd.items():
+        d["init/" + k] = v
+    try:
+        for i, call in enumerate(calls):
+            data = {k: torch.from_numpy(v.copy()) for k, v in data_np.items()}
+            out = call(data)
+            tb = out[0] if isinstance(out, tuple) else out
+            if tb is not None and "tb_keys" not in d:
+                d["tb_keys"] = np.array(list(tb.keys()))
+                d["tb_vals"] = np.array([float(v) for v in tb.values()])
+            for k, v in alg.networks.state_dict().items():
+                d[f"after{i}/" + k] = v.detach().numpy().copy()
+    finally:
+        tdn._standard_normal = orig
+    for i, e in enumerate(eps_log):
+        d[f"eps{i}"] = e
+    d["n_eps"] = np.int64(len(eps_log))
+    d.update(extra_fn() if extra_fn else {})
+    np.savez_compressed(os.path.join(OUT, f"{tag}_update.npz"), **d)
+    print(f"{tag}_update:", {k: round(float(v), 5) for k, v in zip(d.get("tb_keys", []), d.get("tb_vals", []))},
+          "eps draws:", len(eps_log))
+
+
+def gen_algs(seed=21):
+    import torch
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    from RL.algorithm.lac import LAC
+    from RL.algorithm.polyc import POLYC
+    from RL.algorithm.ppo import PPO
+    from RL.algorithm.sac import SAC
+
+    # SAC: two model_update calls (iteration 0: Q + target + 2 policy/alpha steps; 1: Q + target)
+    torch.manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    kw = _alg_kwargs()
+    kw.update(value_func_name="ActionValue", q_learning_rate=1e-3, policy_learning_rate=3e-4, alpha_learning_rate=1e-3,
+              gamma=0.99, tau=0.005, alpha=1.0, auto_alpha=True, policy_frequency=2, target_network_frequency=1)
+    alg = SAC(**kw)
+    data = _off_batch(rng, "QuadTracking", 64)
+    _record_updates(alg, data, [lambda d: alg.model_update(d, 0), lambda d: alg.model_update(d, 1)], "sac")
+
+    torch.manual_seed(seed + 1)
+    rng = np.random.default_rng(seed + 1)
+    kw = _alg_kwargs("Pendulum")
+    kw.update(value_func_name="ActionValue", l_learning_rate=1e-3, policy_learning_rate=3e-4, alpha_learning_rate=1e-3,
+              beta_learning_rate=1e-3, gamma=0.99, tau=0.005, alpha=1.0, beta=1.0, auto_alpha=True, alpha3=0.01,
+              policy_frequency=2, target_network_frequency=1)
+    alg = LAC(**kw)
+    data = _off_batch(rng, "Pendulum", 64)
+    _record_updates(alg, data, [lambda d: alg.model_update(d, 0), lambda d: alg.model_update(d, 1)], "lac")
+
+    # PPO / POLYC: one model_update on a synthetic on-policy batch; np.random drives the shuffles
+    for tag, Alg in (("ppo", PPO), ("polyc", POLYC)):
+        torch.manual_seed(seed + 2)
+        rng = np.random.default_rng(seed + 2)
+        env = "DuctedFan"
+        kw = _alg_kwargs(env)
+        cls = OE.ENVS[env]
+        kw.update(value_func_name="StateValue", lyapunov_func_name="LyapunovValue", lyapunov_func_type="MLP",
+                  lyapunov_hidden_sizes=[64, 64], lyapunov_hidden_activation="tanh", lyapunov_output_dim=32,
+                  lyapunov_output_activation="linear", lyapunov_single_input_dim=False, learning_rate=1e-3,
+                  policy_learning_rate=3e-4, loss_coefficient_value=1.0, loss_coefficient_entropy=0.01,
+                  loss_coefficient_kl=0.2, loss_value_clip=True, value_clip=0.5, beta=0.3, gamma=0.99,
+                  schedule_adam="linear", schedule_clip="linear", clip=0.1, max_iteration=100, num_repeat=2,
+                  num_mini_batch=4, mini_batch_size=16, sample_batch_size=64, env_num=2)
+        if tag == "polyc":  # polyc.py:36 builds the Lyapunov net from the TOP-LEVEL kwargs
+            kw.update(apprfunc="MLP", name="LyapunovValue", input_dim=cls.obs_dim, output_dim=32, hidden_sizes=[64, 64],
+                      hidden_activation="tanh", output_activation="linear")
+        alg = Alg(**kw)
+        N = 128
+        D, A = cls.obs_dim, cls.act_dim
+        obs = (rng.standard_normal((N, D)) * 0.3).astype(F32)
+        act = (cls.act_low + (cls.act_high - cls.act_low) * rng.uniform(0.05, 0.95, size=(N, A))).astype(F32)
+        with torch.no_grad():
+            dist = alg.networks.create_action_distributions(alg.networks.policy(torch.from_numpy(obs)))
+            lp = dist.log_prob(torch.from_numpy(act)).numpy()
+        data = dict(obs=obs, obs2=(obs + rng.standard_normal((N, D)).astype(F32) * 0.05).astype(F32), act=act,
+                    rew=(rng.standard_normal(N)).astype(F32), cost=rng.uniform(0, 5, N).astype(F32),
+                    done=np.zeros(N, np.bool_), logp=(lp + rng.normal(0, 0.3, N)).astype(F32),
+                    adv=(rng.standard_normal(N) * 2).astype(F32), ret=(rng.standard_normal(N) * 3).astype(F32),
+                    val=(rng.standard_normal(N) * 3).astype(F32))
+        np.random.seed(seed + 3)
+        _record_updates(alg, data, [lambda d: alg.model_update(d)], tag,
+                        extra_fn=lambda: dict(np_seed=np.int64(seed + 3), indices_after=alg.indices.copy()))
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    which = sys.argv[1:] or ["env", "reset", "nstep", "msacl"]
+    which = sys.argv[1:] or ["env", "reset", "nstep", "msacl", "step", "onpolicy", "algs"]
     if "env" in which:
         for nm in OE.ENVS:
             gen_env_pairs(nm)
@@ -406,3 +691,11 @@ if __name__ == "__main__":
         gen_nstep_trace("VanderPol", E=16, T=60, n_step=20, seed=5, tag="_n20")
     if "msacl" in which:
         gen_msacl()
+    if "step" in which:
+        for nm in ("VanderPol", "TwoLink", "QuadTracking"):
+            gen_step_trace(nm)
+    if "algs" in which:
+        gen_algs()
+    if "onpolicy" in which:
+        for nm in ("Pendulum", "DuctedFan", "QuadTracking"):
+            gen_onpolicy_trace(nm)
