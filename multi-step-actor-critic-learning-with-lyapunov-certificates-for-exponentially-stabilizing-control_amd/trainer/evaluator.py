@@ -1,8 +1,12 @@
 """Deterministic-policy evaluation on the device env kernels (RL/trainer/evaluator.py:9-212).
 
-Same metric as the reference: every eval env runs one episode with the distribution's mode()
-action; per-episode per-step-mean reward and cost (rew_plus_cost scales), then mean/std over
-episodes. The rollout is the HIP env step; the loop checks completion on the host each step.
+Same metrics as the reference: parallel evaluation runs num_eval_episode envs in lockstep, one
+episode each with the distribution's mode() action, and reports the mean/std over episodes of
+the per-step MEAN scaled reward and cost (rew_plus_cost scales); sequential evaluation runs
+episodes on one env and reports mean/std of the episode SUMS. The rollout is the HIP env step
+kernel; per-episode means accumulate on the device in float64 (the reference's np.mean of a
+float32 list sums pairwise in float32), episode sums in float32 in step order exactly like the
+reference's sum(); completion is checked on the host once every 8 lockstep steps.
 """
 import numpy as np
 import torch
@@ -35,42 +39,63 @@ class Evaluator:
         self.networks.load_state_dict(state_dict)
 
     @torch.no_grad()
-    def _episodes(self):
-        obs, _ = self.envs.reset()
+    def _episodes(self, initial_states=None):
+        """Run every env until its first episode ends (mode() actions). Returns per-env sums of
+        the scaled reward and cost over the episode and the episode lengths (float64).
+        `initial_states` [E][reset_dim] injects the initial states (parity mode); resets after
+        an env's episode ended do not enter the metric, so they are never injected."""
+        obs, _ = self.envs.reset(reset_states=initial_states)
         E = self.envs.num_envs
         dev = self.device
         sum_r = torch.zeros(E, dtype=torch.float64, device=dev)
         sum_c = torch.zeros(E, dtype=torch.float64, device=dev)
         cnt = torch.zeros(E, dtype=torch.float64, device=dev)
+        # float32 running sums in step order: the reference's run_an_episode uses Python's
+        # sum() over float32 scalars (evaluator.py:114-115), i.e. sequential float32 adds
+        sum_r32 = torch.zeros(E, dtype=torch.float32, device=dev)
+        sum_c32 = torch.zeros(E, dtype=torch.float32, device=dev)
         finished = torch.zeros(E, dtype=torch.bool, device=dev)
-        for _ in range(self.max_eval_steps + 1):
+        for k in range(self.max_eval_steps + 1):
             act = self.networks.create_action_distributions(self.networks.policy(obs)).mode().float().contiguous()
             nxt, rew, term, trunc, info = self.envs.step(act)
             real = info["final_observation"]
-            r = rew * self.reward_scale
+            r = rew * self.reward_scale                                  # rew_plus_cost.py:18-21
             c = (real ** 2).sum(dim=1) * self.cost_scale
             live = (~finished).double()
             sum_r += r.double() * live
             sum_c += c.double() * live
+            sum_r32 = torch.where(finished, sum_r32, sum_r32 + r)
+            sum_c32 = torch.where(finished, sum_c32, sum_c32 + c)
             cnt += live
             finished |= term | trunc
             obs = nxt
-            if bool(finished.all()):
+            if k % 8 == 7 and bool(finished.all()):  # one host sync per 8 lockstep steps
                 break
+        self._last_sums32 = (sum_r32, sum_c32)
+        return sum_r, sum_c, cnt
+
+    def run_parallel_episodes(self, initial_states=None):
+        """evaluator.py:145-197: per-episode per-step-MEAN reward/cost, then mean/std over the
+        num_eval_episode parallel episodes."""
+        sum_r, sum_c, cnt = self._episodes(initial_states)
         ret = (sum_r / cnt.clamp_min(1)).cpu().numpy()
         cost = (sum_c / cnt.clamp_min(1)).cpu().numpy()
-        return ret, cost
-
-    def run_parallel_episodes(self):
-        ret, cost = self._episodes()
         return np.mean(ret), np.std(ret), np.mean(cost), np.std(cost)
 
-    def run_n_episodes(self, n, iteration):
+    def run_an_episode(self, iteration, render=False, initial_state=None):
+        """evaluator.py:59-117: episode SUM of reward and cost of env 0 (float32 running sum)."""
+        self._episodes(initial_state)
+        sum_r32, sum_c32 = self._last_sums32
+        return float(sum_r32[0]), float(sum_c32[0])
+
+    def run_n_episodes(self, n, iteration, initial_states=None):
+        """evaluator.py:119-134: n sequential episodes, mean/std of their sums."""
         rets, costs = [], []
-        for _ in range(n):
-            r, c = self._episodes()
-            rets.append(float(r[0]))
-            costs.append(float(c[0]))
+        for i in range(n):
+            r, c = self.run_an_episode(iteration, self.render,
+                                       None if initial_states is None else initial_states[i:i + 1])
+            rets.append(r)
+            costs.append(c)
         return np.mean(rets), np.std(rets), np.mean(costs), np.std(costs)
 
     def run_evaluation(self, iteration):

@@ -81,3 +81,30 @@ def test_on_policy_train_loop(tmp_path, alg_name):
     data, _ = sampler.sample()
     assert data["obs"].shape == (512 * 64, 6) and data["done"].dtype == torch.bool
     assert torch.isfinite(data["adv"]).all() and torch.isfinite(data["ret"]).all()
+
+
+@pytest.mark.parametrize("name", ["VanderPol", "DuctedFan", "QuadTracking"])
+def test_evaluator_matches_reference(tmp_path, name):
+    """Parallel and sequential evaluation vs the reference Evaluator (tests/golden/eval_*.npz):
+    same policy weights, same initial states. Deterministic mode() actions; the metric equals the
+    reference's to 1e-4 relative (GPU vs CPU policy GEMMs differ in the last ulp and the
+    reference accumulates in float32, the device in float64)."""
+    from msacl_amd.create_pkg.create_evaluator import create_evaluator
+    from msacl_amd.create_pkg.create_envs import create_envs
+    from msacl_amd.utils.init_args import init_args
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"eval_{name}.npz"))
+    E = g["init"].shape[0]
+    args = default_msacl_args(env_name=name, env_num=4, save_folder=str(tmp_path), seed=0, num_eval_episode=E,
+                              policy_hidden_sizes=[64, 64], value_hidden_sizes=[64, 64], lyapunov_hidden_sizes=[64, 64])
+    args = init_args(create_envs(**args), **args)
+    ev = create_evaluator(**args)
+    ev.networks.policy.load_state_dict({k[7:]: torch.as_tensor(g[k]) for k in g.files if k.startswith("policy/")})
+    ev.networks.to(ev.device)
+    par = ev.run_parallel_episodes(initial_states=g["init"])
+    np.testing.assert_allclose(par, g["parallel"], rtol=1e-4, atol=1e-3)
+    args1 = dict(args, is_parallel_eval=False)
+    ev1 = create_evaluator(**args1)
+    ev1.networks.load_state_dict(ev.networks.state_dict())
+    ev1.networks.to(ev1.device)
+    seq = ev1.run_n_episodes(3, 0, initial_states=g["seq_init"])
+    np.testing.assert_allclose(seq, g["sequential"], rtol=1e-4, atol=1e-2)

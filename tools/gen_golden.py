@@ -472,6 +472,58 @@ def gen_onpolicy_trace(name, E=16, H=40, seed=6):
     print(f"onpolicy_{name}: E={E} H={H} dones={int(done.sum())}")
 
 
+def gen_evaluator(name, E=8, seed=9):
+    """Evaluator.run_parallel_episodes and run_an_episode (RL/trainer/evaluator.py:59-204),
+    compiled from the reference source, with a reference StochaPolicy (mode() actions) and
+    injected initial states (resets after an episode's end do not enter the metric)."""
+    import torch
+    torch.manual_seed(seed)
+    ev, _ = load_ref_methods("RL/trainer/evaluator.py", "Evaluator", ["run_parallel_episodes", "run_an_episode",
+                                                                      "run_n_episodes"],
+                             skip_modules=("RL.create_pkg.create_envs",))
+    cls = OE.ENVS[name]
+    rng = np.random.default_rng(seed)
+
+    def draw(k):
+        if name == "QuadTracking":
+            return cls.reset_draw(rng, k, gauss=lambda m: rng.standard_normal((m, 3)))
+        return cls.reset_draw(rng, k)
+    init = draw(E)
+    seq_init = draw(3)
+    policy, make_dist, _ = _ref_policy_and_recorder(name)
+    net = types.SimpleNamespace(policy=policy, create_action_distributions=lambda lg: policy.get_act_dist_cls(lg))
+    mod = load_env(name)
+
+    class EvalEnvs(RefVectorEnv):
+        def __init__(self, inits):
+            self.inits = list(inits)
+            super().__init__(mod, name, len(self.inits[0]), self.inits[0], np.zeros(len(self.inits[0]), np.int64),
+                             draw(4096))
+            self.k = 0
+
+        def reset(self, seed=None):
+            rs = self.inits[self.k]
+            self.k += 1
+            for i, e in enumerate(self.envs):
+                e.current_step = 0
+            return np.stack([ref_reset(self.mod, e, self.name, rs[i]) for i, e in enumerate(self.envs)]), {}
+
+    def make_self(envs, n):
+        smp = types.SimpleNamespace(env_id=name, envs=envs, networks=net, target_value=0.0, cost_scale=100.0,
+                                    reward_scale=100.0, num_eval_episode=n, render=False)
+        for nm, fn in ev.items():
+            setattr(smp, nm, types.MethodType(fn, smp))
+        return smp
+    with torch.no_grad():
+        par = make_self(EvalEnvs([init]), E).run_parallel_episodes()
+        seq = make_self(EvalEnvs([seq_init[i:i + 1] for i in range(3)]), 1).run_n_episodes(3, 0)
+        # per-episode lengths of the parallel run, for the test's diagnostics
+    np.savez_compressed(os.path.join(OUT, f"eval_{name}.npz"), init=init, seq_init=seq_init,
+                        parallel=np.array(par, np.float64), sequential=np.array(seq, np.float64),
+                        **{"policy/" + k: v.numpy().copy() for k, v in policy.state_dict().items()})
+    print(f"eval_{name}: parallel={np.round(par, 4)} sequential={np.round(seq, 4)}")
+
+
 # ---------------------------------------------------------------------- MSACL update
 def gen_msacl(B=64, n=20, seed=11):
     import torch
@@ -679,7 +731,7 @@ def gen_algs(seed=21):
 
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    which = sys.argv[1:] or ["env", "reset", "nstep", "msacl", "step", "onpolicy", "algs"]
+    which = sys.argv[1:] or ["env", "reset", "nstep", "msacl", "step", "onpolicy", "algs", "eval"]
     if "env" in which:
         for nm in OE.ENVS:
             gen_env_pairs(nm)
@@ -694,6 +746,9 @@ if __name__ == "__main__":
     if "step" in which:
         for nm in ("VanderPol", "TwoLink", "QuadTracking"):
             gen_step_trace(nm)
+    if "eval" in which:
+        for nm in ("VanderPol", "DuctedFan", "QuadTracking"):
+            gen_evaluator(nm)
     if "algs" in which:
         gen_algs()
     if "onpolicy" in which:
