@@ -9,6 +9,7 @@ events (tools/gputime.py), algorithmic bytes per launch, achieved GB/s and the f
   +emit         followed by the fused window emission into an HBM store, E = 65,536
   gather        mh_replay_gather of B windows (random indices) from a 1M-window store
   msacl         q_target / lyapunov / stability_adv / ppo_clip at the replay batch B = 256, n = 20
+  gae           mh_gae over [E][H] on-policy trajectory blocks (65,536 x 64 and 65,536 x 1,600)
 
 Prints one JSON object per line; --out writes the list as JSON.
 Usage: python tools/kernel_bench.py [--sizes 65536,4194304] [--reps 20] [--out file]
@@ -193,6 +194,25 @@ def bench_msacl(reps, dev, B=256, n=20, D=12):
     return res
 
 
+def bench_gae(E, H, reps, dev, p_done=0.02):
+    """mh_gae over an [E][H] trajectory block (on-policy sampler, csrc/gae.hip)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    val = torch.randn(E, H, device=dev, generator=g)
+    val2 = torch.randn(E, H, device=dev, generator=g)
+    rew = torch.randn(E, H, device=dev, generator=g)
+    done = (torch.rand(E, H, device=dev, generator=g) < p_done).to(torch.uint8)
+    adv, ret = torch.empty(E, H, device=dev), torch.empty(E, H, device=dev)
+    st = N.stream_of(dev)
+
+    def fn():
+        N.lib().mh_gae(N.ptr(val), N.ptr(val2), N.ptr(rew), N.ptr(done), E, H, 0.99, 0.95, N.ptr(adv), N.ptr(ret), st)
+    ms = time_launches(fn, reps)
+    # val, rew, done in + adv, ret out, plus the bootstrap read at every segment end
+    per = 4 + 4 + 1 + 4 + 4 + 4 * (p_done + 1.0 / H)
+    return row("gae", "-", E * H, "steps", round(per, 3), ms, envs=E, horizon=H)
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--sizes", default="65536,4194304")
@@ -218,6 +238,9 @@ def main():
             rows.append(bench_gather("QuadTracking", B, a.reps, dev))
     if "msacl" not in skip:
         rows += bench_msacl(a.reps, dev)
+    if "gae" not in skip:
+        for E, H in ((65536, 64), (65536, 1600)):
+            rows.append(bench_gae(E, H, a.reps, dev))
     if a.out:
         with open(a.out, "w") as f:
             json.dump(rows, f, indent=1)
