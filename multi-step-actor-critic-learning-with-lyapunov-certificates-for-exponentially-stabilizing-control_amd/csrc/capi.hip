@@ -1,5 +1,6 @@
 // capi.hip — C ABI (include/msacl_hip.h): env handles, lockstep rollout, window store, gather.
 #include <string>
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -106,6 +107,11 @@ struct mh_env_s {
     a.log_std_lo = log_std_lo;
     a.log_std_hi = log_std_hi;
     a.act_noise = act_noise;
+    // TanhGaussDistribution's constant log-Jacobian term, torch.log((high - low) / 2).sum(-1)
+    // (act_distribution_cls.py:51-55), once on the host in float32
+    float ls = 0.0f;
+    for (int i = 0; i < info.act_dim; ++i) ls = ls + logf((info.act_high[i] - info.act_low[i]) / 2.0f);
+    a.log_half_sum = ls;
     return a;
   }
 };

@@ -478,7 +478,7 @@ struct SingleTrackCar {
 // ---------------------------------------------------------------- QuadTracking
 // RL/env/QuadTracking.py:20-424. Persistent f32 state x[3] v[3] R[9] (row-major) W[3];
 // float64 Rd_last[9]; desired trajectory rows are a host table indexed by steps-since-reset.
-constexpr int QT_ROW = 16;  // T, DT, XD[3], B1[3], VD[3] (f32 values), AD[3] (f32 values), pad[2]
+constexpr int QT_ROW = 16;  // T, DT, XD[3], B1[3], VD[3] (f32 values), AD[3] (f32 values), pad, 1/DT
 
 struct QuadConst {
   static constexpr double m = 4.34;
@@ -545,13 +545,83 @@ MH_HD void ns_step3_mixed(double* X, const double* G) {
     }
 }
 
+// Third-order Newton-Schulz step X <- X (15I - 10G + 3G^2)/8 = X (I - E/2 + 3E^2/8), E = G - I
+// (the binomial series of G^{-1/2} to second order): max|X^T X - I| goes e -> ~(5/8) e^3, so a
+// rotation perturbed by one Euler substep (e ~ 1e-4 .. 1e-2) is at ~1e-7 after ONE step where
+// the quadratic iteration needs two or three. G is symmetric; E^2 uses its 6 unique entries.
+MH_HD void ns3_step3(double* X, const double* G) {
+  const double E00 = G[0] - 1.0, E11 = G[4] - 1.0, E22 = G[8] - 1.0;
+  const double E01 = G[1], E02 = G[2], E12 = G[5];
+  const double Q00 = fma(E02, E02, fma(E01, E01, E00 * E00));
+  const double Q11 = fma(E12, E12, fma(E11, E11, E01 * E01));
+  const double Q22 = fma(E22, E22, fma(E12, E12, E02 * E02));
+  const double Q01 = fma(E02, E12, fma(E01, E11, E00 * E01));
+  const double Q02 = fma(E02, E22, fma(E01, E12, E00 * E02));
+  const double Q12 = fma(E12, E22, fma(E11, E12, E01 * E02));
+  const double M[9] = {fma(0.375, Q00, -0.5 * E00), fma(0.375, Q01, -0.5 * E01), fma(0.375, Q02, -0.5 * E02),
+                       fma(0.375, Q01, -0.5 * E01), fma(0.375, Q11, -0.5 * E11), fma(0.375, Q12, -0.5 * E12),
+                       fma(0.375, Q02, -0.5 * E02), fma(0.375, Q12, -0.5 * E12), fma(0.375, Q22, -0.5 * E22)};
+  double Y[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      double acc = X[i * 3 + 0] * M[0 * 3 + j];
+      acc = fma(X[i * 3 + 1], M[1 * 3 + j], acc);
+      acc = fma(X[i * 3 + 2], M[2 * 3 + j], acc);
+      Y[i * 3 + j] = X[i * 3 + j] + acc;
+    }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) X[i] = Y[i];
+}
+
 // Orthogonal polar factor of a float32 3x3, with the det<0 column flip of
 // NormalizeOrientMatrix (QuadTracking.py:308-315; U @ Vh of a float32 SVD).
 // The integrator keeps R within ~(0.01|W|)^2 of SO(3), where Newton-Schulz converges
 // quadratically without a division (2-3 steps to max|X^T X - I| < 1e-12, i.e. the
 // float64-exact polar factor before the final rounding). Inputs farther than 0.25 from
 // orthogonal take the float64 Newton iteration X <- (X + X^-T)/2.
+MH_HD void polar3_general(const float* Rin, float* Rout);
+
+// Fast path for what the integrator produces every substep: a proper rotation perturbed by one
+// Euler step (max|X^T X - I| = e < 0.25, det > 0). One or two third-order steps bring e to
+// < 1e-6 (e -> ~(5/8) e^3), then, when e is still >= 1e-12, one quadratic step with its f32
+// correction finishes (error < 1e-12 before the final rounding): straight-line code without the
+// general routine's iteration control, determinant and rare-branch code, converging to the same
+// float64 polar factor (the final float32 rounding differs in ~3 of 1e6 elements, by 1 ulp).
 MH_HD void polar3(const float* Rin, float* Rout) {
+#ifdef MH_EXP_NO_POLAR  // cost-attribution experiment only (tools/exp_variants.sh)
+  for (int i = 0; i < 9; ++i) Rout[i] = Rin[i];
+  return;
+#endif
+  double X[9], G[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) X[i] = (double)Rin[i];
+  double e = orth_err3<double>(X, G);
+  // sign of det: |det| is within a few % of 1 here, so float32 decides it exactly
+  const float det = Rin[0] * (Rin[4] * Rin[8] - Rin[5] * Rin[7]) - Rin[1] * (Rin[3] * Rin[8] - Rin[5] * Rin[6]) +
+                    Rin[2] * (Rin[3] * Rin[7] - Rin[4] * Rin[6]);
+  if (__builtin_expect(e < 0.25 && det > 0.5f, 1)) {
+    if (e >= 1e-7) {
+      ns3_step3(X, G);
+      e = orth_err3<double>(X, G);
+    }
+    if (e >= 1e-6) {  // e0 in [~0.01, 0.25): a second third-order step (0.25 -> 0.01 -> 6e-7)
+      ns3_step3(X, G);
+      e = orth_err3<double>(X, G);
+    }
+    if (__builtin_expect(e < 1e-6, 1)) {
+      if (e >= 1e-12) ns_step3_mixed(X, G);  // e -> 0.75 e^2 + ~3e-14
+#pragma unroll
+      for (int i = 0; i < 9; ++i) Rout[i] = (float)X[i];
+      return;
+    }
+  }
+  polar3_general(Rin, Rout);
+}
+
+// General polar factor: any conditioning, det < 0 flip.
+MH_HD void polar3_general(const float* Rin, float* Rout) {
   double X[9], G[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) X[i] = (double)Rin[i];
@@ -559,8 +629,14 @@ MH_HD void polar3(const float* Rin, float* Rout) {
   const bool near = e < 0.25;
   if (near) {
     for (int it = 0; it < 8 && e >= 1e-12; ++it) {
+      if (e < 1e-7) {  // quadratic step, f32 correction: e -> 0.75 e^2 + ~3e-14 < 1e-13, done
+        ns_step3_mixed(X, G);
+        break;
+      }
       if (e < 1e-6)
         ns_step3_mixed(X, G);
+      else if (e < 0.05)
+        ns3_step3(X, G);
       else
         ns_step3(X, G);
       e = orth_err3<double>(X, G);
@@ -714,7 +790,7 @@ struct QuadTracking {
     float Od[3] = {0.0f, 0.0f, 0.0f};
     double Odd[3] = {0.0, 0.0, 0.0};
     if (have_last) {
-      const double idt = 1.0 / row[1];
+      const double idt = row[15];  // 1.0 / row[1], tabulated (quad_fill_table)
       float Rdot[9];
       for (int i = 0; i < 9; ++i) Rdot[i] = (float)((Rd[i] - Rdl[i]) * idt);   // RDerive
       // getOmega: So3ToVec(Rd^T @ Rdot) -> f32
@@ -763,7 +839,11 @@ struct QuadTracking {
     const float f = a[0];
     const float* M = a + 1;
     const float mf = (float)Q::m;
+#ifdef MH_EXP_NO_SUBSTEPS  // cost-attribution experiment only
+    for (int it = 0; it < 0; ++it) {
+#else
     for (int it = 0; it < K; ++it) {
+#endif
       float* x = s;
       float* v = s + 3;
       float* R = s + 6;
@@ -792,9 +872,14 @@ struct QuadTracking {
       for (int i = 0; i < 9; ++i) R[i] = Rn[i];
     }
     const double* row = tab + (size_t)(k + 1) * QT_ROW;
+#ifdef MH_EXP_NO_DESIRED  // cost-attribution experiment only
+    for (int i = 0; i < 12; ++i) obs[i] = s[i] * 1e-3f;
+    (void)row;
+#else
     double Rd[9];
     desired_and_obs(s, row, true, xs, Rd, obs);
     for (int i = 0; i < 9; ++i) xs[i] = Rd[i];
+#endif
     // reward (QuadTracking.py:250-273), reward type 1 (linear bonus)
     float sx[3], sv[3], sr[3], sw[3], su[4];
     for (int i = 0; i < 3; ++i) {
@@ -850,7 +935,7 @@ inline void quad_fill_table(double* tab, int rows) {
     r[12] = (double)(float)(-0.4 * sin(t));
     r[13] = (double)(float)(-0.6 * cos(t));
     r[14] = 0.0;
-    r[15] = 0.0;
+    r[15] = 1.0 / dt;  // reciprocal of the step for Omega_d = vee(Rd^T (Rd - Rd_last) / dt)
   }
 }
 

@@ -51,6 +51,24 @@ struct Rng {
     out[2] = b * c4;
     out[3] = b * s4;
   }
+  // 4 standard normals via Box-Muller on the hardware transcendentals (v_log_f32, v_sqrt_f32,
+  // v_sin_f32/v_cos_f32, which take the angle in revolutions: sin(2 pi u) = v_sin_f32(u)).
+  // ~1 ulp each; used for the policy's action noise, whose values are distribution-matched only
+  // (torch's CPU generator cannot be replayed on the device).
+  __device__ __forceinline__ void normal4f_fast(uint32_t stream, float* out) const {
+    u32x4 r = draw(stream);
+    const float u1 = 1.0f - (float)(r.x >> 8) * 5.9604644775390625e-08f;
+    const float u2 = (float)(r.y >> 8) * 5.9604644775390625e-08f;
+    const float u3 = 1.0f - (float)(r.z >> 8) * 5.9604644775390625e-08f;
+    const float u4 = (float)(r.w >> 8) * 5.9604644775390625e-08f;
+    const float ln2x2 = -2.0f * 0.693147180559945309f;  // -2 ln(u) = -2 ln2 log2(u)
+    const float a = __builtin_amdgcn_sqrtf(ln2x2 * __builtin_amdgcn_logf(u1));
+    const float b = __builtin_amdgcn_sqrtf(ln2x2 * __builtin_amdgcn_logf(u3));
+    out[0] = a * __builtin_amdgcn_cosf(u2);
+    out[1] = a * __builtin_amdgcn_sinf(u2);
+    out[2] = b * __builtin_amdgcn_cosf(u4);
+    out[3] = b * __builtin_amdgcn_sinf(u4);
+  }
   // 4 standard normals via Box-Muller (float64 internally)
   __host__ __device__ __forceinline__ void normal4(uint32_t stream, double* out) const {
     u32x4 r = draw(stream);

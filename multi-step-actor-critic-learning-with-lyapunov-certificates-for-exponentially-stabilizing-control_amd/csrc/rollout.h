@@ -46,6 +46,7 @@ struct StepArgs {
   float reward_scale, cost_scale;
   int raw_log_std;               // logits second half is log_std: std = exp(clamp(., lo, hi))
   float log_std_lo, log_std_hi;  // StochaPolicy min/max_log_std (mlp.py:125-136)
+  float log_half_sum;            // sum_i log((high_i - low_i) / 2) of the action box (float32)
   const float* act_noise;        // device scalar added to every sampled action before the clip
                                  // (GaussNoise.sample, explore_noise.py:9; base.py:136-137) or null
   // on-policy trajectory store (OnSampler mb_* arrays, on_sampler.py:22-41): [E][H][.] rows,

@@ -115,29 +115,49 @@ __global__ __launch_bounds__(BLK) void k_rollout(StepArgs a) {
       for (int i = 0; i < A; ++i) u[i] = a.act_in[e * A + i];
       if (a.logp_in) logp = a.logp_in[e];
     } else {
+#ifdef MH_EXP_NO_SAMPLE  // cost-attribution experiment only
+#pragma unroll
+      for (int i = 0; i < A; ++i) u[i] = fminf(fmaxf(a.logits[e * 2 * A + i], Env::act_lo(i)), Env::act_hi(i));
+      if (false) {
+#else
+      {
+#endif
       float nz[4];
-      rng.normal4f(0, nz);
-      float lg = -0.0f, lt = -0.0f, ls = -0.0f;
+      rng.normal4f_fast(0, nz);
+      // TanhGaussDistribution.sample (act_distribution_cls.py:45-57): z = mu + std * eps,
+      // logp = Normal(mu, std).log_prob(z) - sum log(1 + 1e-6 - tanh(z)^2) - sum log((h-l)/2),
+      // on the hardware transcendentals (v_exp/v_log/v_rcp_f32, ~1 ulp).
+      float lg = -0.0f, lt = -0.0f;
 #pragma unroll
       for (int i = 0; i < A; ++i) {
         const float mu = a.logits[e * 2 * A + i];
-        float sd = a.logits[e * 2 * A + A + i];
-        if (a.raw_log_std) sd = expf(fminf(fmaxf(sd, a.log_std_lo), a.log_std_hi));  // clamp(.).exp()
+        const float raw = a.logits[e * 2 * A + A + i];
+        float sd, log_sd;
+        if (a.raw_log_std) {  // std = clamp(log_std, lo, hi).exp(): log(std) is the clamped value
+          const float c = fminf(fmaxf(raw, a.log_std_lo), a.log_std_hi);
+          sd = __builtin_amdgcn_exp2f(c * 1.44269504088896341f);
+          log_sd = c;
+        } else {
+          sd = raw;
+          log_sd = __builtin_amdgcn_logf(sd) * 0.693147180559945309f;
+        }
         const float z = mu + sd * nz[i];
-        // Normal.log_prob: -((z-mu)^2)/(2 var) - log(std) - log(sqrt(2 pi))
-        const float df = z - mu;
-        lg = lg + ((-(df * df) / (2.0f * (sd * sd)) - logf(sd)) - 0.918938533204672742f);
-        const float th = tanhf(z);
-        lt = lt + logf(1.000001f - th * th);
+        const float df = z - mu;  // not sd * eps: keeps the reference's rounding for tiny std
+        lg = lg + ((-(df * df) * __builtin_amdgcn_rcpf(2.0f * (sd * sd)) - log_sd) - 0.918938533204672742f);
+        // tanh(z) = sign(z) (1 - t) / (1 + t), t = exp(-2|z|)
+        const float t = __builtin_amdgcn_exp2f(-2.88539008177792682f * fabsf(z));
+        const float th = copysignf((1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t), z);
+        lt = lt + __builtin_amdgcn_logf(1.000001f - th * th) * 0.693147180559945309f;
         const float lo = Env::act_lo(i), hi = Env::act_hi(i);
         const float half = (hi - lo) / 2.0f, mid = (hi + lo) / 2.0f;
-        ls = ls + logf(half);
         float act = half * th + mid;
         if (a.act_noise) act = act + a.act_noise[0];  // GaussNoise: one scalar per lockstep step
         act = fminf(fmaxf(act, lo), hi);  // actions.clip(low, high)
         u[i] = act;
       }
+      const float ls = a.log_half_sum;
       logp = (lg - lt) - ls;
+      }
     }
     if (a.act_out) {
 #pragma unroll
@@ -162,7 +182,17 @@ __global__ __launch_bounds__(BLK) void k_rollout(StepArgs a) {
     const float rew = r * a.reward_scale;
     // ---- autoreset (gymnasium 0.28.1 SyncVectorEnv.step)
     float obsn[D];
+#ifdef MH_EXP_NO_RESET  // cost-attribution experiment only: trivial reset (state := 0, R := I)
     if (done) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) s[i] = (S == 18 && (i == 6 || i == 10 || i == 14)) ? 1.0f : 0.0f;
+#pragma unroll
+      for (int i = 0; i < D; ++i) obsn[i] = 0.0f;
+      k1 = 0;
+    } else if (false) {
+#else
+    if (done) {
+#endif
       float rs[RS];
       if (a.reset_in) {
 #pragma unroll
