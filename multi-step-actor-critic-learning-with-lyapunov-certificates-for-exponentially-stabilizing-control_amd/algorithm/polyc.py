@@ -15,7 +15,7 @@ import torch
 
 from ..utils.tensorboard_setup import tb_tags  # noqa: F401  (tb keys shared with PPO)
 from ._update_graph import step
-from .ppo import PPO
+from .ppo import PPO, batch_normalize
 from .ppo import ApproxContainer as _PPOContainer
 
 
@@ -34,8 +34,7 @@ class POLYC(PPO):
         with torch.no_grad():
             data["lya"] = self.networks.lyapunov(data["obs"])
             data["lya2"] = self.networks.lyapunov(data["obs2"])
-        d = data["lya2"] - data["lya"]
-        d = (d - d.mean()) / (d.std() + self.EPS)
+        d = batch_normalize(data["lya2"] - data["lya"], self.EPS)
         d = torch.min(-d, torch.zeros_like(d))
         data["diff_lya"] = d
         data["adv"] = (1 - self.beta) * data["adv"] + self.beta * d

@@ -7,8 +7,9 @@ permutation for the same seed) and take `num_mini_batch` mini-batches, each a po
 (clipped surrogate + entropy + KL to the pre-update policy, :221-250) and a value step
 (optionally clipped, :253-283). The permutation is uploaded once per pass and mini-batches are
 gathered on the device. The Lyapunov network exists (and its lr is annealed) as in the
-reference but PPO never trains it. Gradients are averaged across ranks (RCCL) before every
-optimiser step when torch.distributed is up.
+reference but PPO never trains it. Data-parallel (one rank per GPU, each with its own envs):
+gradients are averaged across ranks (one RCCL all-reduce per optimiser step) and the advantage
+normalisation uses the global batch's statistics; each rank shuffles its local indices.
 """
 __all__ = ["ApproxContainer", "PPO"]
 
@@ -20,9 +21,25 @@ import torch
 import torch.nn as nn
 
 from ..create_pkg.create_apprfunc import create_apprfunc
+from ..utils import dist as D
 from ..utils.common_utils import get_apprfunc_dict
 from ..utils.tensorboard_setup import tb_tags
 from ._update_graph import fused_adam, step
+
+
+def batch_normalize(x, eps):
+    """(x - mean) / (std + eps) with torch's unbiased std (ppo.py:162). Under torch.distributed the
+    statistics are the GLOBAL batch's: (sum, sum of squares, count) are all-reduced (float64), so
+    data-parallel ranks normalise exactly like one process holding the whole sample batch."""
+    if D.world_size() == 1:
+        return (x - x.mean()) / (x.std() + eps)
+    xd = x.double()
+    st = torch.stack([xd.sum(), (xd * xd).sum(), torch.tensor(float(x.numel()), dtype=torch.float64, device=x.device)])
+    D.allreduce_(st)
+    n = st[2]
+    mean = st[0] / n
+    std = ((st[1] - n * mean * mean) / (n - 1)).clamp_min(0).sqrt()
+    return (x - mean.to(x.dtype)) / (std.to(x.dtype) + eps)
 
 
 class ApproxContainer(nn.Module):
@@ -108,7 +125,7 @@ class PPO:
             data["obs2"][:, 8] -= self.target_value
         with torch.no_grad():
             data["logits"] = self.networks.policy(data["obs"])
-        data["adv"] = (data["adv"] - data["adv"].mean()) / (data["adv"].std() + self.EPS)
+        data["adv"] = batch_normalize(data["adv"], self.EPS)
         return data
 
     def _before_minibatches(self, data):
