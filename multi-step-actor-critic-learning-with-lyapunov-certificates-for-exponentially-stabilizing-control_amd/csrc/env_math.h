@@ -582,6 +582,16 @@ MH_HD void ns3_step3(double* X, const double* G) {
 // float64-exact polar factor before the final rounding). Inputs farther than 0.25 from
 // orthogonal take the float64 Newton iteration X <- (X + X^-T)/2.
 MH_HD void polar3_general(const float* Rin, float* Rout);
+struct F9 {
+  float v[9];
+};
+// Out-of-line entry to the general routine, by value: the rare path's registers and code stay
+// out of the rollout kernel's allocation (a call only where a lane needs it).
+static __host__ __device__ __noinline__ F9 polar3_general_call(F9 in) {
+  F9 out;
+  polar3_general(in.v, out.v);
+  return out;
+}
 
 // Fast path for what the integrator produces every substep: a proper rotation perturbed by one
 // Euler step (max|X^T X - I| = e < 0.25, det > 0). One or two third-order steps bring e to
@@ -617,7 +627,12 @@ MH_HD void polar3(const float* Rin, float* Rout) {
       return;
     }
   }
-  polar3_general(Rin, Rout);
+  F9 in;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) in.v[i] = Rin[i];
+  const F9 out = polar3_general_call(in);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) Rout[i] = out.v[i];
 }
 
 // General polar factor: any conditioning, det < 0 flip.

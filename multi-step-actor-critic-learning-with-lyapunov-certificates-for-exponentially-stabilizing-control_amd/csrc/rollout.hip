@@ -84,7 +84,10 @@ struct ResetDraw<QuadTracking> {  // QuadTracking.py:169-186
 
 // --------------------------------------------------------------- fused lockstep step
 template <class Env>
-__global__ __launch_bounds__(BLK) void k_rollout(StepArgs a) {
+#ifndef MH_ROLLOUT_MIN_WAVES
+#define MH_ROLLOUT_MIN_WAVES 2  // <= 256 VGPRs: 2 waves per SIMD once E exceeds one wave per SIMD
+#endif
+__global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs a) {
   constexpr int D = Env::D, A = Env::A, S = Env::S, XS = Env::XS, RS = Env::RS;
   constexpr int F = rec_floats(D, A);
   const int64_t E = a.E;
