@@ -172,6 +172,22 @@ int mh_rollout_traj_step(mh_env_t h, const float* logits, const float* act_in, c
 int mh_gae(const float* val, const float* val2, const float* rew, const uint8_t* done, int64_t num_envs,
            int32_t horizon, double gamma, double gae_lambda, float* adv, float* ret, void* stream);
 
+/* ---- sampler policy forward: StochaPolicy's MLP (RL/apprfunc/mlp.py:111-136, obs -> Linear ->
+ * ReLU -> Linear -> ReLU -> Linear -> (mean | log_std)) as one fused f32-MFMA kernel. Supported
+ * shape: hidden sizes 256 x 256 (every reference script's default), obs_dim <= 16,
+ * out_dim (= 2 * act_dim) <= 32; other shapes return MH_EINVAL (the caller uses PyTorch). ---- */
+/* floats of the packed parameter buffer for a given obs_dim */
+int mh_policy_packed_size(int32_t obs_dim, int64_t* floats_out);
+/* Pack nn.Linear parameters (row-major [out][in] weights, [out] biases, device pointers) into the
+ * per-lane MFMA fragment order; run once per parameter update (inside a captured sample()). */
+int mh_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
+                   const float* b3, int32_t obs_dim, int32_t hidden1, int32_t hidden2, int32_t out_dim,
+                   float* packed, void* stream);
+/* logits [num_envs][out_dim] = MLP(obs [num_envs][obs_dim]), the raw head output (the log_std
+ * half is clamped/exponentiated by the rollout kernel, mh_nstep_set_log_std_clamp). */
+int mh_policy_forward(const float* packed, const float* obs, int64_t num_envs, int32_t obs_dim, int32_t out_dim,
+                      float* logits, void* stream);
+
 /* Per-kernel HIP-event timing of mh_rollout_step (profiling aid; do not enable inside a
  * captured hipGraph). read_timing drains the pending events (host sync) and returns the summed
  * milliseconds of {step kernel, window scan, window emission} and the number of timed calls. */

@@ -69,6 +69,9 @@ _PROTOS = {
     "mh_env_set_action_noise": (ctypes.c_int, [c_vp, c_vp]),
     "mh_rollout_traj_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(TrajStore), c_i32,
                                             c_vp, c_vp, c_vp]),
+    "mh_policy_packed_size": (ctypes.c_int, [c_i32, ctypes.POINTER(c_i64)]),
+    "mh_policy_pack": (ctypes.c_int, [c_vp] * 6 + [c_i32] * 4 + [c_vp, c_vp]),
+    "mh_policy_forward": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "mh_gae": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f64, c_f64, c_vp, c_vp, c_vp]),
     "mh_env_set_timing": (ctypes.c_int, [c_vp, c_i32]),
     "mh_env_read_timing": (ctypes.c_int, [c_vp, ctypes.POINTER(c_f64), ctypes.POINTER(c_i64), c_i32]),

@@ -422,6 +422,33 @@ int mh_gae(const float* val, const float* val2, const float* rew, const uint8_t*
   return MH_OK;
 }
 
+int mh_policy_packed_size(int32_t obs_dim, int64_t* floats_out) {
+  if (!floats_out) return fail(MH_EINVAL, "mh_policy_packed_size: null out");
+  if (obs_dim <= 0 || obs_dim > 16) return fail(MH_EINVAL, "mh_policy_packed_size: obs_dim must be in [1, 16]");
+  *floats_out = mh::policy_packed_floats(obs_dim);
+  return MH_OK;
+}
+
+int mh_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
+                   const float* b3, int32_t obs_dim, int32_t hidden1, int32_t hidden2, int32_t out_dim,
+                   float* packed, void* stream) {
+  if (!W1 || !b1 || !W2 || !b2 || !W3 || !b3 || !packed) return fail(MH_EINVAL, "mh_policy_pack: null pointer");
+  if (hidden1 != 256 || hidden2 != 256) return fail(MH_EINVAL, "mh_policy_pack: hidden sizes must be 256 x 256");
+  if (obs_dim <= 0 || obs_dim > 16) return fail(MH_EINVAL, "mh_policy_pack: obs_dim must be in [1, 16]");
+  if (out_dim <= 0 || out_dim > 32) return fail(MH_EINVAL, "mh_policy_pack: out_dim must be in [1, 32]");
+  MH_HIP(mh::launch_policy_pack(W1, b1, W2, b2, W3, b3, obs_dim, out_dim, packed, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_policy_forward(const float* packed, const float* obs, int64_t num_envs, int32_t obs_dim, int32_t out_dim,
+                      float* logits, void* stream) {
+  if (!packed || !obs || !logits) return fail(MH_EINVAL, "mh_policy_forward: null pointer");
+  if (obs_dim <= 0 || obs_dim > 16 || out_dim <= 0 || out_dim > 32 || num_envs < 0)
+    return fail(MH_EINVAL, "mh_policy_forward: shape out of range");
+  MH_HIP(mh::launch_policy_forward(packed, obs, num_envs, obs_dim, out_dim, logits, (hipStream_t)stream));
+  return MH_OK;
+}
+
 int mh_nstep_set_log_std_clamp(mh_env_t h, int32_t enable, float lo, float hi) {
   if (!h) return fail(MH_EINVAL, "mh_nstep_set_log_std_clamp: null handle");
   if (enable && !(lo <= hi)) return fail(MH_EINVAL, "mh_nstep_set_log_std_clamp: lo > hi");

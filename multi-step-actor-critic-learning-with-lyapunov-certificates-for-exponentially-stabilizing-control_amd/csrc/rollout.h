@@ -93,6 +93,11 @@ hipError_t launch_rollout(int env_id, const StepArgs& a, hipStream_t st);
 hipError_t launch_gae(const float* val, const float* val2, const float* rew, const uint8_t* done, int64_t E,
                       int H, double gamma, double lam, float* adv, float* ret, hipStream_t st);
 hipError_t launch_reset(int env_id, const StepArgs& a, hipStream_t st);
+int64_t policy_packed_floats(int D);
+hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
+                              const float* b3, int D, int N3, float* P, hipStream_t st);
+hipError_t launch_policy_forward(const float* P, const float* obs, int64_t E, int D, int N3, float* logits,
+                                 hipStream_t st);
 hipError_t launch_finalize(const int32_t* block_count, int32_t nb, int32_t* block_offset, int64_t* meta,
                            int64_t* cursor, int64_t capacity, hipStream_t st);
 hipError_t launch_emit(const EmitArgs& a, hipStream_t st);

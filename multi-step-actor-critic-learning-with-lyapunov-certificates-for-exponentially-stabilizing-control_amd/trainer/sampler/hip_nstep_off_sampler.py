@@ -1,9 +1,11 @@
 """Device n-step off-policy sampler (drop-in for RL/trainer/sampler/nstep_off_sampler.py +
 BaseSampler._n_step, RL/trainer/sampler/base.py:118-222).
 
-Per lockstep step: the policy MLP runs in PyTorch-ROCm on the [E, obs_dim] observation tensor
-(hidden layers as hipBLASLt GEMMs with the ReLU fused into the GEMM epilogue; the head's
-clamp(log_std).exp() is folded into the rollout kernel), then ONE fused gfx950 kernel samples
+Per lockstep step: the policy MLP forward on the [E, obs_dim] observation tensor — for the
+reference's default StochaPolicy shape [D -> 256 -> 256 -> 2A] one fused f32-MFMA kernel
+(csrc/policy_mlp.hip, parameters packed from the nn.Module once per sample()), otherwise the
+PyTorch module (hipBLASLt GEMMs with the ReLU in the epilogue); the head's clamp(log_std).exp()
+is folded into the rollout kernel either way — then ONE fused gfx950 kernel samples
 the TanhGauss action, clips it, integrates the env, computes reward/cost, autoresets, pushes
 the n-step deque and flags full windows; a scan and an emission kernel write every full window
 straight into the bound replay store (env-index order, base.py:178-213).
@@ -54,6 +56,8 @@ class HipNstepOffSampler:
         self.td_lambda = kwargs.get("retrace_lambda", 0.95)
         self.sync_timing = bool(kwargs.get("sampler_sync_timing", True))
         self.use_graph = bool(kwargs.get("sampler_use_graph", True))
+        self.use_fused_policy = bool(kwargs.get("sampler_fused_policy", True))
+        self._packed = None
         self._h = self.envs.handle()
         N.check(N.lib().mh_nstep_attach(self._h, self.n_step, self.reward_scale, self.cost_scale), "mh_nstep_attach")
         # GaussNoise (explore_noise.py:3-9; base.py:83-88,136-137): ONE scalar
@@ -101,6 +105,54 @@ class HipNstepOffSampler:
         return self._staging
 
     # ------------------------------------------------------------------ policy head
+    def _fused_layers(self):
+        """The three nn.Linear of a StochaPolicy [D -> 256 -> ReLU -> 256 -> ReLU -> 2A] MLP
+        (mlp.py:18-30 layout), or None when the policy is another shape (PyTorch path)."""
+        if not self.use_fused_policy:
+            return None
+        pol = self.networks.policy
+        seq = getattr(pol, "policy", None)
+        if getattr(pol, "action_distribution_cls", None) is not TanhGaussDistribution or not isinstance(seq, nn.Sequential):
+            return None
+        mods = list(seq)
+        if len(mods) != 6:
+            return None
+        l1, a1, l2, a2, l3, a3 = mods
+        if not (isinstance(l1, nn.Linear) and isinstance(l2, nn.Linear) and isinstance(l3, nn.Linear)
+                and isinstance(a1, nn.ReLU) and isinstance(a2, nn.ReLU) and isinstance(a3, nn.Identity)):
+            return None
+        D = self.envs.obs_dim
+        if (l1.in_features != D or l1.out_features != 256 or l2.in_features != 256 or l2.out_features != 256
+                or l3.in_features != 256 or l3.out_features != 2 * self.envs.act_dim or D > 16):
+            return None
+        if any(p.device != self.device or p.dtype != torch.float32 for p in seq.parameters()):
+            return None
+        return l1, l2, l3
+
+    def _pack_policy(self):
+        """Pack the policy's current parameters into the fused kernel's fragment order (once per
+        sample(); captured into the sampler graph). Returns False for the PyTorch path."""
+        layers = self._fused_layers()
+        if layers is None:
+            return False
+        D, N3 = self.envs.obs_dim, 2 * self.envs.act_dim
+        if self._packed is None:
+            n = ctypes.c_int64()
+            N.check(N.lib().mh_policy_packed_size(D, ctypes.byref(n)), "mh_policy_packed_size")
+            self._packed = torch.empty(n.value, dtype=torch.float32, device=self.device)
+        l1, l2, l3 = layers
+        ps = [t.detach().contiguous() for t in (l1.weight, l1.bias, l2.weight, l2.bias, l3.weight, l3.bias)]
+        N.check(N.lib().mh_policy_pack(*[N.ptr(t) for t in ps], D, 256, 256, N3, N.ptr(self._packed),
+                                       N.stream_of(self.device)), "mh_policy_pack")
+        return True
+
+    def _policy_fused(self):
+        logits = torch.empty(self.num_envs, 2 * self.envs.act_dim, dtype=torch.float32, device=self.device)
+        N.check(N.lib().mh_policy_forward(N.ptr(self._packed), N.ptr(self.obs), self.num_envs, self.envs.obs_dim,
+                                          2 * self.envs.act_dim, N.ptr(logits), N.stream_of(self.device)),
+                "mh_policy_forward")
+        return logits, True
+
     def _policy_raw(self):
         """StochaPolicy.forward (mlp.py:132-136) up to the head: returns (logits, raw) where raw
         means the second half is log_std before clamp/exp (the kernel finishes it)."""
@@ -139,17 +191,18 @@ class HipNstepOffSampler:
         if self._noise is not None:
             self._noise.normal_(self._noise_mean, self._noise_std)
 
-    def _policy_step(self, store):
+    def _policy_step(self, store, fused=False):
         self._draw_noise()
-        logits, raw = self._policy_raw()
+        logits, raw = self._policy_fused() if fused else self._policy_raw()
         pol = self.networks.policy
         N.check(N.lib().mh_nstep_set_log_std_clamp(self._h, int(raw), float(getattr(pol, "min_log_std", -20.0)),
                                                    float(getattr(pol, "max_log_std", 1.0))), "log_std clamp")
         self._lockstep(store, logits=logits)
 
     def _horizon(self, store):
+        fused = self._pack_policy()
         for _ in range(self.horizon):
-            self._policy_step(store)
+            self._policy_step(store, fused)
 
     def _graph_for(self, store):
         key = (id(store), id(self.networks.policy), tuple(p.data_ptr() for p in self.networks.policy.parameters()),

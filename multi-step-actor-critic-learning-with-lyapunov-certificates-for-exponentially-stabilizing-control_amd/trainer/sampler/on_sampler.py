@@ -62,9 +62,10 @@ class OnSampler(HipNstepOffSampler):
 
     def _horizon(self, store):
         pol = self.networks.policy
+        fused = self._pack_policy()
         for t in range(self.horizon):
             self._draw_noise()
-            logits, raw = self._policy_raw()
+            logits, raw = self._policy_fused() if fused else self._policy_raw()
             N.check(N.lib().mh_nstep_set_log_std_clamp(self._h, int(raw), float(getattr(pol, "min_log_std", -20.0)),
                                                        float(getattr(pol, "max_log_std", 1.0))), "log_std clamp")
             self._traj_step(t, logits=logits)

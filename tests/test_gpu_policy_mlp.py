@@ -1,0 +1,74 @@
+"""GPU: the fused f32-MFMA policy forward (csrc/policy_mlp.hip) against the PyTorch StochaPolicy
+MLP it replaces in the sampler (RL/apprfunc/mlp.py:111-136): same parameters, same observations,
+raw head output (mean | log_std) within float32 summation-order rounding (K = 256 sums:
+rtol 1e-5, atol 1e-5 of the output scale)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+import msacl_amd  # noqa: F401
+import msacl_amd._native as N
+
+pytestmark = pytest.mark.gpu
+
+
+def _mlp(D, A, seed):
+    torch.manual_seed(seed)
+    return nn.Sequential(nn.Linear(D, 256), nn.ReLU(), nn.Linear(256, 256), nn.ReLU(), nn.Linear(256, 2 * A),
+                         nn.Identity()).cuda()
+
+
+def _fused(net, obs, D, N3):
+    n = ctypes.c_int64()
+    N.check(N.lib().mh_policy_packed_size(D, ctypes.byref(n)), "size")
+    P = torch.empty(n.value, device="cuda")
+    ps = [net[0].weight, net[0].bias, net[2].weight, net[2].bias, net[4].weight, net[4].bias]
+    ps = [p.detach().contiguous() for p in ps]
+    N.check(N.lib().mh_policy_pack(*[N.ptr(p) for p in ps], D, 256, 256, N3, N.ptr(P), N.stream_of()), "pack")
+    out = torch.empty(obs.shape[0], N3, device="cuda")
+    N.check(N.lib().mh_policy_forward(N.ptr(P), N.ptr(obs), obs.shape[0], D, N3, N.ptr(out), N.stream_of()), "fwd")
+    return out
+
+
+@pytest.mark.parametrize("D,A,E", [(12, 4, 65536), (12, 4, 1000), (2, 1, 777), (6, 2, 4097), (7, 2, 64), (16, 16, 96)])
+def test_fused_policy_forward_matches_torch(D, A, E):
+    net = _mlp(D, A, seed=D * 100 + A)
+    g = torch.Generator(device="cuda").manual_seed(E)
+    obs = (torch.randn(E, D, device="cuda", generator=g) * 2).contiguous()
+    with torch.no_grad():
+        ref = net(obs).double()
+        # float64 reference for the tolerance: both float32 paths sit within a few ulps of it
+        net64 = _mlp(D, A, seed=D * 100 + A).double()
+        exact = net64(obs.double())
+    got = _fused(net, obs, D, 2 * A).double()
+    scale = exact.abs().max().item()
+    np.testing.assert_allclose(got.cpu().numpy(), exact.cpu().numpy(), rtol=1e-5, atol=1e-5 * scale)
+    np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-5, atol=1e-5 * scale)
+
+
+def test_fused_policy_rejects_unsupported_shapes():
+    n = ctypes.c_int64()
+    assert N.lib().mh_policy_packed_size(17, ctypes.byref(n)) == -1
+    z = torch.zeros(1, device="cuda")
+    assert N.lib().mh_policy_pack(*[N.ptr(z)] * 6, 12, 128, 256, 8, N.ptr(z), N.stream_of()) == -1
+    assert N.lib().mh_policy_pack(*[N.ptr(z)] * 6, 12, 256, 256, 40, N.ptr(z), N.stream_of()) == -1
+
+
+def test_sampler_uses_fused_policy_and_matches_torch_path():
+    """The n-step sampler picks the fused kernel for the default policy shape; its logits for
+    the current observations equal the PyTorch path's."""
+    from msacl_amd.utils.config import build_pipeline, default_msacl_args
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        args = default_msacl_args(env_name="QuadTracking", env_num=4096, buffer_warm_size=0, max_iteration=0,
+                                  save_folder=td, seed=0)
+        _, alg, sampler, buffer, _, trainer = build_pipeline(args)
+        assert sampler._fused_layers() is not None
+        assert sampler._pack_policy()
+        fused, raw = sampler._policy_fused()
+        torch_logits, raw2 = sampler._policy_raw()
+        assert raw and raw2
+        np.testing.assert_allclose(fused.detach().cpu().numpy(), torch_logits.detach().cpu().numpy(), rtol=1e-5, atol=1e-5)

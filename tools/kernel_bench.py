@@ -10,6 +10,7 @@ events (tools/gputime.py), algorithmic bytes per launch, achieved GB/s and the f
   gather        mh_replay_gather of B windows (random indices) from a 1M-window store
   msacl         q_target / lyapunov / stability_adv / ppo_clip at the replay batch B = 256, n = 20
   gae           mh_gae over [E][H] on-policy trajectory blocks (65,536 x 64 and 65,536 x 1,600)
+  policy        fused f32-MFMA policy MLP forward vs the PyTorch GEMM path (TFLOP/s vs 157.3 peak)
 
 Prints one JSON object per line; --out writes the list as JSON.
 Usage: python tools/kernel_bench.py [--sizes 65536,4194304] [--reps 20] [--out file]
@@ -213,6 +214,43 @@ def bench_gae(E, H, reps, dev, p_done=0.02):
     return row("gae", "-", E * H, "steps", round(per, 3), ms, envs=E, horizon=H)
 
 
+def bench_policy(E, reps, dev, D=12, A=4):
+    """Sampler policy forward: fused f32-MFMA kernel (csrc/policy_mlp.hip) vs the PyTorch
+    StochaPolicy MLP (hipBLASLt GEMMs, ReLU epilogues) on the same parameters."""
+    import torch.nn as nn
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Linear(D, 256), nn.ReLU(), nn.Linear(256, 256), nn.ReLU(), nn.Linear(256, 2 * A)).to(dev)
+    obs = torch.randn(E, D, device=dev)
+    n = ctypes.c_int64()
+    N.check(N.lib().mh_policy_packed_size(D, ctypes.byref(n)), "size")
+    P = torch.empty(n.value, device=dev)
+    ps = [t.detach().contiguous() for t in (net[0].weight, net[0].bias, net[2].weight, net[2].bias, net[4].weight,
+                                            net[4].bias)]
+    st = N.stream_of(dev)
+    N.check(N.lib().mh_policy_pack(*[N.ptr(t) for t in ps], D, 256, 256, 2 * A, N.ptr(P), st), "pack")
+    out = torch.empty(E, 2 * A, device=dev)
+
+    def fused():
+        N.lib().mh_policy_forward(N.ptr(P), N.ptr(obs), E, D, 2 * A, N.ptr(out), st)
+
+    def torch_path():
+        with torch.no_grad():
+            h = torch._addmm_activation(net[0].bias, obs, net[0].weight.t())
+            h = torch._addmm_activation(net[2].bias, h, net[2].weight.t())
+            torch.addmm(net[4].bias, h, net[4].weight.t())
+
+    flops = 2.0 * (D * 256 + 256 * 256 + 256 * 2 * A)
+    rows = []
+    for name, fn in (("policy_mlp_fused", fused), ("policy_mlp_torch", torch_path)):
+        ms = time_launches(fn, reps)
+        tf = E * flops / (ms * 1e-3) / 1e12
+        r = {"kernel": name, "envs": E, "avg_us": round(ms * 1e3, 3), "TFLOPs": round(tf, 2),
+             "frac_f32_mfma": round(tf / 157.3, 4)}
+        print(json.dumps(r), flush=True)
+        rows.append(r)
+    return rows
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--sizes", default="65536,4194304")
@@ -238,6 +276,9 @@ def main():
             rows.append(bench_gather("QuadTracking", B, a.reps, dev))
     if "msacl" not in skip:
         rows += bench_msacl(a.reps, dev)
+    if "policy" not in skip:
+        for E in (65536, 262144):
+            rows += bench_policy(E, a.reps, dev)
     if "gae" not in skip:
         for E, H in ((65536, 64), (65536, 1600)):
             rows.append(bench_gae(E, H, a.reps, dev))
