@@ -30,7 +30,7 @@ constexpr int PM_H = 256;           // hidden width (both layers)
 constexpr int PM_NB = PM_H / 32;    // 32-row blocks per hidden layer
 
 // packed parameter layout (floats):
-//   W1p [NB][K1][64]        W1[blk*32 + (l&31)][2s + (l>>5)]
+//   W1p [NB][K1][64]        W1[blk*32 + (l&31)][2s + (l>>5)]; k = D holds b1 (constant-1 input)
 //   b1p [NB][64][16]        b1[blk*32 + row(r, l)]
 //   W2p [NB ob][NB ib][4 q][64][4]   W2[ob*32 + (l&31)][ib*32 + row(4q + j, l)]
 //   b2p [NB][64][16]
@@ -58,6 +58,7 @@ __global__ __launch_bounds__(256) void k_policy_pack(const float* __restrict__ W
       const int l = (int)(q % 64), s = (int)((q / 64) % K1), blk = (int)(q / (64 * K1));
       const int k = 2 * s + (l >> 5);
       if (k < D) v = W1[(int64_t)(blk * 32 + (l & 31)) * D + k];
+      else if (k == D) v = b1[blk * 32 + (l & 31)];  // bias as the weight of a constant-1 input
     } else if (q < pm_off_w2(K1)) {
       const int64_t o = q - pm_off_b1(K1);
       const int r = (int)(o % 16), l = (int)((o / 16) % 64), blk = (int)(o / (16 * 64));
@@ -83,106 +84,129 @@ __global__ __launch_bounds__(256) void k_policy_pack(const float* __restrict__ W
   }
 }
 
-template <int K1>
+// K1 = k-steps of layer 1 = ceil((D + 1) / 2): the observation plus a constant-1 input that
+// carries the layer-1 bias inside the MFMA. Persistent: each wave walks tiles tile0,
+// tile0 + nwaves, ...; W1 fragments stay in registers, the W2 ring runs on across tiles (the
+// same weights for every tile) and the next tile's observations are fetched a tile ahead.
 #ifndef MH_POLICY_MIN_WAVES
 #define MH_POLICY_MIN_WAVES 1
 #endif
-__global__ __launch_bounds__(256, MH_POLICY_MIN_WAVES) void k_policy_forward(const float* __restrict__ P, const float* __restrict__ obs,
-                                                           int64_t E, int D, int N3, float* __restrict__ logits) {
+template <int K1>
+__global__ __launch_bounds__(256, MH_POLICY_MIN_WAVES) void k_policy_forward(const float* __restrict__ P,
+                                                                            const float* __restrict__ obs, int64_t E,
+                                                                            int D, int N3, float* __restrict__ logits) {
   const int lane = threadIdx.x & 63;
-  const int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int64_t b0 = tile * 32;
-  if (b0 >= E) return;
-  const int64_t brow = min(b0 + (lane & 31), E - 1);  // padded tail rows read the last env
+  const int64_t ntiles = (E + 31) / 32;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  int64_t tile = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tile >= ntiles) return;
   const float* W1p = P;
-  const float* b1p = P + pm_off_b1(K1);
   const f32x4* W2p = reinterpret_cast<const f32x4*>(P + pm_off_w2(K1));
   const float* b2p = P + pm_off_b2(K1);
   const f32x4* W3p = reinterpret_cast<const f32x4*>(P + pm_off_w3(K1));
   const float* b3 = P + pm_off_b3(K1);
+  constexpr int PF = 8;                 // W2 prefetch distance (16-B fragments)
+#ifndef MH_POLICY_NACC
+#define MH_POLICY_NACC 1
+#endif
+  constexpr int NACC = MH_POLICY_NACC;  // accumulation chains of layer 2
+  constexpr int STEPS = PM_NB * 4;      // fragments per output block
+  constexpr int ALL = PM_NB * STEPS;    // fragments of W2 (the ring wraps: same W2 every tile)
 
-  // ---- layer 1: H1^T blocks (32 hidden x 32 envs), bias + ReLU
-  float xo[K1];
+  float w1f[PM_NB][K1];
 #pragma unroll
-  for (int s = 0; s < K1; ++s) {
-    const int k = 2 * s + (lane >> 5);
-    xo[s] = k < D ? obs[brow * D + k] : 0.0f;
-  }
-  f32x16 h1[PM_NB];
+  for (int blk = 0; blk < PM_NB; ++blk)
 #pragma unroll
-  for (int blk = 0; blk < PM_NB; ++blk) {
-    f32x16 acc = {};
+    for (int s = 0; s < K1; ++s) w1f[blk][s] = W1p[(blk * K1 + s) * 64 + lane];
+  auto load_obs = [&](int64_t t, float* xo) {
+    const int64_t brow = min(t * 32 + (lane & 31), E - 1);  // padded tail rows read the last env
 #pragma unroll
-    for (int s = 0; s < K1; ++s)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(W1p[(blk * K1 + s) * 64 + lane], xo[s], acc, 0, 0, 0);
-    const f32x4* bb = reinterpret_cast<const f32x4*>(b1p + (blk * 64 + lane) * 16);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const f32x4 b = bb[q];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[4 * q + j] = fmaxf(acc[4 * q + j] + b[j], 0.0f);
+    for (int s = 0; s < K1; ++s) {
+      const int k = 2 * s + (lane >> 5);
+      xo[s] = k < D ? obs[brow * D + k] : (k == D ? 1.0f : 0.0f);
     }
-    h1[blk] = acc;
-  }
-  // ---- layers 2 and 3: each H2^T block in turn, folded into out^T right away. The W2 fragments
-  // stream through a ring of PF registers loaded PF steps ahead of their MFMAs (one step = one
-  // 16-B load feeding four MFMAs = 256 MFMA cycles), crossing block boundaries, so the L2
-  // latency hides behind the MFMA pipe; bias/W3 fragments of a block are fetched at its start.
-  constexpr int PF = 8;
-  constexpr int STEPS = PM_NB * 4;  // 16-B fragments per output block
-  f32x16 o3 = {};
+  };
+  float xo[K1];
+  load_obs(tile, xo);
   f32x4 ring[PF];
 #pragma unroll
   for (int t = 0; t < PF; ++t) ring[t] = W2p[t * 64 + lane];
-  for (int ob = 0; ob < PM_NB; ++ob) {
-    const f32x4* bb = reinterpret_cast<const f32x4*>(b2p + (ob * 64 + lane) * 16);
-    const f32x4* w3 = W3p + (int64_t)ob * 4 * 64 + lane;
-    f32x4 bias[4], w3f[4];
+
+  for (; tile < ntiles; tile += nwaves) {
+    // ---- layer 1: H1^T blocks (32 hidden x 32 envs) = ReLU(W1 [obs; 1]), bias inside the MFMA
+    f32x16 h1[PM_NB];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      bias[q] = bb[q];
-      w3f[q] = w3[q * 64];
+    for (int blk = 0; blk < PM_NB; ++blk) {
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < K1; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w1f[blk][s], xo[s], acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] = fmaxf(acc[r], 0.0f);
+      h1[blk] = acc;
     }
-    // fragment t of block ob is W2p[(ob * STEPS + t) * 64 + lane]; the prefetch of step t + PF runs
-    // into block ob + 1 near the end (for the last block it reads the b2 region: in bounds, unused)
-    const f32x4* w2 = W2p + (int64_t)ob * STEPS * 64 + lane;
-    f32x16 acc = {};
+    const int64_t next = tile + nwaves;
+    if (next < ntiles) load_obs(next, xo);  // a whole tile of MFMAs to land
+    // ---- layers 2 and 3: each H2^T block in turn, folded into out^T right away. W2 fragments
+    // stream through a ring of PF registers loaded PF steps ahead of their MFMAs (one step = one
+    // 16-B load feeding four MFMAs = 256 MFMA cycles); bias/W3 fragments at the block start.
+    f32x16 o3 = {};
+    for (int ob = 0; ob < PM_NB; ++ob) {
+      const f32x4* bb = reinterpret_cast<const f32x4*>(b2p + (ob * 64 + lane) * 16);
+      const f32x4* w3 = W3p + (int64_t)ob * 4 * 64 + lane;
+      f32x4 bias[4], w3f[4];
 #pragma unroll
-    for (int t = 0; t < STEPS; ++t) {
-      const f32x4 a = ring[t % PF];
-      ring[t % PF] = w2[(t + PF) * 64];
-      const int ib = t >> 2, q = t & 3;
+      for (int q = 0; q < 4; ++q) {
+        bias[q] = bb[q];
+        w3f[q] = w3[q * 64];
+      }
+      // NACC independent accumulation chains (k interleaved), summed at the end: one dependent
+      // chain of v_mfma_f32_32x32x2_f32 does not keep the MFMA pipe full
+      f32x16 accs[NACC];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], h1[ib][4 * q + j], acc, 0, 0, 0);
-      // keep the prefetch in this step: without a barrier the scheduler sinks every load next
-      // to its first use and the MFMA pipe waits on L2 latency each step
-      __builtin_amdgcn_sched_barrier(0);
+      for (int c = 0; c < NACC; ++c) accs[c] = f32x16{};
+#pragma unroll
+      for (int t = 0; t < STEPS; ++t) {
+        const f32x4 a = ring[t % PF];
+        int nxt = ob * STEPS + t + PF;
+        nxt = nxt >= ALL ? nxt - ALL : nxt;
+        ring[t % PF] = W2p[nxt * 64 + lane];
+        const int ib = t >> 2, q = t & 3;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          accs[j % NACC] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[j], h1[ib][4 * q + j], accs[j % NACC], 0, 0, 0);
+        // keep the prefetch in this step: without a barrier the scheduler sinks every load next
+        // to its first use and the MFMA pipe waits on L2 latency each step
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      f32x16 acc = accs[0];
+#pragma unroll
+      for (int c = 1; c < NACC; ++c) acc = acc + accs[c];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[4 * q + j] = fmaxf(acc[4 * q + j] + bias[q][j], 0.0f);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o3 = __builtin_amdgcn_mfma_f32_32x32x2f32(w3f[q][j], acc[4 * q + j], o3, 0, 0, 0);
     }
+    // ---- out^T rows o = row(r, lane) for env column lane & 31: + b3, store [E][N3]
+    const int64_t b = tile * 32 + (lane & 31);
+    if (b < E) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[4 * q + j] = fmaxf(acc[4 * q + j] + bias[q][j], 0.0f);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o3 = __builtin_amdgcn_mfma_f32_32x32x2f32(w3f[q][j], acc[4 * q + j], o3, 0, 0, 0);
-  }
-  // ---- out^T rows o = row(r, lane) for env column lane & 31: + b3, store [E][N3]
-  const int64_t b = b0 + (lane & 31);
-  if (b < E) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int o = pm_row(r, lane);
-      if (o < N3) logits[b * N3 + o] = o3[r] + b3[o];
+      for (int r = 0; r < 16; ++r) {
+        const int o = pm_row(r, lane);
+        if (o < N3) logits[b * N3 + o] = o3[r] + b3[o];
+      }
     }
   }
 }
 
-int64_t policy_packed_floats(int D) { return pm_packed_floats((D + 1) / 2); }
+int64_t policy_packed_floats(int D) { return pm_packed_floats(D / 2 + 1); }
 
 hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
                               const float* b3, int D, int N3, float* P, hipStream_t st) {
-  const int K1 = (D + 1) / 2;
+  const int K1 = D / 2 + 1;  // ceil((D + 1) / 2): observation + the bias input
   const int64_t total = pm_packed_floats(K1);
   const int grid = (int)((total + 255) / 256 < 1024 ? (total + 255) / 256 : 1024);
   k_policy_pack<<<grid, 256, 0, st>>>(W1, b1, W2, b2, W3, b3, D, N3, K1, P);
@@ -193,14 +217,24 @@ template <int K1>
 static hipError_t launch_fwd_t(const float* P, const float* obs, int64_t E, int D, int N3, float* logits,
                                hipStream_t st) {
   const int64_t tiles = (E + 31) / 32;
-  k_policy_forward<K1><<<(unsigned)((tiles + 3) / 4), 256, 0, st>>>(P, obs, E, D, N3, logits);
+  // persistent: at most one 4-wave workgroup per CU (one wave per SIMD), >= 1 tile per wave
+  static int cus = 0;  // CU count of the (single) device this process drives, queried once
+  if (cus <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const int64_t want = (tiles + 3) / 4;
+  const int grid = (int)(want < cus ? want : cus);
+  k_policy_forward<K1><<<grid, 256, 0, st>>>(P, obs, E, D, N3, logits);
   return hipGetLastError();
 }
 
 hipError_t launch_policy_forward(const float* P, const float* obs, int64_t E, int D, int N3, float* logits,
                                  hipStream_t st) {
   if (E <= 0) return hipSuccess;
-  switch ((D + 1) / 2) {
+  switch (D / 2 + 1) {
     case 1: return launch_fwd_t<1>(P, obs, E, D, N3, logits, st);
     case 2: return launch_fwd_t<2>(P, obs, E, D, N3, logits, st);
     case 3: return launch_fwd_t<3>(P, obs, E, D, N3, logits, st);
@@ -209,6 +243,7 @@ hipError_t launch_policy_forward(const float* P, const float* obs, int64_t E, in
     case 6: return launch_fwd_t<6>(P, obs, E, D, N3, logits, st);
     case 7: return launch_fwd_t<7>(P, obs, E, D, N3, logits, st);
     case 8: return launch_fwd_t<8>(P, obs, E, D, N3, logits, st);
+    case 9: return launch_fwd_t<9>(P, obs, E, D, N3, logits, st);
     default: return hipErrorInvalidValue;
   }
 }
