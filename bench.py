@@ -34,6 +34,8 @@ def parse():
                    help="init: PyTorch default init (SURVEY 8d); hover: action mean [mg,0,0,0], long episodes")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--blas", choices=["hipblaslt", "rocblas"], default=None,
+                   help="GEMM library of the PyTorch parts (update MLPs); default: the config's (rocblas)")
     return p.parse_args()
 
 
@@ -95,6 +97,8 @@ def main():
                              buffer_warm_size=5000, max_iteration=10 ** 9, eval_interval=10 ** 9,
                              log_save_interval=10 ** 9, apprfunc_save_interval=10 ** 9, save_folder=tmp,
                              num_eval_episode=1, sampler_sync_timing=False, device=dev)
+    if a.blas is not None:
+        cfg["blas_backend"] = a.blas
     if a.policy == "hover":
         cfg["buffer_warm_size"] = 0
     args, alg, sampler, buffer, evaluator, trainer = build_pipeline(cfg)
