@@ -188,6 +188,39 @@ int mh_policy_pack(const float* W1, const float* b1, const float* W2, const floa
 int mh_policy_forward(const float* packed, const float* obs, int64_t num_envs, int32_t obs_dim, int32_t out_dim,
                       float* logits, void* stream);
 
+/* ---- PyTorch MLP training helpers (the MLPs stay nn.Modules; these replace kernels inside their
+ * autograd backward / optimiser step) ---- */
+/* Rows of scratch `partial` needed by mh_act_grad_colsum for M rows: partial is [chunks][N]. */
+int mh_act_grad_chunks(int64_t rows, int32_t* chunks_out);
+/* g = dy * act'(y) (act: 0 identity, 1 ReLU via y > 0, 2 tanh via 1 - y^2) and db = column sums of
+ * g, all [rows][cols] row-major; g may be NULL (identity activation: g is dy), db may be NULL.
+ * Replaces threshold_backward / tanh_backward + the bias-gradient reduction of a Linear layer
+ * (RL/apprfunc/mlp.py:18-30 layers under autograd). Deterministic (fixed summation order). */
+int mh_act_grad_colsum(const float* dy, const float* y, int64_t rows, int32_t cols, int32_t act, float* g,
+                       float* db, float* partial, void* stream);
+/* One torch.optim.Adam step (betas b1, b2, eps; no weight decay / amsgrad) over a contiguous
+ * parameter buffer p with gradient g and moments m, v (all n floats). step: DEVICE int64 step
+ * count (read, then advanced by one); ticket: DEVICE uint32 initialised to 0 (kept at 0 between
+ * calls). zero_grad != 0 also zeroes g. Capturable (no host sync). */
+int mh_adam_step(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
+                 int32_t zero_grad, int64_t* step, uint32_t* ticket, void* stream);
+
+/* TanhGaussDistribution (RL/utils/act_distribution_cls.py:15-85) on [rows][2A] logits (mean | std)
+ * with DEVICE action bounds high/low [A] (A <= 8), forward and backward as single launches:
+ *   rsample   (eps [rows][A] standard normals) -> act [rows][A], logp [rows]
+ *   log_prob  (act [rows][A])                  -> logp [rows]
+ * The backward entry points return d_logits [rows][2A]; d_act / d_logp may be NULL (zero). */
+int mh_tanh_gauss_rsample(const float* logits, const float* eps, const float* high, const float* low, int64_t rows,
+                          int32_t act_dim, float* act, float* logp, void* stream);
+int mh_tanh_gauss_rsample_backward(const float* logits, const float* eps, const float* high, const float* low,
+                                   const float* d_act, const float* d_logp, int64_t rows, int32_t act_dim,
+                                   float* d_logits, void* stream);
+int mh_tanh_gauss_log_prob(const float* logits, const float* act, const float* high, const float* low, int64_t rows,
+                           int32_t act_dim, float* logp, void* stream);
+int mh_tanh_gauss_log_prob_backward(const float* logits, const float* act, const float* high, const float* low,
+                                    const float* d_logp, int64_t rows, int32_t act_dim, float* d_logits,
+                                    void* stream);
+
 /* Per-kernel HIP-event timing of mh_rollout_step (profiling aid; do not enable inside a
  * captured hipGraph). read_timing drains the pending events (host sync) and returns the summed
  * milliseconds of {step kernel, window scan, window emission} and the number of timed calls. */

@@ -72,6 +72,13 @@ _PROTOS = {
     "mh_policy_packed_size": (ctypes.c_int, [c_i32, ctypes.POINTER(c_i64)]),
     "mh_policy_pack": (ctypes.c_int, [c_vp] * 6 + [c_i32] * 4 + [c_vp, c_vp]),
     "mh_policy_forward": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
+    "mh_act_grad_chunks": (ctypes.c_int, [c_i64, ctypes.POINTER(c_i32)]),
+    "mh_act_grad_colsum": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "mh_adam_step": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_f32, c_f32, c_f32, c_f32, c_i32, c_vp, c_vp, c_vp]),
+    "mh_tanh_gauss_rsample": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_i32, c_vp, c_vp, c_vp]),
+    "mh_tanh_gauss_rsample_backward": (ctypes.c_int, [c_vp] * 6 + [c_i64, c_i32, c_vp, c_vp]),
+    "mh_tanh_gauss_log_prob": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_i32, c_vp, c_vp]),
+    "mh_tanh_gauss_log_prob_backward": (ctypes.c_int, [c_vp] * 5 + [c_i64, c_i32, c_vp, c_vp]),
     "mh_gae": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f64, c_f64, c_vp, c_vp, c_vp]),
     "mh_env_set_timing": (ctypes.c_int, [c_vp, c_i32]),
     "mh_env_read_timing": (ctypes.c_int, [c_vp, ctypes.POINTER(c_f64), ctypes.POINTER(c_i64), c_i32]),

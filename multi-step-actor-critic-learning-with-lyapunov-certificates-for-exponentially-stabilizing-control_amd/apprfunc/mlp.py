@@ -8,16 +8,18 @@ import torch.nn as nn
 
 from ..utils.act_distribution_cls import Action_Distribution_Cls
 from ..utils.common_utils import get_activation_func
+from ._fused import MLP
 
 
 def mlp(sizes, activation, output_activation=nn.Identity):
-    """Linear layers with `activation` between them and `output_activation` after the last."""
+    """Linear layers with `activation` between them and `output_activation` after the last
+    (an nn.Sequential; on HIP tensors each layer runs fused, apprfunc/_fused.py)."""
     layers = []
     last = len(sizes) - 2
     for j, (a, b) in enumerate(zip(sizes[:-1], sizes[1:])):
         layers.append(nn.Linear(a, b))
         layers.append((output_activation if j == last else activation)())
-    return nn.Sequential(*layers)
+    return MLP(*layers)
 
 
 def _acts(kw):

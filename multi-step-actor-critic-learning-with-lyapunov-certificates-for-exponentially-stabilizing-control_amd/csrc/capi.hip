@@ -449,6 +449,70 @@ int mh_policy_forward(const float* packed, const float* obs, int64_t num_envs, i
   return MH_OK;
 }
 
+int mh_act_grad_chunks(int64_t rows, int32_t* chunks_out) {
+  if (!chunks_out || rows < 0) return fail(MH_EINVAL, "mh_act_grad_chunks: bad argument");
+  *chunks_out = mh::act_grad_chunks(rows);
+  return MH_OK;
+}
+
+int mh_act_grad_colsum(const float* dy, const float* y, int64_t rows, int32_t cols, int32_t act, float* g,
+                       float* db, float* partial, void* stream) {
+  if (!dy || (act != 0 && (!y || !g)) || !partial) return fail(MH_EINVAL, "mh_act_grad_colsum: null pointer");
+  if (act < 0 || act > 2) return fail(MH_EINVAL, "mh_act_grad_colsum: act must be 0, 1 or 2");
+  if (rows < 0 || cols <= 0) return fail(MH_EINVAL, "mh_act_grad_colsum: bad shape");
+  MH_HIP(mh::launch_act_grad_colsum(dy, y, rows, cols, act, act == 0 ? nullptr : g, db, partial,
+                                    (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_adam_step(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
+                 int32_t zero_grad, int64_t* step, uint32_t* ticket, void* stream) {
+  if (!p || !g || !m || !v || !step || !ticket) return fail(MH_EINVAL, "mh_adam_step: null pointer");
+  if (n < 0) return fail(MH_EINVAL, "mh_adam_step: negative size");
+  MH_HIP(mh::launch_adam(p, g, m, v, n, lr, b1, b2, eps, zero_grad, step, ticket, (hipStream_t)stream));
+  return MH_OK;
+}
+
+#define MH_TG_CHECK(name)                                                                           \
+  if (rows < 0 || act_dim <= 0 || act_dim > 8) return fail(MH_EINVAL, name ": act_dim must be in [1, 8]"); \
+  if (rows == 0) return MH_OK;                                                                     \
+  if (!logits || !high || !low) return fail(MH_EINVAL, name ": null pointer")
+
+int mh_tanh_gauss_rsample(const float* logits, const float* eps, const float* high, const float* low, int64_t rows,
+                          int32_t act_dim, float* act, float* logp, void* stream) {
+  MH_TG_CHECK("mh_tanh_gauss_rsample");
+  if (!eps || !act || !logp) return fail(MH_EINVAL, "mh_tanh_gauss_rsample: null pointer");
+  MH_HIP(mh::launch_tg_rsample(logits, eps, high, low, rows, act_dim, act, logp, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_tanh_gauss_rsample_backward(const float* logits, const float* eps, const float* high, const float* low,
+                                   const float* d_act, const float* d_logp, int64_t rows, int32_t act_dim,
+                                   float* d_logits, void* stream) {
+  MH_TG_CHECK("mh_tanh_gauss_rsample_backward");
+  if (!eps || !d_logits) return fail(MH_EINVAL, "mh_tanh_gauss_rsample_backward: null pointer");
+  MH_HIP(mh::launch_tg_rsample_bwd(logits, eps, high, low, d_act, d_logp, rows, act_dim, d_logits,
+                                   (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_tanh_gauss_log_prob(const float* logits, const float* act, const float* high, const float* low, int64_t rows,
+                           int32_t act_dim, float* logp, void* stream) {
+  MH_TG_CHECK("mh_tanh_gauss_log_prob");
+  if (!act || !logp) return fail(MH_EINVAL, "mh_tanh_gauss_log_prob: null pointer");
+  MH_HIP(mh::launch_tg_log_prob(logits, act, high, low, rows, act_dim, logp, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_tanh_gauss_log_prob_backward(const float* logits, const float* act, const float* high, const float* low,
+                                    const float* d_logp, int64_t rows, int32_t act_dim, float* d_logits,
+                                    void* stream) {
+  MH_TG_CHECK("mh_tanh_gauss_log_prob_backward");
+  if (!act || !d_logp || !d_logits) return fail(MH_EINVAL, "mh_tanh_gauss_log_prob_backward: null pointer");
+  MH_HIP(mh::launch_tg_log_prob_bwd(logits, act, high, low, d_logp, rows, act_dim, d_logits, (hipStream_t)stream));
+  return MH_OK;
+}
+
 int mh_nstep_set_log_std_clamp(mh_env_t h, int32_t enable, float lo, float hi) {
   if (!h) return fail(MH_EINVAL, "mh_nstep_set_log_std_clamp: null handle");
   if (enable && !(lo <= hi)) return fail(MH_EINVAL, "mh_nstep_set_log_std_clamp: lo > hi");

@@ -1,0 +1,145 @@
+// dist_kernels.hip — TanhGaussDistribution's reparameterised sample and log-prob, forward and
+// backward, as single kernels (gfx950). RL/utils/act_distribution_cls.py:15-85:
+//   rsample:  z = mu + std * eps,  a = h tanh(z) + m   (h = (high - low)/2, m = (high + low)/2)
+//             logp = sum_i [-(z - mu)^2 / (2 std^2) - log std - log sqrt(2 pi)]
+//                    - sum_i log(1 + 1e-6 - tanh(z)^2) - sum_i log h
+//   log_prob(a): z = atanh((1 - 1e-6)(2a - (high + low)) / (high - low))
+//             logp = sum_i [Normal(mu, std).log_prob(z)] - sum_i log(h (1 + 1e-6 - tanh(z)^2))
+// logits = [mean | std] rows (StochaPolicy output). In PyTorch each of these is ~25 elementwise
+// and reduction launches forward and ~30 backward; here one launch each way, one thread per row
+// (A <= 8 action dims). The backward recomputes z/tanh from (logits, eps) and follows the
+// derivative of each reference expression (including the z - mu terms that cancel in exact
+// arithmetic), so gradients agree with autograd's to float32 rounding. Accurate libm functions
+// (tanhf/logf/atanhf), float32 throughout, as torch evaluates the reference expressions.
+#include "rollout.h"
+
+namespace mh {
+
+constexpr float kLogSqrt2Pi = 0.918938533204672742f;  // math.log(math.sqrt(2 * math.pi))
+
+// rsample forward: act [M][A], logp [M]
+__global__ __launch_bounds__(256) void k_tg_rsample(const float* __restrict__ logits, const float* __restrict__ eps,
+                                                    const float* __restrict__ high, const float* __restrict__ low,
+                                                    int64_t M, int A, float* __restrict__ act,
+                                                    float* __restrict__ logp) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= M) return;
+  float lg = 0.0f, lt = 0.0f, lh = 0.0f;
+  for (int i = 0; i < A; ++i) {
+    const float mu = logits[r * 2 * A + i], sd = logits[r * 2 * A + A + i];
+    const float z = mu + sd * eps[r * A + i];
+    const float df = z - mu;
+    const float var = sd * sd;
+    lg = lg + ((-(df * df) / (2.0f * var) - logf(sd)) - kLogSqrt2Pi);
+    const float t = tanhf(z);
+    lt = lt + logf(1.000001f - t * t);
+    const float h = (high[i] - low[i]) / 2.0f, m = (high[i] + low[i]) / 2.0f;
+    lh = lh + logf(h);
+    act[r * A + i] = h * t + m;
+  }
+  logp[r] = (lg - lt) - lh;
+}
+
+// rsample backward: d_logits [M][2A] from d_act [M][A] (nullable) and d_logp [M] (nullable)
+__global__ __launch_bounds__(256) void k_tg_rsample_bwd(const float* __restrict__ logits,
+                                                        const float* __restrict__ eps,
+                                                        const float* __restrict__ high, const float* __restrict__ low,
+                                                        const float* __restrict__ d_act,
+                                                        const float* __restrict__ d_logp, int64_t M, int A,
+                                                        float* __restrict__ d_logits) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= M) return;
+  const float gl = d_logp ? d_logp[r] : 0.0f;
+  for (int i = 0; i < A; ++i) {
+    const float mu = logits[r * 2 * A + i], sd = logits[r * 2 * A + A + i];
+    const float e = eps[r * A + i];
+    const float z = mu + sd * e;
+    const float df = z - mu;
+    const float var = sd * sd;
+    const float t = tanhf(z);
+    const float h = (high[i] - low[i]) / 2.0f;
+    const float ga = d_act ? d_act[r * A + i] : 0.0f;
+    // a = h t + m ; -log(1 + 1e-6 - t^2) ; t = tanh z
+    const float u = 1.000001f - t * t;
+    const float dt = ga * h + gl * (2.0f * t / u);
+    float dz = dt * (1.0f - t * t);
+    // Normal log-prob: -(df^2) / (2 var) with df = z - mu, var = sd^2; - log sd
+    const float q = df / var;
+    dz = dz + gl * (-q);
+    const float dmu = dz + gl * q;
+    const float dvar = gl * (df * df) / (2.0f * var * var);
+    const float dsd = dz * e + dvar * (2.0f * sd) - gl / sd;
+    d_logits[r * 2 * A + i] = dmu;
+    d_logits[r * 2 * A + A + i] = dsd;
+  }
+}
+
+// log_prob(action) forward
+__global__ __launch_bounds__(256) void k_tg_log_prob(const float* __restrict__ logits, const float* __restrict__ a,
+                                                     const float* __restrict__ high, const float* __restrict__ low,
+                                                     int64_t M, int A, float* __restrict__ logp) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= M) return;
+  float lg = 0.0f, lj = 0.0f;
+  for (int i = 0; i < A; ++i) {
+    const float mu = logits[r * 2 * A + i], sd = logits[r * 2 * A + A + i];
+    const float hl = high[i] + low[i], dl = high[i] - low[i];
+    const float z = atanhf(0.999999f * (2.0f * a[r * A + i] - hl) / dl);  // float32(1 - 1e-6)
+    const float df = z - mu;
+    lg = lg + ((-(df * df) / (2.0f * (sd * sd)) - logf(sd)) - kLogSqrt2Pi);
+    const float t = tanhf(z);
+    lj = lj + logf(dl / 2.0f * (1.000001f - t * t));
+  }
+  logp[r] = lg - lj;
+}
+
+// log_prob backward w.r.t. logits (the action is data)
+__global__ __launch_bounds__(256) void k_tg_log_prob_bwd(const float* __restrict__ logits,
+                                                         const float* __restrict__ a,
+                                                         const float* __restrict__ high,
+                                                         const float* __restrict__ low,
+                                                         const float* __restrict__ d_logp, int64_t M, int A,
+                                                         float* __restrict__ d_logits) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= M) return;
+  const float gl = d_logp[r];
+  for (int i = 0; i < A; ++i) {
+    const float mu = logits[r * 2 * A + i], sd = logits[r * 2 * A + A + i];
+    const float hl = high[i] + low[i], dl = high[i] - low[i];
+    const float z = atanhf(0.999999f * (2.0f * a[r * A + i] - hl) / dl);  // float32(1 - 1e-6)
+    const float df = z - mu;
+    const float var = sd * sd;
+    d_logits[r * 2 * A + i] = gl * (df / var);
+    d_logits[r * 2 * A + A + i] = gl * ((df * df) / (2.0f * var * var)) * (2.0f * sd) - gl / sd;
+  }
+}
+
+static inline unsigned grid_rows(int64_t M) { return (unsigned)((M + 255) / 256); }
+
+hipError_t launch_tg_rsample(const float* logits, const float* eps, const float* high, const float* low, int64_t M,
+                             int A, float* act, float* logp, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  k_tg_rsample<<<grid_rows(M), 256, 0, st>>>(logits, eps, high, low, M, A, act, logp);
+  return hipGetLastError();
+}
+hipError_t launch_tg_rsample_bwd(const float* logits, const float* eps, const float* high, const float* low,
+                                 const float* d_act, const float* d_logp, int64_t M, int A, float* d_logits,
+                                 hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  k_tg_rsample_bwd<<<grid_rows(M), 256, 0, st>>>(logits, eps, high, low, d_act, d_logp, M, A, d_logits);
+  return hipGetLastError();
+}
+hipError_t launch_tg_log_prob(const float* logits, const float* a, const float* high, const float* low, int64_t M,
+                              int A, float* logp, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  k_tg_log_prob<<<grid_rows(M), 256, 0, st>>>(logits, a, high, low, M, A, logp);
+  return hipGetLastError();
+}
+hipError_t launch_tg_log_prob_bwd(const float* logits, const float* a, const float* high, const float* low,
+                                  const float* d_logp, int64_t M, int A, float* d_logits, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  k_tg_log_prob_bwd<<<grid_rows(M), 256, 0, st>>>(logits, a, high, low, d_logp, M, A, d_logits);
+  return hipGetLastError();
+}
+
+}  // namespace mh

@@ -94,6 +94,20 @@ hipError_t launch_gae(const float* val, const float* val2, const float* rew, con
                       int H, double gamma, double lam, float* adv, float* ret, hipStream_t st);
 hipError_t launch_reset(int env_id, const StepArgs& a, hipStream_t st);
 int64_t policy_packed_floats(int D);
+int act_grad_chunks(int64_t M);
+hipError_t launch_tg_rsample(const float* logits, const float* eps, const float* high, const float* low, int64_t M,
+                             int A, float* act, float* logp, hipStream_t st);
+hipError_t launch_tg_rsample_bwd(const float* logits, const float* eps, const float* high, const float* low,
+                                 const float* d_act, const float* d_logp, int64_t M, int A, float* d_logits,
+                                 hipStream_t st);
+hipError_t launch_tg_log_prob(const float* logits, const float* a, const float* high, const float* low, int64_t M,
+                              int A, float* logp, hipStream_t st);
+hipError_t launch_tg_log_prob_bwd(const float* logits, const float* a, const float* high, const float* low,
+                                  const float* d_logp, int64_t M, int A, float* d_logits, hipStream_t st);
+hipError_t launch_act_grad_colsum(const float* dy, const float* y, int64_t M, int N, int act, float* g, float* db,
+                                  float* partial, hipStream_t st);
+hipError_t launch_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
+                       int zero_grad, int64_t* step, uint32_t* ticket, hipStream_t st);
 hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
                               const float* b3, int D, int N3, float* P, hipStream_t st);
 hipError_t launch_policy_forward(const float* P, const float* obs, int64_t E, int D, int N3, float* logits,

@@ -3,8 +3,16 @@
 Same math and the same torch.distributions objects as the reference, so log-probabilities and
 the reparameterised noise path (Normal.rsample -> _standard_normal) are identical. The device
 rollout samples in-kernel instead (csrc/rollout.hip, TanhGauss + clip fused into the env step).
+
+On HIP float32 logits, TanhGaussDistribution.rsample / log_prob run as one kernel forward and
+one backward each (csrc/dist_kernels.hip via the mh_tanh_gauss_* C ABI) instead of ~25 + ~30
+elementwise/reduction launches; the noise is still drawn by torch's `_standard_normal`, so the
+sample path, seeding and the tests' noise injection are unchanged.
 """
+import ctypes
+
 import torch
+import torch.distributions.normal as tdn
 
 EPS = 1e-6
 
@@ -25,6 +33,69 @@ def _independent_normal(mean, std):
     # device->host sync per construction (and forbids HIP-graph capture); numerics unchanged.
     return torch.distributions.Independent(torch.distributions.Normal(mean, std, validate_args=False),
                                            reinterpreted_batch_ndims=1, validate_args=False)
+
+
+def _native():
+    from .. import _native as N
+    return N
+
+
+class _TanhGaussRsample(torch.autograd.Function):
+    """(logits, eps) -> (act, logp); act_distribution_cls.py:39-55 math, csrc/dist_kernels.hip."""
+
+    @staticmethod
+    def forward(ctx, logits, eps, high, low):
+        N = _native()
+        M, A = eps.shape
+        act = torch.empty_like(eps)
+        logp = torch.empty(M, dtype=eps.dtype, device=eps.device)
+        N.check(N.lib().mh_tanh_gauss_rsample(N.ptr(logits), N.ptr(eps), N.ptr(high), N.ptr(low), M, A,
+                                              N.ptr(act), N.ptr(logp), N.stream_of(eps.device)),
+                "mh_tanh_gauss_rsample")
+        ctx.save_for_backward(logits, eps, high, low)
+        return act, logp
+
+    @staticmethod
+    def backward(ctx, d_act, d_logp):
+        logits, eps, high, low = ctx.saved_tensors
+        if not ctx.needs_input_grad[0]:
+            return None, None, None, None
+        N = _native()
+        M, A = eps.shape
+        d_logits = torch.empty_like(logits)
+        d_act = None if d_act is None else d_act.contiguous()
+        d_logp = None if d_logp is None else d_logp.contiguous()
+        N.check(N.lib().mh_tanh_gauss_rsample_backward(
+            N.ptr(logits), N.ptr(eps), N.ptr(high), N.ptr(low), N.ptr(d_act), N.ptr(d_logp), M, A,
+            N.ptr(d_logits), N.stream_of(logits.device)), "mh_tanh_gauss_rsample_backward")
+        return d_logits, None, None, None
+
+
+class _TanhGaussLogProb(torch.autograd.Function):
+    """(logits, act) -> logp; act_distribution_cls.py:57-62 math, csrc/dist_kernels.hip."""
+
+    @staticmethod
+    def forward(ctx, logits, act, high, low):
+        N = _native()
+        M, A = act.shape
+        logp = torch.empty(M, dtype=act.dtype, device=act.device)
+        N.check(N.lib().mh_tanh_gauss_log_prob(N.ptr(logits), N.ptr(act), N.ptr(high), N.ptr(low), M, A,
+                                               N.ptr(logp), N.stream_of(act.device)), "mh_tanh_gauss_log_prob")
+        ctx.save_for_backward(logits, act, high, low)
+        return logp
+
+    @staticmethod
+    def backward(ctx, d_logp):
+        logits, act, high, low = ctx.saved_tensors
+        if not ctx.needs_input_grad[0]:
+            return None, None, None, None
+        N = _native()
+        M, A = act.shape
+        d_logits = torch.empty_like(logits)
+        N.check(N.lib().mh_tanh_gauss_log_prob_backward(
+            N.ptr(logits), N.ptr(act), N.ptr(high), N.ptr(low), N.ptr(d_logp.contiguous()), M, A,
+            N.ptr(d_logits), N.stream_of(logits.device)), "mh_tanh_gauss_log_prob_backward")
+        return d_logits, None, None, None
 
 
 class TanhGaussDistribution:
@@ -51,11 +122,38 @@ class TanhGaussDistribution:
         z = self.gauss_distribution.sample()
         return self._squash(z), self._logp_of_pre_tanh(z)
 
+    def _fused_bounds(self):
+        """(logits2d, high, low) when the device kernels apply, else None."""
+        lg = self.logits
+        if not (lg.is_cuda and lg.dtype == torch.float32 and lg.dim() >= 1):
+            return None
+        A = lg.shape[-1] // 2
+        hi, lo = self.act_high_lim, self.act_low_lim
+        if not (0 < A <= 8 and lg.shape[-1] == 2 * A and hi.shape == (A,) and lo.shape == (A,)
+                and hi.dtype == torch.float32 and lo.dtype == torch.float32
+                and hi.device == lg.device and lo.device == lg.device):
+            return None
+        return lg.reshape(-1, 2 * A).contiguous(), hi.contiguous(), lo.contiguous()
+
     def rsample(self):
+        fb = self._fused_bounds()
+        if fb is not None:
+            lg, hi, lo = fb
+            eps = tdn._standard_normal(self.mean.shape, dtype=self.mean.dtype, device=self.mean.device)
+            lead = self.mean.shape[:-1]
+            act, logp = _TanhGaussRsample.apply(lg, eps.reshape(lg.shape[0], lg.shape[1] // 2).contiguous(), hi, lo)
+            return act.reshape(self.mean.shape), logp.reshape(lead)
         z = self.gauss_distribution.rsample()
         return self._squash(z), self._logp_of_pre_tanh(z)
 
     def log_prob(self, action_limited):
+        fb = self._fused_bounds()
+        if fb is not None and action_limited.shape == self.mean.shape \
+                and action_limited.dtype == torch.float32 and action_limited.device == self.logits.device \
+                and not action_limited.requires_grad:
+            lg, hi, lo = fb
+            a = action_limited.reshape(lg.shape[0], lg.shape[1] // 2).contiguous()
+            return _TanhGaussLogProb.apply(lg, a, hi, lo).reshape(self.mean.shape[:-1])
         z = torch.atanh((1 - EPS) * (2 * action_limited - (self.act_high_lim + self.act_low_lim))
                         / (self.act_high_lim - self.act_low_lim))
         return self.gauss_distribution.log_prob(z) - torch.log(

@@ -72,3 +72,34 @@ def test_sampler_uses_fused_policy_and_matches_torch_path():
         torch_logits, raw2 = sampler._policy_raw()
         assert raw and raw2
         np.testing.assert_allclose(fused.detach().cpu().numpy(), torch_logits.detach().cpu().numpy(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("act", [nn.ReLU, nn.Tanh, nn.Identity])
+def test_fused_linear_act_forward_backward_matches_torch(act):
+    """apprfunc/_fused.py LinearAct (GEMM epilogue activation, mh_act_grad_colsum backward) vs the
+    plain nn.Sequential forward/backward: outputs and every gradient (x, W, b) to float32 rounding;
+    frozen parameters get no gradient."""
+    from msacl_amd.apprfunc._fused import MLP
+    torch.manual_seed(3)
+    layers = [nn.Linear(16, 256), act(), nn.Linear(256, 256), act(), nn.Linear(256, 3), nn.Identity()]
+    fused = MLP(*layers).cuda()
+    plain = nn.Sequential(*[type(m)() if not isinstance(m, nn.Linear) else m for m in layers]).cuda()
+    plain.load_state_dict(fused.state_dict())
+    x = torch.randn(5120 + 37, 16, device="cuda")
+    outs, grads = [], []
+    for net in (fused, plain):
+        xi = x.clone().requires_grad_(True)
+        y = net(xi)
+        (y * torch.linspace(-1, 1, 3, device="cuda")).pow(2).sum().backward()
+        outs.append(y.detach())
+        grads.append([xi.grad] + [p.grad.clone() for p in net.parameters()])
+        net.zero_grad(set_to_none=True)
+    np.testing.assert_allclose(outs[0].cpu().numpy(), outs[1].cpu().numpy(), rtol=1e-5, atol=1e-5)
+    for a, b in zip(*grads):
+        scale = b.abs().max().item()
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), rtol=1e-4, atol=1e-5 * scale)
+    for p in fused[2].parameters():
+        p.requires_grad_(False)
+    xi = x.clone().requires_grad_(True)
+    fused(xi).sum().backward()
+    assert fused[2].weight.grad is None and fused[0].weight.grad is not None and xi.grad is not None
