@@ -21,13 +21,14 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+PEAK_F32_MFMA_TFS = 157.3  # MI355X dense f32 matrix peak (v_mfma_f32_*_f32)
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--env", default="QuadTracking")
     p.add_argument("--envs", type=int, default=65536, help="parallel envs per GPU")
     p.add_argument("--policy", choices=["init", "hover"], default="init",
@@ -164,6 +165,14 @@ def main():
         N.lib().mh_rollout_step(h, N.ptr(logits), None, None, None, N.ptr(sampler.obs), ctypes.byref(buffer.ws),
                                 None, None, st)
 
+    have_fused = sampler._pack_policy() if hasattr(sampler, "_pack_policy") else False
+    pol_out = torch.empty(a.envs, 2 * sampler.envs.act_dim, dtype=torch.float32, device=dev)
+
+    def k_policy():  # the sampler's fused f32-MFMA policy forward (csrc/policy_mlp.hip)
+        N.lib().mh_policy_forward(N.ptr(sampler._packed), N.ptr(sampler.obs), a.envs, sampler.envs.obs_dim,
+                                  2 * sampler.envs.act_dim, N.ptr(pol_out), st)
+
+    t_pol = time_launches(k_policy, reps) * 1e-3 if have_fused else None
     t_step = time_launches(k_roll, reps) * 1e-3
     win1 = int(buffer.cursor[2].item())
     t_pair = time_launches(k_pair, reps, warm=0) * 1e-3
@@ -184,6 +193,13 @@ def main():
                         "GBps": round(bytes_emit / t_emit / 1e9, 1)},
         "method": f"HIP events around {reps} back-to-back launches after a GPU spin; emit = (rollout+emit) - rollout",
     }
+    if t_pol is not None:
+        D0, A2 = sampler.envs.obs_dim, 2 * sampler.envs.act_dim
+        flops = 2.0 * a.envs * (D0 * 256 + 256 * 256 + 256 * A2)
+        kernels["policy_forward"] = {"avg_us": round(t_pol * 1e6, 3), "flops": flops,
+                                     "TFLOPs": round(flops / t_pol / 1e12, 2),
+                                     "frac_f32_mfma": round(flops / t_pol / 1e12 / PEAK_F32_MFMA_TFS, 4),
+                                     "note": "per lockstep step; f32 MFMA bound, not HBM"}
     dom = "rollout_step" if t_step >= t_emit else "window_emit"
     ach = kernels[dom]["GBps"]
     traffic = None

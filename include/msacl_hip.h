@@ -65,6 +65,7 @@ int mh_env_info(int32_t env_id, mh_env_info_t* out);
 /* Replaces create_envs (RL/create_pkg/create_envs.py:9-35): a batch of `num_envs` envs of one
  * id, stepped in lockstep on the device. `seed` keys the in-kernel Philox stream used for
  * throughput-mode resets and action noise. */
+/* num_envs is bounded so each persistent SoA array stays under 2 GiB (QuadTracking: ~29.8M envs). */
 int mh_env_create(int32_t env_id, int64_t num_envs, uint64_t seed, mh_env_t* out);
 int mh_env_destroy(mh_env_t h);
 

@@ -157,6 +157,12 @@ int mh_env_create(int32_t env_id, int64_t num_envs, uint64_t seed, mh_env_t* out
     delete h;
     return rc;
   }
+  // the step kernel addresses the SoA state through 32-bit buffer offsets
+  if (num_envs * h->info.state_dim * (int64_t)sizeof(float) > (int64_t)INT32_MAX ||
+      num_envs * h->info.xstate_dim * (int64_t)sizeof(double) > (int64_t)INT32_MAX) {
+    delete h;
+    return fail(MH_EINVAL, "mh_env_create: num_envs too large for this env (state bytes must fit in 31 bits)");
+  }
   h->env_id = env_id;
   h->E = num_envs;
   h->seed = seed;

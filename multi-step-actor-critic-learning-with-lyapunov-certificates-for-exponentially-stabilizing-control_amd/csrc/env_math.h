@@ -854,6 +854,13 @@ struct QuadTracking {
     const float f = a[0];
     const float* M = a + 1;
     const float mf = (float)Q::m;
+    // the desired-trajectory row of this step, loaded before the substeps (its latency hides
+    // behind them instead of stalling desired_and_obs)
+    double rowv[QT_ROW];
+    {
+      const double* rp = tab + (size_t)(k + 1) * QT_ROW;
+      for (int i = 2; i < QT_ROW; ++i) rowv[i] = rp[i];
+    }
 #ifdef MH_EXP_NO_SUBSTEPS  // cost-attribution experiment only
     for (int it = 0; it < 0; ++it) {
 #else
@@ -886,7 +893,7 @@ struct QuadTracking {
       polar3(R, Rn);
       for (int i = 0; i < 9; ++i) R[i] = Rn[i];
     }
-    const double* row = tab + (size_t)(k + 1) * QT_ROW;
+    const double* row = rowv;
 #ifdef MH_EXP_NO_DESIRED  // cost-attribution experiment only
     for (int i = 0; i < 12; ++i) obs[i] = s[i] * 1e-3f;
     (void)row;

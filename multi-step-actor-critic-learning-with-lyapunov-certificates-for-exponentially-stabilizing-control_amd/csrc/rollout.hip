@@ -82,6 +82,13 @@ struct ResetDraw<QuadTracking> {  // QuadTracking.py:169-186
   }
 };
 
+// --------------------------------------------------------------- SoA buffer access
+typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
+// raw buffer resource over [p, p + bytes) (gfx9 dword3: 32-bit data format, no swizzle)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t soa_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
 // --------------------------------------------------------------- fused lockstep step
 template <class Env>
 #ifndef MH_ROLLOUT_MIN_WAVES
@@ -94,13 +101,30 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
   const int64_t e = (int64_t)blockIdx.x * BLK + threadIdx.x;
   const bool live = e < E;
   bool emit = false;
+  // store-cursor snapshot for the emission kernel, loaded up front by one thread (the grid
+  // finishes with its slowest wave: three dependent round trips at the end would be exposed)
+  const bool snap = a.ring && a.cursor && blockIdx.x == 0 && threadIdx.x == 0;
+  int64_t cur0 = 0, cur1 = 0, cur2 = 0;
+  if (snap) {
+    cur0 = a.cursor[0];
+    cur1 = a.cursor[1];
+    cur2 = a.cursor[2];
+  }
   if (live) {
     float s[S];
     double xs[XS > 0 ? XS : 1];
+    // SoA state through buffer resources: one VGPR byte offset per env plus a scalar offset per
+    // component, instead of a 64-bit address pair per component held live from load to store
+    // (mh_env_create bounds E so every byte offset fits in 31 bits)
+    const __amdgpu_buffer_rsrc_t rs_state = soa_rsrc(a.state, (uint32_t)(S * E * 4));
+    const __amdgpu_buffer_rsrc_t rs_xstate = soa_rsrc(a.xstate, (uint32_t)(XS * E * 8));
+    const int vo4 = (int)(e * 4), vo8 = (int)(e * 8);
 #pragma unroll
-    for (int i = 0; i < S; ++i) s[i] = a.state[(int64_t)i * E + e];
+    for (int i = 0; i < S; ++i)
+      s[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_state, vo4, (int)(i * E * 4), 0));
 #pragma unroll
-    for (int i = 0; i < XS; ++i) xs[i] = a.xstate[(int64_t)i * E + e];
+    for (int i = 0; i < XS; ++i)
+      xs[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs_xstate, vo8, (int)(i * E * 8), 0));
     const int k = a.steps[e];
     const uint32_t ctr = a.ctr[e];  // per-env counter: graph replays need no host RNG state
     const Rng rng = make_rng(a.seed, (uint64_t)e, ctr);
@@ -210,9 +234,11 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
       for (int i = 0; i < D; ++i) obsn[i] = obs2[i];
     }
 #pragma unroll
-    for (int i = 0; i < S; ++i) a.state[(int64_t)i * E + e] = s[i];
+    for (int i = 0; i < S; ++i)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, s[i]), rs_state, vo4, (int)(i * E * 4), 0);
 #pragma unroll
-    for (int i = 0; i < XS; ++i) a.xstate[(int64_t)i * E + e] = xs[i];
+    for (int i = 0; i < XS; ++i)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, xs[i]), rs_xstate, vo8, (int)(i * E * 8), 0);
     a.steps[e] = k1;
     a.ctr[e] = ctr + 1u;
     if (a.obs) {
@@ -290,11 +316,11 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
       a.emit_rank[e] = rank;
     }
     if (threadIdx.x == 0) a.block_count[blockIdx.x] = tot;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && a.cursor) {
+    if (snap) {
       // snapshot of the store cursor for the emission kernel (which rewrites the cursor)
-      a.meta[META_BASE] = a.cursor[0];
-      a.meta[META_SIZE] = a.cursor[1];
-      a.meta[META_GTOTAL] = a.cursor[2];
+      a.meta[META_BASE] = cur0;
+      a.meta[META_SIZE] = cur1;
+      a.meta[META_GTOTAL] = cur2;
     }
   }
 }
