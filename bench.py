@@ -35,6 +35,8 @@ def parse():
                    help="init: PyTorch default init (SURVEY 8d); hover: action mean [mg,0,0,0], long episodes")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--update-gemm", dest="update_gemm", choices=["auto", "hip", "blas"], default=None,
+                   help="GEMMs of the update MLPs: auto (default: mh_gemm_f32 where faster), hip or blas")
     p.add_argument("--blas", choices=["hipblaslt", "rocblas"], default=None,
                    help="GEMM library of the PyTorch parts (update MLPs); default: the config's (rocblas)")
     return p.parse_args()
@@ -100,6 +102,8 @@ def main():
                              num_eval_episode=1, sampler_sync_timing=False, device=dev)
     if a.blas is not None:
         cfg["blas_backend"] = a.blas
+    if a.update_gemm is not None:
+        cfg["update_gemm"] = a.update_gemm
     if a.policy == "hover":
         cfg["buffer_warm_size"] = 0
     args, alg, sampler, buffer, evaluator, trainer = build_pipeline(cfg)

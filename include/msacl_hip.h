@@ -206,6 +206,18 @@ int mh_act_grad_colsum(const float* dy, const float* y, int64_t rows, int32_t co
 int mh_adam_step(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
                  int32_t zero_grad, int64_t* step, uint32_t* ticket, void* stream);
 
+/* f32 GEMM on the f32 MFMA (csrc/gemm.hip) for the update phase's nn.Linear layers
+ * (RL/apprfunc/mlp.py:18-30 forward; autograd's input / weight gradients):
+ *   C[M][N] = act(op(A)[M][K] . op(B)[K][N] + bias[N]),  act 0 identity, 1 ReLU, 2 tanh
+ *   op(A)(m,k) = trans_a ? A[k*lda + m] : A[m*lda + k];  op(B)(k,n) = trans_b ? B[n*ldb + k] : B[k*ldb + n]
+ * bias may be NULL. Shapes whose plan splits K across workgroups need a `workspace` of the
+ * float count mh_gemm_workspace reports (0 = not needed); the split partials are summed in
+ * split order by a second launch (deterministic). */
+int mh_gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t* workspace_floats);
+int mh_gemm_f32(const float* A, const float* B, const float* bias, float* C, int64_t M, int64_t N, int64_t K,
+                int64_t lda, int64_t ldb, int64_t ldc, int32_t trans_a, int32_t trans_b, int32_t act,
+                float* workspace, void* stream);
+
 /* TanhGaussDistribution (RL/utils/act_distribution_cls.py:15-85) on [rows][2A] logits (mean | std)
  * with DEVICE action bounds high/low [A] (A <= 8), forward and backward as single launches:
  *   rsample   (eps [rows][A] standard normals) -> act [rows][A], logp [rows]

@@ -75,6 +75,8 @@ _PROTOS = {
     "mh_act_grad_chunks": (ctypes.c_int, [c_i64, ctypes.POINTER(c_i32)]),
     "mh_act_grad_colsum": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "mh_adam_step": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_f32, c_f32, c_f32, c_f32, c_i32, c_vp, c_vp, c_vp]),
+    "mh_gemm_workspace": (ctypes.c_int, [c_i64, c_i64, c_i64, ctypes.POINTER(c_i64)]),
+    "mh_gemm_f32": (ctypes.c_int, [c_vp] * 4 + [c_i64] * 6 + [c_i32] * 3 + [c_vp, c_vp]),
     "mh_tanh_gauss_rsample": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_i32, c_vp, c_vp, c_vp]),
     "mh_tanh_gauss_rsample_backward": (ctypes.c_int, [c_vp] * 6 + [c_i64, c_i32, c_vp, c_vp]),
     "mh_tanh_gauss_log_prob": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_i32, c_vp, c_vp]),

@@ -3,13 +3,22 @@
 The networks stay nn.Modules (nn.Sequential of nn.Linear + activation modules, the reference's
 parameters and state_dict keys); on HIP tensors their forward runs each (Linear, activation)
 pair as one autograd Function:
-  forward   y = act(x W^T + b): ReLU fused into the GEMM epilogue (torch._addmm_activation),
-            tanh applied in place on the GEMM output, identity = the GEMM alone
+  forward   y = act(x W^T + b): one mh_gemm_f32 launch (csrc/gemm.hip, f32 MFMA) with the bias
+            and ReLU / tanh in its epilogue
   backward  g = dy * act'(y) and the bias gradient (column sums of g) in one pass of
             mh_act_grad_colsum (csrc/mlp_grad.hip) instead of an elementwise backward kernel
-            plus a reduction; then dx = g W and dW = g^T x as two GEMMs, each only when autograd
-            needs it (frozen critics in the policy update skip dW / db).
-Same math as the module's own forward/backward; the GEMM reduction order is the library's.
+            plus a reduction; then dx = g W and dW = g^T x as two mh_gemm_f32 launches, each only
+            when autograd needs it (frozen critics in the policy update skip dW / db).
+Same math as the module's own forward/backward, f32 throughout; the GEMM summation order is the
+kernel's. Backend (`set_gemm_backend`, config key `update_gemm`):
+  "auto" (default)  mh_gemm_f32 where it measured faster than the BLAS library on the update's
+                    shapes (tools/gemm_shapes.py, profiles/r01_gemm_shapes.json): forwards on
+                    <= 1,024 rows (the B = 256 rows of the first-step networks: 8 vs 63 us, where
+                    the library runs a 256^3 product on one workgroup) or into one output column
+                    (critic heads), and weight gradients of one-output layers; the library
+                    (torch.addmm / _addmm_activation / mm) elsewhere
+  "hip"             every GEMM through mh_gemm_f32
+  "blas"            every GEMM through the library
 CPU tensors (and activations other than identity/ReLU/tanh) take the plain nn.Sequential path.
 """
 from __future__ import annotations
@@ -27,10 +36,60 @@ def _native():
     return N
 
 
+_GEMM_BACKEND = {"name": "auto"}
+_WS = {}
+
+
+def set_gemm_backend(name: str):
+    """"auto" (default), "hip" (mh_gemm_f32 everywhere) or "blas" (PyTorch's GEMM library)."""
+    if name not in ("auto", "hip", "blas"):
+        raise ValueError(f"update_gemm must be 'auto', 'hip' or 'blas', got {name!r}")
+    _GEMM_BACKEND["name"] = name
+
+
+def _hip_forward(rows, out_features):
+    b = _GEMM_BACKEND["name"]
+    return b == "hip" or (b == "auto" and (rows <= 1024 or out_features == 1))
+
+
+def _hip_dx():
+    return _GEMM_BACKEND["name"] == "hip"
+
+
+def _hip_dw(out_features):
+    b = _GEMM_BACKEND["name"]
+    return b == "hip" or (b == "auto" and out_features == 1)
+
+
+def gemm_backend() -> str:
+    return _GEMM_BACKEND["name"]
+
+
+def gemm(a, b, bias, M, N, K, lda, ldb, ta, tb, act=0):
+    """C[M][N] = act(op(a) op(b) + bias) on the f32 MFMA (include/msacl_hip.h: mh_gemm_f32)."""
+    N_ = _native()
+    key = (M, N, K)
+    wsf = _WS.get(key)
+    if wsf is None:
+        wf = ctypes.c_int64()
+        N_.check(N_.lib().mh_gemm_workspace(M, N, K, ctypes.byref(wf)), "mh_gemm_workspace")
+        wsf = _WS[key] = wf.value
+    dev = a.device
+    c = torch.empty(M, N, dtype=torch.float32, device=dev)
+    work = torch.empty(wsf, dtype=torch.float32, device=dev) if wsf else None
+    N_.check(N_.lib().mh_gemm_f32(N_.ptr(a), N_.ptr(b), N_.ptr(bias), N_.ptr(c), M, N, K, lda, ldb, N, ta, tb, act,
+                                  N_.ptr(work), N_.stream_of(dev)), "mh_gemm_f32")
+    return c
+
+
 class LinearAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, act):
-        if act == 1:
+        M, K = x.shape
+        Nout = weight.shape[0]
+        if _hip_forward(M, Nout):
+            y = gemm(x, weight.contiguous(), bias.contiguous(), M, Nout, K, K, K, 0, 1, act)
+        elif act == 1:
             y = torch._addmm_activation(bias, x, weight.t())
         else:
             y = torch.addmm(bias, x, weight.t())
@@ -60,8 +119,13 @@ class LinearAct(torch.autograd.Function):
             N.check(N.lib().mh_act_grad_colsum(N.ptr(dy), N.ptr(y.contiguous()) if act else None, M, C, act,
                                                N.ptr(g) if act else None, N.ptr(db), N.ptr(partial),
                                                N.stream_of(dy.device)), "mh_act_grad_colsum")
-        dx = g.mm(weight) if need_x else None
-        dw = g.t().mm(x) if need_w else None
+        M, Nout = g.shape
+        K = x.shape[1]
+        dx = dw = None
+        if need_x:
+            dx = gemm(g, weight.contiguous(), None, M, K, Nout, Nout, K, 0, 0) if _hip_dx() else g.mm(weight)
+        if need_w:
+            dw = gemm(g, x, None, Nout, K, M, Nout, K, 1, 0) if _hip_dw(Nout) else g.t().mm(x)
         return dx, dw, db, None
 
 

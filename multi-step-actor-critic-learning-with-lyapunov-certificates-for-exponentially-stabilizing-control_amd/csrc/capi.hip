@@ -479,6 +479,29 @@ int mh_adam_step(float* p, float* g, float* m, float* v, int64_t n, float lr, fl
   return MH_OK;
 }
 
+int mh_gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t* workspace_floats) {
+  if (!workspace_floats) return fail(MH_EINVAL, "mh_gemm_workspace: null out");
+  if (M < 0 || N < 0 || K < 0) return fail(MH_EINVAL, "mh_gemm_workspace: negative size");
+  *workspace_floats = (M > 0 && N > 0) ? mh::gemm_workspace_floats(M, N, K > 0 ? K : 1) : 0;
+  return MH_OK;
+}
+
+int mh_gemm_f32(const float* A, const float* B, const float* bias, float* C, int64_t M, int64_t N, int64_t K,
+                int64_t lda, int64_t ldb, int64_t ldc, int32_t trans_a, int32_t trans_b, int32_t act,
+                float* workspace, void* stream) {
+  if (M < 0 || N < 0 || K < 0) return fail(MH_EINVAL, "mh_gemm_f32: negative size");
+  if (M == 0 || N == 0) return MH_OK;
+  if (act < 0 || act > 2) return fail(MH_EINVAL, "mh_gemm_f32: act must be 0 (identity), 1 (relu) or 2 (tanh)");
+  if (!C || (K > 0 && (!A || !B))) return fail(MH_EINVAL, "mh_gemm_f32: null operand");
+  if (ldc < N || (K > 0 && (lda < (trans_a ? M : K) || ldb < (trans_b ? K : N))))
+    return fail(MH_EINVAL, "mh_gemm_f32: leading dimension smaller than the matrix");
+  if (mh::gemm_workspace_floats(M, N, K > 0 ? K : 1) > 0 && !workspace)
+    return fail(MH_EINVAL, "mh_gemm_f32: this shape needs the workspace of mh_gemm_workspace");
+  MH_HIP(mh::launch_gemm(A, B, bias, C, M, N, K, lda, ldb, ldc, trans_a != 0, trans_b != 0, act, workspace,
+                         (hipStream_t)stream));
+  return MH_OK;
+}
+
 #define MH_TG_CHECK(name)                                                                           \
   if (rows < 0 || act_dim <= 0 || act_dim > 8) return fail(MH_EINVAL, name ": act_dim must be in [1, 8]"); \
   if (rows == 0) return MH_OK;                                                                     \

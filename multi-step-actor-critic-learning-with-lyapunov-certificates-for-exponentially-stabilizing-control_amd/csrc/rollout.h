@@ -95,6 +95,10 @@ hipError_t launch_gae(const float* val, const float* val2, const float* rew, con
 hipError_t launch_reset(int env_id, const StepArgs& a, hipStream_t st);
 int64_t policy_packed_floats(int D);
 int act_grad_chunks(int64_t M);
+hipError_t launch_gemm(const float* A, const float* B, const float* bias, float* C, int64_t M, int64_t N, int64_t K,
+                       int64_t lda, int64_t ldb, int64_t ldc, int ta, int tb, int act, float* workspace,
+                       hipStream_t st);
+int64_t gemm_workspace_floats(int64_t M, int64_t N, int64_t K);
 hipError_t launch_tg_rsample(const float* logits, const float* eps, const float* high, const float* low, int64_t M,
                              int A, float* act, float* logp, hipStream_t st);
 hipError_t launch_tg_rsample_bwd(const float* logits, const float* eps, const float* high, const float* low,

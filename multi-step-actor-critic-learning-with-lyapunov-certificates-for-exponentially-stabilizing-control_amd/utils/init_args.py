@@ -26,6 +26,10 @@ def init_args(envs, **args):
         blas = args.get("blas_backend", "rocblas")
         if blas in ("rocblas", "hipblaslt"):
             torch.backends.cuda.preferred_blas_library("cublas" if blas == "rocblas" else "cublaslt")
+        # the MLP layers' GEMMs: "auto" = mh_gemm_f32 (csrc/gemm.hip) on the shapes where it beats
+        # the library above, "hip" / "blas" = one of the two everywhere
+        from ..apprfunc._fused import set_gemm_backend
+        set_gemm_backend(args.get("update_gemm", "auto"))
     else:
         if args.get("enable_cuda", True):
             warnings.warn("HIP device is not available, use CPU instead")

@@ -1,0 +1,95 @@
+"""GPU: mh_gemm_f32 (csrc/gemm.hip, f32 MFMA) against a float64 product of the same float32
+operands, for the update's layer shapes (B x n = 5,120 and 256 rows; 256-wide hidden layers;
+1- and 8-wide heads; the transposed weight-gradient form with K = 5,120, which takes the
+cross-workgroup split + reduce launch) and ragged edges. Tolerance: f32 accumulation over K terms,
+|err| <= 2e-6 * sqrt(K) * sum_k |a_k b_k| + 1e-6 (the k-ordered fma chain's bound with margin)."""
+import ctypes
+
+import pytest
+import torch
+
+import msacl_amd  # noqa: F401
+import msacl_amd._native as N
+from msacl_amd.apprfunc._fused import gemm
+
+pytestmark = pytest.mark.gpu
+
+
+def _op(t, trans):
+    return t.t() if trans else t
+
+
+def _ref(a, b, bias, ta, tb, act):
+    A = _op(a.double(), ta)
+    B = _op(b.double(), tb)
+    c = A @ B
+    mag = A.abs() @ B.abs()
+    if bias is not None:
+        c = c + bias.double()
+        mag = mag + bias.double().abs()
+    if act == 1:
+        c = torch.relu(c)
+    elif act == 2:
+        c = torch.tanh(c)
+    return c, mag
+
+
+SHAPES = [  # (M, N, K)
+    (5120, 256, 16), (5120, 256, 256), (5120, 1, 256), (5120, 8, 256), (256, 256, 256), (256, 256, 12),
+    (256, 8, 256), (256, 256, 5120), (8, 256, 5120), (1, 256, 5120), (16, 256, 5120), (256, 16, 5120),
+    (333, 77, 45), (1, 1, 1), (65, 33, 129), (7, 300, 1000),
+]
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("ta,tb", [(0, 1), (0, 0), (1, 0), (1, 1)])
+def test_gemm_matches_f64(M, N, K, ta, tb):
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N * 3 + K + 10 * ta + tb)
+    a = torch.randn(*((K, M) if ta else (M, K)), device="cuda", generator=g)
+    b = torch.randn(*((N, K) if tb else (K, N)), device="cuda", generator=g)
+    bias = torch.randn(N, device="cuda", generator=g)
+    act = (M + N + K) % 3
+    lda = a.shape[1]
+    ldb = b.shape[1]
+    c = gemm(a, b, bias, M, N, K, lda, ldb, ta, tb, act)
+    ref, mag = _ref(a, b, bias, ta, tb, act)
+    err = (c.double() - ref).abs()
+    tol = 2e-6 * (K ** 0.5) * mag + 1e-6
+    assert bool((err <= tol).all()), f"max err {float(err.max()):.3e}"
+
+
+def test_gemm_weight_gradient_form_is_deterministic():
+    """dW = g^T x (op(A) transposed, K = 5,120 rows): the split partials are summed in split
+    order, so repeated launches agree bit for bit."""
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    gr = torch.randn(5120, 256, device="cuda", generator=gen)
+    x = torch.randn(5120, 256, device="cuda", generator=gen)
+    c1 = gemm(gr, x, None, 256, 256, 5120, 256, 256, 1, 0)
+    c2 = gemm(gr, x, None, 256, 256, 5120, 256, 256, 1, 0)
+    assert torch.equal(c1, c2)
+    ref = gr.double().t() @ x.double()
+    assert float((c1.double() - ref).abs().max()) < 1e-3
+
+
+def test_gemm_asymmetric_exact_integers():
+    """Exact small-integer data: catches any row/column swap of the MFMA C map."""
+    M, N, K = 96, 80, 64
+    a = (torch.arange(M * K, device="cuda") % 7 - 3).float().reshape(M, K)
+    b = (torch.arange(K * N, device="cuda") % 5 - 2).float().reshape(K, N) * (1 + torch.arange(N, device="cuda")) % 4
+    c = gemm(a, b.contiguous(), None, M, N, K, K, N, 0, 0)
+    assert torch.equal(c, a @ b)
+
+
+def test_gemm_rejects_bad_leading_dimension():
+    a = torch.zeros(4, 4, device="cuda")
+    out = torch.empty(4, 4, device="cuda")
+    rc = N.lib().mh_gemm_f32(N.ptr(a), N.ptr(a), None, N.ptr(out), 4, 4, 4, 2, 4, 4, 0, 0, 0, None, N.stream_of())
+    assert rc != 0 and b"leading dimension" in N.lib().mh_last_error()
+
+
+def test_gemm_workspace_query():
+    wf = ctypes.c_int64()
+    assert N.lib().mh_gemm_workspace(256, 256, 5120, ctypes.byref(wf)) == 0
+    assert wf.value > 0 and wf.value % (256 * 256) == 0
+    assert N.lib().mh_gemm_workspace(5120, 256, 256, ctypes.byref(wf)) == 0
+    assert wf.value == 0

@@ -74,18 +74,30 @@ def test_sampler_uses_fused_policy_and_matches_torch_path():
         np.testing.assert_allclose(fused.detach().cpu().numpy(), torch_logits.detach().cpu().numpy(), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("backend", ["auto", "hip", "blas"])
 @pytest.mark.parametrize("act", [nn.ReLU, nn.Tanh, nn.Identity])
-def test_fused_linear_act_forward_backward_matches_torch(act):
-    """apprfunc/_fused.py LinearAct (GEMM epilogue activation, mh_act_grad_colsum backward) vs the
-    plain nn.Sequential forward/backward: outputs and every gradient (x, W, b) to float32 rounding;
-    frozen parameters get no gradient."""
-    from msacl_amd.apprfunc._fused import MLP
+@pytest.mark.parametrize("rows", [5120 + 37, 256])
+def test_fused_linear_act_forward_backward_matches_torch(act, backend, rows):
+    """apprfunc/_fused.py LinearAct (GEMM epilogue activation, mh_act_grad_colsum backward) under
+    each GEMM backend (mh_gemm_f32 / library / per-shape choice) vs the plain nn.Sequential
+    forward/backward: outputs and every gradient (x, W, b) to float32 rounding; frozen parameters
+    get no gradient."""
+    from msacl_amd.apprfunc._fused import MLP, gemm_backend, set_gemm_backend
+    prev = gemm_backend()
+    set_gemm_backend(backend)
+    try:
+        _linear_act_case(MLP, act, rows)
+    finally:
+        set_gemm_backend(prev)
+
+
+def _linear_act_case(MLP, act, rows):
     torch.manual_seed(3)
     layers = [nn.Linear(16, 256), act(), nn.Linear(256, 256), act(), nn.Linear(256, 3), nn.Identity()]
     fused = MLP(*layers).cuda()
     plain = nn.Sequential(*[type(m)() if not isinstance(m, nn.Linear) else m for m in layers]).cuda()
     plain.load_state_dict(fused.state_dict())
-    x = torch.randn(5120 + 37, 16, device="cuda")
+    x = torch.randn(rows, 16, device="cuda")
     outs, grads = [], []
     for net in (fused, plain):
         xi = x.clone().requires_grad_(True)

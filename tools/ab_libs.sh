@@ -6,7 +6,7 @@
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG=multi-step-actor-critic-learning-with-lyapunov-certificates-for-exponentially-stabilizing-control_amd
-SRCS="rollout capi msacl_kernels per gae policy_mlp mlp_grad optim dist_kernels"
+SRCS="rollout capi msacl_kernels per gae policy_mlp mlp_grad optim dist_kernels gemm"
 build_dir() {  # $1 = csrc dir, $2 = include dir, $3 = out dir
   mkdir -p "$3"
   ( cd "$1" && for f in $SRCS; do

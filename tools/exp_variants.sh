@@ -10,7 +10,7 @@ if [ "$1" != "run" ]; then
   for v in $VARIANTS; do
     out="$ROOT/exp_libs/$v"; mkdir -p "$out"
     def=""; [ "$v" != "base" ] && def="-DMH_EXP_$v"
-    ( cd "$CS" && for f in rollout capi msacl_kernels per gae policy_mlp mlp_grad optim dist_kernels; do
+    ( cd "$CS" && for f in rollout capi msacl_kernels per gae policy_mlp mlp_grad optim dist_kernels gemm; do
         /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
           -I"$ROOT/include" -I. $def ${EXTRA_FLAGS} -c $f.hip -o "$out/$f.o" & done; wait
       /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$out/libmsacl_hip.so" "$out"/*.o )
