@@ -210,8 +210,8 @@ int mh_adam_step(float* p, float* g, float* m, float* v, int64_t n, float lr, fl
  * (RL/apprfunc/mlp.py:18-30 forward; autograd's input / weight gradients):
  *   C[M][N] = act(op(A)[M][K] . op(B)[K][N] + bias[N]),  act 0 identity, 1 ReLU, 2 tanh
  *   op(A)(m,k) = trans_a ? A[k*lda + m] : A[m*lda + k];  op(B)(k,n) = trans_b ? B[n*ldb + k] : B[k*ldb + n]
- * bias may be NULL. Shapes whose plan splits K across workgroups need a `workspace` of the
- * float count mh_gemm_workspace reports (0 = not needed); the split partials are summed in
+ * bias may be NULL; each operand must be smaller than 2 GiB. Shapes whose plan splits K across
+ * workgroups need a `workspace` of the float count mh_gemm_workspace reports (0 = not needed); the split partials are summed in
  * split order by a second launch (deterministic). */
 int mh_gemm_workspace(int64_t M, int64_t N, int64_t K, int64_t* workspace_floats);
 int mh_gemm_f32(const float* A, const float* B, const float* bias, float* C, int64_t M, int64_t N, int64_t K,

@@ -495,6 +495,8 @@ int mh_gemm_f32(const float* A, const float* B, const float* bias, float* C, int
   if (!C || (K > 0 && (!A || !B))) return fail(MH_EINVAL, "mh_gemm_f32: null operand");
   if (ldc < N || (K > 0 && (lda < (trans_a ? M : K) || ldb < (trans_b ? K : N))))
     return fail(MH_EINVAL, "mh_gemm_f32: leading dimension smaller than the matrix");
+  if ((trans_a ? K : M) * lda * 4 >= ((int64_t)1 << 31) - 64 || (trans_b ? N : K) * ldb * 4 >= ((int64_t)1 << 31) - 64)
+    return fail(MH_EINVAL, "mh_gemm_f32: each operand must be smaller than 2 GiB");
   if (mh::gemm_workspace_floats(M, N, K > 0 ? K : 1) > 0 && !workspace)
     return fail(MH_EINVAL, "mh_gemm_f32: this shape needs the workspace of mh_gemm_workspace");
   MH_HIP(mh::launch_gemm(A, B, bias, C, M, N, K, lda, ldb, ldc, trans_a != 0, trans_b != 0, act, workspace,

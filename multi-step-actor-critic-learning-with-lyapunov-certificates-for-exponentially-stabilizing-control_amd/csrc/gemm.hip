@@ -12,13 +12,15 @@
 // workgroup for 47 us (profiles/r01_update_mix_v2.txt). Here every shape fills the chip:
 //   * workgroup = 4 waves; wave tile 32 x 32 (2 x 2 accumulators of 16 x 16, 4 independent MFMA
 //     chains: the 40-cycle dependent latency hides behind the 32-cycle issue);
-//   * the 4 waves tile the workgroup's (32 WM) x (32 WN) block and split each 64-deep K chunk
+//   * the 4 waves tile the workgroup's (32 WM) x (32 WN) block and split each 32-deep K chunk
 //     KS = 4 / (WM WN) ways, reduced through LDS in fixed order;
 //   * small output grids split K across workgroups (S-way): each writes its partial tile and
 //     k_gemm_reduce sums the S partials in split order with the epilogue (deterministic);
-//   * operands are staged through LDS per 64-deep chunk, the next chunk's global loads in flight
-//     during the current chunk's MFMAs (register double buffer); interior tiles and full chunks
-//     load without bounds checks.
+//   * operands are staged through LDS per 32-deep chunk, the next chunk's global loads in flight
+//     during the current chunk's MFMAs (register double buffer); the loads go through raw buffer
+//     resources with 32-bit byte offsets (one VGPR per thread and operand instead of a 64-bit
+//     address per element: 80-110 VGPRs, two workgroups per CU), and an element outside the
+//     matrix gets an out-of-range offset, which the buffer unit returns as 0 (no branches).
 // Numerics: each output is an f32 fma chain over k (MFMA f32 is exact per product, one rounding
 // per accumulate), split partials added in order; agrees with the BLAS result to f32
 // summation-order rounding.
@@ -40,7 +42,7 @@ struct GemmArgs {
   float* partial;    // [S][M][N] when S > 1
 };
 
-constexpr int KC = 64;  // K depth of one LDS stage
+constexpr int KC = 32;  // K depth of one LDS stage
 
 __device__ __forceinline__ float gemm_act(float v, int act) {
   if (act == 1) return v < 0.0f ? 0.0f : v;  // relu (NaN passes through, as torch.relu)
@@ -81,39 +83,30 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
     const int idx = tid + 256 * i;
     if (TB) { k = idx % KC; n = idx / KC; } else { n = idx % TN; k = idx / TN; }
   };
-  const bool interior_a = m0 + TM <= g.M, interior_b = n0 + TN <= g.N;
+  const __amdgpu_buffer_rsrc_t ra_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(g.A), (short)0, (int)((TA ? g.K : g.M) * g.lda * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(g.B), (short)0, (int)((TB ? g.N : g.K) * g.ldb * 4), 0x00020000);
+  constexpr int OOB = 0x7ffffff0;  // beyond every buffer (host keeps them below 2 GiB): reads 0
   auto load_chunk = [&](int64_t c) {
-    const int64_t k0 = c * KC;
-    if (k0 + KC <= g.K && interior_a && interior_b) {
-      const float* Ab = TA ? g.A + k0 * g.lda + m0 : g.A + m0 * g.lda + k0;
-      const float* Bb = TB ? g.B + n0 * g.ldb + k0 : g.B + k0 * g.ldb + n0;
-#pragma unroll
-      for (int i = 0; i < NA; ++i) {
-        int m, k;
-        a_idx(i, m, k);
-        ra[i] = TA ? Ab[(int64_t)k * g.lda + m] : Ab[(int64_t)m * g.lda + k];
-      }
-#pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        int n, k;
-        b_idx(i, n, k);
-        rb[i] = TB ? Bb[(int64_t)n * g.ldb + k] : Bb[(int64_t)k * g.ldb + n];
-      }
-      return;
-    }
+    const int k0 = (int)(c * KC);
 #pragma unroll
     for (int i = 0; i < NA; ++i) {
       int m, k;
       a_idx(i, m, k);
-      const int64_t gm = m0 + m, gk = k0 + k;
-      ra[i] = (gm < g.M && gk < g.K) ? (TA ? g.A[gk * g.lda + gm] : g.A[gm * g.lda + gk]) : 0.0f;
+      const int gm = (int)m0 + m, gk = k0 + k;
+      const int off = TA ? (gk * (int)g.lda + gm) * 4 : (gm * (int)g.lda + gk) * 4;
+      const bool ok = gm < (int)g.M && gk < (int)g.K;
+      ra[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ra_rs, ok ? off : OOB, 0, 0));
     }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       int n, k;
       b_idx(i, n, k);
-      const int64_t gn = n0 + n, gk = k0 + k;
-      rb[i] = (gn < g.N && gk < g.K) ? (TB ? g.B[gn * g.ldb + gk] : g.B[gk * g.ldb + gn]) : 0.0f;
+      const int gn = (int)n0 + n, gk = k0 + k;
+      const int off = TB ? (gn * (int)g.ldb + gk) * 4 : (gk * (int)g.ldb + gn) * 4;
+      const bool ok = gn < (int)g.N && gk < (int)g.K;
+      rb[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb_rs, ok ? off : OOB, 0, 0));
     }
   };
 
@@ -256,7 +249,7 @@ static GemmPlan gemm_plan(int64_t M, int64_t N, int64_t K) {
     S = (chunks + kc_per - 1) / kc_per;
     const int64_t wgs = tiles * S;
     // rounds of resident workgroups x per-wave work (MFMA issue + chunk staging latency)
-    const double rounds = (double)((wgs + 511) / 512);
+    const double rounds = (double)((wgs + 1023) / 1024);  // <= 110 VGPRs: 4 workgroups per CU
     const double per_chunk = (KC / 4.0 / KS) * 4.0 * 32.0 + 1500.0;
     const double cost = rounds * (double)kc_per * per_chunk + (S > 1 ? 6000.0 : 0.0) + (KS > 1 ? 300.0 : 0.0);
     if (cost < best_cost - 1e-9) {
@@ -285,6 +278,9 @@ hipError_t launch_gemm(const float* A, const float* B, const float* bias, float*
                        int64_t lda, int64_t ldb, int64_t ldc, int ta, int tb, int act, float* workspace,
                        hipStream_t st) {
   if (M <= 0 || N <= 0) return hipSuccess;
+  // 32-bit buffer offsets (load_chunk): both operands below 2 GiB
+  if ((ta ? K : M) * lda * 4 >= ((int64_t)1 << 31) - 64 || (tb ? N : K) * ldb * 4 >= ((int64_t)1 << 31) - 64)
+    return hipErrorInvalidValue;
   const GemmPlan p = gemm_plan(M, N, K > 0 ? K : 1);
   GemmArgs g{A, B, bias, C, M, N, K, lda, ldb, ldc, act, p.S, p.kc_per, workspace};
   const int64_t grid = p.tiles * p.S;
