@@ -199,12 +199,23 @@ int mh_act_grad_chunks(int64_t rows, int32_t* chunks_out);
  * (RL/apprfunc/mlp.py:18-30 layers under autograd). Deterministic (fixed summation order). */
 int mh_act_grad_colsum(const float* dy, const float* y, int64_t rows, int32_t cols, int32_t act, float* g,
                        float* db, float* partial, void* stream);
-/* One torch.optim.Adam step (betas b1, b2, eps; no weight decay / amsgrad) over a contiguous
- * parameter buffer p with gradient g and moments m, v (all n floats). step: DEVICE int64 step
- * count (read, then advanced by one); ticket: DEVICE uint32 initialised to 0 (kept at 0 between
- * calls). zero_grad != 0 also zeroes g. Capturable (no host sync). */
-int mh_adam_step(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
-                 int32_t zero_grad, int64_t* step, uint32_t* ticket, void* stream);
+/* One torch.optim.Adam step (torch.optim.Adam(fused/capturable) math: betas, eps, no weight decay /
+ * amsgrad / maximize) over a list of parameter tensors in one launch per 32 tensors, replacing
+ * the optimiser.step() of every reference algorithm (RL/algorithm/{msacl,sac,lac,ppo,polyc}.py). Each entry: param,
+ * grad, exp_avg, exp_avg_sq (numel floats each, contiguous, DEVICE) and step (DEVICE float32
+ * scalar, the PyTorch capturable state; read, then advanced by one). ticket: DEVICE uint32, zero
+ * on entry, left zero (one per stream). Capturable (no host sync); the list itself is host memory
+ * passed by value in the kernel arguments. */
+typedef struct {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  float* step;
+  int64_t numel;
+} mh_adam_tensor_t;
+int mh_adam_multi(const mh_adam_tensor_t* tensors, int32_t n, double lr, double beta1, double beta2, double eps,
+                  uint32_t* ticket, void* stream);
 
 /* f32 GEMM on the f32 MFMA (csrc/gemm.hip) for the update phase's nn.Linear layers
  * (RL/apprfunc/mlp.py:18-30 forward; autograd's input / weight gradients):

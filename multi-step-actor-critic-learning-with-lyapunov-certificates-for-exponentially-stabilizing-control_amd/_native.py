@@ -37,6 +37,12 @@ class EnvInfo(ctypes.Structure):
     ]
 
 
+class AdamTensor(ctypes.Structure):
+    """mh_adam_tensor_t (include/msacl_hip.h)."""
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("step", ctypes.c_void_p), ("numel", ctypes.c_int64)]
+
+
 class TrajStore(ctypes.Structure):
     _fields_ = [
         ("obs", c_vp), ("act", c_vp), ("rew", c_vp), ("cost", c_vp), ("obs2", c_vp), ("done", c_vp),
@@ -74,7 +80,8 @@ _PROTOS = {
     "mh_policy_forward": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "mh_act_grad_chunks": (ctypes.c_int, [c_i64, ctypes.POINTER(c_i32)]),
     "mh_act_grad_colsum": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
-    "mh_adam_step": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_f32, c_f32, c_f32, c_f32, c_i32, c_vp, c_vp, c_vp]),
+    "mh_adam_multi": (ctypes.c_int, [c_vp, c_i32, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                     c_vp, c_vp]),
     "mh_gemm_workspace": (ctypes.c_int, [c_i64, c_i64, c_i64, ctypes.POINTER(c_i64)]),
     "mh_gemm_f32": (ctypes.c_int, [c_vp] * 4 + [c_i64] * 6 + [c_i32] * 3 + [c_vp, c_vp]),
     "mh_tanh_gauss_rsample": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_i32, c_vp, c_vp, c_vp]),

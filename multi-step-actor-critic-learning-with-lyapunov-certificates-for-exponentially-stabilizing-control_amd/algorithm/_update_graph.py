@@ -1,8 +1,12 @@
 """Shared pieces of the device algorithms (not an algorithm plugin: the leading underscore keeps
 it out of the create_alg registry, RL/create_pkg/create_alg.py:38-47).
 
-* fused_adam: torch's single-kernel Adam, capturable (step counter on the device), so an update
-  that contains optimiser steps can be captured into a HIP graph.
+* fused_adam: the algorithms' Adam. On HIP float32 parameters a HipAdam: torch.optim.Adam's
+  capturable state (device float32 step, exp_avg, exp_avg_sq; same state_dict) whose step() is
+  ONE mh_adam_multi launch per optimiser (csrc/optim.hip) — PyTorch's fused kernel gives each
+  65,536-element chunk one workgroup (31 us per step for a 256 x 256 MLP) and increments the
+  step counters in a second launch. Elsewhere torch's fused / plain Adam. Capturable either way,
+  so an update that contains optimiser steps can be captured into a HIP graph.
 * UpdateGraph: replays a whole model update as ONE HIP graph per branch key (e.g. the
   (update-target, update-policy) flags of an iteration). First call per branch runs eagerly on
   static input copies (lazy hipBLASLt / Adam state init), the second captures, later calls copy
@@ -18,12 +22,69 @@ from torch.optim import Adam
 from ..utils import dist as D
 
 
+class HipAdam(Adam):
+    """torch.optim.Adam (betas, eps; no weight decay / amsgrad / maximize) with capturable state.
+    step(): one mh_adam_multi launch per parameter group when every parameter with a gradient is
+    a contiguous HIP float32 tensor; otherwise torch's own step (fused where available) on the
+    same state. The choice is made at each step: the algorithms build their optimisers before
+    moving the networks to the device."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, fused=None):
+        super().__init__(params, lr=lr, betas=betas, eps=eps, capturable=True, fused=fused)
+        self._ticket = None
+
+    def _hip_entries(self, group):
+        entries = []
+        for p in group["params"]:
+            if p.grad is None:
+                continue
+            if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.grad.is_contiguous()
+                    and p.grad.dtype == torch.float32):
+                return None
+            st = self.state[p]
+            if len(st) == 0:
+                st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            m, v, stp = st["exp_avg"], st["exp_avg_sq"], st["step"]
+            if not (m.is_contiguous() and v.is_contiguous() and stp.is_cuda and stp.dtype == torch.float32):
+                return None
+            entries.append((p, p.grad, m, v, stp))
+        return entries
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        groups = [(g, self._hip_entries(g)) for g in self.param_groups]
+        if any(e is None for _, e in groups) or any(torch.is_tensor(g["lr"]) for g, _ in groups):
+            return super().step(closure)
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        from .. import _native as N
+        for group, entries in groups:
+            if not entries:
+                continue
+            dev = entries[0][0].device
+            if self._ticket is None or self._ticket.device != dev:
+                self._ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+            b1, b2 = group["betas"]
+            arr = (N.AdamTensor * len(entries))()
+            for i, (p, g, m, v, stp) in enumerate(entries):
+                arr[i] = N.AdamTensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), stp.data_ptr(),
+                                      p.numel())
+            N.check(N.lib().mh_adam_multi(arr, len(entries), float(group["lr"]), float(b1), float(b2),
+                                          float(group["eps"]), N.ptr(self._ticket), N.stream_of(dev)),
+                    "mh_adam_multi")
+        return loss
+
+
 def fused_adam(params, lr):
     params = list(params)
     try:
-        return Adam(params, lr=lr, fused=True, capturable=True)
+        return HipAdam(params, lr=lr, fused=True)
     except (RuntimeError, TypeError, ValueError):
-        return Adam(params, lr=lr)
+        return HipAdam(params, lr=lr)
 
 
 class UpdateGraph:

@@ -32,13 +32,10 @@ from ..utils.tensorboard_setup import tb_tags
 
 
 def _adam(params, lr):
-    """Fused single-kernel Adam, capturable (step counter on device) so the whole update can
-    be replayed as a HIP graph."""
-    params = list(params)
-    try:
-        return Adam(params, lr=lr, fused=True, capturable=True)
-    except (RuntimeError, TypeError, ValueError):
-        return Adam(params, lr=lr)
+    """Single-launch capturable Adam (algorithm/_update_graph.py fused_adam: mh_adam_multi on HIP
+    float32 parameters), so the whole update can be replayed as a HIP graph."""
+    from ._update_graph import fused_adam
+    return fused_adam(params, lr)
 
 
 class ApproxContainer(nn.Module):

@@ -471,11 +471,26 @@ int mh_act_grad_colsum(const float* dy, const float* y, int64_t rows, int32_t co
   return MH_OK;
 }
 
-int mh_adam_step(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
-                 int32_t zero_grad, int64_t* step, uint32_t* ticket, void* stream) {
-  if (!p || !g || !m || !v || !step || !ticket) return fail(MH_EINVAL, "mh_adam_step: null pointer");
-  if (n < 0) return fail(MH_EINVAL, "mh_adam_step: negative size");
-  MH_HIP(mh::launch_adam(p, g, m, v, n, lr, b1, b2, eps, zero_grad, step, ticket, (hipStream_t)stream));
+int mh_adam_multi(const mh_adam_tensor_t* tensors, int32_t n, double lr, double beta1, double beta2, double eps,
+                  uint32_t* ticket, void* stream) {
+  if (n < 0 || (n > 0 && (!tensors || !ticket))) return fail(MH_EINVAL, "mh_adam_multi: bad argument");
+  for (int32_t base = 0; base < n; base += mh::ADAM_MAX_TENSORS) {
+    mh::AdamList L{};
+    L.n = n - base < mh::ADAM_MAX_TENSORS ? n - base : mh::ADAM_MAX_TENSORS;
+    L.start[0] = 0;
+    for (int k = 0; k < L.n; ++k) {
+      const mh_adam_tensor_t& t = tensors[base + k];
+      if (!t.param || !t.grad || !t.exp_avg || !t.exp_avg_sq || !t.step || t.numel < 0)
+        return fail(MH_EINVAL, "mh_adam_multi: null pointer or negative size in the tensor list");
+      L.p[k] = t.param;
+      L.g[k] = t.grad;
+      L.m[k] = t.exp_avg;
+      L.v[k] = t.exp_avg_sq;
+      L.step[k] = t.step;
+      L.start[k + 1] = L.start[k] + t.numel;
+    }
+    MH_HIP(mh::launch_adam_multi(L, lr, beta1, beta2, eps, ticket, (hipStream_t)stream));
+  }
   return MH_OK;
 }
 

@@ -1,62 +1,72 @@
-// optim.hip — Adam over one network's FLAT parameter buffer (gfx950).
+// optim.hip — one Adam step over a list of parameter tensors in ONE launch (gfx950).
 //
-// The update step of torch.optim.Adam (defaults of every reference algorithm: betas (0.9, 0.999),
-// eps 1e-8, no weight decay, no amsgrad; RL/algorithm/*.py `Adam(net.parameters(), lr=...)`):
+// torch.optim.Adam as every reference algorithm builds it (RL/algorithm/*.py
+// `Adam(net.parameters(), lr=...)`: betas (0.9, 0.999), eps 1e-8, no weight decay, no amsgrad),
+// in the form of PyTorch's fused / capturable implementation (float32 step counter on the
+// device, bias corrections formed in float32 from it):
 //   t += 1
-//   m = lerp(m, g, 1 - b1)                 (torch lerp: m + w (g - m) for w < 0.5)
+//   m = lerp(m, g, 1 - b1)
 //   v = b2 v + (1 - b2) g^2
 //   p -= (lr / (1 - b1^t)) m / (sqrt(v) / sqrt(1 - b2^t) + eps)
-// with the network's parameters, gradients and both moments each laid out contiguously (the
-// Python side re-points every nn.Parameter's .data / .grad at views of the flat buffers), so one
-// launch updates a whole network and zeroes its gradients for the next backward, where the
-// PyTorch optimiser issues multi-tensor kernels plus a gradient fill per network. The step count
-// lives on the device (incremented by the last workgroup to finish) so the update can be
-// captured into a HIP graph; the bias corrections are formed in float64 from it, as PyTorch forms
-// them in Python floats. HBM-bound: 4 arrays read, 4 written (the gradient zeroed).
+// PyTorch's multi-tensor kernel gives each 65,536-element chunk of a tensor ONE workgroup, so a
+// 256 x 256 MLP's update runs on a handful of workgroups (31 us per optimiser step, measured in
+// the MSACL update) plus a separate step-count increment kernel. Here the tensors of one
+// optimiser (pointer table passed by value in the kernel arguments: graph-capturable, no upload)
+// are one flat index space over a full grid, and the step counters are advanced in the same
+// launch by the last workgroup to finish (every workgroup has read the old count by then).
+// HBM-bound: 4 arrays read, 3 written per element.
 #include "rollout.h"
 
 namespace mh {
 
-__global__ __launch_bounds__(256) void k_adam(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
-                                              float* __restrict__ v, int64_t n, float lr, float b1, float b2,
-                                              float eps, int zero_grad, int64_t* __restrict__ step,
-                                              uint32_t* __restrict__ ticket) {
-  const int64_t t = *step + 1;
-  const double bc1 = 1.0 - pow((double)b1, (double)t);
-  const double bc2 = 1.0 - pow((double)b2, (double)t);
-  const float step_size = (float)((double)lr / bc1);
-  const float bc2_sqrt = (float)sqrt(bc2);
-  const float w1 = 1.0f - b1, w2 = 1.0f - b2;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const float gi = g[i];
-    float mi = m[i];
-    mi = mi + w1 * (gi - mi);
-    float vi = v[i];
-    vi = vi * b2 + w2 * (gi * gi);
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    p[i] = p[i] - step_size * (mi / denom);
-    m[i] = mi;
-    v[i] = vi;
-    if (zero_grad) g[i] = 0.0f;
+__global__ __launch_bounds__(256) void k_adam_multi(AdamList L, double lr, double b1, double b2, double eps,
+                                                    uint32_t* __restrict__ ticket) {
+  // the scalars as PyTorch forms them from the Python floats: (1 - beta) and the bias
+  // corrections in double, each rounded once to float32 where the element math uses it; one
+  // step counter per tensor (a tensor without a gradient on some steps has its own count)
+  __shared__ float s_step_size[ADAM_MAX_TENSORS], s_bc2[ADAM_MAX_TENSORS], s_t[ADAM_MAX_TENSORS];
+  if ((int)threadIdx.x < L.n) {
+    const float t = *L.step[threadIdx.x] + 1.0f;
+    s_t[threadIdx.x] = t;
+    s_step_size[threadIdx.x] = (float)(lr / (1.0 - pow(b1, (double)t)));
+    s_bc2[threadIdx.x] = (float)sqrt(1.0 - pow(b2, (double)t));
   }
-  // the last workgroup to finish advances the step counter (every workgroup read the old one)
+  __syncthreads();
+  const float w1 = (float)(1.0 - b1), w2 = (float)(1.0 - b2);
+  const float fb2 = (float)b2, feps = (float)eps;
+  const int64_t total = L.start[L.n];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    int k = 0;
+    while (k + 1 < L.n && i >= L.start[k + 1]) ++k;  // <= MH_ADAM_MAX_TENSORS, uniform mostly
+    const int64_t j = i - L.start[k];
+    const float g = L.g[k][j];
+    float m = L.m[k][j], v = L.v[k][j];
+    m = m + w1 * (g - m);  // exp_avg.lerp_(grad, 1 - beta1)
+    v = fb2 * v + w2 * (g * g);
+    const float denom = sqrtf(v) / s_bc2[k] + feps;
+    L.p[k][j] = L.p[k][j] - s_step_size[k] * m / denom;
+    L.m[k][j] = m;
+    L.v[k][j] = v;
+  }
+  // the last workgroup to finish advances every step counter
   __syncthreads();
   if (threadIdx.x == 0) {
-    __atomic_thread_fence(__ATOMIC_RELEASE);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
     const uint32_t done = atomicAdd(ticket, 1u);
     if (done == gridDim.x - 1) {
-      *step = t;
+      for (int k = 0; k < L.n; ++k) *L.step[k] = s_t[k];
       *ticket = 0u;
     }
   }
 }
 
-hipError_t launch_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
-                       int zero_grad, int64_t* step, uint32_t* ticket, hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  const int64_t want = (n + 255) / 256;
-  const int grid = (int)(want < 1024 ? want : 1024);
-  k_adam<<<grid, 256, 0, st>>>(p, g, m, v, n, lr, b1, b2, eps, zero_grad, step, ticket);
+hipError_t launch_adam_multi(const AdamList& L, double lr, double b1, double b2, double eps, uint32_t* ticket,
+                             hipStream_t st) {
+  if (L.n <= 0) return hipSuccess;
+  const int64_t total = L.start[L.n];
+  const int64_t want = (total + 255) / 256;
+  const int grid = (int)(want < 1 ? 1 : (want < 2048 ? want : 2048));
+  k_adam_multi<<<grid, 256, 0, st>>>(L, lr, b1, b2, eps, ticket);
   return hipGetLastError();
 }
 

@@ -110,8 +110,18 @@ hipError_t launch_tg_log_prob_bwd(const float* logits, const float* a, const flo
                                   const float* d_logp, int64_t M, int A, float* d_logits, hipStream_t st);
 hipError_t launch_act_grad_colsum(const float* dy, const float* y, int64_t M, int N, int act, float* g, float* db,
                                   float* partial, hipStream_t st);
-hipError_t launch_adam(float* p, float* g, float* m, float* v, int64_t n, float lr, float b1, float b2, float eps,
-                       int zero_grad, int64_t* step, uint32_t* ticket, hipStream_t st);
+constexpr int ADAM_MAX_TENSORS = 32;
+struct AdamList {  // one optimiser's tensors, passed by value in the kernel arguments
+  float* p[ADAM_MAX_TENSORS];
+  const float* g[ADAM_MAX_TENSORS];
+  float* m[ADAM_MAX_TENSORS];
+  float* v[ADAM_MAX_TENSORS];
+  float* step[ADAM_MAX_TENSORS];
+  int64_t start[ADAM_MAX_TENSORS + 1];  // prefix sums of the element counts
+  int n;
+};
+hipError_t launch_adam_multi(const AdamList& L, double lr, double b1, double b2, double eps, uint32_t* ticket,
+                             hipStream_t st);
 hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
                               const float* b3, int D, int N3, float* P, hipStream_t st);
 hipError_t launch_policy_forward(const float* P, const float* obs, int64_t E, int D, int N3, float* logits,
