@@ -196,9 +196,12 @@ int mh_act_grad_chunks(int64_t rows, int32_t* chunks_out);
 /* g = dy * act'(y) (act: 0 identity, 1 ReLU via y > 0, 2 tanh via 1 - y^2) and db = column sums of
  * g, all [rows][cols] row-major; g may be NULL (identity activation: g is dy), db may be NULL.
  * Replaces threshold_backward / tanh_backward + the bias-gradient reduction of a Linear layer
- * (RL/apprfunc/mlp.py:18-30 layers under autograd). Deterministic (fixed summation order). */
+ * (RL/apprfunc/mlp.py:18-30 layers under autograd). Deterministic (fixed summation order).
+ * partial: mh_act_grad_chunks(rows) x cols floats of workspace. tickets: NULL (two launches) or a
+ * DEVICE uint32 array of ceil(cols / 64) counters, zero on entry and left zero (one per stream):
+ * the bias gradient is then finished inside the same launch. */
 int mh_act_grad_colsum(const float* dy, const float* y, int64_t rows, int32_t cols, int32_t act, float* g,
-                       float* db, float* partial, void* stream);
+                       float* db, float* partial, uint32_t* tickets, void* stream);
 /* One torch.optim.Adam step (torch.optim.Adam(fused/capturable) math: betas, eps, no weight decay /
  * amsgrad / maximize) over a list of parameter tensors in one launch per 32 tensors, replacing
  * the optimiser.step() of every reference algorithm (RL/algorithm/{msacl,sac,lac,ppo,polyc}.py). Each entry: param,
@@ -216,6 +219,16 @@ typedef struct {
 } mh_adam_tensor_t;
 int mh_adam_multi(const mh_adam_tensor_t* tensors, int32_t n, double lr, double beta1, double beta2, double eps,
                   uint32_t* ticket, void* stream);
+
+/* Polyak averaging of a target network, target = target * polyak + (1 - polyak) * source
+ * (both scalars rounded to float32, two roundings as p_t.mul_(polyak); p_t.add_((1 - polyak) * p)
+ * in RL/algorithm/sac.py:204-217 and msacl.py:445-460), over a tensor list in one launch per 32. */
+typedef struct {
+  float* target;
+  const float* source;
+  int64_t numel;
+} mh_polyak_tensor_t;
+int mh_polyak_multi(const mh_polyak_tensor_t* tensors, int32_t n, double polyak, void* stream);
 
 /* f32 GEMM on the f32 MFMA (csrc/gemm.hip) for the update phase's nn.Linear layers
  * (RL/apprfunc/mlp.py:18-30 forward; autograd's input / weight gradients):

@@ -43,6 +43,11 @@ class AdamTensor(ctypes.Structure):
                 ("exp_avg_sq", ctypes.c_void_p), ("step", ctypes.c_void_p), ("numel", ctypes.c_int64)]
 
 
+class PolyakTensor(ctypes.Structure):
+    """mh_polyak_tensor_t (include/msacl_hip.h)."""
+    _fields_ = [("target", ctypes.c_void_p), ("source", ctypes.c_void_p), ("numel", ctypes.c_int64)]
+
+
 class TrajStore(ctypes.Structure):
     _fields_ = [
         ("obs", c_vp), ("act", c_vp), ("rew", c_vp), ("cost", c_vp), ("obs2", c_vp), ("done", c_vp),
@@ -79,7 +84,8 @@ _PROTOS = {
     "mh_policy_pack": (ctypes.c_int, [c_vp] * 6 + [c_i32] * 4 + [c_vp, c_vp]),
     "mh_policy_forward": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "mh_act_grad_chunks": (ctypes.c_int, [c_i64, ctypes.POINTER(c_i32)]),
-    "mh_act_grad_colsum": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "mh_act_grad_colsum": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mh_polyak_multi": (ctypes.c_int, [c_vp, c_i32, ctypes.c_double, c_vp]),
     "mh_adam_multi": (ctypes.c_int, [c_vp, c_i32, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                      c_vp, c_vp]),
     "mh_gemm_workspace": (ctypes.c_int, [c_i64, c_i64, c_i64, ctypes.POINTER(c_i64)]),

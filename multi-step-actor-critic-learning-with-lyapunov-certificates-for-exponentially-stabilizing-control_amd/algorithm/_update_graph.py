@@ -12,7 +12,7 @@ it out of the create_alg registry, RL/create_pkg/create_alg.py:38-47).
   static input copies (lazy hipBLASLt / Adam state init), the second captures, later calls copy
   the new batch into the static inputs and replay. Off under torch.distributed (the gradient
   all-reduces are not captured) and when disabled.
-* polyak_: target-network averaging as multi-tensor ops (p_t <- (1-tau) p_t + tau p).
+* polyak_: target-network averaging (p_t <- (1-tau) p_t + tau p), one mh_polyak_multi launch.
 """
 from __future__ import annotations
 
@@ -127,12 +127,24 @@ class UpdateGraph:
 
 def polyak_(net, target, tau):
     """p_t.mul_(polyak); p_t.add_((1 - polyak) * p) with polyak = 1 - tau, the reference's exact
-    scalars (sac.py:204-217)."""
+    scalars (sac.py:204-217): one mh_polyak_multi launch on contiguous HIP float32 parameters,
+    multi-tensor PyTorch ops otherwise."""
     polyak = 1 - tau
     with torch.no_grad():
         tp = [p.data for p in target.parameters()]
+        sp = [p.data for p in net.parameters()]
+        if tp and all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and s.is_contiguous()
+                      and s.dtype == torch.float32 and t.shape == s.shape for t, s in zip(tp, sp)) \
+                and len(tp) == len(sp):
+            from .. import _native as N
+            arr = (N.PolyakTensor * len(tp))()
+            for i, (t, s) in enumerate(zip(tp, sp)):
+                arr[i] = N.PolyakTensor(t.data_ptr(), s.data_ptr(), t.numel())
+            N.check(N.lib().mh_polyak_multi(arr, len(tp), float(polyak), N.stream_of(tp[0].device)),
+                    "mh_polyak_multi")
+            return
         torch._foreach_mul_(tp, polyak)
-        torch._foreach_add_(tp, torch._foreach_mul([p.data for p in net.parameters()], 1 - polyak))
+        torch._foreach_add_(tp, torch._foreach_mul(sp, 1 - polyak))
 
 
 def set_requires_grad(modules, flag):

@@ -326,10 +326,7 @@ class MSACL:
                 self.networks.log_alpha.clamp_(max=math.log(self.alpha_bound))
 
     def _target_update(self):
-        """Polyak averaging (msacl.py:445-460) as two multi-tensor ops per net."""
-        with torch.no_grad():
-            polyak = 1 - self.tau
-            for net, targ in ((self.networks.q1, self.networks.q1_target), (self.networks.q2, self.networks.q2_target)):
-                tp = [p.data for p in targ.parameters()]
-                torch._foreach_mul_(tp, polyak)
-                torch._foreach_add_(tp, torch._foreach_mul([p.data for p in net.parameters()], 1 - polyak))
+        """Polyak averaging (msacl.py:445-460): one mh_polyak_multi launch per net."""
+        from ._update_graph import polyak_
+        for net, targ in ((self.networks.q1, self.networks.q1_target), (self.networks.q2, self.networks.q2_target)):
+            polyak_(net, targ, self.tau)

@@ -37,6 +37,18 @@ def _native():
 
 
 _GEMM_BACKEND = {"name": "auto"}
+_COLSUM_TICKETS = {}
+
+
+def _colsum_tickets(dev, cols):
+    """Per-device arrival counters of mh_act_grad_colsum's in-launch bias-gradient finish (zeroed
+    once, left zero by every launch; the update runs its layers in stream order on one stream)."""
+    need = (cols + 63) // 64
+    t = _COLSUM_TICKETS.get(dev)
+    if t is None or t.numel() < need:
+        t = torch.zeros(max(need, 64), dtype=torch.int32, device=dev)
+        _COLSUM_TICKETS[dev] = t
+    return t
 _WS = {}
 
 
@@ -118,7 +130,8 @@ class LinearAct(torch.autograd.Function):
             db = torch.empty(C, dtype=dy.dtype, device=dy.device) if need_b else None
             N.check(N.lib().mh_act_grad_colsum(N.ptr(dy), N.ptr(y.contiguous()) if act else None, M, C, act,
                                                N.ptr(g) if act else None, N.ptr(db), N.ptr(partial),
-                                               N.stream_of(dy.device)), "mh_act_grad_colsum")
+                                               N.ptr(_colsum_tickets(dy.device, C)), N.stream_of(dy.device)),
+                    "mh_act_grad_colsum")
         M, Nout = g.shape
         K = x.shape[1]
         dx = dw = None

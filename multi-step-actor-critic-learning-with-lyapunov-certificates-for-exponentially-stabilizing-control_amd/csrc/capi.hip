@@ -462,11 +462,11 @@ int mh_act_grad_chunks(int64_t rows, int32_t* chunks_out) {
 }
 
 int mh_act_grad_colsum(const float* dy, const float* y, int64_t rows, int32_t cols, int32_t act, float* g,
-                       float* db, float* partial, void* stream) {
+                       float* db, float* partial, uint32_t* tickets, void* stream) {
   if (!dy || (act != 0 && (!y || !g)) || !partial) return fail(MH_EINVAL, "mh_act_grad_colsum: null pointer");
   if (act < 0 || act > 2) return fail(MH_EINVAL, "mh_act_grad_colsum: act must be 0, 1 or 2");
   if (rows < 0 || cols <= 0) return fail(MH_EINVAL, "mh_act_grad_colsum: bad shape");
-  MH_HIP(mh::launch_act_grad_colsum(dy, y, rows, cols, act, act == 0 ? nullptr : g, db, partial,
+  MH_HIP(mh::launch_act_grad_colsum(dy, y, rows, cols, act, act == 0 ? nullptr : g, db, partial, tickets,
                                     (hipStream_t)stream));
   return MH_OK;
 }
@@ -490,6 +490,24 @@ int mh_adam_multi(const mh_adam_tensor_t* tensors, int32_t n, double lr, double 
       L.start[k + 1] = L.start[k] + t.numel;
     }
     MH_HIP(mh::launch_adam_multi(L, lr, beta1, beta2, eps, ticket, (hipStream_t)stream));
+  }
+  return MH_OK;
+}
+
+int mh_polyak_multi(const mh_polyak_tensor_t* tensors, int32_t n, double polyak, void* stream) {
+  if (n < 0 || (n > 0 && !tensors)) return fail(MH_EINVAL, "mh_polyak_multi: bad argument");
+  for (int32_t base = 0; base < n; base += mh::ADAM_MAX_TENSORS) {
+    mh::PolyakList L{};
+    L.n = n - base < mh::ADAM_MAX_TENSORS ? n - base : mh::ADAM_MAX_TENSORS;
+    for (int k = 0; k < L.n; ++k) {
+      const mh_polyak_tensor_t& t = tensors[base + k];
+      if (!t.target || !t.source || t.numel < 0)
+        return fail(MH_EINVAL, "mh_polyak_multi: null pointer or negative size in the tensor list");
+      L.t[k] = t.target;
+      L.s[k] = t.source;
+      L.start[k + 1] = L.start[k] + t.numel;
+    }
+    MH_HIP(mh::launch_polyak_multi(L, polyak, (hipStream_t)stream));
   }
   return MH_OK;
 }

@@ -8,8 +8,12 @@
 // a separate reduction (14 us for 5,120 x 256 on MI355X). Here: a 2-D grid streams dy/y once,
 // coalesced along the columns (64 columns x 4 row lanes per workgroup, every load of a thread
 // issued before the first add: memory-level parallelism, not a latency chain), writes g and
-// per-row-chunk column sums; a second small kernel adds the chunk sums in a fixed order
-// (deterministic, no float atomics).
+// per-row-chunk column sums; the LAST workgroup of each column group to finish (agent-scope
+// arrival counter) adds the chunk sums in a fixed order, so the bias gradient is deterministic
+// and the layer backward is one launch. Cross-XCD hand-off per cdna_hip_programming.md's
+// publish/consume recipe: the chunk sums are stored write-through (sc1), every storing wave
+// drains (vmcnt(0)) before the workgroup barrier and the counter add, and the reducing
+// workgroup reads them with sc1 loads (no stale L1/L2 copy can be hit).
 #include "rollout.h"
 
 namespace mh {
@@ -20,7 +24,8 @@ constexpr int AG_ROWS = 4 * AG_RPT;  // rows per workgroup (4 row lanes)
 
 __global__ __launch_bounds__(256) void k_act_grad_colsum(const float* __restrict__ dy, const float* __restrict__ y,
                                                          int64_t M, int N, int act, float* __restrict__ g,
-                                                         float* __restrict__ partial) {
+                                                         float* __restrict__ partial, float* __restrict__ db,
+                                                         uint32_t* __restrict__ tickets) {
   __shared__ float red[4][AG_COLS];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int n = blockIdx.x * AG_COLS + tx;
@@ -35,19 +40,65 @@ __global__ __launch_bounds__(256) void k_act_grad_colsum(const float* __restrict
       d[j] = ok ? dy[m * N + n] : 0.0f;
       t[j] = (ok && act != 0) ? y[m * N + n] : 0.0f;
     }
+    // all of g first, then the stores: a store between two uses of loaded values would make
+    // every later wait on the load queue also wait for that store (vmcnt counts both in order)
+    float gv[AG_RPT];
 #pragma unroll
     for (int j = 0; j < AG_RPT; ++j) {
-      float gv = d[j];
-      if (act == 1) gv = t[j] > 0.0f ? gv : 0.0f;
-      else if (act == 2) gv = gv * (1.0f - t[j] * t[j]);
-      const int64_t m = m0 + 4 * j;
-      if (g && m < M) g[m * N + n] = gv;
-      acc += gv;
+      gv[j] = d[j];
+      if (act == 1) gv[j] = t[j] > 0.0f ? d[j] : 0.0f;
+      else if (act == 2) gv[j] = d[j] * (1.0f - t[j] * t[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < AG_RPT; ++j) acc += gv[j];
+    if (g) {
+#pragma unroll
+      for (int j = 0; j < AG_RPT; ++j) {
+        const int64_t m = m0 + 4 * j;
+        if (m < M) g[m * N + n] = gv[j];
+      }
     }
   }
   red[ty][tx] = acc;
   __syncthreads();
-  if (ty == 0 && n < N) partial[(int64_t)blockIdx.y * N + n] = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
+  const float csum = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
+  if (!tickets) {
+    if (ty == 0 && n < N) partial[(int64_t)blockIdx.y * N + n] = csum;
+    return;
+  }
+  // fused finish: publish this chunk's sums write-through, count arrivals per column group
+  if (ty == 0 && n < N)
+    __hip_atomic_store(partial + (int64_t)blockIdx.y * N + n, csum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+    const uint32_t a = __hip_atomic_fetch_add(tickets + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (a == gridDim.y - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const int R = (int)gridDim.y;
+  float s = 0.0f;
+  if (n < N) {
+    int r = ty;
+    for (; r + 12 < R; r += 16) {
+      const float a0 = __hip_atomic_load(partial + (int64_t)r * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float a1 = __hip_atomic_load(partial + (int64_t)(r + 4) * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float a2 = __hip_atomic_load(partial + (int64_t)(r + 8) * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float a3 = __hip_atomic_load(partial + (int64_t)(r + 12) * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s = s + a0;
+      s = s + a1;
+      s = s + a2;
+      s = s + a3;
+    }
+    for (; r < R; r += 4) s += __hip_atomic_load(partial + (int64_t)r * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();  // everyone has read red[] above
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && n < N) db[n] = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
+  if (threadIdx.x == 0) __hip_atomic_store(tickets + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // db[n] = sum_r partial[r][n], r ascending within each of 4 interleaved lanes, lanes added in order
@@ -76,14 +127,17 @@ __global__ __launch_bounds__(256) void k_colsum_finish(const float* __restrict__
 
 int act_grad_chunks(int64_t M) { return (int)((M + AG_ROWS - 1) / AG_ROWS); }
 
+int act_grad_tickets(int N) { return (N + AG_COLS - 1) / AG_COLS; }
+
 hipError_t launch_act_grad_colsum(const float* dy, const float* y, int64_t M, int N, int act, float* g, float* db,
-                                  float* partial, hipStream_t st) {
+                                  float* partial, uint32_t* tickets, hipStream_t st) {
   if (M <= 0 || N <= 0) return hipSuccess;
   const int R = act_grad_chunks(M);
   const int cg = (N + AG_COLS - 1) / AG_COLS;
-  k_act_grad_colsum<<<dim3(cg, R), 256, 0, st>>>(dy, y, M, N, act, g, partial);
+  // with tickets: one launch (the last chunk of each column group reduces); without: two
+  k_act_grad_colsum<<<dim3(cg, R), 256, 0, st>>>(dy, y, M, N, act, g, partial, db, db ? tickets : nullptr);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || !db) return e;
+  if (e != hipSuccess || !db || tickets) return e;
   k_colsum_finish<<<cg, 256, 0, st>>>(partial, R, N, db);
   return hipGetLastError();
 }

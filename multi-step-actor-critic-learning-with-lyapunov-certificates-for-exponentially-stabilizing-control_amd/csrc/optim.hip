@@ -70,4 +70,28 @@ hipError_t launch_adam_multi(const AdamList& L, double lr, double b1, double b2,
   return hipGetLastError();
 }
 
+// Polyak averaging of target networks (sac.py:204-217, msacl.py:445-460):
+//   p_t.mul_(polyak); p_t.add_((1 - polyak) * p)      (both scalars float32, two roundings)
+// over a tensor list in one launch (PyTorch: three multi-tensor kernels per network).
+__global__ __launch_bounds__(256) void k_polyak_multi(PolyakList L, float a, float b) {
+  const int64_t total = L.start[L.n];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    int k = 0;
+    while (k + 1 < L.n && i >= L.start[k + 1]) ++k;
+    const int64_t j = i - L.start[k];
+    const float t = L.t[k][j] * a;
+    L.t[k][j] = t + L.s[k][j] * b;
+  }
+}
+
+hipError_t launch_polyak_multi(const PolyakList& L, double polyak, hipStream_t st) {
+  if (L.n <= 0) return hipSuccess;
+  const int64_t total = L.start[L.n];
+  if (total <= 0) return hipSuccess;
+  const int64_t want = (total + 255) / 256;
+  const int grid = (int)(want < 2048 ? want : 2048);
+  k_polyak_multi<<<grid, 256, 0, st>>>(L, (float)polyak, (float)(1.0 - polyak));
+  return hipGetLastError();
+}
+
 }  // namespace mh

@@ -109,7 +109,8 @@ hipError_t launch_tg_log_prob(const float* logits, const float* a, const float* 
 hipError_t launch_tg_log_prob_bwd(const float* logits, const float* a, const float* high, const float* low,
                                   const float* d_logp, int64_t M, int A, float* d_logits, hipStream_t st);
 hipError_t launch_act_grad_colsum(const float* dy, const float* y, int64_t M, int N, int act, float* g, float* db,
-                                  float* partial, hipStream_t st);
+                                  float* partial, uint32_t* tickets, hipStream_t st);
+int act_grad_tickets(int N);
 constexpr int ADAM_MAX_TENSORS = 32;
 struct AdamList {  // one optimiser's tensors, passed by value in the kernel arguments
   float* p[ADAM_MAX_TENSORS];
@@ -120,6 +121,13 @@ struct AdamList {  // one optimiser's tensors, passed by value in the kernel arg
   int64_t start[ADAM_MAX_TENSORS + 1];  // prefix sums of the element counts
   int n;
 };
+struct PolyakList {
+  float* t[ADAM_MAX_TENSORS];
+  const float* s[ADAM_MAX_TENSORS];
+  int64_t start[ADAM_MAX_TENSORS + 1];
+  int n;
+};
+hipError_t launch_polyak_multi(const PolyakList& L, double polyak, hipStream_t st);
 hipError_t launch_adam_multi(const AdamList& L, double lr, double b1, double b2, double eps, uint32_t* ticket,
                              hipStream_t st);
 hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,

@@ -70,3 +70,20 @@ def test_hip_adam_state_dict_round_trip_and_graph_capture():
         gph.replay()
     torch.cuda.synchronize()
     assert float(opt.state[a[0]]["step"]) == 5.0  # 1 eager + 1 warm-up + 3 replays (capture runs nothing)
+
+
+def test_polyak_kernel_matches_foreach_bit_exact():
+    """mh_polyak_multi (algorithm/_update_graph.py polyak_) vs the multi-tensor PyTorch ops it
+    replaces, p_t.mul_(1 - tau); p_t.add_(tau * p): the same two float32 roundings, bit-exact."""
+    from msacl_amd.algorithm._update_graph import polyak_
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(16, 256), torch.nn.ReLU(), torch.nn.Linear(256, 1)).cuda()
+    targ = torch.nn.Sequential(torch.nn.Linear(16, 256), torch.nn.ReLU(), torch.nn.Linear(256, 1)).cuda()
+    ref = [p.detach().clone() for p in targ.parameters()]
+    for _ in range(3):
+        polyak_(net, targ, 0.005)
+        with torch.no_grad():
+            torch._foreach_mul_(ref, 1 - 0.005)
+            torch._foreach_add_(ref, torch._foreach_mul([p.data for p in net.parameters()], 0.005))
+    for a, b in zip(targ.parameters(), ref):
+        assert torch.equal(a.detach(), b)
