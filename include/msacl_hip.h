@@ -242,6 +242,15 @@ int mh_gemm_f32(const float* A, const float* B, const float* bias, float* C, int
                 int64_t lda, int64_t ldb, int64_t ldc, int32_t trans_a, int32_t trans_b, int32_t act,
                 float* workspace, void* stream);
 
+/* StochaPolicy's head (RL/apprfunc/mlp.py:132-136) on [rows][2 act_dim] rows:
+ *   out = [mean | exp(clamp(log_std, min_log_std, max_log_std))] of raw = [mean | log_std]
+ * and its backward d_raw = [d_mean | d_std * std * (min <= log_std <= max)], one launch each
+ * (PyTorch: chunk + clamp + exp + cat forward, four kernels backward). */
+int mh_stocha_head(const float* raw, int64_t rows, int32_t act_dim, float min_log_std, float max_log_std, float* out,
+                   void* stream);
+int mh_stocha_head_backward(const float* raw, const float* out, const float* d_out, int64_t rows, int32_t act_dim,
+                            float min_log_std, float max_log_std, float* d_raw, void* stream);
+
 /* TanhGaussDistribution (RL/utils/act_distribution_cls.py:15-85) on [rows][2A] logits (mean | std)
  * with DEVICE action bounds high/low [A] (A <= 8), forward and backward as single launches:
  *   rsample   (eps [rows][A] standard normals) -> act [rows][A], logp [rows]

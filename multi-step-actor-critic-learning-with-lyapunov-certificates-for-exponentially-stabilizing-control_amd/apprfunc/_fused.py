@@ -142,6 +142,35 @@ class LinearAct(torch.autograd.Function):
         return dx, dw, db, None
 
 
+class StochaHead(torch.autograd.Function):
+    """[mean | log_std] -> [mean | exp(clamp(log_std, lo, hi))] (StochaPolicy.forward, mlp.py:132-136)
+    as one launch forward and one backward (mh_stocha_head[_backward], csrc/dist_kernels.hip)."""
+
+    @staticmethod
+    def forward(ctx, raw, lo, hi):
+        N = _native()
+        A = raw.shape[-1] // 2
+        rows = raw.numel() // max(2 * A, 1)
+        out = torch.empty_like(raw)
+        N.check(N.lib().mh_stocha_head(N.ptr(raw), rows, A, lo, hi, N.ptr(out), N.stream_of(raw.device)),
+                "mh_stocha_head")
+        ctx.save_for_backward(raw, out)
+        ctx.lo, ctx.hi = lo, hi
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        raw, out = ctx.saved_tensors
+        N = _native()
+        A = raw.shape[-1] // 2
+        rows = raw.numel() // max(2 * A, 1)
+        d_raw = torch.empty_like(raw)
+        N.check(N.lib().mh_stocha_head_backward(N.ptr(raw), N.ptr(out), N.ptr(d_out.contiguous()), rows, A, ctx.lo,
+                                                ctx.hi, N.ptr(d_raw), N.stream_of(raw.device)),
+                "mh_stocha_head_backward")
+        return d_raw, None, None
+
+
 def fusable(seq: nn.Sequential) -> bool:
     mods = list(seq)
     if len(mods) % 2:

@@ -8,7 +8,7 @@ import torch.nn as nn
 
 from ..utils.act_distribution_cls import Action_Distribution_Cls
 from ..utils.common_utils import get_activation_func
-from ._fused import MLP
+from ._fused import MLP, StochaHead
 
 
 def mlp(sizes, activation, output_activation=nn.Identity):
@@ -85,7 +85,10 @@ class StochaPolicy(nn.Module, Action_Distribution_Cls):
         self.action_distribution_cls = kw["action_distribution_cls"]
 
     def forward(self, obs):
-        mean, log_std = torch.chunk(self.policy(obs), chunks=2, dim=-1)
+        raw = self.policy(obs)
+        if raw.is_cuda and raw.dtype == torch.float32:
+            return StochaHead.apply(raw.contiguous(), float(self.min_log_std), float(self.max_log_std))
+        mean, log_std = torch.chunk(raw, chunks=2, dim=-1)
         return torch.cat((mean, torch.clamp(log_std, self.min_log_std, self.max_log_std).exp()), dim=-1)
 
 

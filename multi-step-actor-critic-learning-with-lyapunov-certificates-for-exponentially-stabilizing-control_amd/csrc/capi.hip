@@ -537,6 +537,23 @@ int mh_gemm_f32(const float* A, const float* B, const float* bias, float* C, int
   return MH_OK;
 }
 
+int mh_stocha_head(const float* raw, int64_t rows, int32_t act_dim, float min_log_std, float max_log_std, float* out,
+                   void* stream) {
+  if (rows < 0 || act_dim <= 0) return fail(MH_EINVAL, "mh_stocha_head: bad shape");
+  if (rows > 0 && (!raw || !out)) return fail(MH_EINVAL, "mh_stocha_head: null pointer");
+  MH_HIP(mh::launch_stocha_head(raw, rows, act_dim, min_log_std, max_log_std, out, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_stocha_head_backward(const float* raw, const float* out, const float* d_out, int64_t rows, int32_t act_dim,
+                            float min_log_std, float max_log_std, float* d_raw, void* stream) {
+  if (rows < 0 || act_dim <= 0) return fail(MH_EINVAL, "mh_stocha_head_backward: bad shape");
+  if (rows > 0 && (!raw || !out || !d_out || !d_raw)) return fail(MH_EINVAL, "mh_stocha_head_backward: null pointer");
+  MH_HIP(mh::launch_stocha_head_bwd(raw, out, d_out, rows, act_dim, min_log_std, max_log_std, d_raw,
+                                    (hipStream_t)stream));
+  return MH_OK;
+}
+
 #define MH_TG_CHECK(name)                                                                           \
   if (rows < 0 || act_dim <= 0 || act_dim > 8) return fail(MH_EINVAL, name ": act_dim must be in [1, 8]"); \
   if (rows == 0) return MH_OK;                                                                     \

@@ -114,7 +114,46 @@ __global__ __launch_bounds__(256) void k_tg_log_prob_bwd(const float* __restrict
   }
 }
 
+// StochaPolicy head (RL/apprfunc/mlp.py:132-136): out = [mean | exp(clamp(log_std, lo, hi))] from the
+// MLP's raw [mean | log_std], and its backward d_raw = [d_mean | d_std * std * (lo <= log_std <= hi)]
+// (torch's exp / clamp backward). One thread per element of the [M][2A] block.
+__global__ __launch_bounds__(256) void k_stocha_head(const float* __restrict__ raw, int64_t total, int A, float lo,
+                                                     float hi, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const float x = raw[i];
+  out[i] = (int)(i % (2 * A)) < A ? x : expf(fminf(fmaxf(x, lo), hi));
+}
+__global__ __launch_bounds__(256) void k_stocha_head_bwd(const float* __restrict__ raw, const float* __restrict__ out,
+                                                         const float* __restrict__ dout, int64_t total, int A,
+                                                         float lo, float hi, float* __restrict__ draw) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const float d = dout[i];
+  if ((int)(i % (2 * A)) < A) {
+    draw[i] = d;
+  } else {
+    const float x = raw[i];
+    const float gx = d * out[i];
+    draw[i] = (x >= lo && x <= hi) ? gx : gx * 0.0f;
+  }
+}
+
 static inline unsigned grid_rows(int64_t M) { return (unsigned)((M + 255) / 256); }
+
+hipError_t launch_stocha_head(const float* raw, int64_t M, int A, float lo, float hi, float* out, hipStream_t st) {
+  const int64_t total = M * 2 * A;
+  if (total <= 0) return hipSuccess;
+  k_stocha_head<<<grid_rows(total), 256, 0, st>>>(raw, total, A, lo, hi, out);
+  return hipGetLastError();
+}
+hipError_t launch_stocha_head_bwd(const float* raw, const float* out, const float* dout, int64_t M, int A, float lo,
+                                  float hi, float* draw, hipStream_t st) {
+  const int64_t total = M * 2 * A;
+  if (total <= 0) return hipSuccess;
+  k_stocha_head_bwd<<<grid_rows(total), 256, 0, st>>>(raw, out, dout, total, A, lo, hi, draw);
+  return hipGetLastError();
+}
 
 hipError_t launch_tg_rsample(const float* logits, const float* eps, const float* high, const float* low, int64_t M,
                              int A, float* act, float* logp, hipStream_t st) {

@@ -99,6 +99,9 @@ hipError_t launch_gemm(const float* A, const float* B, const float* bias, float*
                        int64_t lda, int64_t ldb, int64_t ldc, int ta, int tb, int act, float* workspace,
                        hipStream_t st);
 int64_t gemm_workspace_floats(int64_t M, int64_t N, int64_t K);
+hipError_t launch_stocha_head(const float* raw, int64_t M, int A, float lo, float hi, float* out, hipStream_t st);
+hipError_t launch_stocha_head_bwd(const float* raw, const float* out, const float* dout, int64_t M, int A, float lo,
+                                  float hi, float* draw, hipStream_t st);
 hipError_t launch_tg_rsample(const float* logits, const float* eps, const float* high, const float* low, int64_t M,
                              int A, float* act, float* logp, hipStream_t st);
 hipError_t launch_tg_rsample_bwd(const float* logits, const float* eps, const float* high, const float* low,

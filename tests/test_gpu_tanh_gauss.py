@@ -160,3 +160,24 @@ def test_fused_path_is_taken(monkeypatch):
     _dist(logits, hi, lo).rsample()
     assert calls == [1]
     np.testing.assert_equal(len(calls), 1)
+
+
+def test_stocha_head_matches_torch():
+    """StochaPolicy head (mh_stocha_head[_backward]) vs chunk + clamp + exp + cat under autograd,
+    including log_std exactly at and beyond the clamp bounds (the gradient mask is inclusive)."""
+    from msacl_amd.apprfunc._fused import StochaHead
+    lo, hi = -20.0, 1.0
+    g = torch.Generator(device="cuda").manual_seed(11)
+    raw = torch.randn(5120, 8, device="cuda", generator=g) * 3
+    raw[0, 4:] = torch.tensor([lo, hi, lo - 1, hi + 1], device="cuda")
+    r1 = raw.clone().requires_grad_(True)
+    r2 = raw.clone().requires_grad_(True)
+    y1 = StochaHead.apply(r1, lo, hi)
+    mean, ls = torch.chunk(r2, 2, dim=-1)
+    y2 = torch.cat((mean, torch.clamp(ls, lo, hi).exp()), dim=-1)
+    torch.testing.assert_close(y1, y2, rtol=2.5e-7, atol=0)
+    w = torch.randn(y1.shape, device="cuda", generator=g)
+    (y1 * w).sum().backward()
+    (y2 * w).sum().backward()
+    torch.testing.assert_close(r1.grad, r2.grad, rtol=5e-7, atol=0)
+    assert float(r1.grad[0, 6]) == 0.0 and float(r1.grad[0, 7]) == 0.0 and float(r1.grad[0, 4]) != 0.0
