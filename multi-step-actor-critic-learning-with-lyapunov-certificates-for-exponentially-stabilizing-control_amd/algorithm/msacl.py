@@ -130,6 +130,10 @@ class MSACL:
         self.last_priority = None
         self._neg_one = torch.tensor(-1.0, device=self.device)
         self.use_graph = bool(kwargs.get("alg_use_graph", True))
+        # the Lyapunov update shares no parameter with the critic update (both only read the
+        # policy and the batch): on one GPU it runs on a second stream, concurrently
+        self.concurrent = bool(kwargs.get("alg_concurrent_streams", True))
+        self._side = None
         self._static = None
         self._static_shapes = None
         self._graphs = {}
@@ -184,12 +188,33 @@ class MSACL:
             return tb_info, data.get("idx"), self.last_priority
         return tb_info
 
+    def _side_stream(self):
+        if not (self.concurrent and D.world_size() == 1 and self.device.type == "cuda"):
+            return None
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
     def _update_body(self, data, do_target, do_policy):
-        """One model_update's device work (msacl.py:193-210); returns device tensors only."""
-        loss_q, q1_mean, q2_mean = self._q_update(data)
-        if do_target:
-            self._target_update()
-        loss_lya = self._lyapunov_update(data)
+        """One model_update's device work (msacl.py:193-210); returns device tensors only. The
+        critic (+ target) and Lyapunov updates are independent (disjoint parameters, read-only
+        policy and batch) and run on two streams (fork/join; captured as parallel graph branches);
+        the policy and alpha updates, which read both, follow the join."""
+        side = self._side_stream()
+        if side is not None:
+            main = torch.cuda.current_stream(self.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                loss_lya = self._lyapunov_update(data)
+            loss_q, q1_mean, q2_mean = self._q_update(data)
+            if do_target:
+                self._target_update()
+            main.wait_stream(side)
+        else:
+            loss_q, q1_mean, q2_mean = self._q_update(data)
+            if do_target:
+                self._target_update()
+            loss_lya = self._lyapunov_update(data)
         loss_policy = entropy = None
         if do_policy:
             for _ in range(self.policy_frequency):
@@ -275,7 +300,7 @@ class MSACL:
         torch.autograd.backward([V, V2], [s.dV, s.dV2])
         D.allreduce_grads(list(self.networks.lyapunov.parameters()))
         self.networks.lyapunov_optimizer.step()
-        return s.loss_lya[0].clone()
+        return s.loss_lya[0]  # a view of the scratch (no allocation on the side stream)
 
     def _policy_update(self, data):
         obs, old_act, obs2, old_logp = data["obs"], data["act"], data["obs2"], data["logp"]

@@ -41,13 +41,15 @@ _COLSUM_TICKETS = {}
 
 
 def _colsum_tickets(dev, cols):
-    """Per-device arrival counters of mh_act_grad_colsum's in-launch bias-gradient finish (zeroed
-    once, left zero by every launch; the update runs its layers in stream order on one stream)."""
+    """Arrival counters of mh_act_grad_colsum's in-launch bias-gradient finish, one set per
+    (device, stream): zeroed once, left zero by every launch, never shared by launches that can
+    run concurrently (the MSACL update runs two streams)."""
     need = (cols + 63) // 64
-    t = _COLSUM_TICKETS.get(dev)
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    t = _COLSUM_TICKETS.get(key)
     if t is None or t.numel() < need:
         t = torch.zeros(max(need, 64), dtype=torch.int32, device=dev)
-        _COLSUM_TICKETS[dev] = t
+        _COLSUM_TICKETS[key] = t
     return t
 _WS = {}
 
