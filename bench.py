@@ -35,6 +35,10 @@ def parse():
                    help="init: PyTorch default init (SURVEY 8d); hover: action mean [mg,0,0,0], long episodes")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--graph-segments", action="store_true",
+                   help="capture the update as graphs cut at its all-reduces (the world size > 1 path)")
+    p.add_argument("--eager-update", action="store_true",
+                   help="run the model update eagerly (no HIP-graph replay), as with world size > 1")
     p.add_argument("--update-gemm", dest="update_gemm", choices=["auto", "hip", "blas"], default=None,
                    help="GEMMs of the update MLPs: auto (default: mh_gemm_f32 where faster), hip or blas")
     p.add_argument("--blas", choices=["hipblaslt", "rocblas"], default=None,
@@ -104,6 +108,10 @@ def main():
         cfg["blas_backend"] = a.blas
     if a.update_gemm is not None:
         cfg["update_gemm"] = a.update_gemm
+    if a.eager_update:
+        cfg["alg_use_graph"] = False
+    if a.graph_segments:
+        cfg["alg_force_graph_segments"] = True
     if a.policy == "hover":
         cfg["buffer_warm_size"] = 0
     args, alg, sampler, buffer, evaluator, trainer = build_pipeline(cfg)

@@ -134,6 +134,7 @@ class MSACL:
         # policy and the batch): on one GPU it runs on a second stream, concurrently
         self.concurrent = bool(kwargs.get("alg_concurrent_streams", True))
         self._side = None
+        self.force_graph_segments = bool(kwargs.get("alg_force_graph_segments", False))
         self._static = None
         self._static_shapes = None
         self._graphs = {}
@@ -189,7 +190,8 @@ class MSACL:
         return tb_info
 
     def _side_stream(self):
-        if not (self.concurrent and D.world_size() == 1 and self.device.type == "cuda"):
+        if not (self.concurrent and D.world_size() == 1 and self.device.type == "cuda"
+                and not self.force_graph_segments and not D.segment_capture_active()):
             return None
         if self._side is None:
             self._side = torch.cuda.Stream(device=self.device)
@@ -225,13 +227,19 @@ class MSACL:
 
     # ------------------------------------------------------------------ HIP-graph replay
     def _graphable(self):
-        return (self.use_graph and not self.anneal_lr and D.world_size() == 1 and torch.cuda.is_available()
+        return (self.use_graph and not self.anneal_lr and torch.cuda.is_available()
                 and not torch.cuda.is_current_stream_capturing())
 
+    def _segmented(self):
+        """World size > 1 (or the test switch): the graph is cut at every collective
+        (utils/dist.py GraphSegments) instead of capturing the update as one graph."""
+        return D.world_size() > 1 or self.force_graph_segments
+
     def _graph_update(self, data, flags):
-        """Replay the whole update (~350 launches) as one HIP graph. The first call per branch
-        (even/odd iteration) runs eagerly on the static inputs (lazy hipBLASLt / Adam state
-        init), the second captures, later calls only copy the new replay batch in and replay."""
+        """Replay the whole update (~250 launches) as one HIP graph (with data parallelism: a
+        chain of graphs cut at the gradient all-reduces, utils/dist.py GraphSegments). The first
+        call per branch (even/odd iteration) runs eagerly on the static inputs (lazy BLAS / Adam
+        state init), the second captures, later calls only copy the new batch in and replay."""
         shapes = tuple((k, tuple(v.shape)) for k, v in sorted(data.items()) if torch.is_tensor(v))
         if self._static is None or self._static_shapes != shapes:
             self._static = {k: v.clone() for k, v in data.items() if torch.is_tensor(v)}
@@ -245,10 +253,16 @@ class MSACL:
             self._warm.add(flags)
             return self._update_body(self._static, *flags)
         if flags not in self._graphs:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                outs = self._update_body(self._static, *flags)
-                prio = self.last_priority
+            if self._segmented():
+                g = D.GraphSegments()
+                with D.capturing(g):
+                    outs = self._update_body(self._static, *flags)
+                    prio = self.last_priority
+            else:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    outs = self._update_body(self._static, *flags)
+                    prio = self.last_priority
             self._graphs[flags] = (g, outs, prio)
         g, outs, prio = self._graphs[flags]
         g.replay()

@@ -42,7 +42,65 @@ def init_from_env(backend=None):
     return True
 
 
-def allreduce_(t: torch.Tensor, average: bool = False) -> torch.Tensor:
+class GraphSegments:
+    """A model update captured as a chain of HIP graphs cut at its collectives (data parallel,
+    world size > 1). While active (`capturing(seg)`), every allreduce_ / allreduce_grads call ends
+    the graph being captured, is recorded, and the capture continues in a new graph of the same
+    memory pool; replay() runs graph 0, collective 0 (eagerly, RCCL on the current stream), graph
+    1, ... So a rank's update costs a handful of graph launches plus its all-reduces instead of
+    ~250 Python-issued kernels, and no collective is ever inside a captured graph."""
+
+    def __init__(self):
+        self.pool = torch.cuda.graph_pool_handle()
+        self.graphs, self.ops = [], []
+        self._ctx = None
+
+    def _begin(self):
+        g = torch.cuda.CUDAGraph()
+        self._ctx = torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local")
+        self._ctx.__enter__()
+        self.graphs.append(g)
+
+    def _cut(self, op):
+        self._ctx.__exit__(None, None, None)
+        self.ops.append(op)
+        self._begin()
+
+    def replay(self):
+        for i, g in enumerate(self.graphs):
+            g.replay()
+            if i < len(self.ops):
+                self.ops[i]()
+
+
+_SEG = {"active": None}
+
+
+class capturing:
+    """Context: capture the enclosed update into `seg` (GraphSegments)."""
+
+    def __init__(self, seg: GraphSegments):
+        self.seg = seg
+
+    def __enter__(self):
+        _SEG["active"] = self.seg
+        self.seg._begin()
+        return self.seg
+
+    def __exit__(self, *exc):
+        try:
+            self.seg._ctx.__exit__(*exc)
+        finally:
+            self.seg._ctx = None
+            _SEG["active"] = None
+        return False
+
+
+def segment_capture_active() -> bool:
+    return _SEG["active"] is not None
+
+
+def _allreduce_now(t, average):
     if world_size() > 1:
         dist.all_reduce(t)
         if average:
@@ -50,8 +108,25 @@ def allreduce_(t: torch.Tensor, average: bool = False) -> torch.Tensor:
     return t
 
 
+def allreduce_(t: torch.Tensor, average: bool = False) -> torch.Tensor:
+    seg = _SEG["active"]
+    if seg is not None:
+        seg._cut(lambda: _allreduce_now(t, average))
+        return t
+    return _allreduce_now(t, average)
+
+
 def allreduce_grads(params) -> None:
     """Average the .grad of `params` across ranks with a single flat all-reduce."""
+    seg = _SEG["active"]
+    if seg is not None:
+        params = list(params)
+        seg._cut(lambda: _allreduce_grads_now(params))
+        return
+    _allreduce_grads_now(params)
+
+
+def _allreduce_grads_now(params) -> None:
     if world_size() <= 1:
         return
     grads = [p.grad for p in params if p.grad is not None]

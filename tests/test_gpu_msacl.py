@@ -178,3 +178,39 @@ def test_graph_replayed_update_trains():
     for mode, h in losses.items():
         assert h[-1] < h[0], (mode, h)
     np.testing.assert_allclose(losses[True][0], losses[False][0], rtol=1e-5)
+
+
+def test_segmented_graph_update_equals_single_graph(monkeypatch):
+    """Data-parallel capture (utils/dist.py GraphSegments: the update graph cut at every
+    all-reduce, forced here on one GPU) replays the same kernels as the single-graph path and the
+    eager path: parameters bit-identical after several updates (fixed rsample noise)."""
+    import torch.distributions.normal as tdn
+    from msacl_amd.algorithm.msacl import MSACL
+    g = np.load(os.path.join(G, "msacl_update.npz"))
+    B, n = int(g["cfg_B"]), int(g["cfg_n"])
+    data = {k: torch.as_tensor(g["in_" + k], device="cuda") for k in ("obs", "act", "rew", "cost", "obs2", "done", "logp")}
+    noise = {}
+
+    def fixed(shape, dtype, device):
+        key = tuple(shape)
+        if key not in noise:
+            gen = torch.Generator(device="cuda").manual_seed(len(noise) + 1)
+            noise[key] = torch.randn(key, dtype=dtype, device=device, generator=gen)
+        return noise[key]
+
+    monkeypatch.setattr(tdn, "_standard_normal", fixed)
+    states = {}
+    for mode in ("eager", "graph", "segments"):
+        alg = MSACL(**_msacl_kwargs(B, n), alg_use_graph=(mode != "eager"),
+                    alg_force_graph_segments=(mode == "segments"))
+        sd = {k[5:]: torch.as_tensor(g[k]) for k in g.files if k.startswith("init/")}
+        alg.networks.load_state_dict(sd)
+        for it in range(6):
+            alg.model_update(data, it)
+        if mode == "segments":
+            seg = alg._graphs[(True, True)][0]
+            assert len(seg.graphs) > 1 and len(seg.ops) == len(seg.graphs) - 1
+        states[mode] = {k: v.detach().clone() for k, v in alg.networks.state_dict().items()}
+    for mode in ("graph", "segments"):
+        for k, v in states["eager"].items():
+            assert torch.equal(v, states[mode][k]), (mode, k)
