@@ -9,9 +9,10 @@ it out of the create_alg registry, RL/create_pkg/create_alg.py:38-47).
   so an update that contains optimiser steps can be captured into a HIP graph.
 * UpdateGraph: replays a whole model update as ONE HIP graph per branch key (e.g. the
   (update-target, update-policy) flags of an iteration). First call per branch runs eagerly on
-  static input copies (lazy hipBLASLt / Adam state init), the second captures, later calls copy
-  the new batch into the static inputs and replay. Off under torch.distributed (the gradient
-  all-reduces are not captured) and when disabled.
+  static input copies (lazy BLAS / Adam state init), the second captures, later calls copy
+  the new batch into the static inputs and replay. Under torch.distributed the capture is cut at
+  every gradient all-reduce (utils/dist.py GraphSegments: the collectives run eagerly between
+  the replays, never inside a graph).
 * polyak_: target-network averaging (p_t <- (1-tau) p_t + tau p), one mh_polyak_multi launch.
 """
 from __future__ import annotations
@@ -97,11 +98,10 @@ class UpdateGraph:
         self._warm = set()
 
     def usable(self):
-        return (self.enabled and D.world_size() == 1 and torch.cuda.is_available()
-                and not torch.cuda.is_current_stream_capturing())
+        return (self.enabled and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing())
 
     def __call__(self, data, key):
-        if not self.usable():
+        if not self.usable() or not all(v.is_cuda for v in data.values() if torch.is_tensor(v)):
             return self.body(data, *key)
         shapes = tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(data.items()) if torch.is_tensor(v))
         if self._static is None or self._shapes != shapes:
@@ -116,9 +116,14 @@ class UpdateGraph:
             self._warm.add(key)
             return self.body(self._static, *key)
         if key not in self._graphs:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                outs = self.body(self._static, *key)
+            if D.graph_segments_wanted():  # graphs cut at the gradient all-reduces (utils/dist.py)
+                g = D.GraphSegments()
+                with D.capturing(g):
+                    outs = self.body(self._static, *key)
+            else:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    outs = self.body(self._static, *key)
             self._graphs[key] = (g, outs)
         g, outs = self._graphs[key]
         g.replay()

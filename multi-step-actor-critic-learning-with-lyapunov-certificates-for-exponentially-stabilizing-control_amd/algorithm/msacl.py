@@ -233,7 +233,7 @@ class MSACL:
     def _segmented(self):
         """World size > 1 (or the test switch): the graph is cut at every collective
         (utils/dist.py GraphSegments) instead of capturing the update as one graph."""
-        return D.world_size() > 1 or self.force_graph_segments
+        return D.graph_segments_wanted() or self.force_graph_segments
 
     def _graph_update(self, data, flags):
         """Replay the whole update (~250 launches) as one HIP graph (with data parallelism: a

@@ -73,7 +73,16 @@ class GraphSegments:
                 self.ops[i]()
 
 
-_SEG = {"active": None}
+_SEG = {"active": None, "force": False}
+
+
+def force_graph_segments(on: bool) -> None:
+    """Test switch: cut update graphs at their collectives even with one rank."""
+    _SEG["force"] = bool(on)
+
+
+def graph_segments_wanted() -> bool:
+    return world_size() > 1 or _SEG["force"]
 
 
 class capturing:

@@ -133,3 +133,44 @@ def test_graph_replayed_update_trains(tag):
     assert len(alg._graph._graphs) == 2
     assert all(torch.isfinite(p).all() for p in alg.networks.parameters())
     assert hist[-1] < hist[0], hist
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", ["sac", "lac"])
+def test_segmented_graph_update_equals_eager(tag, monkeypatch):
+    """UpdateGraph cut at the gradient all-reduces (the world size > 1 capture, forced on one GPU
+    with utils/dist.py force_graph_segments) and the single graph replay the eager update's
+    kernels: parameters bit-identical after several updates (fixed rsample noise)."""
+    import torch.distributions.normal as tdn
+    from msacl_amd.utils import dist as D
+    g = np.load(os.path.join(G, f"{tag}_update.npz"))
+    keys = [k[3:] for k in g.files if k.startswith("in_")]
+    data = {k: torch.as_tensor(g["in_" + k], device="cuda") for k in keys}
+    noise = {}
+
+    def fixed(shape, dtype, device):
+        key = tuple(shape)
+        if key not in noise:
+            gen = torch.Generator(device="cuda").manual_seed(len(noise) + 1)
+            noise[key] = torch.randn(key, dtype=dtype, device=device, generator=gen)
+        return noise[key]
+
+    monkeypatch.setattr(tdn, "_standard_normal", fixed)
+    states = {}
+    try:
+        for mode in ("eager", "graph", "segments"):
+            D.force_graph_segments(mode == "segments")
+            alg = make_alg(tag, "cuda")
+            alg.networks.load_state_dict({k[5:]: torch.as_tensor(g[k]) for k in g.files if k.startswith("init/")})
+            alg._graph.enabled = mode != "eager"
+            for it in range(6):
+                alg.model_update(data, it)
+            if mode == "segments":
+                seg = next(iter(alg._graph._graphs.values()))[0]
+                assert isinstance(seg, D.GraphSegments) and len(seg.graphs) > 1
+            states[mode] = {k: v.detach().clone() for k, v in alg.networks.state_dict().items()}
+    finally:
+        D.force_graph_segments(False)
+    for mode in ("graph", "segments"):
+        for k, v in states["eager"].items():
+            assert torch.equal(v, states[mode][k]), (mode, k)
