@@ -463,9 +463,10 @@ int mh_act_grad_chunks(int64_t rows, int32_t* chunks_out) {
 
 int mh_act_grad_colsum(const float* dy, const float* y, int64_t rows, int32_t cols, int32_t act, float* g,
                        float* db, float* partial, uint32_t* tickets, void* stream) {
-  if (!dy || (act != 0 && (!y || !g)) || !partial) return fail(MH_EINVAL, "mh_act_grad_colsum: null pointer");
   if (act < 0 || act > 2) return fail(MH_EINVAL, "mh_act_grad_colsum: act must be 0, 1 or 2");
   if (rows < 0 || cols <= 0) return fail(MH_EINVAL, "mh_act_grad_colsum: bad shape");
+  if (rows > 0 && (!dy || (act != 0 && (!y || !g)) || !partial))
+    return fail(MH_EINVAL, "mh_act_grad_colsum: null pointer");
   MH_HIP(mh::launch_act_grad_colsum(dy, y, rows, cols, act, act == 0 ? nullptr : g, db, partial, tickets,
                                     (hipStream_t)stream));
   return MH_OK;

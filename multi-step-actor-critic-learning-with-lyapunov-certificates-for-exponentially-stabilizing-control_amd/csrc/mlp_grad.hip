@@ -131,7 +131,8 @@ int act_grad_tickets(int N) { return (N + AG_COLS - 1) / AG_COLS; }
 
 hipError_t launch_act_grad_colsum(const float* dy, const float* y, int64_t M, int N, int act, float* g, float* db,
                                   float* partial, uint32_t* tickets, hipStream_t st) {
-  if (M <= 0 || N <= 0) return hipSuccess;
+  if (N <= 0) return hipSuccess;
+  if (M <= 0) return db ? hipMemsetAsync(db, 0, sizeof(float) * (size_t)N, st) : hipSuccess;  // empty sum
   const int R = act_grad_chunks(M);
   const int cg = (N + AG_COLS - 1) / AG_COLS;
   // with tickets: one launch (the last chunk of each column group reduces); without: two

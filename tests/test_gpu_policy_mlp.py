@@ -115,3 +115,21 @@ def _linear_act_case(MLP, act, rows):
     xi = x.clone().requires_grad_(True)
     fused(xi).sum().backward()
     assert fused[2].weight.grad is None and fused[0].weight.grad is not None and xi.grad is not None
+
+
+@pytest.mark.parametrize("backend", ["hip", "blas"])
+def test_fused_mlp_empty_batch(backend):
+    """Zero rows: empty outputs, zero weight and bias gradients (the empty sum), as nn.Sequential."""
+    from msacl_amd.apprfunc._fused import MLP, gemm_backend, set_gemm_backend
+    prev = gemm_backend()
+    set_gemm_backend(backend)
+    try:
+        torch.manual_seed(0)
+        net = MLP(nn.Linear(12, 256), nn.ReLU(), nn.Linear(256, 256), nn.Tanh(), nn.Linear(256, 8), nn.Identity()).cuda()
+        y = net(torch.zeros(0, 12, device="cuda"))
+        assert y.shape == (0, 8)
+        y.sum().backward()
+        for p in net.parameters():
+            assert p.grad is not None and torch.equal(p.grad, torch.zeros_like(p))
+    finally:
+        set_gemm_backend(prev)
