@@ -14,8 +14,9 @@ kernel's. Backend (`set_gemm_backend`, config key `update_gemm`):
   "auto" (default)  mh_gemm_f32 where it measured faster than the BLAS library on the update's
                     shapes (tools/gemm_shapes.py, profiles/r01_gemm_shapes.json): forwards on
                     <= 1,024 rows (the B = 256 rows of the first-step networks: 8 vs 63 us, where
-                    the library runs a 256^3 product on one workgroup) or into one output column
-                    (critic heads), and weight gradients of one-output layers; the library
+                    the library runs a 256^3 product on one workgroup), into one output column
+                    (critic heads) or through tanh from a short input (epilogue instead of a
+                    separate tanh launch), and weight gradients of one-output layers; the library
                     (torch.addmm / _addmm_activation / mm) elsewhere
   "hip"             every GEMM through mh_gemm_f32
   "blas"            every GEMM through the library
@@ -61,9 +62,10 @@ def set_gemm_backend(name: str):
     _GEMM_BACKEND["name"] = name
 
 
-def _hip_forward(rows, out_features):
+def _hip_forward(rows, out_features, act=0, in_features=0):
     b = _GEMM_BACKEND["name"]
-    return b == "hip" or (b == "auto" and (rows <= 1024 or out_features == 1))
+    # tanh layers with a short K: the epilogue saves the library path's separate tanh launch
+    return b == "hip" or (b == "auto" and (rows <= 1024 or out_features == 1 or (act == 2 and in_features <= 64)))
 
 
 def _hip_dx():
@@ -101,7 +103,7 @@ class LinearAct(torch.autograd.Function):
     def forward(ctx, x, weight, bias, act):
         M, K = x.shape
         Nout = weight.shape[0]
-        if _hip_forward(M, Nout):
+        if _hip_forward(M, Nout, act, K):
             y = gemm(x, weight.contiguous(), bias.contiguous(), M, Nout, K, K, K, 0, 1, act)
         elif act == 1:
             y = torch._addmm_activation(bias, x, weight.t())

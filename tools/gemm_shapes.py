@@ -67,13 +67,17 @@ def main():
         else:
             blas_fn = lambda: opA.mm(opB)  # noqa: E731
         blas = timed(blas_fn)
+        prev_lib = torch.backends.cuda.preferred_blas_library()
+        torch.backends.cuda.preferred_blas_library("cublaslt")
+        blaslt = timed(blas_fn)
+        torch.backends.cuda.preferred_blas_library(prev_lib)
         r = {"M": M, "N": N, "K": K, "ta": ta, "tb": tb, "act": act, "bias": has_b, "calls_per_update": calls,
-             "hip_us": round(hip, 2), "blas_us": round(blas, 2)}
+             "hip_us": round(hip, 2), "blas_us": round(blas, 2), "hipblaslt_us": round(blaslt, 2)}
         rows.append(r)
         print(json.dumps(r), flush=True)
     tot_h = sum(r["hip_us"] * r["calls_per_update"] for r in rows)
     tot_b = sum(r["blas_us"] * r["calls_per_update"] for r in rows)
-    tot_min = sum(min(r["hip_us"], r["blas_us"]) * r["calls_per_update"] for r in rows)
+    tot_min = sum(min(r["hip_us"], r["blas_us"], r["hipblaslt_us"]) * r["calls_per_update"] for r in rows)
     print(json.dumps({"per_update_us": {"hip": round(tot_h, 1), "blas": round(tot_b, 1), "best_of": round(tot_min, 1)}}))
     if a.out:
         json.dump(rows, open(a.out, "w"), indent=1)
