@@ -31,6 +31,7 @@ __global__ __launch_bounds__(256) void k_act_grad_colsum(const float* __restrict
   const int n = blockIdx.x * AG_COLS + tx;
   const int64_t m0 = (int64_t)blockIdx.y * AG_ROWS + ty;
   float acc = 0.0f;
+  float gv[AG_RPT];
   if (n < N) {
     float d[AG_RPT], t[AG_RPT];
 #pragma unroll
@@ -42,7 +43,6 @@ __global__ __launch_bounds__(256) void k_act_grad_colsum(const float* __restrict
     }
     // all of g first, then the stores: a store between two uses of loaded values would make
     // every later wait on the load queue also wait for that store (vmcnt counts both in order)
-    float gv[AG_RPT];
 #pragma unroll
     for (int j = 0; j < AG_RPT; ++j) {
       gv[j] = d[j];
@@ -51,19 +51,24 @@ __global__ __launch_bounds__(256) void k_act_grad_colsum(const float* __restrict
     }
 #pragma unroll
     for (int j = 0; j < AG_RPT; ++j) acc += gv[j];
-    if (g) {
+  }
+  red[ty][tx] = acc;
+  __syncthreads();
+  const float csum = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
+  // g is written after the chunk sums are published: the drain before the arrival count then
+  // waits for one store per thread, not for this thread's 16 g stores as well
+  auto store_g = [&]() {
+    if (g && n < N) {
 #pragma unroll
       for (int j = 0; j < AG_RPT; ++j) {
         const int64_t m = m0 + 4 * j;
         if (m < M) g[m * N + n] = gv[j];
       }
     }
-  }
-  red[ty][tx] = acc;
-  __syncthreads();
-  const float csum = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
+  };
   if (!tickets) {
     if (ty == 0 && n < N) partial[(int64_t)blockIdx.y * N + n] = csum;
+    store_g();
     return;
   }
   // fused finish: publish this chunk's sums write-through, count arrivals per column group
@@ -76,23 +81,27 @@ __global__ __launch_bounds__(256) void k_act_grad_colsum(const float* __restrict
     const uint32_t a = __hip_atomic_fetch_add(tickets + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = (a == gridDim.y - 1);
   }
+  store_g();
   __syncthreads();
   if (!s_last) return;
   const int R = (int)gridDim.y;
   float s = 0.0f;
   if (n < N) {
-    int r = ty;
-    for (; r + 12 < R; r += 16) {
-      const float a0 = __hip_atomic_load(partial + (int64_t)r * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const float a1 = __hip_atomic_load(partial + (int64_t)(r + 4) * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const float a2 = __hip_atomic_load(partial + (int64_t)(r + 8) * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const float a3 = __hip_atomic_load(partial + (int64_t)(r + 12) * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s = s + a0;
-      s = s + a1;
-      s = s + a2;
-      s = s + a3;
+    // the write-through loads go to memory: issue a batch of 16 before the first add, so a
+    // batch costs one round trip (rows ty, ty + 4, ... in ascending order, as before)
+    constexpr int NB = 16;
+    for (int base = ty; base < R; base += 4 * NB) {
+      float v[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int r = base + 4 * j;
+        v[j] = r < R ? __hip_atomic_load(partial + (int64_t)r * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : 0.0f;
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        if (base + 4 * j < R) s = s + v[j];
     }
-    for (; r < R; r += 4) s += __hip_atomic_load(partial + (int64_t)r * N + n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();  // everyone has read red[] above
   red[ty][tx] = s;
