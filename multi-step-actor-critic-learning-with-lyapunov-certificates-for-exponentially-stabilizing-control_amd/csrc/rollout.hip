@@ -101,6 +101,7 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
   const int64_t e = (int64_t)blockIdx.x * BLK + threadIdx.x;
   const bool live = e < E;
   bool emit = false;
+  int emit_pos = 0;  // ring slot of the window's oldest record (the position after this push)
   // store-cursor snapshot for the emission kernel, loaded up front by one thread (the grid
   // finishes with its slowest wave: three dependent round trips at the end would be exposed)
   const bool snap = a.ring && a.cursor && blockIdx.x == 0 && threadIdx.x == 0;
@@ -291,6 +292,7 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
       pos = pos + 1 == n ? 0 : pos + 1;
       len = len + 1 < n ? len + 1 : n;
       emit = (len == n);
+      emit_pos = pos;
       if (done) len = 0;  // deque.clear() when the newest item is done
       a.ring_len[e] = len;
       a.ring_pos[e] = pos;
@@ -311,7 +313,9 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
     }
     const int rank = emit ? base + __popcll(m & ((1ull << lane) - 1ull)) : -1;
     if (a.emit_list) {
-      if (emit) a.emit_list[(int64_t)blockIdx.x * BLK + rank] = (int32_t)(e - (int64_t)blockIdx.x * BLK);
+      // (block-local env index | oldest ring slot << 8): the emission kernel needs no ring_pos load
+      static_assert(BLK == 256, "emit_list packs the block-local env index into 8 bits");  // n <= 4096
+      if (emit) a.emit_list[(int64_t)blockIdx.x * BLK + rank] = (int32_t)(e - (int64_t)blockIdx.x * BLK) | (emit_pos << 8);
     } else if (live) {
       a.emit_rank[e] = rank;
     }
@@ -523,8 +527,9 @@ __global__ __launch_bounds__(256) void k_emit_fused(EmitArgs a) {
       if ((int64_t)offs[mid] <= g) bl = mid; else bh = mid - 1;
     }
     const int r = (int)(g - offs[bl]);
-    const int64_t e = (int64_t)bl * BLK + a.emit_list[(int64_t)bl * BLK + r];
-    int slot = a.ring_pos[e] + j;
+    const int packed = a.emit_list[(int64_t)bl * BLK + r];
+    const int64_t e = (int64_t)bl * BLK + (packed & (BLK - 1));
+    int slot = (packed >> 8) + j;
     slot = slot >= n ? slot - n : slot;
     float rec[F];
     const float4* src = reinterpret_cast<const float4*>(a.ring + (e * n + slot) * (int64_t)F);
