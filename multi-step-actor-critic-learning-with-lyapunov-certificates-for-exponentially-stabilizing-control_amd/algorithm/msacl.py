@@ -76,7 +76,9 @@ class _Scratch:
         self.backup, self.dq1, self.dq2 = f(B, n), f(B, n), f(B, n)
         self.abs_td, self.loss_q = f(B), f(1)
         self.is_clip, self.esl, self.lya_diff, self.loss_lya = f(B, n), f(B, n), f(B), f(1)
-        self.dV, self.dV2 = f(B, n), f(B, n)
+        # dV | dV2 as the two halves of one buffer: the two Lyapunov evaluations run as one batch
+        self.dV_both = f(2 * B, n)
+        self.dV, self.dV2 = self.dV_both[:B], self.dV_both[B:]
         self.adv_raw, self.adv, self.loss_ppo, self.d_ratio = f(B), f(B), f(1), f(B)
         self.stats = torch.empty(2, dtype=torch.float64, device=device)
 
@@ -302,8 +304,10 @@ class MSACL:
         with torch.no_grad():
             dist = self.networks.create_action_distributions(self.networks.policy(obs))
             logp = dist.log_prob(act).contiguous()
-        V = self.networks.lyapunov(obs)
-        V2 = self.networks.lyapunov(obs2)
+        # V(obs) and V(obs2) (msacl.py:275-276) as ONE batch through the network: one forward and
+        # one backward instead of two each (the weight gradients sum the same 2 B n rows)
+        V_both = self.networks.lyapunov(torch.cat([obs, obs2], 0))
+        V, V2 = V_both[:B], V_both[B:]
         N.check(N.lib().mh_msacl_lyapunov(
             N.ptr(logp), N.ptr(old_logp), N.ptr(V.detach().contiguous()), N.ptr(V2.detach().contiguous()), N.ptr(obs),
             N.ptr(obs2), N.ptr(self.start_obs_norm_coef), N.ptr(self.lya_diff_coef), N.ptr(self.start_lya_coef),
@@ -311,7 +315,7 @@ class MSACL:
             obs.shape[-1], N.ptr(s.is_clip), N.ptr(s.esl), N.ptr(s.lya_diff), N.ptr(s.loss_lya), N.ptr(s.dV),
             N.ptr(s.dV2), N.stream_of(self.device)), "mh_msacl_lyapunov")
         self.networks.lyapunov_optimizer.zero_grad()
-        torch.autograd.backward([V, V2], [s.dV, s.dV2])
+        torch.autograd.backward([V_both], [s.dV_both])
         D.allreduce_grads(list(self.networks.lyapunov.parameters()))
         self.networks.lyapunov_optimizer.step()
         return s.loss_lya[0]  # a view of the scratch (no allocation on the side stream)
@@ -332,8 +336,11 @@ class MSACL:
         ratio = torch.exp(dist.log_prob(old_act) - old_logp)
         is_ratio = ratio[:, 0]
         with torch.no_grad():
-            V0 = self.networks.lyapunov(obs[:, 0]).contiguous()
-            V2 = self.networks.lyapunov(obs2).contiguous()
+            # V(obs_0) and V(obs2) as one batch (msacl.py:395-396)
+            D_ = obs.shape[-1]
+            V_all = self.networks.lyapunov(torch.cat([obs[:, 0], obs2.reshape(-1, D_)], 0))
+            V0 = V_all[:B].contiguous()
+            V2 = V_all[B:].reshape(B, n).contiguous()
         N.check(N.lib().mh_msacl_stability_adv(N.ptr(V0), N.ptr(V2), N.ptr(self.lya_diff_coef), N.ptr(self.start_lya_coef),
                                                B, n, N.ptr(s.adv_raw), N.ptr(s.stats), N.stream_of(self.device)),
                 "mh_msacl_stability_adv")
