@@ -129,16 +129,17 @@ def allreduce_grads(params) -> None:
     """Average the .grad of `params` across ranks with a single flat all-reduce."""
     seg = _SEG["active"]
     if seg is not None:
-        params = list(params)
-        seg._cut(lambda: _allreduce_grads_now(params))
+        # the gradient tensors the captured graphs write, bound now: another capture (the other
+        # branch of the update) re-points p.grad at tensors of its own memory pool
+        grads = [p.grad for p in params if p.grad is not None]
+        seg._cut(lambda: _allreduce_tensors_now(grads))
         return
-    _allreduce_grads_now(params)
+    _allreduce_tensors_now([p.grad for p in params if p.grad is not None])
 
 
-def _allreduce_grads_now(params) -> None:
+def _allreduce_tensors_now(grads) -> None:
     if world_size() <= 1:
         return
-    grads = [p.grad for p in params if p.grad is not None]
     if not grads:
         return
     flat = torch._utils._flatten_dense_tensors(grads)

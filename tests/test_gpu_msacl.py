@@ -214,3 +214,40 @@ def test_segmented_graph_update_equals_single_graph(monkeypatch):
     for mode in ("graph", "segments"):
         for k, v in states["eager"].items():
             assert torch.equal(v, states[mode][k]), (mode, k)
+
+
+def test_segmented_graph_collectives_bind_the_captured_gradients(monkeypatch):
+    """Data-parallel replay with a stand-in collective (world size 2 faked; all_reduce multiplies
+    by 3, so every all-reduced gradient is scaled by 1.5 after the average): the graph chain of
+    each update branch must all-reduce the gradient tensors ITS graphs write, although the
+    other branch's capture re-points p.grad. Eager and segmented runs agree bit for bit."""
+    import torch.distributions.normal as tdn
+    from msacl_amd.algorithm.msacl import MSACL
+    from msacl_amd.utils import dist as D
+    g = np.load(os.path.join(G, "msacl_update.npz"))
+    B, n = int(g["cfg_B"]), int(g["cfg_n"])
+    data = {k: torch.as_tensor(g["in_" + k], device="cuda") for k in ("obs", "act", "rew", "cost", "obs2", "done", "logp")}
+    noise = {}
+
+    def fixed(shape, dtype, device):
+        key = tuple(shape)
+        if key not in noise:
+            gen = torch.Generator(device="cuda").manual_seed(len(noise) + 1)
+            noise[key] = torch.randn(key, dtype=dtype, device=device, generator=gen)
+        return noise[key]
+
+    monkeypatch.setattr(tdn, "_standard_normal", fixed)
+    monkeypatch.setattr(D, "world_size", lambda: 2)
+    monkeypatch.setattr(D.dist, "all_reduce", lambda t, *a, **k: t.mul_(3.0))
+    states = {}
+    for mode in ("eager", "segments"):
+        alg = MSACL(**_msacl_kwargs(B, n), alg_use_graph=(mode != "eager"))
+        sd = {k[5:]: torch.as_tensor(g[k]) for k in g.files if k.startswith("init/")}
+        alg.networks.load_state_dict(sd)
+        for it in range(8):
+            alg.model_update(data, it)
+        if mode == "segments":
+            assert len(alg._graphs) == 2 and all(isinstance(v[0], D.GraphSegments) for v in alg._graphs.values())
+        states[mode] = {k: v.detach().clone() for k, v in alg.networks.state_dict().items()}
+    for k, v in states["eager"].items():
+        assert torch.equal(v, states["segments"][k]), k
