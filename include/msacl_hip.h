@@ -330,6 +330,19 @@ int mh_msacl_stability_adv(const float* lya_obs0, const float* lya_obs2, const f
 int mh_msacl_ppo_clip(const float* ratio, const float* adv_raw, const double* stats,
                       double n_total, float clip_eps, int32_t B, float* adv, float* loss_out,
                       float* d_ratio, void* stream);
+/* The policy loss of msacl.py:383-391 on B*n elements: loss = (min(q1, q2) - exp(log_alpha) logp).mean()
+ * and entropy = -logp.mean() (one workgroup, fixed-order sums), and its autograd backward for a
+ * DEVICE upstream gradient g_loss (min: the smaller input, ties half each). */
+int mh_msacl_policy_loss(const float* q1, const float* q2, const float* logp, const float* log_alpha, int64_t N,
+                         float* loss_out, float* entropy_out, void* stream);
+int mh_msacl_policy_loss_backward(const float* q1, const float* q2, const float* log_alpha, const float* g_loss,
+                                  int64_t N, float* dq1, float* dq2, float* dlogp, void* stream);
+/* is_ratio = exp(logp_new - old_logp)[:, 0] on [B][n] (msacl.py:392-394) and its backward
+ * (d_logp_new: g * ratio in step 0, zero elsewhere). */
+int mh_msacl_ratio0(const float* logp_new, const float* old_logp, int32_t B, int32_t n, float* ratio_out,
+                    void* stream);
+int mh_msacl_ratio0_backward(const float* ratio, const float* g_ratio, int32_t B, int32_t n, float* d_logp_new,
+                             void* stream);
 
 /* ---- prioritized replay (new: the reference trainer expects buffer.update_batch(idx, prio),
  * RL/trainer/nstep_off_serial_trainer.py:93-95, but ships no prioritized buffer) ---- */

@@ -68,6 +68,55 @@ class ApproxContainer(nn.Module):
         return self.policy.get_act_dist_cls(logits)
 
 
+class _PolicyQLoss(torch.autograd.Function):
+    """(min(q1, q2) - alpha * logp).mean() and -logp.mean() (msacl.py:383-391) in one launch,
+    backward in one launch (mh_msacl_policy_loss[_backward])."""
+
+    @staticmethod
+    def forward(ctx, q1, q2, logp, log_alpha):
+        out = torch.empty(2, dtype=torch.float32, device=q1.device)
+        N.check(N.lib().mh_msacl_policy_loss(N.ptr(q1), N.ptr(q2), N.ptr(logp), N.ptr(log_alpha), q1.numel(),
+                                             N.ptr(out[0:1]), N.ptr(out[1:2]), N.stream_of(q1.device)),
+                "mh_msacl_policy_loss")
+        ctx.save_for_backward(q1, q2, log_alpha)
+        loss, entropy = out[0], out[1]
+        ctx.mark_non_differentiable(entropy)
+        return loss, entropy
+
+    @staticmethod
+    def backward(ctx, g_loss, g_entropy):
+        q1, q2, log_alpha = ctx.saved_tensors
+        dq1, dq2, dlogp = torch.empty_like(q1), torch.empty_like(q2), torch.empty_like(q1)
+        N.check(N.lib().mh_msacl_policy_loss_backward(N.ptr(q1), N.ptr(q2), N.ptr(log_alpha),
+                                                      N.ptr(g_loss.contiguous()), q1.numel(), N.ptr(dq1), N.ptr(dq2),
+                                                      N.ptr(dlogp), N.stream_of(q1.device)),
+                "mh_msacl_policy_loss_backward")
+        return dq1, dq2, dlogp, None
+
+
+class _Ratio0(torch.autograd.Function):
+    """exp(logp_new - old_logp)[:, 0] (msacl.py:392-394) and its backward, one launch each."""
+
+    @staticmethod
+    def forward(ctx, lp, old):
+        B, n = lp.shape
+        ratio = torch.empty(B, dtype=torch.float32, device=lp.device)
+        N.check(N.lib().mh_msacl_ratio0(N.ptr(lp), N.ptr(old), B, n, N.ptr(ratio), N.stream_of(lp.device)),
+                "mh_msacl_ratio0")
+        ctx.save_for_backward(ratio)
+        ctx.n = n
+        return ratio
+
+    @staticmethod
+    def backward(ctx, g):
+        (ratio,) = ctx.saved_tensors
+        B, n = ratio.shape[0], ctx.n
+        dlp = torch.empty(B, n, dtype=torch.float32, device=ratio.device)
+        N.check(N.lib().mh_msacl_ratio0_backward(N.ptr(ratio), N.ptr(g.contiguous()), B, n, N.ptr(dlp),
+                                                 N.stream_of(ratio.device)), "mh_msacl_ratio0_backward")
+        return dlp, None
+
+
 class _Scratch:
     """Per-shape device work buffers for the fused kernels (allocated once per batch shape)."""
 
@@ -330,11 +379,11 @@ class MSACL:
         new_act, new_act_logp = dist.rsample()
         q1 = self.networks.q1(obs, new_act)
         q2 = self.networks.q2(obs, new_act)
-        # alpha as a 0-d device tensor (the reference's alpha.item() float has the same f32 value)
-        alpha = self.networks.log_alpha.detach().exp()
-        loss_policy_q = (torch.min(q1, q2) - alpha * new_act_logp).mean()
-        ratio = torch.exp(dist.log_prob(old_act) - old_logp)
-        is_ratio = ratio[:, 0]
+        # (min(q1, q2) - alpha logp).mean() with alpha = exp(log_alpha) read on the device (the
+        # reference's alpha.item() float has the same f32 value), and the entropy, in one kernel
+        loss_policy_q, entropy = _PolicyQLoss.apply(q1.contiguous(), q2.contiguous(), new_act_logp.contiguous(),
+                                                    self.networks.log_alpha.detach())
+        is_ratio = _Ratio0.apply(dist.log_prob(old_act).contiguous(), old_logp.contiguous())
         with torch.no_grad():
             # V(obs_0) and V(obs2) as one batch (msacl.py:395-396)
             D_ = obs.shape[-1]
@@ -355,7 +404,7 @@ class MSACL:
         torch.autograd.backward([loss_policy_q, is_ratio], [self._neg_one, -s.d_ratio])
         D.allreduce_grads(list(self.networks.policy.parameters()))
         self.networks.policy_optimizer.step()
-        entropy = -new_act_logp.mean().detach()
+        entropy = entropy.detach()
         for p in list(self.networks.q1.parameters()) + list(self.networks.q2.parameters()):
             p.requires_grad = True
         return loss_policy.detach(), entropy

@@ -315,6 +315,59 @@ __global__ __launch_bounds__(TPB) void k_ppo_clip(const float* ratio, const floa
   if (threadIdx.x == 0) loss_out[0] = (float)(t / (double)B);
 }
 
+// --------------------------------------------------- policy loss pieces (msacl.py:383-405)
+// loss_policy_q = (min(q1, q2) - alpha * logp).mean(), alpha = exp(log_alpha) (the reference's
+// alpha.item()), and the entropy -logp.mean() as a by-product: one workgroup, fixed-order sums.
+__device__ __forceinline__ float torch_min(float a, float b) {
+  return (a != a || b != b) ? __builtin_nanf("") : (a < b ? a : b);  // torch.min propagates NaN
+}
+__global__ __launch_bounds__(TPB) void k_policy_loss(const float* q1, const float* q2, const float* logp,
+                                                     const float* log_alpha, int64_t N, float* loss,
+                                                     float* entropy) {
+  __shared__ double sh[TPB];
+  const float alpha = expf(*log_alpha);
+  double a = 0.0, b = 0.0;
+  for (int64_t i = threadIdx.x; i < N; i += TPB) {
+    const float m = torch_min(q1[i], q2[i]);
+    const float lp = logp[i];
+    a += (double)(m - alpha * lp);
+    b += (double)lp;
+  }
+  const double ta = block_sum(a, sh);
+  const double tb = block_sum(b, sh);
+  if (threadIdx.x == 0) {
+    loss[0] = (float)(ta / (double)N);
+    entropy[0] = -(float)(tb / (double)N);
+  }
+}
+// autograd's backward of that expression for an upstream gradient g (device scalar):
+// mean -> g / N; sub -> (+, -); mul by alpha; minimum -> the smaller input (ties: half each)
+__global__ __launch_bounds__(256) void k_policy_loss_bwd(const float* q1, const float* q2, const float* log_alpha,
+                                                         const float* g, int64_t N, float* dq1, float* dq2,
+                                                         float* dlogp) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= N) return;
+  const float alpha = expf(*log_alpha);
+  const float gg = *g * (1.0f / (float)N);  // PyTorch's division by a scalar: times its f32 reciprocal
+  const float a = q1[i], b = q2[i];
+  // torch minimum's backward: where(a == b, g / 2, g), zeroed where the other input is smaller
+  // (so a NaN pair passes the gradient to both, as autograd does)
+  dq1[i] = a == b ? gg / 2.0f : (a > b ? 0.0f : gg);
+  dq2[i] = a == b ? gg / 2.0f : (a < b ? 0.0f : gg);
+  dlogp[i] = (-gg) * alpha;
+}
+// is_ratio = exp(logp_new - old_logp)[:, 0] (msacl.py:392-394; only step 0 of each window is used)
+__global__ __launch_bounds__(256) void k_ratio0(const float* lp, const float* old, int B, int n, float* ratio) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b < B) ratio[b] = expf(lp[(int64_t)b * n] - old[(int64_t)b * n]);
+}
+__global__ __launch_bounds__(256) void k_ratio0_bwd(const float* ratio, const float* g, int B, int n, float* dlp) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)B * n) return;
+  const int64_t b = i / n;
+  dlp[i] = (i - b * n) == 0 ? g[b] * ratio[b] : 0.0f;
+}
+
 thread_local std::string g_merr;
 
 }  // namespace
@@ -376,6 +429,40 @@ int mh_msacl_ppo_clip(const float* ratio, const float* adv_raw, const double* st
   k_ppo_clip<<<1, TPB, 0, (hipStream_t)stream>>>(ratio, adv_raw, stats, n_total, clip_eps, B, adv, loss_out,
                                                  d_ratio);
   MH_CHECK_LAUNCH("ppo_clip");
+  return MH_OK;
+}
+
+int mh_msacl_policy_loss(const float* q1, const float* q2, const float* logp, const float* log_alpha, int64_t N,
+                         float* loss_out, float* entropy_out, void* stream) {
+  if (!q1 || !q2 || !logp || !log_alpha || !loss_out || !entropy_out || N <= 0) return MH_EINVAL;
+  k_policy_loss<<<1, TPB, 0, (hipStream_t)stream>>>(q1, q2, logp, log_alpha, N, loss_out, entropy_out);
+  MH_CHECK_LAUNCH("policy_loss");
+  return MH_OK;
+}
+
+int mh_msacl_policy_loss_backward(const float* q1, const float* q2, const float* log_alpha, const float* g_loss,
+                                  int64_t N, float* dq1, float* dq2, float* dlogp, void* stream) {
+  if (!q1 || !q2 || !log_alpha || !g_loss || !dq1 || !dq2 || !dlogp || N <= 0) return MH_EINVAL;
+  k_policy_loss_bwd<<<(unsigned)((N + 255) / 256), 256, 0, (hipStream_t)stream>>>(q1, q2, log_alpha, g_loss, N, dq1,
+                                                                                  dq2, dlogp);
+  MH_CHECK_LAUNCH("policy_loss_bwd");
+  return MH_OK;
+}
+
+int mh_msacl_ratio0(const float* logp_new, const float* old_logp, int32_t B, int32_t n, float* ratio_out,
+                    void* stream) {
+  if (!logp_new || !old_logp || !ratio_out || B <= 0 || n <= 0) return MH_EINVAL;
+  k_ratio0<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(logp_new, old_logp, B, n, ratio_out);
+  MH_CHECK_LAUNCH("ratio0");
+  return MH_OK;
+}
+
+int mh_msacl_ratio0_backward(const float* ratio, const float* g_ratio, int32_t B, int32_t n, float* d_logp_new,
+                             void* stream) {
+  if (!ratio || !g_ratio || !d_logp_new || B <= 0 || n <= 0) return MH_EINVAL;
+  const int64_t total = (int64_t)B * n;
+  k_ratio0_bwd<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(ratio, g_ratio, B, n, d_logp_new);
+  MH_CHECK_LAUNCH("ratio0_bwd");
   return MH_OK;
 }
 

@@ -1,0 +1,62 @@
+"""GPU: the fused MSACL policy-loss pieces (csrc/msacl_kernels.hip k_policy_loss / k_ratio0,
+used by algorithm/msacl.py `_policy_update`, reference msacl.py:383-405) against the PyTorch
+expressions they replace, forward and backward:
+  loss = (min(q1, q2) - exp(log_alpha) * logp).mean(), entropy = -logp.mean()
+  is_ratio = exp(logp_new - old_logp)[:, 0]
+Tolerance: the loss/entropy sums run in double on the device (torch: float32 tree), so they
+agree to 1e-6 relative of sum|terms|; element-wise gradients are bit-exact except the step-0
+ratio gradient (one float32 multiply of the same values: exact as well)."""
+import pytest
+import torch
+
+import msacl_amd  # noqa: F401
+from msacl_amd.algorithm.msacl import _PolicyQLoss, _Ratio0
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("B,n", [(256, 20), (1, 1), (3, 7), (1000, 33)])
+def test_policy_q_loss_matches_torch(B, n):
+    g = torch.Generator(device="cuda").manual_seed(B * 31 + n)
+    q1 = torch.randn(B, n, device="cuda", generator=g)
+    q2 = torch.randn(B, n, device="cuda", generator=g)
+    q2[:, ::3] = q1[:, ::3]  # ties: autograd gives each input half the gradient
+    lp = torch.randn(B, n, device="cuda", generator=g)
+    log_alpha = torch.tensor(-0.7, device="cuda")
+    a = [t.clone().requires_grad_(True) for t in (q1, q2, lp)]
+    b = [t.clone().requires_grad_(True) for t in (q1, q2, lp)]
+    loss, ent = _PolicyQLoss.apply(a[0], a[1], a[2], log_alpha)
+    ref = (torch.min(b[0], b[1]) - log_alpha.exp() * b[2]).mean()
+    ref_ent = -b[2].mean().detach()
+    scale = float((torch.min(q1, q2).abs() + lp.abs() * log_alpha.exp()).mean()) + 1e-30
+    assert abs(float(loss) - float(ref)) <= 1e-6 * scale
+    assert abs(float(ent) - float(ref_ent)) <= 1e-6 * (float(lp.abs().mean()) + 1e-30)
+    assert not ent.requires_grad
+    up = torch.tensor(-1.3, device="cuda")
+    torch.autograd.backward([loss], [up])
+    torch.autograd.backward([ref], [up])
+    for x, y in zip(a, b):
+        torch.testing.assert_close(x.grad, y.grad, rtol=0, atol=0)
+
+
+def test_policy_q_loss_nan_propagates():
+    q1 = torch.tensor([[1.0, float("nan")]], device="cuda")
+    q2 = torch.tensor([[0.5, 2.0]], device="cuda")
+    lp = torch.zeros(1, 2, device="cuda")
+    loss, _ = _PolicyQLoss.apply(q1, q2, lp, torch.tensor(0.0, device="cuda"))
+    assert torch.isnan(loss)
+
+
+@pytest.mark.parametrize("B,n", [(256, 20), (1, 1), (17, 5)])
+def test_ratio0_matches_torch(B, n):
+    g = torch.Generator(device="cuda").manual_seed(B + n)
+    lp = (torch.randn(B, n, device="cuda", generator=g) * 0.3).requires_grad_(True)
+    old = torch.randn(B, n, device="cuda", generator=g) * 0.3
+    lp2 = lp.detach().clone().requires_grad_(True)
+    r = _Ratio0.apply(lp, old)
+    ref = torch.exp(lp2 - old)[:, 0]
+    assert torch.equal(r, ref)
+    up = torch.randn(B, device="cuda", generator=g)
+    torch.autograd.backward([r], [up])
+    torch.autograd.backward([ref], [up])
+    assert torch.equal(lp.grad, lp2.grad)
