@@ -16,8 +16,9 @@ kernel's. Backend (`set_gemm_backend`, config key `update_gemm`):
                     <= 1,024 rows (the B = 256 rows of the first-step networks: 8 vs 63 us, where
                     the library runs a 256^3 product on one workgroup), into one output column
                     (critic heads) or through tanh from a short input (epilogue instead of a
-                    separate tanh launch), and weight gradients of one-output layers; the library
-                    (torch.addmm / _addmm_activation / mm) elsewhere
+                    separate tanh launch), forwards and input gradients of the B x n-row
+                    256-wide layers (the tall-product kernel), and weight gradients of one-output
+                    layers; the library (torch.addmm / _addmm_activation / mm) elsewhere
   "hip"             every GEMM through mh_gemm_f32
   "blas"            every GEMM through the library
 CPU tensors (and activations other than identity/ReLU/tanh) take the plain nn.Sequential path.
@@ -62,14 +63,23 @@ def set_gemm_backend(name: str):
     _GEMM_BACKEND["name"] = name
 
 
+def _tall(rows, n, k):
+    """mh_gemm_f32's tall-product kernel (k_gemm_tall: >= 2,048 rows, N % 64 == 0) on a K deep
+    enough for its pipeline: 10.6 vs 12.4 us (forward) and 10.9 vs 12.1 us (input gradient) at
+    5,120 x 256 x 256 (tools/tall_probe.py); the library stays faster for K < 64."""
+    return rows >= 2048 and n % 64 == 0 and k % 4 == 0 and k >= 64
+
+
 def _hip_forward(rows, out_features, act=0, in_features=0):
     b = _GEMM_BACKEND["name"]
     # tanh layers with a short K: the epilogue saves the library path's separate tanh launch
-    return b == "hip" or (b == "auto" and (rows <= 1024 or out_features == 1 or (act == 2 and in_features <= 64)))
+    return b == "hip" or (b == "auto" and (rows <= 1024 or out_features == 1 or (act == 2 and in_features <= 64)
+                                           or _tall(rows, out_features, in_features)))
 
 
-def _hip_dx():
-    return _GEMM_BACKEND["name"] == "hip"
+def _hip_dx(rows=0, in_features=0, out_features=0):
+    b = _GEMM_BACKEND["name"]
+    return b == "hip" or (b == "auto" and _tall(rows, in_features, out_features))
 
 
 def _hip_dw(out_features):
@@ -140,7 +150,7 @@ class LinearAct(torch.autograd.Function):
         K = x.shape[1]
         dx = dw = None
         if need_x:
-            dx = gemm(g, weight.contiguous(), None, M, K, Nout, Nout, K, 0, 0) if _hip_dx() else g.mm(weight)
+            dx = gemm(g, weight.contiguous(), None, M, K, Nout, Nout, K, 0, 0) if _hip_dx(M, K, Nout) else g.mm(weight)
         if need_w:
             dw = gemm(g, x, None, Nout, K, M, Nout, K, 1, 0) if _hip_dw(Nout) else g.t().mm(x)
         return dx, dw, db, None

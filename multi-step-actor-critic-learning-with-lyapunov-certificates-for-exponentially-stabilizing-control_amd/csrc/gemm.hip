@@ -224,6 +224,222 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs g) {
   }
 }
 
+// ------------------------------------------------------------------ tall products
+// C = act(A[M][K] . op(B) + bias) for M >> N (the B x n = 5,120-row layers of the update:
+// forward x W^T and input gradient g W, N = 256): the output is only M x 256, so a 64 x 64 or
+// 128 x 128 tiling leaves most of the 256 CUs idle or runs two uneven rounds (the BLAS kernels
+// for these shapes: 160 workgroups, 10.5-14 us). Here
+//   * workgroup = 4 waves = (16 RB rows) x 64 columns, wave w owning columns 16w..16w+15 over all
+//     RB row blocks (RB chosen so that the workgroup count fills whole rounds of 256 CUs: RB = 5,
+//     80 x 64 tiles, 256 workgroups at M = 5,120, N = 256);
+//   * 64-deep k chunks staged through LDS (double buffered, one barrier per chunk): the global
+//     loads are row-contiguous float4 (a quarter-wave reads 256 B of one row), issued two
+//     chunks ahead (two register sets), so each chunk's loads have two chunks' MFMAs (2 x 80
+//     per wave) to land. Loading the MFMA
+//     fragments straight from global memory instead puts 16 rows under every quarter-wave: 64
+//     cache-line lookups per load instruction, and the vector L1 then takes 17 us for what the
+//     MFMAs do in 5;
+//   * fragments are read from LDS as float4 along k: MFMA j of a 16-deep group takes, in lane l,
+//     k = 4 (l >> 4) + j for both operands (the k order inside a group is permuted, the same way
+//     for A and B); op(B) is stored [n][k] in LDS whatever its global layout;
+//   * blockIdx -> tile is XCD-aware: each XCD (blockIdx mod 8) gets whole row tiles, so an A row
+//     block is fetched into one L2 only.
+// K % 4 == 0, N % 64 == 0, 16-B aligned rows (A, op(B), C, bias), operands below 1 GiB.
+constexpr int TK = 64;       // k depth of one LDS stage
+constexpr int TLD = TK + 4;  // LDS row stride (floats): 16 rows of a b128 read hit distinct banks
+
+template <int RB, bool TB, int NCH>
+__global__ __launch_bounds__(256) void k_gemm_tall(GemmArgs g, int tiles_n) {
+  constexpr int RM = 16 * RB;
+  constexpr int NA = RM * TK / 4 / 256;  // float4 loads of A per thread per chunk
+  constexpr int NB = 64 * TK / 4 / 256;  // ... of op(B)
+  static_assert(RM * TK / 4 % 256 == 0, "A chunk must split evenly over 256 threads");
+  __shared__ float lds[2][(RM + 64) * TLD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int T = (int)gridDim.x;
+  const int bid = (int)blockIdx.x;
+  const int t = (T % 8 == 0) ? (bid % 8) * (T / 8) + bid / 8 : bid;
+  const int tm = t / tiles_n, tn = t - tm * tiles_n;
+  const int m0 = tm * RM, n0 = tn * 64;
+  const int M = (int)g.M, K = (int)g.K, lda = (int)g.lda, ldb = (int)g.ldb;
+  const __amdgpu_buffer_rsrc_t ra_rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.A), (short)0, (int)(g.M * g.lda * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(g.B), (short)0, (int)((TB ? g.N : g.K) * g.ldb * 4), 0x00020000);
+  // rows past M start at 1 GiB, beyond the buffer (the host keeps operands below 1 GiB): they
+  // read 0 with no per-load select
+  constexpr int OOB_ROW = 0x40000000;
+  // this thread's float4 slots of a chunk: A slot f -> (row f / 16, k 4 (f % 16)); op(B) slot f
+  // -> TB: (n f / 16, k 4 (f % 16)), !TB: (k f / 16, n 4 (f % 16))
+  int aoff[NA], boff[NB];
+#pragma unroll
+  for (int s = 0; s < NA; ++s) {
+    const int f = tid + 256 * s, m = m0 + f / 16;
+    aoff[s] = m < M ? m * lda * 4 + (f % 16) * 16 : OOB_ROW;
+  }
+#pragma unroll
+  for (int s = 0; s < NB; ++s) {
+    const int f = tid + 256 * s;
+    boff[s] = TB ? ((n0 + f / 16) * ldb * 4 + (f % 16) * 16) : ((f / 16) * ldb * 4 + (n0 + 4 * (f % 16)) * 4);
+  }
+  // epilogue slots: float4 f = tid + 256 s of the RM x 64 tile -> (row f / 16, cols 4 (f % 16)..);
+  // the bias of those columns (the same for every s) is fetched now, used after the last chunk
+  const f32x4 bv = g.bias ? *reinterpret_cast<const f32x4*>(g.bias + n0 + 4 * (tid % 16)) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  f32x4 ra[2][NA], rb[2][NB];  // two chunks in flight ahead of the LDS stage
+  auto load = [&](int c, int p) {
+#ifdef MH_TALL_EXP_NOLOAD  // cost-attribution experiment only
+    if (g.K > 0) return;
+#endif
+#pragma unroll
+    for (int s = 0; s < NA; ++s)
+      ra[p][s] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra_rs, aoff[s] + c * TK * 4, 0, 0));
+#pragma unroll
+    for (int s = 0; s < NB; ++s)
+      rb[p][s] = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb_rs, boff[s] + (TB ? c * TK * 4 : c * TK * ldb * 4), 0, 0));
+  };
+  auto stage = [&](int c, int p) {
+    if (NCH == 0 && c * TK + TK > K) {  // k >= K: A (and op(B) of TB) read the next row there
+#pragma unroll
+      for (int s = 0; s < NA; ++s)
+        if (c * TK + 4 * ((tid + 256 * s) % 16) >= K) ra[p][s] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      if (TB) {
+#pragma unroll
+        for (int s = 0; s < NB; ++s)
+          if (c * TK + 4 * ((tid + 256 * s) % 16) >= K) rb[p][s] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+      // !TB: rows k >= K lie past the buffer end and read 0
+    }
+    float* As = lds[c & 1];
+    float* Bs = lds[c & 1] + RM * TLD;
+#pragma unroll
+    for (int s = 0; s < NA; ++s) {
+      const int f = tid + 256 * s;
+      *reinterpret_cast<f32x4*>(As + (f / 16) * TLD + 4 * (f % 16)) = ra[p][s];
+    }
+#pragma unroll
+    for (int s = 0; s < NB; ++s) {
+      const int f = tid + 256 * s;
+      // TB: [n][k] rows; !TB: [k][n] rows (the MFMA loop reads the fragment per k there)
+      *reinterpret_cast<f32x4*>(Bs + (f / 16) * TLD + 4 * (f % 16)) = rb[p][s];
+    }
+  };
+  f32x4 acc[RB];
+#pragma unroll
+  for (int i = 0; i < RB; ++i) acc[i] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  const int nch = NCH > 0 ? NCH : (K + TK - 1) / TK;
+  const int r = lane & 15, kk = lane >> 4;
+  auto mma = [&](int c) {
+#ifdef MH_TALL_EXP_NOMMA  // cost-attribution experiment only
+    if (g.K > 0) return;
+#endif
+    const float* As = lds[c & 1];
+    const float* Bs = lds[c & 1] + RM * TLD;
+#pragma unroll
+    for (int gq = 0; gq < TK / 16; ++gq) {
+      f32x4 bf;
+      if (TB) {
+        bf = *reinterpret_cast<const f32x4*>(Bs + (wave * 16 + r) * TLD + gq * 16 + 4 * kk);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[j] = Bs[(gq * 16 + 4 * kk + j) * TLD + wave * 16 + r];
+      }
+      f32x4 af[RB];
+#pragma unroll
+      for (int i = 0; i < RB; ++i) af[i] = *reinterpret_cast<const f32x4*>(As + (16 * i + r) * TLD + gq * 16 + 4 * kk);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < RB; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][j], bf[j], acc[i], 0, 0, 0);
+    }
+  };
+  // chunk c: loads of c + 2 issued, MFMAs on LDS buffer c & 1, chunk c + 1 staged into the other
+  // buffer (last read in chunk c - 1), one barrier
+  auto body = [&](int c, int p) {
+    if (c + 2 < nch) load(c + 2, p);
+    mma(c);
+    if (c + 1 < nch) stage(c + 1, p ^ 1);
+    __syncthreads();
+  };
+  load(0, 0);
+  if (nch > 1) load(1, 1);
+  stage(0, 0);
+  __syncthreads();
+  if constexpr (NCH > 0) {
+    // K known: straight-line code, so each stage waits only for its own chunk's loads
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) body(c, c & 1);
+  } else {
+    for (int c = 0; c < nch; c += 2) {
+      body(c, 0);
+      if (c + 1 < nch) body(c + 1, 1);
+    }
+  }
+  // C tile through LDS (both buffers are free after the last barrier) so that each quarter-wave
+  // stores 256 contiguous bytes of one row instead of 16 scattered columns of four rows
+  float* Cs = lds[0];
+#pragma unroll
+  for (int i = 0; i < RB; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Cs[(16 * i + 4 * kk + q) * TLD + wave * 16 + r] = acc[i][q];
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < RM * 16 / 256; ++s) {
+    const int f = tid + 256 * s, row = m0 + f / 16;
+    f32x4 v = *reinterpret_cast<const f32x4*>(Cs + (f / 16) * TLD + 4 * (f % 16));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = gemm_act(g.bias ? v[q] + bv[q] : v[q], g.act);
+#ifdef MH_TALL_EXP_NOSTORE  // cost-attribution experiment only
+    if (!(v[0] != v[0])) continue;
+#endif
+    if (row < M) *reinterpret_cast<f32x4*>(g.C + (int64_t)row * g.ldc + n0 + 4 * (f % 16)) = v;
+  }
+}
+
+// row blocks per workgroup for a tall product: fewest (rounds of 256 workgroups) x RB
+static int tall_rb(int64_t M, int64_t N) {
+#ifdef MH_TALL_RB
+  return MH_TALL_RB;
+#endif
+  const int64_t tn = N / 64;
+  int best = 0;
+  int64_t best_cost = INT64_MAX;
+  for (int rb = 1; rb <= 8; ++rb) {
+    const int64_t wgs = ((M + 16 * rb - 1) / (16 * rb)) * tn;
+    const int64_t cost = ((wgs + 255) / 256) * (rb + 1);  // + 1: per-workgroup fixed cost
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = rb;
+    }
+  }
+  return best;
+}
+
+static bool tall_ok(const float* A, const float* B, const float* bias, const float* C, int64_t M, int64_t N,
+                    int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int ta) {
+#ifdef MH_NO_TALL_GEMM
+  return false;
+#endif
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  return !ta && M >= 2048 && N % 64 == 0 && K % 4 == 0 && K > 0 && lda % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 &&
+         al16(A) && al16(B) && al16(C) && al16(bias) && M * lda * 4 < ((int64_t)1 << 30) &&
+         K * 4 < ((int64_t)1 << 28);
+}
+
+template <int RB>
+static hipError_t launch_tall(const GemmArgs& g, bool tb, hipStream_t st) {
+  const int tiles_n = (int)(g.N / 64);
+  const int64_t grid = ((g.M + 16 * RB - 1) / (16 * RB)) * tiles_n;
+  if (g.K == 256) {  // the hidden layers of every reference MLP: 4 chunks, unrolled
+    if (tb) k_gemm_tall<RB, true, 4><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
+    else k_gemm_tall<RB, false, 4><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
+  } else {
+    if (tb) k_gemm_tall<RB, true, 0><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
+    else k_gemm_tall<RB, false, 0><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
+  }
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------ launch plan
 struct GemmPlan {
   int wm, wn, S;
@@ -281,6 +497,19 @@ hipError_t launch_gemm(const float* A, const float* B, const float* bias, float*
   // 32-bit buffer offsets (load_chunk): both operands below 2 GiB
   if ((ta ? K : M) * lda * 4 >= ((int64_t)1 << 31) - 64 || (tb ? N : K) * ldb * 4 >= ((int64_t)1 << 31) - 64)
     return hipErrorInvalidValue;
+  if (tall_ok(A, B, bias, C, M, N, K, lda, ldb, ldc, ta) && (tb ? N : K) * ldb * 4 < ((int64_t)1 << 30)) {
+    GemmArgs g{A, B, bias, C, M, N, K, lda, ldb, ldc, act, 1, 0, nullptr};
+    switch (tall_rb(M, N)) {
+      case 1: return launch_tall<1>(g, tb, st);
+      case 2: return launch_tall<2>(g, tb, st);
+      case 3: return launch_tall<3>(g, tb, st);
+      case 4: return launch_tall<4>(g, tb, st);
+      case 5: return launch_tall<5>(g, tb, st);
+      case 6: return launch_tall<6>(g, tb, st);
+      case 7: return launch_tall<7>(g, tb, st);
+      default: return launch_tall<8>(g, tb, st);
+    }
+  }
   const GemmPlan p = gemm_plan(M, N, K > 0 ? K : 1);
   GemmArgs g{A, B, bias, C, M, N, K, lda, ldb, ldc, act, p.S, p.kc_per, workspace};
   const int64_t grid = p.tiles * p.S;

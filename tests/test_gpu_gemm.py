@@ -38,6 +38,8 @@ SHAPES = [  # (M, N, K)
     (5120, 256, 16), (5120, 256, 256), (5120, 1, 256), (5120, 8, 256), (256, 256, 256), (256, 256, 12),
     (256, 8, 256), (256, 256, 5120), (8, 256, 5120), (1, 256, 5120), (16, 256, 5120), (256, 16, 5120),
     (333, 77, 45), (1, 1, 1), (65, 33, 129), (7, 300, 1000),
+    # tall products (k_gemm_tall when op(A) is A: M >= 2,048, N % 64 == 0, K % 4 == 0)
+    (5120, 256, 12), (5120, 64, 4), (3001, 128, 20), (2048, 192, 36), (4100, 256, 256),
 ]
 
 
@@ -93,3 +95,19 @@ def test_gemm_workspace_query():
     assert wf.value > 0 and wf.value % (256 * 256) == 0
     assert N.lib().mh_gemm_workspace(5120, 256, 256, ctypes.byref(wf)) == 0
     assert wf.value == 0
+
+
+@pytest.mark.parametrize("tb", [0, 1])
+def test_tall_gemm_strided_operands(tb):
+    """Tall path with leading dimensions larger than the row (views into wider buffers)."""
+    g = torch.Generator(device="cuda").manual_seed(11 + tb)
+    M, N, K = 5120, 128, 64
+    abuf = torch.randn(M, K + 12, device="cuda", generator=g)
+    bbuf = torch.randn(*((N, K + 8) if tb else (K, N + 64)), device="cuda", generator=g)
+    a = abuf[:, :K]
+    b = bbuf[:, :K] if tb else bbuf[:, :N]
+    bias = torch.randn(N, device="cuda", generator=g)
+    c = gemm(abuf, bbuf, bias, M, N, K, abuf.shape[1], bbuf.shape[1], 0, tb, 1)
+    ref, mag = _ref(a.contiguous(), b.contiguous(), bias, 0, tb, 1)
+    err = (c.double() - ref).abs()
+    assert bool((err <= 2e-6 * (K ** 0.5) * mag + 1e-6).all()), f"max err {float(err.max()):.3e}"
