@@ -82,9 +82,12 @@ def _hip_dx(rows=0, in_features=0, out_features=0):
     return b == "hip" or (b == "auto" and _tall(rows, in_features, out_features))
 
 
-def _hip_dw(out_features):
+def _hip_dw(out_features, in_features=0, rows=0):
+    """Weight gradients: one-output layers, and g^T x of 64-multiple layers over >= 1,024 rows
+    (the deep-product kernel k_gemm_deep: 14.7 vs 18.6 us at 256 x 256 x 5,120)."""
     b = _GEMM_BACKEND["name"]
-    return b == "hip" or (b == "auto" and out_features == 1)
+    return b == "hip" or (b == "auto" and (out_features == 1 or (out_features % 64 == 0 and in_features % 64 == 0
+                                                                   and rows >= 1024)))
 
 
 def gemm_backend() -> str:
@@ -152,7 +155,7 @@ class LinearAct(torch.autograd.Function):
         if need_x:
             dx = gemm(g, weight.contiguous(), None, M, K, Nout, Nout, K, 0, 0) if _hip_dx(M, K, Nout) else g.mm(weight)
         if need_w:
-            dw = gemm(g, x, None, Nout, K, M, Nout, K, 1, 0) if _hip_dw(Nout) else g.t().mm(x)
+            dw = gemm(g, x, None, Nout, K, M, Nout, K, 1, 0) if _hip_dw(Nout, K, M) else g.t().mm(x)
         return dx, dw, db, None
 
 

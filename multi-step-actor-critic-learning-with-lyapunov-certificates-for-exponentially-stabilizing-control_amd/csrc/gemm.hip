@@ -217,8 +217,16 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs g) {
   const int64_t MN = g.M * g.N;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < MN; i += (int64_t)gridDim.x * 256) {
-    float v = g.partial[i];
-    for (int sp = 1; sp < g.S; ++sp) v += g.partial[(int64_t)sp * MN + i];
+    // eight partials in flight per batch (a load-add loop waits one round trip per split)
+    float v = 0.0f;
+    for (int s0 = 0; s0 < g.S; s0 += 8) {
+      float x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = s0 + u < g.S ? g.partial[(int64_t)(s0 + u) * MN + i] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (s0 + u < g.S) v = (s0 + u == 0) ? x[u] : v + x[u];
+    }
     const int64_t row = i / g.N, col = i - row * g.N;
     g.C[row * g.ldc + col] = gemm_act(g.bias ? v + g.bias[col] : v, g.act);
   }
@@ -396,6 +404,149 @@ __global__ __launch_bounds__(256) void k_gemm_tall(GemmArgs g, int tiles_n) {
   }
 }
 
+// ------------------------------------------------------------------ deep products
+// C[M][N] = A^T B with A [K][M], B [K][N] and K >> M, N: the weight gradients g^T x of the
+// update's layers (M = N = 256, K = B x n = 5,120). The BLAS kernel for this shape runs 18.6 us.
+// Here the K range splits S ways (S x (M/64)(N/64) ~ 256 workgroups: S = 16 at 256 x 256) and
+// each workgroup forms a 64 x 64 partial over its K slice:
+//   * 64-deep chunks of both operands staged through LDS as [k][64] rows (row-contiguous float4
+//     global loads: a quarter-wave reads 256 B of one k row), two chunks ahead in registers;
+//   * wave w owns the 32 x 32 quadrant (w & 1, w >> 1): 2 x 2 MFMAs per 4-deep k step, the
+//     fragments read from LDS per k row (row stride 80 floats: the four k rows of one read land
+//     in distinct banks);
+//   * partials go to [S][M][N] and k_gemm_reduce adds them in split order (deterministic).
+// M % 64 == 0, N % 64 == 0, 16-B aligned rows, no bias / activation (a weight gradient).
+constexpr int DLD = 80;
+
+template <int NCH>
+__global__ __launch_bounds__(256) void k_gemm_deep(GemmArgs g, int tiles_m) {
+  constexpr int NF = 64 * TK / 4 / 256;  // float4 loads per operand per thread per chunk (4)
+  __shared__ float lds[2][2 * TK * DLD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles = tiles_m * (int)(g.N / 64);
+  const int bid = (int)blockIdx.x;
+  const int tile = bid % tiles, split = bid / tiles;
+  const int m0 = (tile % tiles_m) * 64, n0 = (tile / tiles_m) * 64;
+  const int K = (int)g.K, lda = (int)g.lda, ldb = (int)g.ldb;
+  const int c0 = split * (int)g.kc_per;
+  const int nchunks = (K + TK - 1) / TK;
+  const int nch = NCH > 0 ? NCH : (c0 + (int)g.kc_per < nchunks ? (int)g.kc_per : nchunks - c0);
+  const __amdgpu_buffer_rsrc_t ra_rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.A), (short)0, (int)(g.K * g.lda * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb_rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.B), (short)0, (int)(g.K * g.ldb * 4), 0x00020000);
+  // slot f = tid + 256 s of a chunk -> (k row f / 16, cols 4 (f % 16)..); k rows past K lie
+  // beyond the buffers (read 0)
+  int aoff[NF], boff[NF];
+#pragma unroll
+  for (int s = 0; s < NF; ++s) {
+    const int f = tid + 256 * s;
+    aoff[s] = (f / 16) * lda * 4 + (m0 + 4 * (f % 16)) * 4;
+    boff[s] = (f / 16) * ldb * 4 + (n0 + 4 * (f % 16)) * 4;
+  }
+  f32x4 ra[2][NF], rb[2][NF];
+  auto load = [&](int c, int p) {
+    const int kb = (c0 + c) * TK;
+#pragma unroll
+    for (int s = 0; s < NF; ++s) {
+      ra[p][s] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra_rs, aoff[s] + kb * lda * 4, 0, 0));
+      rb[p][s] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb_rs, boff[s] + kb * ldb * 4, 0, 0));
+    }
+  };
+  auto stage = [&](int c, int p) {
+    float* As = lds[c & 1];
+    float* Bs = lds[c & 1] + TK * DLD;
+#pragma unroll
+    for (int s = 0; s < NF; ++s) {
+      const int f = tid + 256 * s;
+      *reinterpret_cast<f32x4*>(As + (f / 16) * DLD + 4 * (f % 16)) = ra[p][s];
+      *reinterpret_cast<f32x4*>(Bs + (f / 16) * DLD + 4 * (f % 16)) = rb[p][s];
+    }
+  };
+  const int r = lane & 15, kk = lane >> 4, wm = wave & 1, wn = wave >> 1;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  auto mma = [&](int c) {
+    const float* As = lds[c & 1];
+    const float* Bs = lds[c & 1] + TK * DLD;
+#pragma unroll
+    for (int t = 0; t < TK / 4; ++t) {
+      const int kr = (4 * t + kk) * DLD;
+      const float a0 = As[kr + 32 * wm + r], a1 = As[kr + 32 * wm + 16 + r];
+      const float b0 = Bs[kr + 32 * wn + r], b1 = Bs[kr + 32 * wn + 16 + r];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+  };
+  auto body = [&](int c, int p) {
+    if (c + 2 < nch) load(c + 2, p);
+    mma(c);
+    if (c + 1 < nch) stage(c + 1, p ^ 1);
+    __syncthreads();
+  };
+  if (nch > 0) {
+    load(0, 0);
+    if (nch > 1) load(1, 1);
+    stage(0, 0);
+    __syncthreads();
+    if constexpr (NCH > 0) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) body(c, c & 1);
+    } else {
+      for (int c = 0; c < nch; c += 2) {
+        body(c, 0);
+        if (c + 1 < nch) body(c + 1, 1);
+      }
+    }
+  }
+  // the 64 x 64 result through LDS (free after the last barrier): each quarter-wave then stores
+  // 256 contiguous bytes of one row
+  float* out = g.S > 1 ? g.partial + (int64_t)split * g.M * g.N : g.C;
+  const int64_t ld = g.S > 1 ? g.N : g.ldc;
+  float* Cs = lds[0];
+  if (nch == 0) __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Cs[(32 * wm + 16 * i + 4 * kk + q) * DLD + 32 * wn + 16 * j + r] = acc[i][j][q];
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int f = tid + 256 * s;
+    *reinterpret_cast<f32x4*>(out + (int64_t)(m0 + f / 16) * ld + n0 + 4 * (f % 16)) =
+        *reinterpret_cast<const f32x4*>(Cs + (f / 16) * DLD + 4 * (f % 16));
+  }
+}
+
+static bool deep_ok(const float* A, const float* B, const float* bias, int64_t M, int64_t N, int64_t K, int64_t lda,
+                    int64_t ldb, int ta, int tb, int act) {
+#ifdef MH_NO_DEEP_GEMM
+  return false;
+#endif
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  return ta && !tb && !bias && act == 0 && M % 64 == 0 && N % 64 == 0 && K >= 1024 && lda % 4 == 0 &&
+         ldb % 4 == 0 && al16(A) && al16(B) && (K + TK) * lda * 4 < ((int64_t)1 << 30) &&
+         (K + TK) * ldb * 4 < ((int64_t)1 << 30);
+}
+
+// K splits: about 256 workgroups, slices of >= 2 chunks
+static int deep_splits(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = (M / 64) * (N / 64);
+  const int64_t chunks = (K + TK - 1) / TK;
+  int64_t S = (256 + tiles - 1) / tiles;
+  if (S > chunks / 2) S = chunks / 2;
+  if (S < 1) S = 1;
+  const int64_t per = (chunks + S - 1) / S;
+  return (int)((chunks + per - 1) / per);
+}
+
 // row blocks per workgroup for a tall product: fewest (rounds of 256 workgroups) x RB
 static int tall_rb(int64_t M, int64_t N) {
 #ifdef MH_TALL_RB
@@ -478,7 +629,12 @@ static GemmPlan gemm_plan(int64_t M, int64_t N, int64_t K) {
 
 int64_t gemm_workspace_floats(int64_t M, int64_t N, int64_t K) {
   const GemmPlan p = gemm_plan(M, N, K);
-  return p.S > 1 ? (int64_t)p.S * M * N : 0;
+  int64_t S = p.S;
+  if (M % 64 == 0 && N % 64 == 0 && K >= 1024) {  // the deep-product path may take this shape
+    const int64_t sd = deep_splits(M, N, K);
+    S = sd > S ? sd : S;
+  }
+  return S > 1 ? S * M * N : 0;
 }
 
 template <int WM, int WN>
@@ -497,6 +653,23 @@ hipError_t launch_gemm(const float* A, const float* B, const float* bias, float*
   // 32-bit buffer offsets (load_chunk): both operands below 2 GiB
   if ((ta ? K : M) * lda * 4 >= ((int64_t)1 << 31) - 64 || (tb ? N : K) * ldb * 4 >= ((int64_t)1 << 31) - 64)
     return hipErrorInvalidValue;
+  if (deep_ok(A, B, bias, M, N, K, lda, ldb, ta, tb, act) && ((uintptr_t)C & 15) == 0 && ldc % 4 == 0 &&
+      (deep_splits(M, N, K) == 1 || (workspace && ((uintptr_t)workspace & 15) == 0))) {
+    const int S = deep_splits(M, N, K);
+    const int64_t chunks = (K + TK - 1) / TK;
+    const int64_t per = (chunks + S - 1) / S;
+    GemmArgs g{A, B, nullptr, C, M, N, K, lda, ldb, ldc, 0, S, per, workspace};
+    const int tiles_m = (int)(M / 64);
+    const unsigned grid = (unsigned)(tiles_m * (N / 64) * S);
+    // every split full (the common case: 5,120 = 16 x 5 chunks) -> unrolled 5-chunk body
+    if (per == 5 && chunks == per * S) k_gemm_deep<5><<<grid, 256, 0, st>>>(g, tiles_m);
+    else k_gemm_deep<0><<<grid, 256, 0, st>>>(g, tiles_m);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || S == 1) return e;
+    const int64_t want = (M * N + 255) / 256;
+    k_gemm_reduce<<<(unsigned)(want < 2048 ? want : 2048), 256, 0, st>>>(g);
+    return hipGetLastError();
+  }
   if (tall_ok(A, B, bias, C, M, N, K, lda, ldb, ldc, ta) && (tb ? N : K) * ldb * 4 < ((int64_t)1 << 30)) {
     GemmArgs g{A, B, bias, C, M, N, K, lda, ldb, ldc, act, 1, 0, nullptr};
     switch (tall_rb(M, N)) {

@@ -111,3 +111,18 @@ def test_tall_gemm_strided_operands(tb):
     ref, mag = _ref(a.contiguous(), b.contiguous(), bias, 0, tb, 1)
     err = (c.double() - ref).abs()
     assert bool((err <= 2e-6 * (K ** 0.5) * mag + 1e-6).all()), f"max err {float(err.max()):.3e}"
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 5120), (256, 256, 10240), (64, 128, 1000), (128, 64, 3000),
+                                   (256, 192, 1088)])
+def test_deep_gemm_weight_gradient(M, N, K):
+    """k_gemm_deep (A^T B, K >> M, N: the weight gradients): K split over workgroups, partials
+    added in split order; ragged K (k rows past K read 0) and a strided B."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    a = torch.randn(K, M, device="cuda", generator=g)
+    bbuf = torch.randn(K, N + 8, device="cuda", generator=g)
+    c = gemm(a, bbuf, None, M, N, K, M, N + 8, 1, 0)
+    ref, mag = _ref(a, bbuf[:, :N].contiguous(), None, 1, 0, 0)
+    err = (c.double() - ref).abs()
+    assert bool((err <= 2e-6 * (K ** 0.5) * mag + 1e-6).all()), f"max err {float(err.max()):.3e}"
+    assert torch.equal(c, gemm(a, bbuf, None, M, N, K, M, N + 8, 1, 0))
