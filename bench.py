@@ -218,7 +218,7 @@ def main():
     # HBM bytes per launch from the committed rocprofv3 PMC passes of this same command
     # (tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)
     import glob
-    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic*.json")))
     if pmcs and a.env == "QuadTracking" and a.envs == 65536:
         try:
             traffic = json.load(open(pmcs[-1])).get(dom, {}).get("bytes_per_launch")
