@@ -242,6 +242,19 @@ int mh_gemm_f32(const float* A, const float* B, const float* bias, float* C, int
                 int64_t lda, int64_t ldb, int64_t ldc, int32_t trans_a, int32_t trans_b, int32_t act,
                 float* workspace, void* stream);
 
+/* One nn.Linear + activation layer's backward (autograd of RL/apprfunc/mlp.py:18-30 layers) for
+ * y = act(x W^T + b), W [n_out][n_in], over `rows` rows, with g = dy * act'(y) formed inside the
+ * GEMMs (never written to memory):
+ *   dx [rows][n_in] = g W;  dw [n_out][n_in] = g^T x;  db [n_out] = column sums of g
+ * Each output may be NULL when not wanted (db needs dw). mh_linear_backward_plan says whether a
+ * request is supported (tall dx: rows >= 2048, n_in % 64 == 0, n_out % 4 == 0, n_out >= 64; dw/db:
+ * n_out and n_in multiples of 64, rows >= 1024) and the workspace floats it needs; matrices
+ * contiguous and 16-byte aligned. Otherwise use mh_act_grad_colsum + mh_gemm_f32. */
+int mh_linear_backward_plan(int64_t rows, int64_t n_out, int64_t n_in, int32_t need_dx, int32_t need_dw,
+                            int32_t need_db, int32_t* supported, int64_t* workspace_floats);
+int mh_linear_backward(const float* dy, const float* y, int32_t act, const float* x, const float* W, int64_t rows,
+                       int64_t n_out, int64_t n_in, float* dx, float* dw, float* db, float* workspace, void* stream);
+
 /* StochaPolicy's head (RL/apprfunc/mlp.py:132-136) on [rows][2 act_dim] rows:
  *   out = [mean | exp(clamp(log_std, min_log_std, max_log_std))] of raw = [mean | log_std]
  * and its backward d_raw = [d_mean | d_std * std * (min <= log_std <= max)], one launch each

@@ -85,6 +85,9 @@ _PROTOS = {
     "mh_policy_forward": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "mh_act_grad_chunks": (ctypes.c_int, [c_i64, ctypes.POINTER(c_i32)]),
     "mh_act_grad_colsum": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mh_linear_backward_plan": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp]),
+    "mh_linear_backward": (ctypes.c_int, [c_vp, c_vp, c_i32, c_vp, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp,
+                                          c_vp]),
     "mh_msacl_policy_loss": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_vp, c_vp, c_vp]),
     "mh_msacl_policy_loss_backward": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_vp, c_vp, c_vp, c_vp]),
     "mh_msacl_ratio0": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),

@@ -5,10 +5,13 @@ parameters and state_dict keys); on HIP tensors their forward runs each (Linear,
 pair as one autograd Function:
   forward   y = act(x W^T + b): one mh_gemm_f32 launch (csrc/gemm.hip, f32 MFMA) with the bias
             and ReLU / tanh in its epilogue
-  backward  g = dy * act'(y) and the bias gradient (column sums of g) in one pass of
-            mh_act_grad_colsum (csrc/mlp_grad.hip) instead of an elementwise backward kernel
-            plus a reduction; then dx = g W and dW = g^T x as two mh_gemm_f32 launches, each only
-            when autograd needs it (frozen critics in the policy update skip dW / db).
+  backward  optionally (MSACL_FUSED_BACKWARD=1) for the B x n-row 256-wide layers,
+            mh_linear_backward (csrc/gemm.hip): dx = g W and dW = g^T x, db = column sums of g,
+            with g = dy * act'(y) formed inside the two GEMMs' operand staging (never written);
+            by default g and the bias gradient in one pass
+            of mh_act_grad_colsum (csrc/mlp_grad.hip) instead of an elementwise backward kernel
+            plus a reduction, then dx = g W and dW = g^T x as two mh_gemm_f32 launches. Each
+            output only when autograd needs it (frozen critics in the policy update skip dW / db).
 Same math as the module's own forward/backward, f32 throughout; the GEMM summation order is the
 kernel's. Backend (`set_gemm_backend`, config key `update_gemm`):
   "auto" (default)  mh_gemm_f32 where it measured faster than the BLAS library on the update's
@@ -26,6 +29,7 @@ CPU tensors (and activations other than identity/ReLU/tanh) take the plain nn.Se
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -111,6 +115,48 @@ def gemm(a, b, bias, M, N, K, lda, ldb, ta, tb, act=0):
     return c
 
 
+_LB_PLAN = {}
+# Off by default: measured neutral in the MSACL update (A/B on one box, update 1.08-1.12 ms
+# either way: the colsum launch it removes overlaps the other stream's work, while the fused
+# GEMMs carry the act' loads); MSACL_FUSED_BACKWARD=1 turns it on.
+_FUSED_BACKWARD = {"on": os.environ.get("MSACL_FUSED_BACKWARD", "0") == "1"}
+
+
+def _linear_backward_fused(dy, y, act, x, weight, need_x, need_w, need_b):
+    """The whole layer backward as mh_linear_backward (csrc/gemm.hip: g = dy * act'(y) formed
+    inside the tall dx and deep dW GEMMs, the bias gradient inside the latter) when the shape and
+    request qualify; None otherwise (the colsum + GEMM path)."""
+    if _GEMM_BACKEND["name"] == "blas" or not (need_x or need_w):
+        return None
+    rows, n_out = dy.shape
+    n_in = x.shape[1]
+    key = (rows, n_out, n_in, bool(need_x), bool(need_w), bool(need_b))
+    plan = _LB_PLAN.get(key)
+    if plan is None:
+        N = _native()
+        ok, ws = ctypes.c_int32(), ctypes.c_int64()
+        N.check(N.lib().mh_linear_backward_plan(rows, n_out, n_in, int(need_x), int(need_w), int(need_b),
+                                                ctypes.byref(ok), ctypes.byref(ws)), "mh_linear_backward_plan")
+        plan = _LB_PLAN[key] = (bool(ok.value), ws.value)
+    if not plan[0]:
+        return None
+    w = weight.contiguous()
+    xc = x.contiguous()
+    yc = y.contiguous()
+    if any(t.data_ptr() % 16 for t in (dy, yc, xc, w)):
+        return None
+    N = _native()
+    dev = dy.device
+    dx = torch.empty(rows, n_in, dtype=dy.dtype, device=dev) if need_x else None
+    dw = torch.empty(n_out, n_in, dtype=dy.dtype, device=dev) if need_w else None
+    db = torch.empty(n_out, dtype=dy.dtype, device=dev) if need_b else None
+    work = torch.empty(plan[1], dtype=torch.float32, device=dev) if plan[1] else None
+    N.check(N.lib().mh_linear_backward(N.ptr(dy), N.ptr(yc) if act else None, act, N.ptr(xc), N.ptr(w), rows, n_out,
+                                       n_in, N.ptr(dx), N.ptr(dw), N.ptr(db), N.ptr(work), N.stream_of(dev)),
+            "mh_linear_backward")
+    return dx, dw, db, None
+
+
 class LinearAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, act):
@@ -134,6 +180,10 @@ class LinearAct(torch.autograd.Function):
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
         act = ctx.act
         dy = dy.contiguous()
+        if _FUSED_BACKWARD["on"]:
+            fused = _linear_backward_fused(dy, y, act, x, weight, need_x, need_w, need_b)
+            if fused is not None:
+                return fused
         db = None
         if act == 0 and not need_b:
             g = dy

@@ -538,6 +538,33 @@ int mh_gemm_f32(const float* A, const float* B, const float* bias, float* C, int
   return MH_OK;
 }
 
+int mh_linear_backward_plan(int64_t rows, int64_t n_out, int64_t n_in, int32_t need_dx, int32_t need_dw,
+                            int32_t need_db, int32_t* supported, int64_t* workspace_floats) {
+  if (!supported || !workspace_floats) return fail(MH_EINVAL, "mh_linear_backward_plan: null out");
+  if (rows < 0 || n_out <= 0 || n_in <= 0) return fail(MH_EINVAL, "mh_linear_backward_plan: bad shape");
+  int64_t ws = 0;
+  *supported = mh::linear_backward_plan(rows, n_out, n_in, need_dx != 0, need_dw != 0, need_db != 0, &ws) ? 1 : 0;
+  *workspace_floats = ws;
+  return MH_OK;
+}
+
+int mh_linear_backward(const float* dy, const float* y, int32_t act, const float* x, const float* W, int64_t rows,
+                       int64_t n_out, int64_t n_in, float* dx, float* dw, float* db, float* workspace, void* stream) {
+  if (act < 0 || act > 2) return fail(MH_EINVAL, "mh_linear_backward: act must be 0, 1 or 2");
+  int64_t ws = 0;
+  if (rows < 0 || n_out <= 0 || n_in <= 0 ||
+      !mh::linear_backward_plan(rows, n_out, n_in, dx != nullptr, dw != nullptr, db != nullptr, &ws))
+    return fail(MH_EINVAL, "mh_linear_backward: shape or request not supported (see mh_linear_backward_plan)");
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!dy || (act != 0 && !y) || (dx && !W) || (dw && !x) || (ws > 0 && !workspace))
+    return fail(MH_EINVAL, "mh_linear_backward: null pointer");
+  if (!al16(dy) || !al16(y) || !al16(x) || !al16(W) || !al16(dx) || !al16(dw) || !al16(workspace))
+    return fail(MH_EINVAL, "mh_linear_backward: every matrix must be 16-byte aligned");
+  MH_HIP(mh::launch_linear_backward(dy, act != 0 ? y : nullptr, act, x, W, rows, n_out, n_in, dx, dw, db, workspace,
+                                    (hipStream_t)stream));
+  return MH_OK;
+}
+
 int mh_stocha_head(const float* raw, int64_t rows, int32_t act_dim, float min_log_std, float max_log_std, float* out,
                    void* stream) {
   if (rows < 0 || act_dim <= 0) return fail(MH_EINVAL, "mh_stocha_head: bad shape");

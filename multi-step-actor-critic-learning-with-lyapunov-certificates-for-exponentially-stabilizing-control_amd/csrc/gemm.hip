@@ -40,7 +40,22 @@ struct GemmArgs {
   int S;             // K splits across workgroups
   int64_t kc_per;    // KC-deep chunks per split
   float* partial;    // [S][M][N] when S > 1
+  // fused layer backward (launch_linear_backward): op(A) = act'(Y) * A elementwise (A = dy,
+  // Y = the layer output, same leading dimension), and in the deep kernel the column sums of
+  // that op(A) over K (the bias gradient): into db directly, or per split into dbp [S][M]
+  const float* Y;
+  int act_a;         // -1: A as is; 0 identity, 1 ReLU, 2 tanh
+  float* db;
+  float* dbp;        // [dbn][M] partial column sums (split-major, then column tile), or null
+  int dbn;
 };
+
+// g = dy * act'(y) exactly as k_act_grad_colsum forms it (mlp_grad.hip)
+__device__ __forceinline__ float act_grad(float d, float t, int act) {
+  if (act == 1) return t > 0.0f ? d : 0.0f;
+  if (act == 2) return d * (1.0f - t * t);
+  return d;
+}
 
 constexpr int KC = 32;  // K depth of one LDS stage
 
@@ -213,9 +228,17 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   }
 }
 
-// C = act(sum_s partial[s] + bias), splits added in order
+// C = act(sum_s partial[s] + bias), splits added in order (and db = sum_s dbp[s] when set)
 __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs g) {
   const int64_t MN = g.M * g.N;
+  if (g.dbp) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < g.M; i += (int64_t)gridDim.x * 256) {
+      float v = g.dbp[i];
+      for (int sp = 1; sp < g.dbn; ++sp) v = v + g.dbp[(int64_t)sp * g.M + i];
+      g.db[i] = v;
+    }
+  }
+  if (g.S <= 1) return;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < MN; i += (int64_t)gridDim.x * 256) {
     // eight partials in flight per batch (a load-add loop waits one round trip per split)
     float v = 0.0f;
@@ -256,7 +279,7 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs g) {
 constexpr int TK = 64;       // k depth of one LDS stage
 constexpr int TLD = TK + 4;  // LDS row stride (floats): 16 rows of a b128 read hit distinct banks
 
-template <int RB, bool TB, int NCH>
+template <int RB, bool TB, int NCH, bool AG>
 __global__ __launch_bounds__(256) void k_gemm_tall(GemmArgs g, int tiles_n) {
   constexpr int RM = 16 * RB;
   constexpr int NA = RM * TK / 4 / 256;  // float4 loads of A per thread per chunk
@@ -294,6 +317,9 @@ __global__ __launch_bounds__(256) void k_gemm_tall(GemmArgs g, int tiles_n) {
   // the bias of those columns (the same for every s) is fetched now, used after the last chunk
   const f32x4 bv = g.bias ? *reinterpret_cast<const f32x4*>(g.bias + n0 + 4 * (tid % 16)) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   f32x4 ra[2][NA], rb[2][NB];  // two chunks in flight ahead of the LDS stage
+  f32x4 ry[AG ? 2 : 1][AG ? NA : 1];
+  const __amdgpu_buffer_rsrc_t ry_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(AG && g.Y ? g.Y : g.A), (short)0, (int)(g.M * g.lda * 4), 0x00020000);
   auto load = [&](int c, int p) {
 #ifdef MH_TALL_EXP_NOLOAD  // cost-attribution experiment only
     if (g.K > 0) return;
@@ -301,6 +327,13 @@ __global__ __launch_bounds__(256) void k_gemm_tall(GemmArgs g, int tiles_n) {
 #pragma unroll
     for (int s = 0; s < NA; ++s)
       ra[p][s] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra_rs, aoff[s] + c * TK * 4, 0, 0));
+    if constexpr (AG) {
+      if (g.act_a > 0) {
+#pragma unroll
+        for (int s = 0; s < NA; ++s)
+          ry[p][s] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry_rs, aoff[s] + c * TK * 4, 0, 0));
+      }
+    }
 #pragma unroll
     for (int s = 0; s < NB; ++s)
       rb[p][s] = __builtin_bit_cast(
@@ -320,6 +353,14 @@ __global__ __launch_bounds__(256) void k_gemm_tall(GemmArgs g, int tiles_n) {
     }
     float* As = lds[c & 1];
     float* Bs = lds[c & 1] + RM * TLD;
+    if constexpr (AG) {
+      if (g.act_a > 0) {
+#pragma unroll
+        for (int s = 0; s < NA; ++s)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ra[p][s][q] = act_grad(ra[p][s][q], ry[p][s][q], g.act_a);
+      }
+    }
 #pragma unroll
     for (int s = 0; s < NA; ++s) {
       const int f = tid + 256 * s;
@@ -418,7 +459,7 @@ __global__ __launch_bounds__(256) void k_gemm_tall(GemmArgs g, int tiles_n) {
 // M % 64 == 0, N % 64 == 0, 16-B aligned rows, no bias / activation (a weight gradient).
 constexpr int DLD = 80;
 
-template <int NCH>
+template <int NCH, bool AG>
 __global__ __launch_bounds__(256) void k_gemm_deep(GemmArgs g, int tiles_m) {
   constexpr int NF = 64 * TK / 4 / 256;  // float4 loads per operand per thread per chunk (4)
   __shared__ float lds[2][2 * TK * DLD];
@@ -445,6 +486,9 @@ __global__ __launch_bounds__(256) void k_gemm_deep(GemmArgs g, int tiles_m) {
     boff[s] = (f / 16) * ldb * 4 + (n0 + 4 * (f % 16)) * 4;
   }
   f32x4 ra[2][NF], rb[2][NF];
+  f32x4 ry[AG ? 2 : 1][AG ? NF : 1];
+  const __amdgpu_buffer_rsrc_t ry_rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(AG && g.Y ? g.Y : g.A), (short)0, (int)(g.K * g.lda * 4), 0x00020000);
   auto load = [&](int c, int p) {
     const int kb = (c0 + c) * TK;
 #pragma unroll
@@ -452,10 +496,25 @@ __global__ __launch_bounds__(256) void k_gemm_deep(GemmArgs g, int tiles_m) {
       ra[p][s] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra_rs, aoff[s] + kb * lda * 4, 0, 0));
       rb[p][s] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb_rs, boff[s] + kb * ldb * 4, 0, 0));
     }
+    if constexpr (AG) {
+      if (g.act_a > 0) {
+#pragma unroll
+        for (int s = 0; s < NF; ++s)
+          ry[p][s] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ry_rs, aoff[s] + kb * lda * 4, 0, 0));
+      }
+    }
   };
   auto stage = [&](int c, int p) {
     float* As = lds[c & 1];
     float* Bs = lds[c & 1] + TK * DLD;
+    if constexpr (AG) {
+      if (g.act_a > 0) {
+#pragma unroll
+        for (int s = 0; s < NF; ++s)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) ra[p][s][q] = act_grad(ra[p][s][q], ry[p][s][q], g.act_a);
+      }
+    }
 #pragma unroll
     for (int s = 0; s < NF; ++s) {
       const int f = tid + 256 * s;
@@ -469,9 +528,19 @@ __global__ __launch_bounds__(256) void k_gemm_deep(GemmArgs g, int tiles_m) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  // bias gradient (AG with db): every workgroup of an (m tile, split) pair holds the same A
+  // chunk, so the ntn column tiles share its column sums: tile tn sums the k rows
+  // tn, tn + ntn, ... (thread: column tid & 63, every fourth of those rows from tid >> 6), in
+  // order, in a register
+  const int ntn = (int)(g.N / 64), tn = tile / tiles_m;
+  const bool colsum = AG && g.dbp;
+  float cs = 0.0f;
   auto mma = [&](int c) {
     const float* As = lds[c & 1];
     const float* Bs = lds[c & 1] + TK * DLD;
+    if (colsum) {
+      for (int kr = tn + ntn * (tid >> 6); kr < TK; kr += 4 * ntn) cs = cs + As[kr * DLD + (tid & 63)];
+    }
 #pragma unroll
     for (int t = 0; t < TK / 4; ++t) {
       const int kr = (4 * t + kk) * DLD;
@@ -516,7 +585,12 @@ __global__ __launch_bounds__(256) void k_gemm_deep(GemmArgs g, int tiles_m) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int q = 0; q < 4; ++q) Cs[(32 * wm + 16 * i + 4 * kk + q) * DLD + 32 * wn + 16 * j + r] = acc[i][j][q];
+  if (colsum) lds[1][tid] = cs;
   __syncthreads();
+  if (colsum && tid < 64) {  // the four row groups of this workgroup's share, in order
+    const float v = ((lds[1][tid] + lds[1][64 + tid]) + lds[1][128 + tid]) + lds[1][192 + tid];
+    g.dbp[((int64_t)split * ntn + tn) * g.M + m0 + tid] = v;
+  }
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int f = tid + 256 * s;
@@ -581,12 +655,16 @@ template <int RB>
 static hipError_t launch_tall(const GemmArgs& g, bool tb, hipStream_t st) {
   const int tiles_n = (int)(g.N / 64);
   const int64_t grid = ((g.M + 16 * RB - 1) / (16 * RB)) * tiles_n;
-  if (g.K == 256) {  // the hidden layers of every reference MLP: 4 chunks, unrolled
-    if (tb) k_gemm_tall<RB, true, 4><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
-    else k_gemm_tall<RB, false, 4><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
+  if (g.act_a >= 0) {  // fused layer backward: dx = (dy * act'(y)) W
+    if (tb) return hipErrorInvalidValue;
+    if (g.K == 256) k_gemm_tall<RB, false, 4, true><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
+    else k_gemm_tall<RB, false, 0, true><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
+  } else if (g.K == 256) {  // the hidden layers of every reference MLP: 4 chunks, unrolled
+    if (tb) k_gemm_tall<RB, true, 4, false><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
+    else k_gemm_tall<RB, false, 4, false><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
   } else {
-    if (tb) k_gemm_tall<RB, true, 0><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
-    else k_gemm_tall<RB, false, 0><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
+    if (tb) k_gemm_tall<RB, true, 0, false><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
+    else k_gemm_tall<RB, false, 0, false><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
   }
   return hipGetLastError();
 }
@@ -658,12 +736,12 @@ hipError_t launch_gemm(const float* A, const float* B, const float* bias, float*
     const int S = deep_splits(M, N, K);
     const int64_t chunks = (K + TK - 1) / TK;
     const int64_t per = (chunks + S - 1) / S;
-    GemmArgs g{A, B, nullptr, C, M, N, K, lda, ldb, ldc, 0, S, per, workspace};
+    GemmArgs g{A, B, nullptr, C, M, N, K, lda, ldb, ldc, 0, S, per, workspace, nullptr, -1, nullptr, nullptr};
     const int tiles_m = (int)(M / 64);
     const unsigned grid = (unsigned)(tiles_m * (N / 64) * S);
     // every split full (the common case: 5,120 = 16 x 5 chunks) -> unrolled 5-chunk body
-    if (per == 5 && chunks == per * S) k_gemm_deep<5><<<grid, 256, 0, st>>>(g, tiles_m);
-    else k_gemm_deep<0><<<grid, 256, 0, st>>>(g, tiles_m);
+    if (per == 5 && chunks == per * S) k_gemm_deep<5, false><<<grid, 256, 0, st>>>(g, tiles_m);
+    else k_gemm_deep<0, false><<<grid, 256, 0, st>>>(g, tiles_m);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || S == 1) return e;
     const int64_t want = (M * N + 255) / 256;
@@ -671,7 +749,7 @@ hipError_t launch_gemm(const float* A, const float* B, const float* bias, float*
     return hipGetLastError();
   }
   if (tall_ok(A, B, bias, C, M, N, K, lda, ldb, ldc, ta) && (tb ? N : K) * ldb * 4 < ((int64_t)1 << 30)) {
-    GemmArgs g{A, B, bias, C, M, N, K, lda, ldb, ldc, act, 1, 0, nullptr};
+    GemmArgs g{A, B, bias, C, M, N, K, lda, ldb, ldc, act, 1, 0, nullptr, nullptr, -1, nullptr, nullptr};
     switch (tall_rb(M, N)) {
       case 1: return launch_tall<1>(g, tb, st);
       case 2: return launch_tall<2>(g, tb, st);
@@ -684,7 +762,7 @@ hipError_t launch_gemm(const float* A, const float* B, const float* bias, float*
     }
   }
   const GemmPlan p = gemm_plan(M, N, K > 0 ? K : 1);
-  GemmArgs g{A, B, bias, C, M, N, K, lda, ldb, ldc, act, p.S, p.kc_per, workspace};
+  GemmArgs g{A, B, bias, C, M, N, K, lda, ldb, ldc, act, p.S, p.kc_per, workspace, nullptr, -1, nullptr, nullptr};
   const int64_t grid = p.tiles * p.S;
   hipError_t e;
   if (p.wm == 2 && p.wn == 2) e = launch_gemm_cfg<2, 2>(g, grid, ta, tb, st);
@@ -695,6 +773,70 @@ hipError_t launch_gemm(const float* A, const float* B, const float* bias, float*
   const int64_t want = (M * N + 255) / 256;
   k_gemm_reduce<<<(unsigned)(want < 2048 ? want : 2048), 256, 0, st>>>(g);
   return hipGetLastError();
+}
+
+// ------------------------------------------------------------------ fused layer backward
+// For y = act(x W^T + b) over `rows` rows (W [n_out][n_in]): dx = g W, dW = g^T x, db = sum_rows g
+// with g = dy * act'(y) formed on the fly inside the two GEMMs' A-operand staging (the tall
+// kernel for dx, the deep kernel for dW and db), instead of k_act_grad_colsum writing g and the
+// bias gradient first: one launch fewer and g never written to or re-read from HBM.
+static bool lb_dx_ok(int64_t rows, int64_t n_out, int64_t n_in) {
+  return rows >= 2048 && n_in % 64 == 0 && n_out % 4 == 0 && n_out >= 64 && rows * n_out * 4 < ((int64_t)1 << 30) &&
+         n_out * n_in * 4 < ((int64_t)1 << 30) && n_out * 4 < ((int64_t)1 << 28);
+}
+static bool lb_dw_ok(int64_t rows, int64_t n_out, int64_t n_in) {
+  return n_out % 64 == 0 && n_in % 64 == 0 && rows >= 1024 && (rows + TK) * n_out * 4 < ((int64_t)1 << 30) &&
+         (rows + TK) * n_in * 4 < ((int64_t)1 << 30);
+}
+
+bool linear_backward_plan(int64_t rows, int64_t n_out, int64_t n_in, bool dx, bool dw, bool db, int64_t* ws) {
+  *ws = 0;
+  if ((!dx && !dw) || (db && !dw)) return false;
+  if (dx && !lb_dx_ok(rows, n_out, n_in)) return false;
+  if (dw && !lb_dw_ok(rows, n_out, n_in)) return false;
+  if (dw) {
+    const int S = deep_splits(n_out, n_in, rows);
+    *ws = (S > 1 ? (int64_t)S * n_out * n_in : 0) + (db ? (int64_t)S * (n_in / 64) * n_out : 0);
+  }
+  return true;
+}
+
+hipError_t launch_linear_backward(const float* dy, const float* y, int act, const float* x, const float* W,
+                                  int64_t rows, int64_t n_out, int64_t n_in, float* dx, float* dw, float* db,
+                                  float* workspace, hipStream_t st) {
+  if (dx) {  // dx[rows][n_in] = g[rows][n_out] . W[n_out][n_in]
+    GemmArgs g{dy, W, nullptr, dx, rows, n_in, n_out, n_out, n_in, n_in, 0, 1, 0, nullptr, y, act, nullptr, nullptr};
+    hipError_t e;
+    switch (tall_rb(rows, n_in)) {
+      case 1: e = launch_tall<1>(g, false, st); break;
+      case 2: e = launch_tall<2>(g, false, st); break;
+      case 3: e = launch_tall<3>(g, false, st); break;
+      case 4: e = launch_tall<4>(g, false, st); break;
+      case 5: e = launch_tall<5>(g, false, st); break;
+      case 6: e = launch_tall<6>(g, false, st); break;
+      case 7: e = launch_tall<7>(g, false, st); break;
+      default: e = launch_tall<8>(g, false, st); break;
+    }
+    if (e != hipSuccess) return e;
+  }
+  if (dw) {  // dW[n_out][n_in] = g^T x over the rows; db[n_out] = column sums of g
+    const int S = deep_splits(n_out, n_in, rows);
+    const int64_t chunks = (rows + TK - 1) / TK;
+    const int64_t per = (chunks + S - 1) / S;
+    float* dbp = db ? workspace + (S > 1 ? (int64_t)S * n_out * n_in : 0) : nullptr;
+    GemmArgs g{dy, x, nullptr, dw, n_out, n_in, rows, n_out, n_in, n_in, 0, S, per, workspace, y, act, db, dbp,
+               S * (int)(n_in / 64)};
+    const int tiles_m = (int)(n_out / 64);
+    const unsigned grid = (unsigned)(tiles_m * (n_in / 64) * S);
+    if (per == 5 && chunks == per * S) k_gemm_deep<5, true><<<grid, 256, 0, st>>>(g, tiles_m);
+    else k_gemm_deep<0, true><<<grid, 256, 0, st>>>(g, tiles_m);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || (S == 1 && !db)) return e;
+    const int64_t want = (n_out * n_in + 255) / 256;
+    k_gemm_reduce<<<(unsigned)(want < 2048 ? want : 2048), 256, 0, st>>>(g);
+    return hipGetLastError();
+  }
+  return hipSuccess;
 }
 
 }  // namespace mh

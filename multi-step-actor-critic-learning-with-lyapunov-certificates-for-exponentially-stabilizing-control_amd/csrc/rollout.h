@@ -99,6 +99,10 @@ hipError_t launch_gemm(const float* A, const float* B, const float* bias, float*
                        int64_t lda, int64_t ldb, int64_t ldc, int ta, int tb, int act, float* workspace,
                        hipStream_t st);
 int64_t gemm_workspace_floats(int64_t M, int64_t N, int64_t K);
+bool linear_backward_plan(int64_t rows, int64_t n_out, int64_t n_in, bool dx, bool dw, bool db, int64_t* ws);
+hipError_t launch_linear_backward(const float* dy, const float* y, int act, const float* x, const float* W,
+                                  int64_t rows, int64_t n_out, int64_t n_in, float* dx, float* dw, float* db,
+                                  float* workspace, hipStream_t st);
 hipError_t launch_stocha_head(const float* raw, int64_t M, int A, float lo, float hi, float* out, hipStream_t st);
 hipError_t launch_stocha_head_bwd(const float* raw, const float* out, const float* dout, int64_t M, int A, float lo,
                                   float hi, float* draw, hipStream_t st);
