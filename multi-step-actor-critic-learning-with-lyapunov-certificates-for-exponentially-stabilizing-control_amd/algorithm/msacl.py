@@ -240,6 +240,11 @@ class MSACL:
             return tb_info, data.get("idx"), self.last_priority
         return tb_info
 
+    def _seg_side_stream(self):
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
+
     def _side_stream(self):
         if not (self.concurrent and D.world_size() == 1 and self.device.type == "cuda"
                 and not self.force_graph_segments and not D.segment_capture_active()):
@@ -263,6 +268,27 @@ class MSACL:
             if do_target:
                 self._target_update()
             main.wait_stream(side)
+        elif self._segmented() and self.concurrent and self.device.type == "cuda":
+            # data parallel: the two backward passes still run as parallel branches, and their
+            # gradients are averaged by ONE all-reduce at the join (one graph cut instead of two,
+            # the branches stay concurrent inside the segment); the optimizer steps follow it.
+            # Same result as the serial order: the critic and Lyapunov losses read disjoint
+            # parameters, and each optimizer step only reads its own network's gradients.
+            main = torch.cuda.current_stream(self.device)
+            side = self._seg_side_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                loss_lya = self._lyapunov_update(data, defer_step=True)
+            loss_q, q1_mean, q2_mean = self._q_update(data, defer_step=True)
+            main.wait_stream(side)
+            nets = self.networks
+            D.allreduce_grads(list(nets.q1.parameters()) + list(nets.q2.parameters()) +
+                              list(nets.lyapunov.parameters()))
+            nets.q1_optimizer.step()
+            nets.q2_optimizer.step()
+            nets.lyapunov_optimizer.step()
+            if do_target:
+                self._target_update()
         else:
             loss_q, q1_mean, q2_mean = self._q_update(data)
             if do_target:
@@ -320,7 +346,7 @@ class MSACL:
         self.last_priority = prio
         return outs
 
-    def _q_update(self, data):
+    def _q_update(self, data, defer_step=False):
         obs, act, rew, obs2, done = data["obs"], data["act"], data["rew"], data["obs2"], data["done"]
         B, n = rew.shape
         s = self._buf(B, n)
@@ -340,13 +366,14 @@ class MSACL:
         self.networks.q1_optimizer.zero_grad()
         self.networks.q2_optimizer.zero_grad()
         torch.autograd.backward([q1, q2], [s.dq1, s.dq2])
-        D.allreduce_grads(list(self.networks.q1.parameters()) + list(self.networks.q2.parameters()))
-        self.networks.q1_optimizer.step()
-        self.networks.q2_optimizer.step()
+        if not defer_step:  # deferred: the caller all-reduces and steps (data-parallel join)
+            D.allreduce_grads(list(self.networks.q1.parameters()) + list(self.networks.q2.parameters()))
+            self.networks.q1_optimizer.step()
+            self.networks.q2_optimizer.step()
         self.last_priority = s.abs_td.clone()
         return s.loss_q[0].clone(), q1.detach().mean(), q2.detach().mean()
 
-    def _lyapunov_update(self, data):
+    def _lyapunov_update(self, data, defer_step=False):
         obs, obs2, act, old_logp = data["obs"], data["obs2"], data["act"], data["logp"]
         B, n = old_logp.shape
         s = self._buf(B, n)
@@ -365,8 +392,9 @@ class MSACL:
             N.ptr(s.dV2), N.stream_of(self.device)), "mh_msacl_lyapunov")
         self.networks.lyapunov_optimizer.zero_grad()
         torch.autograd.backward([V_both], [s.dV_both])
-        D.allreduce_grads(list(self.networks.lyapunov.parameters()))
-        self.networks.lyapunov_optimizer.step()
+        if not defer_step:
+            D.allreduce_grads(list(self.networks.lyapunov.parameters()))
+            self.networks.lyapunov_optimizer.step()
         return s.loss_lya[0]  # a view of the scratch (no allocation on the side stream)
 
     def _policy_update(self, data):
