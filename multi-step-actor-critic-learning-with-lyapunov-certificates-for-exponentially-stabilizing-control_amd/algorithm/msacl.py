@@ -296,10 +296,18 @@ class MSACL:
             loss_lya = self._lyapunov_update(data)
         loss_policy = entropy = None
         if do_policy:
+            # data parallel: the policy and alpha gradients share one all-reduce (the alpha loss
+            # reads the policy forward's entropy, not the stepped policy), then both steps
+            merge = self._segmented() and self.auto_alpha
             for _ in range(self.policy_frequency):
-                loss_policy, entropy = self._policy_update(data=data)
+                loss_policy, entropy = self._policy_update(data=data, defer_step=merge)
                 if self.auto_alpha:
-                    self._alpha_update(entropy=entropy)
+                    self._alpha_update(entropy=entropy, defer_step=merge)
+                if merge:
+                    nets = self.networks
+                    D.allreduce_grads(list(nets.policy.parameters()) + [nets.log_alpha])
+                    nets.policy_optimizer.step()
+                    self._alpha_step()
         return loss_q, q1_mean, q2_mean, loss_lya, loss_policy, entropy
 
     # ------------------------------------------------------------------ HIP-graph replay
@@ -397,7 +405,7 @@ class MSACL:
             self.networks.lyapunov_optimizer.step()
         return s.loss_lya[0]  # a view of the scratch (no allocation on the side stream)
 
-    def _policy_update(self, data):
+    def _policy_update(self, data, defer_step=False):
         obs, old_act, obs2, old_logp = data["obs"], data["act"], data["obs2"], data["logp"]
         B, n = old_logp.shape
         s = self._buf(B, n)
@@ -430,19 +438,24 @@ class MSACL:
         loss_policy = -loss_policy_q.detach() - s.loss_ppo[0]
         self.networks.policy_optimizer.zero_grad()
         torch.autograd.backward([loss_policy_q, is_ratio], [self._neg_one, -s.d_ratio])
-        D.allreduce_grads(list(self.networks.policy.parameters()))
-        self.networks.policy_optimizer.step()
+        if not defer_step:
+            D.allreduce_grads(list(self.networks.policy.parameters()))
+            self.networks.policy_optimizer.step()
         entropy = entropy.detach()
         for p in list(self.networks.q1.parameters()) + list(self.networks.q2.parameters()):
             p.requires_grad = True
         return loss_policy.detach(), entropy
 
-    def _alpha_update(self, entropy):
+    def _alpha_update(self, entropy, defer_step=False):
         alpha = self._get_alpha(requires_grad=True)
         loss_alpha = alpha * (entropy - self.target_entropy)
         self.networks.alpha_optimizer.zero_grad()
         loss_alpha.backward()
-        D.allreduce_grads([self.networks.log_alpha])
+        if not defer_step:
+            D.allreduce_grads([self.networks.log_alpha])
+            self._alpha_step()
+
+    def _alpha_step(self):
         self.networks.alpha_optimizer.step()
         if self.set_alpha_bound:
             with torch.no_grad():
