@@ -94,7 +94,7 @@ def main():
 
     D.init_from_env()
     rank, world = D.rank(), D.world_size()
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = D.local_device_index()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     horizon = 20

@@ -27,15 +27,25 @@ def rank() -> int:
     return dist.get_rank() if is_initialized() else 0
 
 
+def local_device_index() -> int:
+    """This rank's GPU: LOCAL_RANK, wrapped onto the visible devices (one rank per GPU in
+    production; several ranks per GPU only in the gloo rehearsal)."""
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n = torch.cuda.device_count()
+    return local % n if n > 0 else local
+
+
 def init_from_env(backend=None):
     """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, MASTER_ADDR/PORT)."""
     if is_initialized() or int(os.environ.get("WORLD_SIZE", "1")) <= 1:
         return False
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # MSACL_DIST_BACKEND=gloo: rehearse the multi-rank path with several ranks on one GPU
+        # (RCCL refuses two ranks per device)
+        backend = os.environ.get("MSACL_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     kw = {}
     if backend == "nccl":
-        local = int(os.environ.get("LOCAL_RANK", "0"))
+        local = local_device_index()
         torch.cuda.set_device(local)
         kw["device_id"] = torch.device("cuda", local)
     dist.init_process_group(backend=backend, **kw)
