@@ -34,7 +34,8 @@ constexpr int PM_NB = PM_H / 32;    // 32-row blocks per hidden layer
 //   b1p [NB][64][16]        b1[blk*32 + row(r, l)]
 //   W2p [NB ob][NB ib][4 q][64][4]   W2[ob*32 + (l&31)][ib*32 + row(4q + j, l)]
 //   b2p [NB][64][16]
-//   W3p [NB][4 q][64][4]    W3[(l&31)][ob*32 + row(4q + j, l)]   (0 for l&31 >= N3)
+//   W3p [NB][4 q][64][4]    W3[(l&15)][ob*32 + row(4q + j, l)] for N3 <= 16 (layer 3 on the
+//                           16x16x1 4-block MFMA), else W3[(l&31)][...]   (0 for rows >= N3)
 //   b3  [32]
 // row(r, l) = (r & 3) + 8 (r >> 2) + 4 (l >> 5): the accumulator row held in register r.
 __host__ __device__ constexpr int64_t pm_off_b1(int K1) { return (int64_t)PM_NB * K1 * 64; }
@@ -75,7 +76,9 @@ __global__ __launch_bounds__(256) void k_policy_pack(const float* __restrict__ W
     } else if (q < pm_off_b3(K1)) {
       const int64_t o = q - pm_off_w3(K1);
       const int j = (int)(o % 4), l = (int)((o / 4) % 64), qq = (int)((o / 256) % 4), ob = (int)(o / 1024);
-      if ((l & 31) < N3) v = W3[(int64_t)(l & 31) * PM_H + ob * 32 + pm_row(4 * qq + j, l)];
+      // N3 <= 16 (layer 3 on v_mfma_f32_16x16x1_4b: output row = lane & 15), else lane & 31
+      const int orow = N3 <= 16 ? (l & 15) : (l & 31);
+      if (orow < N3) v = W3[(int64_t)orow * PM_H + ob * 32 + pm_row(4 * qq + j, l)];
     } else {
       const int o = (int)(q - pm_off_b3(K1));
       if (o < N3) v = b3[o];
@@ -91,7 +94,7 @@ __global__ __launch_bounds__(256) void k_policy_pack(const float* __restrict__ W
 #ifndef MH_POLICY_MIN_WAVES
 #define MH_POLICY_MIN_WAVES 1
 #endif
-template <int K1>
+template <int K1, bool L3B4>
 __global__ __launch_bounds__(256, MH_POLICY_MIN_WAVES) void k_policy_forward(const float* __restrict__ P,
                                                                             const float* __restrict__ obs, int64_t E,
                                                                             int D, int N3, float* __restrict__ logits) {
@@ -185,18 +188,44 @@ __global__ __launch_bounds__(256, MH_POLICY_MIN_WAVES) void k_policy_forward(con
       for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[4 * q + j] = fmaxf(acc[4 * q + j] + bias[q][j], 0.0f);
+      if constexpr (L3B4) {
+        // N3 <= 16: v_mfma_f32_16x16x1_4b_f32, 16 output rows instead of 32 (half the cycles).
+        // Block b (lanes 16b..16b+15) takes B = acc[r] there: envs 16 (b & 1) + (l & 15), the
+        // k row of half b >> 1; A = W3[l & 15][that k]. Blocks b and b + 2 hold the two k halves
+        // of the same envs, in registers 4b..4b+3 and 4b+8..4b+11 of the same lane
+        // (tools/mfma_probe.hip: C of block b at reg 4b + q, row 4 (l >> 4) + q, column l & 15).
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+        for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o3 = __builtin_amdgcn_mfma_f32_32x32x2f32(w3f[q][j], acc[4 * q + j], o3, 0, 0, 0);
+          for (int j = 0; j < 4; ++j) o3 = __builtin_amdgcn_mfma_f32_16x16x1f32(w3f[q][j], acc[4 * q + j], o3, 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o3 = __builtin_amdgcn_mfma_f32_32x32x2f32(w3f[q][j], acc[4 * q + j], o3, 0, 0, 0);
+      }
     }
-    // ---- out^T rows o = row(r, lane) for env column lane & 31: + b3, store [E][N3]
-    const int64_t b = tile * 32 + (lane & 31);
-    if (b < E) {
+    if constexpr (L3B4) {
+      // ---- out^T row o = 4 (lane >> 4) + q for envs (lane & 15) + 16 h: the two k halves
+      // (blocks h and h + 2) added, + b3, store [E][N3]
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int o = pm_row(r, lane);
-        if (o < N3) logits[b * N3 + o] = o3[r] + b3[o];
+      for (int h = 0; h < 2; ++h) {
+        const int64_t b = tile * 32 + (lane & 15) + 16 * h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int o = 4 * (lane >> 4) + q;
+          if (b < E && o < N3) logits[b * N3 + o] = (o3[4 * h + q] + o3[4 * h + 8 + q]) + b3[o];
+        }
+      }
+    } else {
+      // ---- out^T rows o = row(r, lane) for env column lane & 31: + b3, store [E][N3]
+      const int64_t b = tile * 32 + (lane & 31);
+      if (b < E) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int o = pm_row(r, lane);
+          if (o < N3) logits[b * N3 + o] = o3[r] + b3[o];
+        }
       }
     }
   }
@@ -227,7 +256,8 @@ static hipError_t launch_fwd_t(const float* P, const float* obs, int64_t E, int 
   }
   const int64_t want = (tiles + 3) / 4;
   const int grid = (int)(want < cus ? want : cus);
-  k_policy_forward<K1><<<grid, 256, 0, st>>>(P, obs, E, D, N3, logits);
+  if (N3 <= 16) k_policy_forward<K1, true><<<grid, 256, 0, st>>>(P, obs, E, D, N3, logits);
+  else k_policy_forward<K1, false><<<grid, 256, 0, st>>>(P, obs, E, D, N3, logits);
   return hipGetLastError();
 }
 

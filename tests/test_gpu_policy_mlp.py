@@ -33,7 +33,8 @@ def _fused(net, obs, D, N3):
     return out
 
 
-@pytest.mark.parametrize("D,A,E", [(12, 4, 65536), (12, 4, 1000), (2, 1, 777), (6, 2, 4097), (7, 2, 64), (16, 16, 96)])
+@pytest.mark.parametrize("D,A,E", [(12, 4, 65536), (12, 4, 1000), (2, 1, 777), (6, 2, 4097), (7, 2, 64), (5, 8, 333),
+                                   (16, 16, 96)])  # 2A <= 16: 16x16x1 4-block layer 3; 2A = 32: 32x32x2
 def test_fused_policy_forward_matches_torch(D, A, E):
     net = _mlp(D, A, seed=D * 100 + A)
     g = torch.Generator(device="cuda").manual_seed(E)
