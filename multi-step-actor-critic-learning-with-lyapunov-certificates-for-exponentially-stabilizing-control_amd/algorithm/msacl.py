@@ -184,6 +184,8 @@ class MSACL:
         # the Lyapunov update shares no parameter with the critic update (both only read the
         # policy and the batch): on one GPU it runs on a second stream, concurrently
         self.concurrent = bool(kwargs.get("alg_concurrent_streams", True))
+        self.twin_streams = bool(kwargs.get("alg_twin_streams", True))  # q1 / q2 branches in parallel
+        self._twin = None
         self._side = None
         self.force_graph_segments = bool(kwargs.get("alg_force_graph_segments", False))
         self._static = None
@@ -239,6 +241,32 @@ class MSACL:
         if self.per_flag:
             return tb_info, data.get("idx"), self.last_priority
         return tb_info
+
+    def _twin_stream(self):
+        """Stream for the second critic's branch (q2 / q2 target forward; autograd runs each
+        backward op on its forward's stream, so the two critics' backward passes overlap too).
+        None when streams are off or on CPU."""
+        if not (self.concurrent and self.device.type == "cuda" and self.twin_streams):
+            return None
+        if self._twin is None:
+            self._twin = torch.cuda.Stream(device=self.device)
+        return self._twin
+
+    def _twin_pair(self, f1, f2):
+        """(f1(), f2()) with f2 on the twin stream (fork/join around it); outputs produced there
+        are recorded for the current stream that consumes them."""
+        tw = self._twin_stream()
+        if tw is None:
+            return f1(), f2()
+        cur = torch.cuda.current_stream(self.device)
+        tw.wait_stream(cur)
+        with torch.cuda.stream(tw):
+            r2 = f2()
+        r1 = f1()
+        cur.wait_stream(tw)
+        for t in (r2 if isinstance(r2, tuple) else (r2,)):
+            t.record_stream(cur)
+        return r1, r2
 
     def _seg_side_stream(self):
         if self._side is None:
@@ -358,13 +386,22 @@ class MSACL:
         obs, act, rew, obs2, done = data["obs"], data["act"], data["rew"], data["obs2"], data["done"]
         B, n = rew.shape
         s = self._buf(B, n)
-        q1 = self.networks.q1(obs, act)
-        q2 = self.networks.q2(obs, act)
         with torch.no_grad():
             dist = self.networks.create_action_distributions(self.networks.policy(obs2))
             next_act, next_logp = dist.rsample()
-            q1t = self.networks.q1_target(obs2, next_act).contiguous()
-            q2t = self.networks.q2_target(obs2, next_act).contiguous()
+        nets = self.networks
+
+        def critic1():
+            q = nets.q1(obs, act)
+            with torch.no_grad():
+                return q, nets.q1_target(obs2, next_act).contiguous()
+
+        def critic2():
+            q = nets.q2(obs, act)
+            with torch.no_grad():
+                return q, nets.q2_target(obs2, next_act).contiguous()
+
+        (q1, q1t), (q2, q2t) = self._twin_pair(critic1, critic2)
         weight = data.get("weight") if self.per_flag else None
         N.check(N.lib().mh_msacl_q_target(
             N.ptr(q1.detach().contiguous()), N.ptr(q2.detach().contiguous()), N.ptr(q1t), N.ptr(q2t),
@@ -413,8 +450,7 @@ class MSACL:
             p.requires_grad = False
         dist = self.networks.create_action_distributions(self.networks.policy(obs))
         new_act, new_act_logp = dist.rsample()
-        q1 = self.networks.q1(obs, new_act)
-        q2 = self.networks.q2(obs, new_act)
+        q1, q2 = self._twin_pair(lambda: self.networks.q1(obs, new_act), lambda: self.networks.q2(obs, new_act))
         # (min(q1, q2) - alpha logp).mean() with alpha = exp(log_alpha) read on the device (the
         # reference's alpha.item() float has the same f32 value), and the entropy, in one kernel
         loss_policy_q, entropy = _PolicyQLoss.apply(q1.contiguous(), q2.contiguous(), new_act_logp.contiguous(),
