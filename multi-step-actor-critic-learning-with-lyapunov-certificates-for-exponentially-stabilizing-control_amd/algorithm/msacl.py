@@ -254,7 +254,15 @@ class MSACL:
 
     def _twin_pair(self, f1, f2):
         """(f1(), f2()) with f2 on the twin stream (fork/join around it); outputs produced there
-        are recorded for the current stream that consumes them."""
+        are recorded for the current stream that consumes them.
+
+        Invariant: no twin-stream work may outlive the join (`cur.wait_stream(tw)` below). The
+        inputs f2 reads (obs, act, next_act, new_act, ...) are allocated on the current stream
+        and are NOT record_stream'ed for the twin stream; they stay safe only because every
+        kernel f2 enqueues is ordered before the join, and autograd runs the backward of f2's ops
+        on this same twin stream before the current stream's later consumers (autograd's own
+        stream sync). Launching further work on the twin stream after the join would let the
+        caching allocator hand those inputs' blocks out while it still reads them."""
         tw = self._twin_stream()
         if tw is None:
             return f1(), f2()

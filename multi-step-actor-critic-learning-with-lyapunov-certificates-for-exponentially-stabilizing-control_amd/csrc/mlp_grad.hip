@@ -78,12 +78,15 @@ __global__ __launch_bounds__(256) void k_act_grad_colsum(const float* __restrict
   __syncthreads();
   __shared__ int s_last;
   if (threadIdx.x == 0) {
-    const uint32_t a = __hip_atomic_fetch_add(tickets + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // release: this workgroup's published sums (drained above, ordered by the barrier) before
+    // the arrival; acquire: the last arrival sees every other workgroup's sums
+    const uint32_t a = __hip_atomic_fetch_add(tickets + blockIdx.x, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     s_last = (a == gridDim.y - 1);
   }
   store_g();
   __syncthreads();
   if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every reading thread, not only thread 0
   const int R = (int)gridDim.y;
   float s = 0.0f;
   if (n < N) {

@@ -51,8 +51,7 @@ __global__ __launch_bounds__(256) void k_adam_multi(AdamList L, double lr, doubl
   // the last workgroup to finish advances every step counter
   __syncthreads();
   if (threadIdx.x == 0) {
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    const uint32_t done = atomicAdd(ticket, 1u);
+    const uint32_t done = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (done == gridDim.x - 1) {
       for (int k = 0; k < L.n; ++k) *L.step[k] = s_t[k];
       *ticket = 0u;

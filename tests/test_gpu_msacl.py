@@ -251,3 +251,37 @@ def test_segmented_graph_collectives_bind_the_captured_gradients(monkeypatch):
         states[mode] = {k: v.detach().clone() for k, v in alg.networks.state_dict().items()}
     for k, v in states["eager"].items():
         assert torch.equal(v, states["segments"][k]), k
+
+
+@pytest.mark.parametrize("mode", ["eager", "graph", "segments"])
+def test_twin_stream_update_equals_serial(monkeypatch, mode):
+    """The forked q1 / q2 branches (alg_twin_streams, and the critic || Lyapunov streams) give
+    the same parameters bit for bit as the serial order (both streams off), under eager, single
+    graph and segmented-graph execution (fixed rsample noise, several even/odd updates)."""
+    import torch.distributions.normal as tdn
+    from msacl_amd.algorithm.msacl import MSACL
+    g = np.load(os.path.join(G, "msacl_update.npz"))
+    B, n = int(g["cfg_B"]), int(g["cfg_n"])
+    data = {k: torch.as_tensor(g["in_" + k], device="cuda") for k in ("obs", "act", "rew", "cost", "obs2", "done", "logp")}
+    noise = {}
+
+    def fixed(shape, dtype, device):
+        key = tuple(shape)
+        if key not in noise:
+            gen = torch.Generator(device="cuda").manual_seed(len(noise) + 1)
+            noise[key] = torch.randn(key, dtype=dtype, device=device, generator=gen)
+        return noise[key]
+
+    monkeypatch.setattr(tdn, "_standard_normal", fixed)
+    states = {}
+    for streams in (True, False):
+        alg = MSACL(**_msacl_kwargs(B, n), alg_use_graph=(mode != "eager"), alg_force_graph_segments=(mode == "segments"),
+                    alg_twin_streams=streams, alg_concurrent_streams=streams)
+        sd = {k[5:]: torch.as_tensor(g[k]) for k in g.files if k.startswith("init/")}
+        alg.networks.load_state_dict(sd)
+        for it in range(6):
+            alg.model_update(data, it)
+        torch.cuda.synchronize()
+        states[streams] = {k: v.detach().clone() for k, v in alg.networks.state_dict().items()}
+    for k, v in states[False].items():
+        assert torch.equal(v, states[True][k]), k
