@@ -603,6 +603,135 @@ def gen_msacl(B=64, n=20, seed=11):
     print("msacl_update:", {k: round(float(v), 6) for k, v in tb0.items()}, "eps draws:", len(eps_log))
 
 
+_INTERMEDIATES = {
+    "_q_update": ("q1", "q2", "next_q", "next_logp", "backup"),
+    "_lyapunov_update": ("logp", "ratio", "is_clip_ratio", "lya_obs", "lya_obs2", "ESL", "lya_diff", "loss_lya2",
+                         "loss_lya3"),
+    "_policy_update": ("new_act_logp", "is_ratio", "start_lya", "lya_obs2", "mb_stability_adv", "loss_policy_q",
+                       "loss_policy_lya"),
+}
+
+
+def gen_msacl_bench(B=256, n=20, seed=13):
+    """msacl_update_bench.npz: two MSACL.model_update calls at the benchmark configuration
+    (example/msacl_train.py defaults: QuadTracking dims, 256-wide critics / Lyapunov (output 256) /
+    policy, B = 256 windows of n = 20) with every per-window intermediate of the reference's
+    update functions (locals at return of _q_update / _lyapunov_update / _policy_update, read by a
+    profile hook: backup, ratio, is_clip_ratio, ESL, lya_diff, normalised stability advantage, ...)
+    and the Adam moments after each call (the parameter gradients: exp_avg = (1 - b1) g on the
+    first step). Windows are chained like the sampler's (obs[k+1] = obs2[k] unless done)."""
+    import torch
+    import torch.distributions.normal as tdn
+
+    torch.Tensor.cuda = lambda self, *a, **k: self   # build container has no GPU (this process only)
+    torch.nn.Module.cuda = lambda self, *a, **k: self
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    from RL.algorithm.msacl import MSACL
+
+    torch.manual_seed(seed)
+    rng = np.random.default_rng(seed)
+    cls = OE.QuadTracking
+    D, A = cls.obs_dim, cls.act_dim
+    kw = dict(env_name="QuadTracking", obs_dim=D, act_dim=A, action_type="continu",
+              action_high_limit=cls.act_high.copy(), action_low_limit=cls.act_low.copy(),
+              value_func_name="ActionValue", value_func_type="MLP", value_hidden_sizes=[256, 256],
+              value_hidden_activation="relu", value_output_activation="linear",
+              lyapunov_func_name="LyapunovValue", lyapunov_func_type="MLP", lyapunov_hidden_sizes=[256, 256],
+              lyapunov_hidden_activation="tanh", lyapunov_output_dim=256, lyapunov_output_activation="linear",
+              lyapunov_single_input_dim=False, policy_func_name="StochaPolicy", policy_func_type="MLP",
+              policy_act_distribution="TanhGaussDistribution", policy_hidden_sizes=[256, 256],
+              policy_hidden_activation="relu", policy_min_log_std=-20, policy_max_log_std=1,
+              q_learning_rate=1e-3, lyapunov_learning_rate=1e-3, policy_learning_rate=3e-4, alpha_learning_rate=1e-3,
+              lya_diff_scale=10.0, lya_zero_scale=1.0, lya_positive_scale=1.0, gamma=0.99, retrace_lambda=0.95,
+              tau=0.005, disable_auto_alpha=False, alpha=1.0, set_alpha_bound=False, alpha_bound=2.0, n_step=n,
+              policy_frequency=2, target_network_frequency=1, anneal_lr=False, alpha1=1, alpha2=2, lya_eta=0.15,
+              clip_coef=0.1, replay_batch_size=B, max_iteration=1000000)
+    alg = MSACL(**kw)
+    init_sd = {k: v.detach().numpy().copy() for k, v in alg.networks.state_dict().items()}
+    # chained windows: a contracting random walk in the 12-d error space, episode ends at slot n-1
+    x = np.zeros((B, n + 1, D), np.float64)
+    x[:, 0] = rng.standard_normal((B, D)) * 0.2
+    for k in range(n):
+        x[:, k + 1] = 0.93 * x[:, k] + rng.standard_normal((B, D)) * 0.03
+    obs, obs2 = x[:, :n].astype(F32), x[:, 1:].astype(F32)
+    lo, hi = cls.act_low, cls.act_high
+    act = (lo + (hi - lo) * rng.uniform(0.05, 0.95, size=(B, n, A))).astype(F32)
+    with torch.no_grad():
+        dist = alg.networks.create_action_distributions(alg.networks.policy(torch.from_numpy(obs)))
+        lp = dist.log_prob(torch.from_numpy(act)).numpy()
+    logp = (lp + rng.normal(0, 0.5, size=lp.shape)).astype(F32)
+    rew = (-(obs2.astype(np.float64) ** 2).sum(-1) * 100 + rng.standard_normal((B, n))).astype(F32)
+    cost = ((obs2.astype(np.float64) ** 2).sum(-1) * 100).astype(F32)
+    done = np.zeros((B, n), F32)
+    done[rng.choice(B, B // 8, replace=False), n - 1] = 1.0
+    data_np = dict(obs=obs, act=act, rew=rew, cost=cost, obs2=obs2, done=done, logp=logp)
+
+    eps_log, inter = [], []
+    orig = tdn._standard_normal
+
+    def rec(shape, dtype, device):
+        e = orig(shape, dtype=dtype, device=device)
+        eps_log.append(e.detach().numpy().copy())
+        return e
+
+    def prof(frame, event, arg):
+        if event == "return" and frame.f_code.co_name in _INTERMEDIATES and "self" in frame.f_locals \
+                and isinstance(frame.f_locals["self"], MSACL):
+            loc = frame.f_locals
+            vals = {k: loc[k].detach().numpy().copy() for k in _INTERMEDIATES[frame.f_code.co_name] if k in loc}
+            if frame.f_code.co_name == "_policy_update":  # Adam moments after each policy step
+                st = loc["self"].networks.policy_optimizer.state_dict()["state"]
+                for i, (pn, _) in enumerate(loc["self"].networks.policy.named_parameters()):
+                    vals[f"adam/{pn}/exp_avg"] = st[i]["exp_avg"].numpy().copy()
+            inter.append((frame.f_code.co_name, vals))
+
+    nets = alg.networks
+    opts = {"q1": (nets.q1, nets.q1_optimizer), "q2": (nets.q2, nets.q2_optimizer),
+            "lyapunov": (nets.lyapunov, nets.lyapunov_optimizer), "policy": (nets.policy, nets.policy_optimizer)}
+    d = {"in_" + k: v for k, v in data_np.items()}
+    for k, v in init_sd.items():
+        d["init/" + k] = v
+    tdn._standard_normal = rec
+    try:
+        for it in range(2):
+            data = {k: torch.from_numpy(v.copy()) for k, v in data_np.items()}
+            inter.clear()
+            sys.setprofile(prof)
+            try:
+                tb = alg.model_update(data, it)
+            finally:
+                sys.setprofile(None)
+            if it == 0:
+                d["tb_keys"] = np.array(list(tb.keys()))
+                d["tb_vals"] = np.array([float(v) for v in tb.values()])
+            else:
+                assert tb is None
+            counts = {}
+            for fn, vals in inter:
+                c = counts.get(fn, 0)
+                counts[fn] = c + 1
+                for k, v in vals.items():
+                    d[f"it{it}/{fn[1:]}{c}/{k}"] = v
+            for k, v in alg.networks.state_dict().items():
+                d[f"after{it}/" + k] = v.detach().numpy().copy()
+            for name, (net, opt) in opts.items():
+                st = opt.state_dict()["state"]
+                for i, (pn, _) in enumerate(net.named_parameters()):
+                    d[f"adam{it}/{name}.{pn}/exp_avg"] = st[i]["exp_avg"].numpy().copy()
+                    d[f"adam{it}/{name}.{pn}/exp_avg_sq"] = st[i]["exp_avg_sq"].numpy().copy()
+    finally:
+        tdn._standard_normal = orig
+        sys.setprofile(None)
+    for i, e in enumerate(eps_log):
+        d[f"eps{i}"] = e
+    d["n_eps"] = np.int64(len(eps_log))
+    d["cfg_B"], d["cfg_n"] = np.int64(B), np.int64(n)
+    np.savez_compressed(os.path.join(OUT, "msacl_update_bench.npz"), **d)
+    print("msacl_update_bench:", {k: round(float(v), 6) for k, v in zip(d["tb_keys"], d["tb_vals"])},
+          "eps draws:", len(eps_log), "intermediates:", sorted({k.split("/")[1] for k in d if k.startswith("it")}))
+
+
 # ---------------------------------------------------------------------- SAC / LAC / PPO / POLYC updates
 def _alg_kwargs(env="QuadTracking", hidden=64):
     cls = OE.ENVS[env]
@@ -743,6 +872,8 @@ if __name__ == "__main__":
         gen_nstep_trace("VanderPol", E=16, T=60, n_step=20, seed=5, tag="_n20")
     if "msacl" in which:
         gen_msacl()
+    if "msacl_bench" in which or "msacl" in which:
+        gen_msacl_bench()
     if "step" in which:
         for nm in ("VanderPol", "TwoLink", "QuadTracking"):
             gen_step_trace(nm)
