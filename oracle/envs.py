@@ -328,8 +328,13 @@ class QuadTracking:
         return rs.astype(F32).copy(), Rd.reshape(n, 9), obs
 
     @staticmethod
-    def polar(R):
-        U, _, Vh = np.linalg.svd(R)
+    def polar(R, f64=False):
+        """NormalizeOrientMatrix (QuadTracking.py:308-315). f64=True: the same factorisation
+        from a float64 SVD of the float32 input (the kernel's arithmetic: an f64 polar factor
+        rounded once); used by the tests to separate the reference's float32-SVD rounding from
+        kernel error (tests/golden/quad_polar64.npz pins this variant against the reference run
+        with the same substitution)."""
+        U, _, Vh = np.linalg.svd(R.astype(F64) if f64 else R)
         out = np.matmul(U, Vh)
         neg = np.linalg.det(out) < 0
         if np.any(neg):
@@ -339,7 +344,7 @@ class QuadTracking:
         return out.astype(F32)
 
     @classmethod
-    def step(cls, s, u, xs, k):
+    def step(cls, s, u, xs, k, polar64=False):
         """env.step (:205-285) for a batch; k = steps since reset before the step."""
         n = s.shape[0]
         x = s[:, 0:3].copy()
@@ -363,7 +368,7 @@ class QuadTracking:
             v += dv * 0.01
             R += dR * 0.01
             W += dW * 0.01
-            R = cls.polar(R)
+            R = cls.polar(R, polar64)
         k1 = k + 1
         Rd_last = xs.reshape(n, 3, 3)
         ex, ev, Rd, Od = cls.desired(x, v, k1, Rd_last)
@@ -387,14 +392,15 @@ ENVS = {
 }
 
 
-def env_step(name, state, act, xstate=None, steps=None):
+def env_step(name, state, act, xstate=None, steps=None, polar64=False):
     """One env.step for a batch: returns (state', xstate', obs, reward f32, terminated, truncated).
-    steps = steps since reset before the step."""
+    steps = steps since reset before the step; polar64: QuadTracking's polar factor from a
+    float64 SVD (QuadTracking.polar)."""
     cls = ENVS[name]
     n = state.shape[0]
     steps = np.zeros(n, np.int64) if steps is None else np.asarray(steps, np.int64)
     if name == "QuadTracking":
-        s2, xs2, obs, rew = cls.step(state, act, xstate, steps)
+        s2, xs2, obs, rew = cls.step(state, act, xstate, steps, polar64)
     else:
         s2, obs, rew = cls.step(state, act)
         xs2 = None

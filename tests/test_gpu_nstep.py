@@ -22,9 +22,14 @@ TOL = dict(rtol=1e-5, atol=1e-5)
 TRACES = sorted(glob.glob(os.path.join(G, "nstep_*.npz")))
 
 
-def _run_trace(path, capacity=None, tile=1):
+def _run_trace(path, capacity=None, tile=1, check_obs=False):
     g = np.load(path)
     name = os.path.basename(path)[6:-4].replace("_n20", "")
+    # TwoLink's upright arm is open-loop unstable: under the trace's recorded (feedback) torques
+    # replayed open loop, ulp-level differences grow ~e-fold every few steps (2e-5 by step 12 of
+    # the n = 20 trace). Re-anchor its state (== obs) to the reference's after every step, so each
+    # window entry is one kernel step from the reference's own state.
+    anchor = name == "TwoLink" and n_of(g) == 20
     E0, T, n = g["init_reset"].shape[0], g["actions"].shape[0], int(g["n_step"])
     E = E0 * tile
     tl = lambda a: np.concatenate([a] * tile, axis=0)  # noqa: E731
@@ -45,6 +50,13 @@ def _run_trace(path, capacity=None, tile=1):
                                         None, None, N.stream_of(dev)), "rollout")
         if tile == 1:
             np.testing.assert_allclose(obs.cpu().numpy(), g["obs_trace"][t + 1], **TOL)
+        elif check_obs:
+            ref = torch.as_tensor(g["obs_trace"][t + 1], device=dev).repeat(tile, 1)
+            assert ((obs - ref).abs() <= TOL["atol"] + TOL["rtol"] * ref.abs()).all(), f"obs at step {t}"
+        if anchor:
+            ref = torch.as_tensor(tl(g["obs_trace"][t + 1]), device=dev).contiguous()
+            env.set_state(ref)
+            obs.copy_(ref)
     torch.cuda.synchronize()
     return g, buf, total, tile
 
@@ -103,3 +115,30 @@ def test_replay_gather_and_indices():
     assert counts.min() > 0.5 * 100000 / total  # roughly uniform
     batch = buf.sample_batch(256)
     assert batch["obs"].shape == (256, int(g["n_step"]), 6) and batch["rew"].shape == (256, int(g["n_step"]))
+
+
+def n_of(g):
+    return int(g["n_step"])
+
+
+N20 = [os.path.join(G, f"nstep_{nm}_n20.npz") for nm in ("QuadTracking", "TwoLink", "DuctedFan")]
+
+
+@pytest.mark.parametrize("path", N20, ids=os.path.basename)
+def test_n20_windows_tiled_to_65536_envs(path):
+    """The benchmark's n = 20 windows for configs 3 / 4 envs (QuadTracking, TwoLink, DuctedFan):
+    the reference's 16-env _n_step trace tiled 4,096 times = 65,536 envs in lockstep; every
+    step's observations and every emitted window (order: per step, env-index order) equal the
+    reference's at rtol = atol = 1e-5, compared on the device."""
+    g, buf, total, tile = _run_trace(path, tile=4096, check_obs=True)
+    assert int(buf.cursor[2]) == total and g["counts"].sum() > 100
+    counts = g["counts"]
+    offs = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    idx = np.concatenate([np.tile(np.arange(o, o + c), tile) for o, c in zip(offs, counts)])
+    idx = torch.as_tensor(idx, device="cuda")
+    for k in KEYS:
+        exp = torch.as_tensor(g["w_" + k], device="cuda")[idx]
+        got = buf.n_step_buf[k][:total]
+        bad = ((got - exp).abs() > TOL["atol"] + TOL["rtol"] * exp.abs()).sum().item()
+        assert bad == 0, (k, bad)
+    assert not buf.n_step_buf["done"][:total, :-1].any()

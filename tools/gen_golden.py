@@ -181,6 +181,110 @@ def gen_quad_reset(N=256, seed=7):
     print(f"reset_QuadTracking: {N}")
 
 
+# ---------------------------------------------------------------------- QuadTracking: polar-factor precision
+def _normalize_orient_f64(mat):
+    """NormalizeOrientMatrix (QuadTracking.py:308-315) with the SVD in float64 (dgesdd on the
+    float32 input) instead of float32 sgesdd; same det < 0 flip, same final float32 cast. Used
+    ONLY here, to measure how much of the reference's own output is float32-SVD rounding."""
+    U, s, Vh = np.linalg.svd(np.asarray(mat, np.float64))
+    R = U @ Vh
+    if np.linalg.det(R) < 0:
+        U[:, -1] *= -1
+        R = U @ Vh
+    return R.astype(np.float32)
+
+
+def _quad_fields(env):
+    return {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in vars(env).items() if not callable(v)}
+
+
+def _quad_step_both(mod, env, twin, act):
+    """Step `env` with the reference as-is and `twin` (a copy of env's state) with the float64
+    polar factor; returns both (obs, reward, terminated, truncated, state')."""
+    for k, v in _quad_fields(env).items():
+        setattr(twin, k, v)
+    out32 = env.step(act.copy())
+    st32 = np.concatenate([env.x, env.v, env.R.reshape(9), env.Omega]).astype(F32)
+    orig = mod.ns["NormalizeOrientMatrix"]
+    mod.ns["NormalizeOrientMatrix"] = _normalize_orient_f64
+    try:
+        out64 = twin.step(act.copy())
+    finally:
+        mod.ns["NormalizeOrientMatrix"] = orig
+    st64 = np.concatenate([twin.x, twin.v, twin.R.reshape(9), twin.Omega]).astype(F32)
+    return out32, st32, out64, st64
+
+
+def gen_quad_polar64(E=256, T=20, seed=11):
+    """quad_polar64.npz — the reference's self-noise from its float32 SVD:
+      pairs/*   the 512 env_QuadTracking.npz inputs stepped with the float64 polar factor;
+      traj/*    E envs x T lockstep steps of the reference under random in-box torques (the
+                action distribution of tests/test_gpu_env.py::test_multi_step_rollout_vs_oracle:
+                box centre +- 20 % of the half range), autoreset from drawn reset states; per step
+                the input state and BOTH outputs (reference as-is; float64 polar factor)."""
+    mod = load_env("QuadTracking")
+    cls = OE.QuadTracking
+    g = np.load(os.path.join(OUT, "env_QuadTracking.npz"))
+    env, twin = mod.make(), mod.make()
+    Tt = cls.T
+    p_obs, p_rew, p_state = [], [], []
+    for i in range(g["state"].shape[0]):
+        k = int(g["steps"][i])
+        S, X = g["state"][i], g["xstate"][i]
+        env.x, env.v, env.R, env.Omega = S[0:3].copy(), S[3:6].copy(), S[6:15].reshape(3, 3).copy(), S[15:18].copy()
+        env.Rd_last = X.reshape(3, 3).astype(np.float64).copy()
+        env.Omega_d_last = np.zeros(3, F32)
+        env.current_step = k
+        env.current_time = float(Tt[k])
+        env.t_last = np.array([Tt[k], Tt[k - 1] if k > 0 else 0.0])
+        out32, st32, out64, st64 = _quad_step_both(mod, env, twin, g["act"][i])
+        assert np.array_equal(np.asarray(out32[0], F32), g["obs"][i])  # the as-is run IS the fixture
+        p_obs.append(np.asarray(out64[0], F32))
+        p_rew.append(float(out64[1]))
+        p_state.append(st64)
+    rng = np.random.default_rng(seed)
+    envs = [mod.make() for _ in range(E)]
+    twins = [mod.make() for _ in range(E)]
+    rs0 = cls.reset_draw(rng, E, gauss=lambda m: rng.standard_normal((m, 3)))
+    for i, e in enumerate(envs):
+        ref_reset(mod, e, "QuadTracking", rs0[i])
+    lo, hi = cls.act_low.astype(np.float64), cls.act_high.astype(np.float64)
+    rec = {k: [] for k in ("state", "xstate", "steps", "act", "obs32", "obs64", "rew32", "rew64", "term32", "term64",
+                           "state32", "state64", "reset")}
+    for t in range(T):
+        act = ((lo + hi) / 2 + (hi - lo) / 2 * 0.2 * rng.uniform(-1, 1, size=(E, lo.size))).astype(F32)
+        pool = cls.reset_draw(rng, E, gauss=lambda m: rng.standard_normal((m, 3)))
+        row = {k: [] for k in rec}
+        for i, e in enumerate(envs):
+            row["state"].append(np.concatenate([e.x, e.v, e.R.reshape(9), e.Omega]).astype(F32))
+            row["xstate"].append(np.asarray(e.Rd_last, np.float64).reshape(9).copy())
+            row["steps"].append(int(e.current_step))
+            row["act"].append(act[i])
+            out32, st32, out64, st64 = _quad_step_both(mod, e, twins[i], act[i])
+            row["obs32"].append(np.asarray(out32[0], F32))
+            row["obs64"].append(np.asarray(out64[0], F32))
+            row["rew32"].append(float(out32[1]))
+            row["rew64"].append(float(out64[1]))
+            row["term32"].append(bool(out32[2]))
+            row["term64"].append(bool(out64[2]))
+            row["state32"].append(st32)
+            row["state64"].append(st64)
+            row["reset"].append(pool[i])
+            if out32[2] or out32[3]:
+                ref_reset(mod, e, "QuadTracking", pool[i])
+        for k in rec:
+            rec[k].append(np.asarray(row[k]))
+    d = {"pairs/obs64": np.stack(p_obs), "pairs/reward64": np.array(p_rew), "pairs/state64": np.stack(p_state)}
+    for k, v in rec.items():
+        d["traj/" + k] = np.stack(v)
+    noise = np.abs(d["traj/obs32"].astype(np.float64) - d["traj/obs64"])
+    np.savez_compressed(os.path.join(OUT, "quad_polar64.npz"), **d)
+    print("quad_polar64: max |obs32 - obs64| per component over the trajectories:",
+          np.array2string(noise.reshape(-1, 12).max(0), precision=2),
+          "pairs:", np.array2string(np.abs(d["pairs/obs64"] - g["obs"]).max(0), precision=2),
+          "terminations:", int(d["traj/term32"].sum()))
+
+
 # ---------------------------------------------------------------------- n-step sampler traces
 class RefVectorEnv:
     """gymnasium 0.28.1 SyncVectorEnv.step autoreset (restated) over reference env objects."""
@@ -240,8 +344,11 @@ def load_n_step():
     return ns["_n_step"]
 
 
-def gen_nstep_trace(name, E=24, T=40, n_step=5, seed=3, tag=""):
+def gen_nstep_trace(name, E=24, T=40, n_step=5, seed=3, tag="", log_std=-1.5, gentle_policy=("QuadTracking",),
+                    pd_gain=None):
     import torch
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
     from RL.apprfunc.mlp import StochaPolicy
     from RL.utils.act_distribution_cls import TanhGaussDistribution
 
@@ -265,12 +372,32 @@ def gen_nstep_trace(name, E=24, T=40, n_step=5, seed=3, tag=""):
                           output_activation="linear", min_log_std=-20, max_log_std=1,
                           act_high_lim=cls.act_high.copy(), act_low_lim=cls.act_low.copy(),
                           action_distribution_cls=TanhGaussDistribution)
-    if name == "QuadTracking":  # keep quads airborne for a while: near-hover mean, small std
+    if pd_gain is not None:
+        # the reference StochaPolicy with weights set to a linear state feedback, so TwoLink
+        # episodes outlive n = 20 (its default-init policy drops the arm within a few steps):
+        # layer 1 = [x, -x] (ReLU keeps both halves), layer 2 passes them on, the mean row of
+        # joint j = -(kp q_j + kd qdot_j) / a_high (tanh squashing ~ identity at small torques)
+        D, A = cls.obs_dim, cls.act_dim
+        kp, kd = pd_gain
+        with torch.no_grad():
+            l1, l2, l3 = policy.policy[0], policy.policy[2], policy.policy[-2]
+            for l in (l1, l2, l3):
+                l.weight.zero_()
+                l.bias.zero_()
+            l1.weight[:D, :] = torch.eye(D)
+            l1.weight[D:2 * D, :] = -torch.eye(D)
+            l2.weight[:2 * D, :2 * D] = torch.eye(2 * D)
+            for j in range(A):
+                for col, k in ((j, kp), (A + j, kd)):
+                    l3.weight[j, col] = -k / float(cls.act_high[j])
+                    l3.weight[j, D + col] = k / float(cls.act_high[j])
+            l3.bias[A:] = log_std
+    if name in gentle_policy:  # keep episodes alive past n: box-centre mean, small std
         with torch.no_grad():
             last = policy.policy[-2]
             last.weight.mul_(0.01)
             last.bias.zero_()
-            last.bias[cls.act_dim:] = -1.5
+            last.bias[cls.act_dim:] = log_std
     logps = []
 
     class Net:
@@ -354,7 +481,7 @@ def _ref_policy_and_recorder(name, hidden=64):
             last = policy.policy[-2]
             last.weight.mul_(0.01)
             last.bias.zero_()
-            last.bias[cls.act_dim:] = -1.5
+            last.bias[cls.act_dim:] = log_std
     logps = []
 
     def make_dist(logits):
@@ -866,10 +993,18 @@ if __name__ == "__main__":
             gen_env_pairs(nm)
     if "reset" in which:
         gen_quad_reset()
+    if "polar64" in which or "env" in which:
+        gen_quad_polar64()
     if "nstep" in which:
         for nm in OE.ENVS:
             gen_nstep_trace(nm)
         gen_nstep_trace("VanderPol", E=16, T=60, n_step=20, seed=5, tag="_n20")
+    if "nstep" in which or "nstep20" in which:
+        # the benchmark's n = 20 for the envs of configs 3 and 4
+        gen_nstep_trace("QuadTracking", E=16, T=60, n_step=20, seed=5, tag="_n20", log_std=-4.0)
+        gen_nstep_trace("TwoLink", E=16, T=60, n_step=20, seed=5, tag="_n20", log_std=-3.0, gentle_policy=(),
+                        pd_gain=(60.0, 12.0))
+        gen_nstep_trace("DuctedFan", E=16, T=60, n_step=20, seed=5, tag="_n20")
     if "msacl" in which:
         gen_msacl()
     if "msacl_bench" in which or "msacl" in which:
