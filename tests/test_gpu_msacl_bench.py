@@ -94,24 +94,32 @@ def _close(name, got, ref, rtol=1e-5, atol=1e-5):
     np.testing.assert_allclose(got, ref, rtol=rtol, atol=atol, err_msg=name)
 
 
-def _check_intermediates(alg, g, it, data_np, tag):
-    B, n = int(g["cfg_B"]), int(g["cfg_n"])
+def _rows(a, rank, world):
+    """Rank `rank`'s contiguous share of a batch-major array (data-parallel split)."""
+    return np.array_split(np.asarray(a), world)[rank]
+
+
+def _check_intermediates(alg, g, it, data_np, tag, rank=0, world=1):
+    n = int(g["cfg_n"])
+    B = data_np["rew"].shape[0]
     s = alg._buf(B, n)
     p = f"it{it}/"
-    _close(f"{tag}{p}backup", s.backup.cpu().numpy(), g[p + "q_update0/backup"])
-    _close(f"{tag}{p}is_clip_ratio", s.is_clip.cpu().numpy(), g[p + "lyapunov_update0/is_clip_ratio"])
-    _close(f"{tag}{p}lya_diff", s.lya_diff.cpu().numpy(), g[p + "lyapunov_update0/lya_diff"])
+    R = lambda k: _rows(g[p + k], rank, world)  # noqa: E731
+    _close(f"{tag}{p}backup", s.backup.cpu().numpy(), R("q_update0/backup"))
+    _close(f"{tag}{p}is_clip_ratio", s.is_clip.cpu().numpy(), R("lyapunov_update0/is_clip_ratio"))
+    _close(f"{tag}{p}lya_diff", s.lya_diff.cpu().numpy(), R("lyapunov_update0/lya_diff"))
     # ESL: exact unless the norm difference is within f32 rounding of zero
     obs, obs2 = data_np["obs"].astype(np.float64), data_np["obs2"].astype(np.float64)
     c = ((1 - 0.15) ** np.arange(1, n + 1) * 2.0) ** 0.5
     diff = np.linalg.norm(obs[:, 0], axis=-1)[:, None] * c[None] - np.linalg.norm(obs2, axis=-1)
-    esl, ref_esl = s.esl.cpu().numpy(), g[p + "lyapunov_update0/ESL"]
+    esl, ref_esl = s.esl.cpu().numpy(), R("lyapunov_update0/ESL")
     mism = esl != ref_esl
     STATS[f"{tag}{p}ESL"] = {"mismatch": int(mism.sum()), "min_abs_diff_at_mismatch":
                              float(np.abs(diff[mism]).min()) if mism.any() else None}
     assert np.all(np.abs(diff[mism]) < 1e-6), "ESL differs away from a tie"
     if it == 0:  # even iteration: policy updates ran (the scratch holds the second one's values)
-        _close(f"{tag}{p}mb_stability_adv", s.adv.cpu().numpy(), g[p + "policy_update1/mb_stability_adv"])
+        # with world > 1 this is the GLOBAL batch's normalisation ((sum, sum of squares) all-reduce)
+        _close(f"{tag}{p}mb_stability_adv", s.adv.cpu().numpy(), R("policy_update1/mb_stability_adv"))
         np.testing.assert_allclose(g[p + "policy_update0/mb_stability_adv"], g[p + "policy_update1/mb_stability_adv"])
 
 
@@ -193,14 +201,18 @@ def _check_params(alg, g, it, tag):
             _close(f"{tag}it{it}/log_alpha", got, ref, rtol=1e-6, atol=1e-7)
 
 
-def _run(mode):
+def _run(mode, rank=0, world=1):
+    """mode: eager | graph | segments. world > 1: this process is rank `rank` of a data-parallel
+    group (initialised by the caller); it updates on its share of the batch and of the recorded
+    noise, and must reproduce the reference's FULL-batch update."""
     import torch.distributions.normal as tdn
     from msacl_amd.algorithm.msacl import MSACL
     g = np.load(G)
     B, n = int(g["cfg_B"]), int(g["cfg_n"])
-    data_np = {k: g["in_" + k] for k in KEYS}
+    data_np = {k: _rows(g["in_" + k], rank, world) for k in KEYS}
     data = {k: torch.as_tensor(v, device="cuda") for k, v in data_np.items()}
-    eps = [g[f"eps{i}"] for i in range(int(g["n_eps"]))]
+    eps = [_rows(g[f"eps{i}"], rank, world) for i in range(int(g["n_eps"]))]
+    B = B // world
     feed = NoiseFeed()
     orig = tdn._standard_normal
     tdn._standard_normal = feed
@@ -223,14 +235,14 @@ def _run(mode):
         torch.cuda.synchronize()
         ref_tb = dict(zip([str(k) for k in g["tb_keys"]], g["tb_vals"]))
         for k, v in tb.items():
-            if "time" not in k.lower():
+            if "time" not in k.lower() and world == 1:  # (with world > 1 the tb values are rank-local)
                 _close(f"{mode}/tb/{k}", v, ref_tb[k], rtol=1e-5, atol=1e-5)
-        _check_intermediates(alg, g, 0, data_np, f"{mode}/")
+        _check_intermediates(alg, g, 0, data_np, f"{mode}/", rank, world)
         _check_params(alg, g, 0, f"{mode}/")
         feed.load(eps[3:4])
         assert alg.model_update(data, 1) is None
         torch.cuda.synchronize()
-        _check_intermediates(alg, g, 1, data_np, f"{mode}/")
+        _check_intermediates(alg, g, 1, data_np, f"{mode}/", rank, world)
         _check_params(alg, g, 1, f"{mode}/")
         if mode != "eager":
             assert replays == [(True, True), (True, False)], replays
@@ -238,10 +250,55 @@ def _run(mode):
         tdn._standard_normal = orig
         out = os.path.join(ROOT, "gpurun_out")
         os.makedirs(out, exist_ok=True)
-        with open(os.path.join(out, f"msacl_bench_parity_{mode}.json"), "w") as fh:
+        suffix = "" if world == 1 else f"_rank{rank}of{world}"
+        with open(os.path.join(out, f"msacl_bench_parity_{mode}{suffix}.json"), "w") as fh:
             json.dump(STATS, fh, indent=1)
 
 
 @pytest.mark.parametrize("mode", ["eager", "graph", "segments"])
 def test_bench_config_update_matches_reference(mode):
     _run(mode)
+
+
+def _dp_worker(rank, world, port, mode, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import sys
+    import traceback
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        _run(mode, rank, world)
+        q.put((rank, "ok"))
+    except BaseException:  # report, then let the parent fail the test
+        q.put((rank, traceback.format_exc()[-3000:]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["eager", "segments"])
+def test_two_rank_data_parallel_update_matches_reference_full_batch(mode):
+    """BASELINE config 5's exchange step at the benchmark shapes: 2 ranks (gloo, both on GPU 0 —
+    RCCL refuses two ranks per device), each with half of the 256 windows and its half of the
+    recorded rsample noise. The flat-bucket gradient all-reduces and the (sum, sum of squares)
+    all-reduce of the stability advantage (msacl.py:400) must make every rank's update equal the
+    reference's single-process FULL-batch update, at the same bar as the 1-rank test: per-window
+    intermediates of the rank's rows (incl. the globally normalised advantage) at 1e-5, every
+    gradient element, and the Adam-conditioned parameter bounds. 'segments' replays the update
+    as the chain of HIP graphs cut at the all-reduces (the world > 1 production path)."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=280) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert res[r] == "ok", res[r]
