@@ -22,6 +22,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PEAK_F32_MFMA_TFS = 157.3  # MI355X dense f32 matrix peak (v_mfma_f32_*_f32)
+PMC_TRAFFIC = "r01_pmc_traffic_v3.json"  # the PMC summary of the current kernels (tools/pmc.sh)
 
 
 def parse():
@@ -33,7 +34,7 @@ def parse():
     p.add_argument("--envs", type=int, default=65536, help="parallel envs per GPU")
     p.add_argument("--policy", choices=["init", "hover"], default="init",
                    help="init: PyTorch default init (SURVEY 8d); hover: action mean [mg,0,0,0], long episodes")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU-baseline leg (1x4 threads, Px1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--graph-segments", action="store_true",
                    help="capture the update as graphs cut at its all-reduces (the world size > 1 path)")
@@ -61,27 +62,26 @@ def set_hover_policy(policy, mg):
             last.bias[A + i] = math.log(s)
 
 
-def cpu_baseline(env_name, policy_net, seconds):
-    """Oracle restatement of the reference sampler (per-env Python loop, NumPy policy), 1 thread."""
-    import numpy as np
-    from threadpoolctl import threadpool_limits
-    from oracle.sampler import CpuPolicy, PerEnvCpuSampler
-    lin = [m for m in policy_net.policy if hasattr(m, "weight")]
-    pol = CpuPolicy([(m.weight.detach().cpu().numpy(), m.bias.detach().cpu().numpy()) for m in lin])
-    n_envs = 64
-    with threadpool_limits(limits=1):
-        import torch
-        torch.set_num_threads(1)
-        smp = PerEnvCpuSampler(env_name, n_envs, 20, pol, seed=0)
-        steps = 0
-        t0 = time.perf_counter()
-        while time.perf_counter() - t0 < seconds:
-            smp.step()
-            steps += n_envs
-        dt = time.perf_counter() - t0
-    return {"value": steps / dt, "unit": "env_steps/s", "cores": 1, "kind": "port",
-            "sample": f"{env_name}, {n_envs} envs x {steps // n_envs} lockstep steps ({dt:.1f} s): oracle restatement of "
-                      "BaseSampler._n_step + SyncVectorEnv (per-env Python loop, NumPy MLP policy 256x256, 1 thread)"}
+def cpu_baseline(env_name, seconds):
+    """SURVEY 8(d) CPU baseline of record (tools/cpu_baseline.py): the oracle restatement of the
+    reference CPU sampler as 1 process x 4 threads and as P processes x 1 thread (P = physical
+    cores usable here, <= the box's per-GPU share of 16), in spawned children; value = the
+    P-process node aggregate. The restatement/reference speed ratio was measured in the build
+    container, where the reference itself runs (tools/cpu_ratio.py -> profiles/r02_cpu_ratio.json),
+    and scales the value to a reference-equivalent figure."""
+    from tools.cpu_baseline import measure
+    out = measure(env_name, seconds=seconds)
+    path = os.path.join(ROOT, "profiles", "r02_cpu_ratio.json")
+    try:
+        cal = json.load(open(path))
+        key = next(k for k in cal if k.endswith("proc_1thr") and not k.startswith("1proc"))
+        ratio = float(cal[key]["ratio_reference_over_restatement"])
+        out["reference_equivalent_value"] = round(out["value"] * ratio, 1)
+        out["calibration"] = {"ratio_reference_over_restatement": ratio, "source": "profiles/r02_cpu_ratio.json",
+                              "measured": f"{cal['env']}, {cal['envs_per_process']} envs/process, {key}, build container"}
+    except (OSError, ValueError, StopIteration, KeyError):
+        out["calibration"] = None
+    return out
 
 
 def main():
@@ -214,19 +214,21 @@ def main():
                                      "note": "per lockstep step; f32 MFMA bound, not HBM"}
     dom = "rollout_step" if t_step >= t_emit else "window_emit"
     ach = kernels[dom]["GBps"]
-    traffic = None
-    # HBM bytes per launch from the committed rocprofv3 PMC passes of this same command
-    # (tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)
-    import glob
-    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic*.json")))
-    if pmcs and a.env == "QuadTracking" and a.envs == 65536:
+    # HBM bytes per launch: PMC counters cannot be read from inside this process (rocprofv3 --pmc
+    # wraps the whole command), so `traffic` is the committed measurement of this same command
+    # (tools/pmc.sh: separate FETCH_SIZE / WRITE_SIZE passes, tools/pmc_summary.py applies the
+    # gfx950 FETCH_SIZE correction), named in traffic_source; null when none matches the config
+    traffic, traffic_src = None, None
+    pmc_path = os.path.join(ROOT, "profiles", PMC_TRAFFIC)
+    if a.env == "QuadTracking" and a.envs == 65536 and os.path.exists(pmc_path):
         try:
-            traffic = json.load(open(pmcs[-1])).get(dom, {}).get("bytes_per_launch")
+            traffic = json.load(open(pmc_path)).get(dom, {}).get("bytes_per_launch")
             traffic = None if traffic is None else round(float(traffic), 1)
+            traffic_src = f"profiles/{PMC_TRAFFIC} (rocprofv3 --pmc passes of this bench command; not measured live)"
         except (OSError, ValueError):
             traffic = None
     roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic}
+            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_source": traffic_src}
 
     out = {
         "metric": "env steps/sec (whole node), QuadrotorTracking 65536 envs, 1/2/4/8 MI355X",
@@ -243,7 +245,7 @@ def main():
         "phases": phases,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(a.env, alg.networks.policy, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(a.env, a.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

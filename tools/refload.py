@@ -117,13 +117,22 @@ class RefModule:
         loc["self"] = obj
         if local_extra:
             loc.update(local_extra)
+        cache = self.__dict__.setdefault("_stmt_cache", {})
         for st in node.body:
-            src = ast.unparse(st)
+            hit = cache.get(id(st))
+            if hit is None:  # unparse + compile once per statement (the timing calibration resets often)
+                src = ast.unparse(st)
+                if isinstance(st, ast.Return):
+                    code = compile(ast.Expression(st.value), self.path, "eval")
+                else:
+                    code = compile(ast.Module(body=[st], type_ignores=[]), self.path, "exec")
+                hit = cache[id(st)] = (src, code, isinstance(st, ast.Return))
+            src, code, is_ret = hit
             if skip_pred(src):
                 continue
-            if isinstance(st, ast.Return):
-                return eval(compile(ast.Expression(st.value), self.path, "eval"), loc)
-            exec(compile(ast.Module(body=[st], type_ignores=[]), self.path, "exec"), loc)
+            if is_ret:
+                return eval(code, loc)
+            exec(code, loc)
         return None
 
 
