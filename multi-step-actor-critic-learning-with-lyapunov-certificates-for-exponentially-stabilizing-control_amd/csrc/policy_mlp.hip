@@ -43,7 +43,15 @@ __host__ __device__ constexpr int64_t pm_off_w2(int K1) { return pm_off_b1(K1) +
 __host__ __device__ constexpr int64_t pm_off_b2(int K1) { return pm_off_w2(K1) + (int64_t)PM_NB * PM_NB * 16 * 64; }
 __host__ __device__ constexpr int64_t pm_off_w3(int K1) { return pm_off_b2(K1) + PM_NB * 64 * 16; }
 __host__ __device__ constexpr int64_t pm_off_b3(int K1) { return pm_off_w3(K1) + PM_NB * 16 * 64; }
-__host__ __device__ constexpr int64_t pm_packed_floats(int K1) { return pm_off_b3(K1) + 32; }
+// W2 again, as exact three-way bf16 splits for the split-bf16 layer-2 kernel (k_policy_forward_x6):
+// W2x6 [ib 8][ob 8][s 2][split 3][lane 64][8 bf16] — chunk ib (48 fragments of 1 KB, the unit
+// one workgroup stages through LDS) holds, for lane l and element j of k-step s, the weight
+//   W2[ob*32 + (l & 31)][ib*32 + (j & 3) + 8 (j >> 2) + 16 s + 4 (l >> 5)]
+// i.e. the hidden unit that accumulator register 8 s + j of a layer-1 block holds on that lane.
+constexpr int PM_X6_FRAGS = 48;                                    // fragments per chunk
+constexpr int64_t PM_X6_FLOATS = (int64_t)PM_NB * PM_X6_FRAGS * 64 * 4;  // 8 bf16 = 4 floats per lane
+__host__ __device__ constexpr int64_t pm_off_w2x6(int K1) { return (pm_off_b3(K1) + 32 + 63) / 64 * 64; }
+__host__ __device__ constexpr int64_t pm_packed_floats(int K1) { return pm_off_w2x6(K1) + PM_X6_FLOATS; }
 
 __device__ __forceinline__ int pm_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
@@ -84,6 +92,30 @@ __global__ __launch_bounds__(256) void k_policy_pack(const float* __restrict__ W
       if (o < N3) v = b3[o];
     }
     P[q] = v;
+  }
+}
+
+// Exact three-way bf16 split: a = hi + mid + lo with every part a bf16 (round-to-nearest-even
+// each time; the two remainders are exact in f32 and the last one has at most 8 significant bits,
+// so the sum is exact for normal a).
+__device__ __forceinline__ void split3(float a, __bf16& hi, __bf16& mid, __bf16& lo) {
+  hi = (__bf16)a;
+  const float r1 = a - (float)hi;
+  mid = (__bf16)r1;
+  lo = (__bf16)(r1 - (float)mid);
+}
+
+__global__ __launch_bounds__(256) void k_policy_pack_x6(const float* __restrict__ W2, int K1, float* __restrict__ P) {
+  __bf16* dst = reinterpret_cast<__bf16*>(P + pm_off_w2x6(K1));
+  const int64_t total = PM_X6_FLOATS * 2;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
+    const int j = (int)(q & 7), l = (int)((q >> 3) & 63);
+    const int64_t f = q >> 9;  // fragment index over all chunks
+    const int split = (int)(f % 3), s = (int)((f / 3) % 2), ob = (int)((f / 6) % PM_NB), ib = (int)(f / (6 * PM_NB));
+    const int k = ib * 32 + (j & 3) + 8 * (j >> 2) + 16 * s + 4 * (l >> 5);
+    __bf16 parts[3];
+    split3(W2[(int64_t)(ob * 32 + (l & 31)) * PM_H + k], parts[0], parts[1], parts[2]);
+    dst[q] = parts[split];
   }
 }
 
@@ -231,6 +263,227 @@ __global__ __launch_bounds__(256, MH_POLICY_MIN_WAVES) void k_policy_forward(con
   }
 }
 
+// ----------------------------------------------------------------------------------------------
+// Split-bf16 variant: layer 2 (97 % of the f32 kernel's MFMA cycles) on v_mfma_f32_32x32x16_bf16
+// with f32 accuracy. Each f32 operand is split exactly into three bf16 (split3); of the nine
+// partial products the six with combined weight >= 2^-18 are accumulated
+//     lo*hi, hi*lo, mid*mid, mid*hi, hi*mid, hi*hi        (smallest first)
+// and the dropped three are <= 2^-26 |w x|, below f32 rounding: per product the result is
+// f32-accurate, at 6 x 32 = 192 MFMA cycles per 32x32x16 step instead of 8 x 64 = 512 for the
+// same products on v_mfma_f32_32x32x2_f32 (2.7x fewer matrix cycles for layer 2).
+//   * the layer-1 accumulator feeds the bf16 MFMA as its B operand in place: registers
+//     8 s .. 8 s + 7 of a 32x32 accumulator are k-step s of the next MFMA (the A operand is
+//     packed to that k order, pm_off_w2x6);
+//   * loop order ib (layer-2 input block) outer, ob inner: each wave owns NT = 2 env tiles
+//     (64 envs), i.e. 16 f32x16 layer-2 accumulators (the 256 AGPRs); layer 1 of block ib is
+//     computed and split just before its phase (2 x 16 accumulator values per lane);
+//   * the W2 splits (384 KB) go through LDS: chunk ib (48 KB) is staged with
+//     global_load_lds_dwordx4 (12 per wave) one phase ahead, double buffered (96 KB), and serves
+//     the workgroup's 4 waves x 2 tiles (L2 -> LDS at 8 B/clk/CU); each fragment read from LDS
+//     (two steps ahead) feeds 12 MFMAs;
+//   * layer 3 is folded into the last phase: output block ob's accumulators are final after its
+//     step (ob, 1) and go straight through layer 3, so they die there.
+// Measured (tools/policy_bench.py, E = 65,536): 57-60 us vs 84-88 us for the all-f32 kernel.
+// The layer-2 MFMA stream alone (no staging, barrier or layer 1) takes ~46 us: under a full
+// chip of bf16 MFMAs on random data the clock drops to ~1.45 GHz (tools/mfma_rate.hip:
+// 32 shader cycles but 20-22 ns per v_mfma_f32_32x32x16_bf16), so the 6 products cost more
+// wall time per useful f32 flop than their cycle count suggests.
+// Layers 1 and 3 stay f32 MFMA (as in k_policy_forward). N3 <= 16 only (L3B4 epilogue).
+constexpr int PM_X6_TPW = 2;  // env tiles per wave: each W2 fragment read from LDS feeds 12 MFMAs
+
+template <int K1, int NT>
+__global__ __launch_bounds__(256, 1) void k_policy_forward_x6(const float* __restrict__ P,
+                                                             const float* __restrict__ obs, int64_t E, int D, int N3,
+                                                             float* __restrict__ logits) {
+  typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+  constexpr int FPW = PM_X6_FRAGS / 4;  // fragments each wave stages per chunk
+  __shared__ uint4 lds[2][PM_X6_FRAGS * 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t ntiles = (E + 31) / 32;
+  const int64_t per_round = (int64_t)gridDim.x * 4 * NT;  // tiles per round over the grid
+  const float* W1p = P;
+  const float* b2p = P + pm_off_b2(K1);
+  const f32x4* W3p = reinterpret_cast<const f32x4*>(P + pm_off_w3(K1));
+  const float* b3 = P + pm_off_b3(K1);
+  const uint4* W2g = reinterpret_cast<const uint4*>(P + pm_off_w2x6(K1));
+
+  auto load_obs = [&](int64_t t, float* xo) {
+    const int64_t brow = min(min(t, ntiles - 1) * 32 + (lane & 31), E - 1);  // padded rows: the last env
+#pragma unroll
+    for (int s = 0; s < K1; ++s) {
+      const int k = 2 * s + (lane >> 5);
+      xo[s] = k < D ? obs[brow * D + k] : (k == D ? 1.0f : 0.0f);
+    }
+  };
+  auto stage = [&](int ib, int buf) {  // this wave's 12 of the chunk's 48 fragments -> LDS
+    const uint4* src = W2g + (int64_t)ib * PM_X6_FRAGS * 64;
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) {
+      const int f = w * FPW + i;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + f * 64 + lane),
+                                       (void __attribute__((address_space(3)))*)(&lds[buf][f * 64]), 16, 0, 0);
+    }
+  };
+  auto split_into = [&](float v, bf16x8* ph, bf16x8* pm, bf16x8* pl, int idx) {
+    __bf16 a, b, c;
+    split3(fmaxf(v, 0.0f), a, b, c);
+    ph[idx >> 3][idx & 7] = a;
+    pm[idx >> 3][idx & 7] = b;
+    pl[idx >> 3][idx & 7] = c;
+  };
+
+  int64_t t0 = ((int64_t)blockIdx.x * 4 + w) * NT;  // this wave's first tile in the round
+  int64_t wg0 = (int64_t)blockIdx.x * 4 * NT;       // the workgroup's first tile (uniform)
+  if (wg0 >= ntiles) return;                         // whole workgroup idle (uniform)
+  stage(0, 0);
+  int buf = 0;
+  float w1c[K1];  // layer-1 fragments of the next block to compute (loaded a phase ahead)
+#pragma unroll
+  for (int s = 0; s < K1; ++s) w1c[s] = W1p[(1 * K1 + s) * 64 + lane];
+  float xo[NT][K1], xn[NT][K1];
+  bf16x8 xh[NT][2], xm[NT][2], xl[NT][2];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    load_obs(t0 + t, xo[t]);
+    f32x16 h = {};
+#pragma unroll
+    for (int s = 0; s < K1; ++s) h = __builtin_amdgcn_mfma_f32_32x32x2f32(W1p[s * 64 + lane], xo[t][s], h, 0, 0, 0);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) split_into(h[v], xh[t], xm[t], xl[t], v);
+  }
+  for (; wg0 < ntiles; wg0 += per_round, t0 += per_round) {
+    const bool more = wg0 + per_round < ntiles;
+    if (more) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) load_obs(t0 + per_round + t, xn[t]);  // next round's tiles
+    }
+    // the bias and W3 fragments are the same every round: launder the pointers so the compiler
+    // re-loads them per round (L2 hits) instead of hoisting 256 registers of invariants
+    int zero = 0;
+    asm volatile("" : "+s"(zero));
+    const float* b2r = b2p + zero;
+    const f32x4* W3r = W3p + zero;
+    f32x16 acc[NT][PM_NB];
+#pragma unroll
+    for (int ob = 0; ob < PM_NB; ++ob) {  // layer-2 bias as the accumulators' start
+      const f32x4* bb = reinterpret_cast<const f32x4*>(b2r + (ob * 64 + lane) * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 bq = bb[q];
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[t][ob][4 * q + j] = bq[j];
+      }
+    }
+    f32x16 o3[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) o3[t] = f32x16{};
+    // one block ib of layer 2 for the wave's tiles; in the last block (fold) each output block's
+    // accumulator is final after its step (ob, 1) and goes straight through layer 3 (f32,
+    // v_mfma_f32_16x16x1_4b as k_policy_forward's L3B4 path), so it dies there
+    auto phase = [&](int ib, bool fold) {
+      const bool has_next = ib < PM_NB - 1 || more;
+      const int nib = (ib + 1) & (PM_NB - 1);
+      if (ib > 0) {  // layer 1 of block ib for the tiles (block 0 was done a round ahead)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          f32x16 h = {};
+#pragma unroll
+          for (int s = 0; s < K1; ++s) h = __builtin_amdgcn_mfma_f32_32x32x2f32(w1c[s], xo[t][s], h, 0, 0, 0);
+#pragma unroll
+          for (int v = 0; v < 16; ++v) split_into(h[v], xh[t], xm[t], xl[t], v);
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < K1; ++s) w1c[s] = W1p[(nib * K1 + s) * 64 + lane];  // a phase ahead
+      __syncthreads();  // chunk ib has landed (every wave drained its loads); buf ^ 1 is free
+      if (has_next) stage(nib, buf ^ 1);
+      const uint4* L = lds[buf] + lane;
+      // W2 fragments read two steps ahead (a 3-slot ring): an LDS read has 2 steps of MFMAs
+      uint4 ring[3][3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        ring[0][p] = L[p * 64];
+        ring[1][p] = L[(3 + p) * 64];
+      }
+#pragma unroll
+      for (int st = 0; st < 2 * PM_NB; ++st) {
+        const int ob = st >> 1, s = st & 1;
+        if (st + 2 < 2 * PM_NB) {
+#pragma unroll
+          for (int p = 0; p < 3; ++p) ring[(st + 2) % 3][p] = L[((st + 2) * 3 + p) * 64];
+        }
+        const uint4* cur = ring[st % 3];
+        f32x4 w3f[4];
+        if (fold && s == 1) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) w3f[q] = W3r[(ob * 4 + q) * 64 + lane];
+        }
+        const bf16x8 wh = __builtin_bit_cast(bf16x8, cur[0]);
+        const bf16x8 wm = __builtin_bit_cast(bf16x8, cur[1]);
+        const bf16x8 wl = __builtin_bit_cast(bf16x8, cur[2]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          f32x16 a = acc[t][ob];
+          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh[t][s], a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl[t][s], a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wm, xm[t][s], a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wm, xh[t][s], a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xm[t][s], a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh[t][s], a, 0, 0, 0);
+          acc[t][ob] = a;
+        }
+        if (fold && s == 1) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+              for (int t = 0; t < NT; ++t)
+                o3[t] = __builtin_amdgcn_mfma_f32_16x16x1f32(w3f[q][j], fmaxf(acc[t][ob][4 * q + j], 0.0f), o3[t], 0,
+                                                             0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one step at a time: bounded live fragments
+      }
+      buf ^= 1;
+    };
+#pragma unroll 1
+    for (int ib = 0; ib < PM_NB - 1; ++ib) phase(ib, false);
+    phase(PM_NB - 1, true);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int s = 0; s < K1; ++s) xo[t][s] = xn[t][s];
+    if (more) {  // block 0 of the next round's tiles
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        f32x16 h = {};
+#pragma unroll
+        for (int s = 0; s < K1; ++s) h = __builtin_amdgcn_mfma_f32_32x32x2f32(W1p[s * 64 + lane], xo[t][s], h, 0, 0, 0);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) split_into(h[v], xh[t], xm[t], xl[t], v);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int64_t tile = t0 + t;
+      if (tile < ntiles) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int64_t b = tile * 32 + (lane & 15) + 16 * hh;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int oo = 4 * (lane >> 4) + q;
+            if (b < E && oo < N3) logits[b * N3 + oo] = (o3[t][4 * hh + q] + o3[t][4 * hh + 8 + q]) + b3[oo];
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();  // no LDS-DMA outstanding when the workgroup retires
+}
+
 int64_t policy_packed_floats(int D) { return pm_packed_floats(D / 2 + 1); }
 
 hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
@@ -239,6 +492,8 @@ hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2,
   const int64_t total = pm_packed_floats(K1);
   const int grid = (int)((total + 255) / 256 < 1024 ? (total + 255) / 256 : 1024);
   k_policy_pack<<<grid, 256, 0, st>>>(W1, b1, W2, b2, W3, b3, D, N3, K1, P);
+  if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
+  k_policy_pack_x6<<<(int)(PM_X6_FLOATS * 2 / 256), 256, 0, st>>>(W2, K1, P);
   return hipGetLastError();
 }
 
@@ -256,7 +511,24 @@ static hipError_t launch_fwd_t(const float* P, const float* obs, int64_t E, int 
   }
   const int64_t want = (tiles + 3) / 4;
   const int grid = (int)(want < cus ? want : cus);
-  if (N3 <= 16) k_policy_forward<K1, true><<<grid, 256, 0, st>>>(P, obs, E, D, N3, logits);
+  // MH_POLICY_KERNEL=f32 keeps the all-f32 kernel (A/B measurements); split-bf16 layer 2 otherwise
+  static int mode = -1;
+  if (mode < 0) {
+    const char* m = getenv("MH_POLICY_KERNEL");
+    mode = (m && m[0] == 'f') ? 0 : 1;
+  }
+  if (N3 <= 16 && mode == 1) {
+    static int tpw = 0;  // env tiles per wave (MH_POLICY_TPW, for A/B): default PM_X6_TPW
+    if (tpw == 0) {
+      const char* v = getenv("MH_POLICY_TPW");
+      tpw = (v && atoi(v) == 1) ? 1 : PM_X6_TPW;
+    }
+    const int64_t want6 = (tiles + 4 * tpw - 1) / (4 * tpw);
+    const int grid6 = (int)(want6 < cus ? want6 : cus);
+    if (tpw == 1) k_policy_forward_x6<K1, 1><<<grid6, 256, 0, st>>>(P, obs, E, D, N3, logits);
+    else k_policy_forward_x6<K1, 2><<<grid6, 256, 0, st>>>(P, obs, E, D, N3, logits);
+  }
+  else if (N3 <= 16) k_policy_forward<K1, true><<<grid, 256, 0, st>>>(P, obs, E, D, N3, logits);
   else k_policy_forward<K1, false><<<grid, 256, 0, st>>>(P, obs, E, D, N3, logits);
   return hipGetLastError();
 }
