@@ -1,4 +1,5 @@
-"""ctypes binding of include/msacl_hip.h (the engine's C ABI).
+"""ctypes binding of include/msacl_hip.h (the engine's C ABI) and include/msacl_host.h (its CPU
+build, config 1: host_lib()).
 
 The library is built in-tree by `make -C csrc` (or __graft_entry__.build()) into
 csrc/build/libmsacl_hip.so. There is no CPU fallback anywhere in the product path: if the
@@ -143,6 +144,79 @@ def lib():
 
 def exported_symbols():
     return list(_PROTOS)
+
+
+# ------------------------------------------------------------------ CPU build (config 1)
+HOST_LIB_PATH = os.environ.get("MSACL_HOST_LIB", os.path.join(_HERE, "csrc", "build", "libmsacl_host.so"))
+_HOST_PROTOS = {
+    "mhh_abi_version": (ctypes.c_int, []),
+    "mhh_last_error": (ctypes.c_char_p, []),
+    "mhh_env_info": (ctypes.c_int, [c_i32, ctypes.POINTER(EnvInfo)]),
+    "mhh_env_create": (ctypes.c_int, [c_i32, c_i64, c_u64, ctypes.POINTER(c_vp)]),
+    "mhh_env_destroy": (ctypes.c_int, [c_vp]),
+    "mhh_env_reset": (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    "mhh_env_step": (ctypes.c_int, [c_vp] * 8),
+    "mhh_env_get_state": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
+    "mhh_env_set_state": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp]),
+    "mhh_msacl_q_target": (ctypes.c_int, [c_vp] * 9 + [c_f32, c_i32, c_i32] + [c_vp] * 5),
+    "mhh_msacl_lyapunov": (ctypes.c_int, [c_vp] * 9 + [c_f32] * 4 + [c_i32] * 3 + [c_vp] * 6),
+    "mhh_msacl_stability_adv": (ctypes.c_int, [c_vp] * 4 + [c_i32, c_i32, c_vp, c_vp]),
+    "mhh_msacl_ppo_clip": (ctypes.c_int, [c_vp, c_vp, c_vp, c_f64, c_f32, c_i32, c_vp, c_vp, c_vp]),
+    "mhh_msacl_policy_loss": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_vp, c_vp]),
+    "mhh_msacl_policy_loss_backward": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_vp, c_vp, c_vp]),
+    "mhh_msacl_ratio0": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_vp]),
+    "mhh_msacl_ratio0_backward": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_vp]),
+}
+_host = None
+
+
+def host_lib():
+    """Load the engine's CPU build (raises if it has not been built). Selected explicitly by
+    device="cpu"; the GPU path never falls back to it."""
+    global _host
+    if _host is None:
+        if not os.path.exists(HOST_LIB_PATH):
+            raise RuntimeError(f"MSACL host engine library not found at {HOST_LIB_PATH}; build it with "
+                               f"`make -C {os.path.join(_HERE, 'csrc')}` (or __graft_entry__.build()).")
+        L = ctypes.CDLL(HOST_LIB_PATH)
+        for name, (res, args) in _HOST_PROTOS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.mhh_abi_version() != 1:
+            raise RuntimeError("libmsacl_host ABI version mismatch")
+        _host = L
+    return _host
+
+
+def host_env_info(name_or_id):
+    eid = ENV_IDS[name_or_id] if isinstance(name_or_id, str) else int(name_or_id)
+    info = EnvInfo()
+    host_check(host_lib().mhh_env_info(eid, ctypes.byref(info)), "mhh_env_info")
+    return info
+
+
+def host_exported_symbols():
+    return list(_HOST_PROTOS)
+
+
+def host_check(rc, what=""):
+    if rc != 0:
+        msg = host_lib().mhh_last_error()
+        raise RuntimeError(f"{what} failed (code {rc}): {msg.decode() if msg else ''}")
+
+
+def hptr(t):
+    """Host pointer of a contiguous CPU tensor or numpy array (None -> NULL)."""
+    if t is None:
+        return None
+    if hasattr(t, "data_ptr"):
+        if t.device.type != "cpu" or not t.is_contiguous():
+            raise ValueError("the host engine takes contiguous CPU tensors")
+        return ctypes.c_void_p(t.data_ptr())
+    if not t.flags["C_CONTIGUOUS"]:
+        raise ValueError("the host engine takes C-contiguous arrays")
+    return ctypes.c_void_p(t.ctypes.data)
 
 
 def check(rc, what=""):

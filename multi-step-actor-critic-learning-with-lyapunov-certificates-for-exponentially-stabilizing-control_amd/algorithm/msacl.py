@@ -12,6 +12,9 @@ network outputs, which is handed to autograd:
 Data-parallel (one rank per GPU): every optimiser step all-reduces its gradients as one flat
 bucket over RCCL, and the advantage normalisation all-reduces its (sum, sumsq) so the batch
 statistic is the global batch's (msacl.py:400).
+With an explicit device="cpu" (BASELINE.json config 1) the same update runs on the CPU, the
+target math through the engine's CPU build (libmsacl_host.so, mhh_msacl_*: the same element
+formulas as host loops) — chosen by configuration, never as a fallback of the HIP path.
 """
 __all__ = ["ApproxContainer", "MSACL"]
 
@@ -36,6 +39,14 @@ def _adam(params, lr):
     float32 parameters), so the whole update can be replayed as a HIP graph."""
     from ._update_graph import fused_adam
     return fused_adam(params, lr)
+
+
+def _engine(name, device, *args):
+    """mh_<name>(*args, stream) on a HIP device; mhh_<name>(*args) of the CPU build on the CPU."""
+    if device.type == "cpu":
+        N.host_check(getattr(N.host_lib(), "mhh_" + name)(*args), "mhh_" + name)
+    else:
+        N.check(getattr(N.lib(), "mh_" + name)(*args, N.stream_of(device)), "mh_" + name)
 
 
 class ApproxContainer(nn.Module):
@@ -75,9 +86,8 @@ class _PolicyQLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q1, q2, logp, log_alpha):
         out = torch.empty(2, dtype=torch.float32, device=q1.device)
-        N.check(N.lib().mh_msacl_policy_loss(N.ptr(q1), N.ptr(q2), N.ptr(logp), N.ptr(log_alpha), q1.numel(),
-                                             N.ptr(out[0:1]), N.ptr(out[1:2]), N.stream_of(q1.device)),
-                "mh_msacl_policy_loss")
+        _engine("msacl_policy_loss", q1.device, N.ptr(q1), N.ptr(q2), N.ptr(logp), N.ptr(log_alpha), q1.numel(),
+                N.ptr(out[0:1]), N.ptr(out[1:2]))
         ctx.save_for_backward(q1, q2, log_alpha)
         loss, entropy = out[0], out[1]
         ctx.mark_non_differentiable(entropy)
@@ -87,10 +97,8 @@ class _PolicyQLoss(torch.autograd.Function):
     def backward(ctx, g_loss, g_entropy):
         q1, q2, log_alpha = ctx.saved_tensors
         dq1, dq2, dlogp = torch.empty_like(q1), torch.empty_like(q2), torch.empty_like(q1)
-        N.check(N.lib().mh_msacl_policy_loss_backward(N.ptr(q1), N.ptr(q2), N.ptr(log_alpha),
-                                                      N.ptr(g_loss.contiguous()), q1.numel(), N.ptr(dq1), N.ptr(dq2),
-                                                      N.ptr(dlogp), N.stream_of(q1.device)),
-                "mh_msacl_policy_loss_backward")
+        _engine("msacl_policy_loss_backward", q1.device, N.ptr(q1), N.ptr(q2), N.ptr(log_alpha),
+                N.ptr(g_loss.contiguous()), q1.numel(), N.ptr(dq1), N.ptr(dq2), N.ptr(dlogp))
         return dq1, dq2, dlogp, None
 
 
@@ -101,8 +109,7 @@ class _Ratio0(torch.autograd.Function):
     def forward(ctx, lp, old):
         B, n = lp.shape
         ratio = torch.empty(B, dtype=torch.float32, device=lp.device)
-        N.check(N.lib().mh_msacl_ratio0(N.ptr(lp), N.ptr(old), B, n, N.ptr(ratio), N.stream_of(lp.device)),
-                "mh_msacl_ratio0")
+        _engine("msacl_ratio0", lp.device, N.ptr(lp), N.ptr(old), B, n, N.ptr(ratio))
         ctx.save_for_backward(ratio)
         ctx.n = n
         return ratio
@@ -112,8 +119,7 @@ class _Ratio0(torch.autograd.Function):
         (ratio,) = ctx.saved_tensors
         B, n = ratio.shape[0], ctx.n
         dlp = torch.empty(B, n, dtype=torch.float32, device=ratio.device)
-        N.check(N.lib().mh_msacl_ratio0_backward(N.ptr(ratio), N.ptr(g.contiguous()), B, n, N.ptr(dlp),
-                                                 N.stream_of(ratio.device)), "mh_msacl_ratio0_backward")
+        _engine("msacl_ratio0_backward", ratio.device, N.ptr(ratio), N.ptr(g.contiguous()), B, n, N.ptr(dlp))
         return dlp, None
 
 
@@ -142,7 +148,7 @@ class MSACL:
         if dev is None:
             dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else None
         if dev is None:
-            raise RuntimeError("MSACL's fused target kernels need a HIP device; no CPU fallback exists")
+            raise RuntimeError("MSACL's fused target kernels need a HIP device (device=\"cpu\" selects the CPU build)")
         self.device = torch.device(dev)
         self.networks = ApproxContainer(**kwargs).to(self.device)
         self.gamma, self.retrace_lambda, self.lya_eta, self.tau = gamma, retrace_lambda, lya_eta, tau
@@ -348,7 +354,7 @@ class MSACL:
 
     # ------------------------------------------------------------------ HIP-graph replay
     def _graphable(self):
-        return (self.use_graph and not self.anneal_lr and torch.cuda.is_available()
+        return (self.use_graph and not self.anneal_lr and self.device.type == "cuda" and torch.cuda.is_available()
                 and not torch.cuda.is_current_stream_capturing())
 
     def _segmented(self):
@@ -411,11 +417,12 @@ class MSACL:
 
         (q1, q1t), (q2, q2t) = self._twin_pair(critic1, critic2)
         weight = data.get("weight") if self.per_flag else None
-        N.check(N.lib().mh_msacl_q_target(
+        _engine(
+            "msacl_q_target", self.device,
             N.ptr(q1.detach().contiguous()), N.ptr(q2.detach().contiguous()), N.ptr(q1t), N.ptr(q2t),
             N.ptr(next_logp.contiguous()), N.ptr(rew), N.ptr(done), N.ptr(self.networks.log_alpha.detach()),
             N.ptr(weight.contiguous() if weight is not None else None), float(self.gamma), B, n, N.ptr(s.backup),
-            N.ptr(s.dq1), N.ptr(s.dq2), N.ptr(s.loss_q), N.ptr(s.abs_td), N.stream_of(self.device)), "mh_msacl_q_target")
+            N.ptr(s.dq1), N.ptr(s.dq2), N.ptr(s.loss_q), N.ptr(s.abs_td))
         self.networks.q1_optimizer.zero_grad()
         self.networks.q2_optimizer.zero_grad()
         torch.autograd.backward([q1, q2], [s.dq1, s.dq2])
@@ -437,12 +444,13 @@ class MSACL:
         # one backward instead of two each (the weight gradients sum the same 2 B n rows)
         V_both = self.networks.lyapunov(torch.cat([obs, obs2], 0))
         V, V2 = V_both[:B], V_both[B:]
-        N.check(N.lib().mh_msacl_lyapunov(
+        _engine(
+            "msacl_lyapunov", self.device,
             N.ptr(logp), N.ptr(old_logp), N.ptr(V.detach().contiguous()), N.ptr(V2.detach().contiguous()), N.ptr(obs),
             N.ptr(obs2), N.ptr(self.start_obs_norm_coef), N.ptr(self.lya_diff_coef), N.ptr(self.start_lya_coef),
             float(self.alpha1), float(self.alpha2), float(self.lya_positive_scale), float(self.lya_diff_scale), B, n,
             obs.shape[-1], N.ptr(s.is_clip), N.ptr(s.esl), N.ptr(s.lya_diff), N.ptr(s.loss_lya), N.ptr(s.dV),
-            N.ptr(s.dV2), N.stream_of(self.device)), "mh_msacl_lyapunov")
+            N.ptr(s.dV2))
         self.networks.lyapunov_optimizer.zero_grad()
         torch.autograd.backward([V_both], [s.dV_both])
         if not defer_step:
@@ -470,15 +478,13 @@ class MSACL:
             V_all = self.networks.lyapunov(torch.cat([obs[:, 0], obs2.reshape(-1, D_)], 0))
             V0 = V_all[:B].contiguous()
             V2 = V_all[B:].reshape(B, n).contiguous()
-        N.check(N.lib().mh_msacl_stability_adv(N.ptr(V0), N.ptr(V2), N.ptr(self.lya_diff_coef), N.ptr(self.start_lya_coef),
-                                               B, n, N.ptr(s.adv_raw), N.ptr(s.stats), N.stream_of(self.device)),
-                "mh_msacl_stability_adv")
+        _engine("msacl_stability_adv", self.device, N.ptr(V0), N.ptr(V2), N.ptr(self.lya_diff_coef),
+                N.ptr(self.start_lya_coef), B, n, N.ptr(s.adv_raw), N.ptr(s.stats))
         D.allreduce_(s.stats)
         n_total = float(B * D.world_size())
         r_det = is_ratio.detach().contiguous()
-        N.check(N.lib().mh_msacl_ppo_clip(N.ptr(r_det), N.ptr(s.adv_raw), N.ptr(s.stats), n_total, float(self.clip_coef), B,
-                                          N.ptr(s.adv), N.ptr(s.loss_ppo), N.ptr(s.d_ratio), N.stream_of(self.device)),
-                "mh_msacl_ppo_clip")
+        _engine("msacl_ppo_clip", self.device, N.ptr(r_det), N.ptr(s.adv_raw), N.ptr(s.stats), n_total,
+                float(self.clip_coef), B, N.ptr(s.adv), N.ptr(s.loss_ppo), N.ptr(s.d_ratio))
         loss_policy = -loss_policy_q.detach() - s.loss_ppo[0]
         self.networks.policy_optimizer.zero_grad()
         torch.autograd.backward([loss_policy_q, is_ratio], [self._neg_one, -s.d_ratio])

@@ -46,7 +46,7 @@ class HipVectorEnv:
         self.env_id = env_id
         self.num_envs = int(num_envs)
         self.seed = int(seed) & ((1 << 64) - 1)
-        self.info = N.env_info(env_id)
+        self.info = self._env_info(env_id)
         D, A = self.info.obs_dim, self.info.act_dim
         self.obs_dim, self.act_dim = D, A
         self.state_dim, self.xstate_dim = self.info.state_dim, self.info.xstate_dim
@@ -59,6 +59,10 @@ class HipVectorEnv:
                                 np.tile(self.single_action_space.high, (self.num_envs, 1)))
         self._device = device
         self._h = None
+
+    @staticmethod
+    def _env_info(env_id):
+        return N.env_info(env_id)
 
     # ------------------------------------------------------------------ device handle
     @property

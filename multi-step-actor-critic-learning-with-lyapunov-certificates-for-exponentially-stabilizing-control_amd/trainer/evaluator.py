@@ -6,13 +6,14 @@ the per-step MEAN scaled reward and cost (rew_plus_cost scales); sequential eval
 episodes on one env and reports mean/std of the episode SUMS. The rollout is the HIP env step
 kernel; per-episode means accumulate on the device in float64 (the reference's np.mean of a
 float32 list sums pairwise in float32), episode sums in float32 in step order exactly like the
-reference's sum(); completion is checked on the host once every 8 lockstep steps.
+reference's sum(); completion is checked on the host once every 8 lockstep steps. With an
+explicit device="cpu" the same loop runs on the engine's CPU build (env/host_vector_env.py).
 """
 import numpy as np
 import torch
 
 from ..create_pkg.create_alg import create_approx_contrainer
-from ..env.hip_vector_env import HipVectorEnv
+from ..env.host_vector_env import make_vector_env
 
 
 class Evaluator:
@@ -27,7 +28,7 @@ class Evaluator:
         dev = kwargs.get("device")
         self.device = torch.device(dev) if dev is not None else torch.device("cuda", torch.cuda.current_device())
         env_num = self.num_eval_episode if self.is_parallel_eval else 1
-        self.envs = HipVectorEnv(self.env_id, env_num, seed=int(self.seed) + 7919 * (index + 1), device=self.device)
+        self.envs = make_vector_env(self.env_id, env_num, seed=int(self.seed) + 7919 * (index + 1), device=self.device)
         self.networks = create_approx_contrainer(**kwargs)
         self.render = kwargs.get("is_render", False)
         self.action_type = kwargs["action_type"]

@@ -18,7 +18,9 @@ def init_args(envs, **args):
         threads = 4 if "serial" in args["trainer"] else 1
     torch.set_num_threads(threads)
 
-    if args.get("enable_cuda", True) and torch.cuda.is_available():
+    dev = args.get("device")
+    cpu_build = dev is not None and torch.device(dev).type == "cpu"  # config 1: the engine's CPU build
+    if args.get("enable_cuda", True) and torch.cuda.is_available() and not cpu_build:
         args["use_gpu"] = True
         # GEMM library behind the PyTorch MLPs of the update: rocBLAS measured 6 % faster than
         # hipBLASLt on the MSACL update shapes (the weight-gradient GEMMs, K = B * n = 5,120 with a
@@ -31,7 +33,7 @@ def init_args(envs, **args):
         from ..apprfunc._fused import set_gemm_backend
         set_gemm_backend(args.get("update_gemm", "auto"))
     else:
-        if args.get("enable_cuda", True):
+        if args.get("enable_cuda", True) and not cpu_build:
             warnings.warn("HIP device is not available, use CPU instead")
         args["use_gpu"] = False
     args["batch_size_per_sampler"] = args["sample_batch_size"]

@@ -142,3 +142,21 @@ def test_n20_windows_tiled_to_65536_envs(path):
         bad = ((got - exp).abs() > TOL["atol"] + TOL["rtol"] * exp.abs()).sum().item()
         assert bad == 0, (k, bad)
     assert not buf.n_step_buf["done"][:total, :-1].any()
+
+
+@pytest.mark.parametrize("path", TRACES, ids=os.path.basename)
+def test_host_and_device_builds_agree(path):
+    """Config 1's CPU build (libmsacl_host.so) and the gfx950 kernels run the same env math: the
+    same injected trace through both gives the same windows (VanderPol bit-exact, the others at
+    the north-star tolerance, their transcendentals coming from two libms)."""
+    from test_host_engine import _cpu_trace
+    g, dbuf, total, _ = _run_trace(path)
+    _, hbuf = _cpu_trace(path)
+    assert hbuf.size == dbuf.size == total
+    for k in KEYS:
+        d = dbuf.n_step_buf[k][:total].cpu().numpy()
+        h = hbuf.n_step_buf[k][:total]
+        if "VanderPol" in path:
+            np.testing.assert_array_equal(h, d, err_msg=k)
+        else:
+            np.testing.assert_allclose(h, d, **TOL, err_msg=k)
