@@ -19,12 +19,15 @@
 //
 // Fixed shape: hidden sizes 256 x 256 (the default of every reference training script), ReLU
 // hidden activation, identity output, D <= 16, N3 <= 32. Other shapes use the PyTorch path.
+#include <type_traits>
+
 #include "rollout.h"
 
 namespace mh {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr int PM_H = 256;           // hidden width (both layers)
 constexpr int PM_NB = PM_H / 32;    // 32-row blocks per hidden layer
@@ -51,7 +54,24 @@ __host__ __device__ constexpr int64_t pm_off_b3(int K1) { return pm_off_w3(K1) +
 constexpr int PM_X6_FRAGS = 48;                                    // fragments per chunk
 constexpr int64_t PM_X6_FLOATS = (int64_t)PM_NB * PM_X6_FRAGS * 64 * 4;  // 8 bf16 = 4 floats per lane
 __host__ __device__ constexpr int64_t pm_off_w2x6(int K1) { return (pm_off_b3(K1) + 32 + 63) / 64 * 64; }
-__host__ __device__ constexpr int64_t pm_packed_floats(int K1) { return pm_off_w2x6(K1) + PM_X6_FLOATS; }
+// The split-f16 kernel's operands (k_policy_forward_x3), every weight scaled by a power of two
+// sw1 / sw2 / sw3 (max |.| of the layer in [2^13, 2^14]) and split into two f16 (hi, lo):
+//   W1x3 [blk 8][split 2][lane 64][8 f16]        W1[blk*32 + (l & 31)][8 (l >> 5) + j] * sw1,
+//                                                b1 at k = D (constant-1 input), 0 beyond
+//   W2x3 [ib 8][ob 8][s 2][split 2][lane 64][8 f16]   the W2x6 k order, * sw2
+//   W3x3 [ob 8][s 2][split 2][lane 64][8 f16]    W3[l & 31][ob*32 + (j & 3) + 8 (j >> 2) + 16 s + 4 (l >> 5)]
+//                                                * sw3 (0 for rows >= N3)
+constexpr int PM_X3_FRAGS = 32;                                      // W2x3 fragments per chunk
+constexpr int64_t PM_X3_FLOATS = (int64_t)PM_NB * PM_X3_FRAGS * 64 * 4;
+constexpr int64_t PM_X3_W1_FLOATS = (int64_t)PM_NB * 2 * 64 * 4;
+constexpr int64_t PM_X3_W3_FLOATS = (int64_t)PM_NB * 4 * 64 * 4;
+__host__ __device__ constexpr int64_t pm_off_w2x3(int K1) { return pm_off_w2x6(K1) + PM_X6_FLOATS; }
+__host__ __device__ constexpr int64_t pm_off_w1x3(int K1) { return pm_off_w2x3(K1) + PM_X3_FLOATS; }
+__host__ __device__ constexpr int64_t pm_off_w3x3(int K1) { return pm_off_w1x3(K1) + PM_X3_W1_FLOATS; }
+// scalars: [0..2] sw1, sw2, sw3; [3..5] their inverses; [6] R1 = max_k (sum_j |W1[k][j]| + |b1[k]|),
+// [7] R2 = max_o (sum_k |W2[o][k]| + |b2[o]|): |H1| <= R1 max(1, max |obs|), |H2| <= R2 max(1, |H1|)
+__host__ __device__ constexpr int64_t pm_off_scal(int K1) { return pm_off_w3x3(K1) + PM_X3_W3_FLOATS; }
+__host__ __device__ constexpr int64_t pm_packed_floats(int K1) { return pm_off_scal(K1) + 64; }
 
 __device__ __forceinline__ int pm_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
@@ -60,7 +80,7 @@ __global__ __launch_bounds__(256) void k_policy_pack(const float* __restrict__ W
                                                      const float* __restrict__ W2, const float* __restrict__ b2,
                                                      const float* __restrict__ W3, const float* __restrict__ b3,
                                                      int D, int N3, int K1, float* __restrict__ P) {
-  const int64_t total = pm_packed_floats(K1);
+  const int64_t total = pm_off_w2x6(K1);  // the f32 regions (the split copies have their own packers)
   for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
     float v = 0.0f;
     if (q < pm_off_b1(K1)) {
@@ -484,16 +504,413 @@ __global__ __launch_bounds__(256, 1) void k_policy_forward_x6(const float* __res
   __syncthreads();  // no LDS-DMA outstanding when the workgroup retires
 }
 
+// ----------------------------------------------------------------------------------------------
+// Split-f16 variant: all three layers on v_mfma_f32_32x32x16_f16 with THREE partial products per
+// operand pair. f16 carries 11 significant bits (bf16: 8), so a two-way split a = hi + lo holds 22
+// bits; keeping hi*hi, hi*lo, lo*hi drops lo*lo (<= 2^-22 |w x|), and the split residual is
+// <= 2^-22 |a| per operand: every product is within ~3 * 2^-22 = 7e-7 of exact (f32: 6e-8 per
+// rounding; the north star allows 1e-5). f16's narrow exponent range is handled by power-of-two
+// scaling, exact in f32: each layer's weights by sw_l (pack time, max |W_l| * sw_l <= 2^14) and
+// each env's input column of each layer by a per-env power of two from a bound on its magnitude
+// (obs: max |obs|; H1: R1 max(1, max |obs|); H2: R2 max(1, bound(H1))), so every split operand is
+// <= 2^14 whatever the observation; accumulators are unscaled exactly (power-of-two products) and
+// the biases join after the unscaling (b1 rides in the MFMA as the weight of a constant input).
+// The splits' subnormal floor is 2^-25 in scaled units, i.e. <= 2^-39 of the operand bound.
+// Layer 2 as k_policy_forward_x6 (LDS-staged W2 chunks, NT = 2 tiles per wave, double-buffered,
+// read two steps ahead) with 32 instead of 48 fragments per chunk and half the MFMAs; layer 1 is
+// 3 MFMAs per 32-row block (K = 16 covers obs + bias for D <= 15); layer 3 is folded into the
+// last phase: output block ob's accumulators are final after its step (ob, 1), go through bias,
+// ReLU and the split, and into 2 x 3 MFMAs against W3x3 staged once per kernel in LDS.
+__device__ __forceinline__ float pm_pow2(int e) {  // 2^e for e in [-126, 127]
+  return __uint_as_float((uint32_t)(127 + e) << 23);
+}
+__device__ __forceinline__ int pm_scale_exp(float bound) {  // 14 - ceil(log2(bound)), clamped
+  if (!(bound > 0.0f) || bound != bound) return 0;
+  int e;
+  (void)frexpf(bound, &e);  // bound = m 2^e, m in [0.5, 1): bound <= 2^e
+  const int k = 14 - e;
+  return k < -40 ? -40 : (k > 40 ? 40 : k);
+}
+
+// One workgroup: the layer scales and the magnitude bounds R1, R2.
+__global__ __launch_bounds__(256) void k_policy_scales(const float* __restrict__ W1, const float* __restrict__ b1,
+                                                       const float* __restrict__ W2, const float* __restrict__ b2,
+                                                       const float* __restrict__ W3, int D, int N3, int K1,
+                                                       float* __restrict__ P) {
+  __shared__ float red[5][256];
+  float m1 = 0.0f, m2 = 0.0f, m3 = 0.0f, r1 = 0.0f, r2 = 0.0f;
+  for (int i = threadIdx.x; i < PM_H * PM_H; i += 256) m2 = fmaxf(m2, fabsf(W2[i]));
+  for (int i = threadIdx.x; i < N3 * PM_H; i += 256) m3 = fmaxf(m3, fabsf(W3[i]));
+  for (int k = threadIdx.x; k < PM_H; k += 256) {
+    float a = fabsf(b1[k]);
+    m1 = fmaxf(m1, a);
+    for (int j = 0; j < D; ++j) {
+      const float v = fabsf(W1[(int64_t)k * D + j]);
+      a += v;
+      m1 = fmaxf(m1, v);
+    }
+    r1 = fmaxf(r1, a);
+    float c = fabsf(b2[k]);
+    for (int j = 0; j < PM_H; ++j) c += fabsf(W2[(int64_t)k * PM_H + j]);
+    r2 = fmaxf(r2, c);
+  }
+  red[0][threadIdx.x] = m1;
+  red[1][threadIdx.x] = m2;
+  red[2][threadIdx.x] = m3;
+  red[3][threadIdx.x] = r1;
+  red[4][threadIdx.x] = r2;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h)
+      for (int q = 0; q < 5; ++q) red[q][threadIdx.x] = fmaxf(red[q][threadIdx.x], red[q][threadIdx.x + h]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    float* sc = P + pm_off_scal(K1);
+    for (int q = 0; q < 3; ++q) {
+      const int k = pm_scale_exp(red[q][0]);
+      sc[q] = pm_pow2(k);
+      sc[3 + q] = pm_pow2(-k);
+    }
+    // rounded up so that the f32 bounds stay upper bounds of the true magnitudes
+    sc[6] = red[3][0] * (1.0f + 1.0f / 1024.0f);
+    sc[7] = red[4][0] * (1.0f + 1.0f / 1024.0f);
+  }
+}
+
+__device__ __forceinline__ void split2h(float a, _Float16& hi, _Float16& lo) {
+  hi = (_Float16)a;
+  lo = (_Float16)(a - (float)hi);  // the remainder is exact in f32
+}
+
+// The kernel's hot splits, three VALU per pair: hi = both values rounded to f16 (one packed
+// convert), lo = f16(a - hi) by v_fma_mix (the f16 hi read as a mixed-precision operand; the
+// f32 difference is exact, rounded once). Written out because the compiler's lowering of
+// (_Float16)(a - (float)hi) spends a convert back, a subtract and a second convert per value.
+__device__ __forceinline__ void split2h_pair(float a, float b, float one, uint32_t& hi, uint32_t& lo) {
+  asm("v_cvt_pk_f16_f32 %0, %2, %3\n\t"
+      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(hi), "=&v"(lo)
+      : "v"(a), "v"(b), "v"(one));
+}
+// max(x, 0) without the canonicalising max(x, x) the compiler adds for values it did not
+// produce itself (MFMA results)
+__device__ __forceinline__ float relu_raw(float x) {
+  float r;
+  asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+// One thread per packed f16 of W2x3, W1x3 and W3x3.
+__global__ __launch_bounds__(256) void k_policy_pack_x3(const float* __restrict__ W1, const float* __restrict__ b1,
+                                                        const float* __restrict__ W2, const float* __restrict__ W3,
+                                                        int D, int N3, int K1, float* __restrict__ P) {
+  const float* sc = P + pm_off_scal(K1);
+  const float sw1 = sc[0], sw2 = sc[1], sw3 = sc[2];
+  constexpr int64_t n2 = PM_X3_FLOATS * 2, n1 = PM_X3_W1_FLOATS * 2, n3 = PM_X3_W3_FLOATS * 2;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n2 + n1 + n3; q += (int64_t)gridDim.x * 256) {
+    float v;
+    int64_t r;
+    _Float16* dst;
+    if (q < n2) {
+      r = q;
+      dst = reinterpret_cast<_Float16*>(P + pm_off_w2x3(K1));
+    } else if (q < n2 + n1) {
+      r = q - n2;
+      dst = reinterpret_cast<_Float16*>(P + pm_off_w1x3(K1));
+    } else {
+      r = q - n2 - n1;
+      dst = reinterpret_cast<_Float16*>(P + pm_off_w3x3(K1));
+    }
+    const int j = (int)(r & 7), l = (int)((r >> 3) & 63);
+    const int64_t f = r >> 9;  // fragment index
+    const int split = (int)(f & 1);
+    if (q < n2) {
+      const int s = (int)((f >> 1) & 1), ob = (int)((f >> 2) % PM_NB), ib = (int)(f / (4 * PM_NB));
+      const int k = ib * 32 + (j & 3) + 8 * (j >> 2) + 16 * s + 4 * (l >> 5);
+      v = W2[(int64_t)(ob * 32 + (l & 31)) * PM_H + k] * sw2;
+    } else if (q < n2 + n1) {
+      const int blk = (int)(f >> 1), k = 8 * (l >> 5) + j, row = blk * 32 + (l & 31);
+      v = k < D ? W1[(int64_t)row * D + k] * sw1 : (k == D ? b1[row] * sw1 : 0.0f);
+    } else {
+      const int s = (int)((f >> 1) & 1), ob = (int)(f >> 2), o = l & 31;
+      const int k = ob * 32 + (j & 3) + 8 * (j >> 2) + 16 * s + 4 * (l >> 5);
+      v = o < N3 ? W3[(int64_t)o * PM_H + k] * sw3 : 0.0f;
+    }
+    _Float16 hi, lo;
+    split2h(v, hi, lo);
+    dst[r] = split ? lo : hi;
+  }
+}
+
+// WAVES = 4 (one wave per SIMD, NT = 2 tiles each) or 8 (two waves per SIMD, NT = 1: the
+// accumulators fit in 128 AGPRs, so two waves share each SIMD and hide each other's VALU and
+// barrier time behind MFMAs). Either way a workgroup covers 8 tiles per staged W2 chunk.
+template <int NT, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(WAVES / 4, WAVES / 4)))
+void k_policy_forward_x3(const float* __restrict__ P,
+                                                             const float* __restrict__ obs, int64_t E, int D, int N3,
+                                                             int K1, float* __restrict__ logits) {
+  typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+  constexpr int FPW = PM_X3_FRAGS / WAVES;  // W2x3 fragments each wave stages per chunk
+  constexpr int FOPW = 2 * PM_NB * 4 / (2 * WAVES);  // fold-operand records per wave (per array)
+  // two distinct LDS arrays (not one [2][...]): with the buffer known at compile time in every
+  // phase, alias analysis proves the next chunk's LDS-DMA writes disjoint from this phase's
+  // ds_reads, so the reads do not wait for the staging to land
+  __shared__ uint4 lds0[PM_X3_FRAGS * 64];
+  __shared__ uint4 lds1[PM_X3_FRAGS * 64];
+  // the fold operands, staged once per kernel: W3x3 [ob][s][split][lane] and the layer-2 bias
+  // as [ob][q][lane] (lane-contiguous 16-B records)
+  __shared__ uint4 lds_w3[PM_NB * 4 * 64];
+  __shared__ uint4 lds_b2[PM_NB * 4 * 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t ntiles = (E + 31) / 32;
+  const int64_t per_round = (int64_t)gridDim.x * WAVES * NT;
+  const float* b3 = P + pm_off_b3(K1);
+  const uint4* W2g = reinterpret_cast<const uint4*>(P + pm_off_w2x3(K1));
+  const uint4* W1g = reinterpret_cast<const uint4*>(P + pm_off_w1x3(K1));
+  const float* scal = P + pm_off_scal(K1);
+  const float isw1 = scal[3], isw2 = scal[4], isw3 = scal[5], R1 = scal[6], R2 = scal[7];
+  const float one = 1.0f;
+
+  // per lane: the 8 inputs k = 8 (lane >> 5) + j of env column lane & 31 (obs, then the
+  // constant-1 bias input at k = D), scaled by 2^ex[0] and split; ex = the env's three exponents
+  auto load_split_obs = [&](int64_t t, f16x8& xh, f16x8& xl, int* ex) {
+    const int64_t brow = min(min(t, ntiles - 1) * 32 + (lane & 31), E - 1);  // padded rows: the last env
+    float x[8];
+    float m = 1.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * (lane >> 5) + j;
+      x[j] = k < D ? obs[brow * D + k] : (k == D ? 1.0f : 0.0f);
+      m = fmaxf(m, fabsf(x[j]));
+    }
+    m = fmaxf(m, __shfl_xor(m, 32));  // lanes l and l ^ 32 hold the same env
+    ex[0] = pm_scale_exp(m);
+    const float b1v = R1 * m;
+    ex[1] = pm_scale_exp(b1v);
+    ex[2] = pm_scale_exp(R2 * fmaxf(1.0f, b1v));
+    const float sx = pm_pow2(ex[0]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      _Float16 a, b;
+      split2h(x[j] * sx, a, b);
+      xh[j] = a;
+      xl[j] = b;
+    }
+  };
+  auto stage = [&](int ib, uint4* dstbuf) {
+    const uint4* src = W2g + (int64_t)ib * PM_X3_FRAGS * 64;
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) {
+      const int f = w * FPW + i;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + f * 64 + lane),
+                                       (void __attribute__((address_space(3)))*)(&dstbuf[f * 64]), 16, 0, 0);
+    }
+  };
+  // layer 1 of one 32-row block for one tile: 3 MFMAs, then ReLU, rescale to the H1 exponent
+  // and split into the layer-2 B operands (registers 8 s .. 8 s + 7 = k-step s)
+  auto layer1 = [&](const uint4* wf, const f16x8& xh, const f16x8& xl, float rescale, f16x8* ph, f16x8* pl) {
+    const f16x8 wh = __builtin_bit_cast(f16x8, wf[0]), wl = __builtin_bit_cast(f16x8, wf[1]);
+    f32x16 h = {};
+    h = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh, h, 0, 0, 0);
+    h = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl, h, 0, 0, 0);
+    h = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh, h, 0, 0, 0);
+    uint32_t hp[8], lp[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {  // rescale (a power of two) commutes with the ReLU
+      const f32x2 y = f32x2{h[2 * p], h[2 * p + 1]} * f32x2{rescale, rescale};
+      split2h_pair(relu_raw(y.x), relu_raw(y.y), one, hp[p], lp[p]);
+    }
+    ph[0] = __builtin_bit_cast(f16x8, uint4{hp[0], hp[1], hp[2], hp[3]});
+    ph[1] = __builtin_bit_cast(f16x8, uint4{hp[4], hp[5], hp[6], hp[7]});
+    pl[0] = __builtin_bit_cast(f16x8, uint4{lp[0], lp[1], lp[2], lp[3]});
+    pl[1] = __builtin_bit_cast(f16x8, uint4{lp[4], lp[5], lp[6], lp[7]});
+  };
+
+  int64_t t0 = ((int64_t)blockIdx.x * WAVES + w) * NT;
+  int64_t wg0 = (int64_t)blockIdx.x * WAVES * NT;
+  if (wg0 >= ntiles) return;  // whole workgroup idle (uniform)
+  {  // fold operands: 2 x 2,048 lane-16-B records over the waves
+    const uint4* w3g = reinterpret_cast<const uint4*>(P + pm_off_w3x3(K1));
+    const uint4* b2g = reinterpret_cast<const uint4*>(P + pm_off_b2(K1));
+#pragma unroll
+    for (int i = 0; i < FOPW; ++i) {
+      const int r = w * FOPW + i;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(w3g + r * 64 + lane),
+                                       (void __attribute__((address_space(3)))*)(&lds_w3[r * 64]), 16, 0, 0);
+      // b2p is [ob][lane][16 floats]: lane-strided source, lane-contiguous destination
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(b2g + ((r >> 2) * 64 + lane) * 4 + (r & 3)),
+                                       (void __attribute__((address_space(3)))*)(&lds_b2[r * 64]), 16, 0, 0);
+    }
+  }
+  stage(0, lds0);
+  uint4 w1c[2];  // layer-1 fragments of the next block (loaded a phase ahead)
+  w1c[0] = W1g[(1 * 2 + 0) * 64 + lane];
+  w1c[1] = W1g[(1 * 2 + 1) * 64 + lane];
+  f16x8 xoh[NT], xol[NT];
+  int ex[NT][3];
+  f16x8 xh[NT][2], xl[NT][2];
+  {
+    uint4 w10[2] = {W1g[lane], W1g[64 + lane]};
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      load_split_obs(t0 + t, xoh[t], xol[t], ex[t]);
+      layer1(w10, xoh[t], xol[t], pm_pow2(ex[t][1] - ex[t][0]) * isw1, xh[t], xl[t]);
+    }
+  }
+  for (; wg0 < ntiles; wg0 += per_round, t0 += per_round) {
+    const bool more = wg0 + per_round < ntiles;
+    float k23[NT], sc3[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      k23[t] = isw2 * pm_pow2(ex[t][2] - ex[t][1]);
+      sc3[t] = pm_pow2(ex[t][2]);
+    }
+    f32x16 acc[NT][PM_NB];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int ob = 0; ob < PM_NB; ++ob) acc[t][ob] = f32x16{};
+    // phase ib reads chunk ib from lds<ib & 1> and stages chunk ib + 1 into the other array
+    auto phase = [&](auto bufc, int ib, bool fold) {
+      constexpr int B = decltype(bufc)::value;
+      uint4* cur_lds = B ? lds1 : lds0;
+      uint4* nxt_lds = B ? lds0 : lds1;
+      const bool has_next = ib < PM_NB - 1 || more;
+      const int nib = (ib + 1) & (PM_NB - 1);
+      if (ib > 0) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          layer1(w1c, xoh[t], xol[t], pm_pow2(ex[t][1] - ex[t][0]) * isw1, xh[t], xl[t]);
+      }
+      // LDS DMA completes on vmcnt: drain this wave's share of chunk ib, then the barrier makes
+      // the whole chunk (and the fold operands) visible to every wave
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      __syncthreads();
+      if (has_next) stage(nib, nxt_lds);
+      w1c[0] = W1g[(nib * 2 + 0) * 64 + lane];  // a phase ahead
+      w1c[1] = W1g[(nib * 2 + 1) * 64 + lane];
+      const uint4* L = cur_lds + lane;
+      uint4 ring[3][2];  // W2 fragments read two steps ahead
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        ring[0][p] = L[p * 64];
+        ring[1][p] = L[(2 + p) * 64];
+      }
+#pragma unroll
+      for (int st = 0; st < 2 * PM_NB; ++st) {
+        const int ob = st >> 1, s = st & 1;
+        if (st + 2 < 2 * PM_NB) {
+#pragma unroll
+          for (int p = 0; p < 2; ++p) ring[(st + 2) % 3][p] = L[((st + 2) * 2 + p) * 64];
+        }
+        const uint4* cur = ring[st % 3];
+        uint4 w3f[4];
+        f32x4 b2f[4];
+        if (fold && s == 1) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            w3f[q] = lds_w3[(ob * 4 + q) * 64 + lane];
+            b2f[q] = __builtin_bit_cast(f32x4, lds_b2[(ob * 4 + q) * 64 + lane]);
+          }
+        }
+        const f16x8 wh = __builtin_bit_cast(f16x8, cur[0]);
+        const f16x8 wl = __builtin_bit_cast(f16x8, cur[1]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          f32x16 a = acc[t][ob];
+          a = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh[t][s], a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl[t][s], a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh[t][s], a, 0, 0, 0);
+          acc[t][ob] = a;
+        }
+        if (fold && s == 1) {  // H2 block ob is final: bias, ReLU, rescale, split, layer 3
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            // h2 * 2^e3 = relu(acc * (2^(e3 - e2) / sw2) + b2 * 2^e3): one packed fma per pair
+            // (powers of two commute with the ReLU and with rounding)
+            uint32_t hp[8], lp[8];
+            const f32x2 k2 = {k23[t], k23[t]}, s2 = {sc3[t], sc3[t]};
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+              const int r = 2 * p;
+              const f32x2 bs = f32x2{b2f[r >> 2][r & 3], b2f[r >> 2][(r & 3) + 1]} * s2;
+              const f32x2 y = __builtin_elementwise_fma(f32x2{acc[t][ob][r], acc[t][ob][r + 1]}, k2, bs);
+              split2h_pair(relu_raw(y.x), relu_raw(y.y), one, hp[p], lp[p]);
+            }
+            const f16x8 hh[2] = {__builtin_bit_cast(f16x8, uint4{hp[0], hp[1], hp[2], hp[3]}),
+                                 __builtin_bit_cast(f16x8, uint4{hp[4], hp[5], hp[6], hp[7]})};
+            const f16x8 hl[2] = {__builtin_bit_cast(f16x8, uint4{lp[0], lp[1], lp[2], lp[3]}),
+                                 __builtin_bit_cast(f16x8, uint4{lp[4], lp[5], lp[6], lp[7]})};
+            // layer 3's accumulator lives in acc[t][0] once block 0 has been folded (its
+            // registers are free from then on), so it needs no registers of its own
+            f32x16 o = ob == 0 ? f32x16{} : acc[t][0];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+              const f16x8 vh = __builtin_bit_cast(f16x8, w3f[2 * ks]);
+              const f16x8 vl = __builtin_bit_cast(f16x8, w3f[2 * ks + 1]);
+              o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, hh[ks], o, 0, 0, 0);
+              o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, hl[ks], o, 0, 0, 0);
+              o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, hh[ks], o, 0, 0, 0);
+            }
+            acc[t][0] = o;
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one step at a time: bounded live fragments
+      }
+    };
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+#pragma unroll 1
+    for (int ib = 0; ib < PM_NB - 2; ib += 2) {
+      phase(B0{}, ib, false);
+      phase(B1{}, ib + 1, false);
+    }
+    phase(B0{}, PM_NB - 2, false);
+    phase(B1{}, PM_NB - 1, true);
+    // logits: o3 holds out^T (rows = outputs, row(r, lane); column = env lane & 31), in units of
+    // sw3 * 2^ex[2]
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int64_t b = (t0 + t) * 32 + (lane & 31);
+      const float iu = isw3 * pm_pow2(-ex[t][2]);
+      if (t0 + t < ntiles && b < E) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int oo = pm_row(r, lane);
+          if (oo < N3) logits[b * N3 + oo] = acc[t][0][r] * iu + b3[oo];
+        }
+      }
+    }
+    if (more) {  // the next round's tiles (loaded here, not a round ahead: registers) and their block 0
+      uint4 w10[2] = {W1g[lane], W1g[64 + lane]};
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        load_split_obs(t0 + per_round + t, xoh[t], xol[t], ex[t]);
+        layer1(w10, xoh[t], xol[t], pm_pow2(ex[t][1] - ex[t][0]) * isw1, xh[t], xl[t]);
+      }
+    }
+  }
+  __syncthreads();  // no LDS-DMA outstanding when the workgroup retires
+}
+
 int64_t policy_packed_floats(int D) { return pm_packed_floats(D / 2 + 1); }
 
 hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
                               const float* b3, int D, int N3, float* P, hipStream_t st) {
   const int K1 = D / 2 + 1;  // ceil((D + 1) / 2): observation + the bias input
-  const int64_t total = pm_packed_floats(K1);
+  const int64_t total = pm_off_w2x6(K1);
   const int grid = (int)((total + 255) / 256 < 1024 ? (total + 255) / 256 : 1024);
   k_policy_pack<<<grid, 256, 0, st>>>(W1, b1, W2, b2, W3, b3, D, N3, K1, P);
   if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
   k_policy_pack_x6<<<(int)(PM_X6_FLOATS * 2 / 256), 256, 0, st>>>(W2, K1, P);
+  if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
+  k_policy_scales<<<1, 256, 0, st>>>(W1, b1, W2, b2, W3, D, N3, K1, P);
+  if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
+  k_policy_pack_x3<<<(int)((PM_X3_FLOATS + PM_X3_W1_FLOATS + PM_X3_W3_FLOATS) * 2 / 256), 256, 0, st>>>(
+      W1, b1, W2, W3, D, N3, K1, P);
   return hipGetLastError();
 }
 
@@ -511,13 +928,24 @@ static hipError_t launch_fwd_t(const float* P, const float* obs, int64_t E, int 
   }
   const int64_t want = (tiles + 3) / 4;
   const int grid = (int)(want < cus ? want : cus);
-  // MH_POLICY_KERNEL=f32 keeps the all-f32 kernel (A/B measurements); split-bf16 layer 2 otherwise
+  // MH_POLICY_KERNEL (A/B measurements): f32 = the all-f32 kernel, x6 = split-bf16 layer 2;
+  // default split-f16 layer 2 (x3)
   static int mode = -1;
   if (mode < 0) {
     const char* m = getenv("MH_POLICY_KERNEL");
-    mode = (m && m[0] == 'f') ? 0 : 1;
+    mode = (m && m[0] == 'f') ? 0 : ((m && m[0] == 'x' && m[1] == '6') ? 1 : 2);
   }
-  if (N3 <= 16 && mode == 1) {
+  if (D <= 15 && mode == 2) {  // K = 16 holds the observation and the bias input
+    static int w8 = -1;  // MH_POLICY_WAVES=4: one wave per SIMD with 2 tiles (A/B); default 8
+    if (w8 < 0) {
+      const char* v = getenv("MH_POLICY_WAVES");
+      w8 = (v && atoi(v) == 4) ? 0 : 1;
+    }
+    const int64_t want3 = (tiles + 7) / 8;  // 8 tiles per workgroup either way
+    const int grid3 = (int)(want3 < cus ? want3 : cus);
+    if (w8) k_policy_forward_x3<1, 8><<<grid3, 512, 0, st>>>(P, obs, E, D, N3, K1, logits);
+    else k_policy_forward_x3<2, 4><<<grid3, 256, 0, st>>>(P, obs, E, D, N3, K1, logits);
+  } else if (N3 <= 16 && mode == 1) {
     static int tpw = 0;  // env tiles per wave (MH_POLICY_TPW, for A/B): default PM_X6_TPW
     if (tpw == 0) {
       const char* v = getenv("MH_POLICY_TPW");

@@ -50,6 +50,36 @@ def test_fused_policy_forward_matches_torch(D, A, E):
     np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-5, atol=1e-5 * scale)
 
 
+@pytest.mark.parametrize("obs_scale,w1_scale,w2_scale", [(1e3, 1.0, 1.0), (1e-3, 1.0, 1.0), (1.0, 30.0, 1e-4),
+                                                    (1.0, 1e-3, 50.0), (20.0, 20.0, 20.0)])
+def test_fused_policy_forward_scaled_operands(obs_scale, w1_scale, w2_scale):
+    """The split-f16 layer 2 scales W2 and every env's layer-1 column by powers of two: across
+    operand magnitudes far from 1 each logit stays within 2e-6 of the magnitude network
+    sum |W3| (sum |W2| |H1| + |b2|) + |b3| (f64) of its float64 value."""
+    D, A, E = 12, 4, 4096
+    net = _mlp(D, A, seed=7)
+    with torch.no_grad():
+        net[0].weight.mul_(w1_scale)
+        net[0].bias.mul_(w1_scale)
+        net[2].weight.mul_(w2_scale)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    obs = (torch.randn(E, D, device="cuda", generator=g) * obs_scale).contiguous()
+    with torch.no_grad():
+        n64 = [m.double() if isinstance(m, nn.Linear) else m for m in (net[0], net[2], net[4])]
+        x = obs.double()
+        h1 = torch.relu(x @ n64[0].weight.T + n64[0].bias)
+        h2 = torch.relu(h1 @ n64[1].weight.T + n64[1].bias)
+        exact = h2 @ n64[2].weight.T + n64[2].bias
+        m2 = h1 @ n64[1].weight.abs().T + n64[1].bias.abs()
+        mag = m2 @ n64[2].weight.abs().T + n64[2].bias.abs()
+        for m in n64:
+            m.float()
+    got = _fused(net, obs, D, 2 * A).double()
+    err = (got - exact).abs()
+    assert torch.isfinite(got).all()
+    assert (err <= 2e-6 * mag + 1e-30).all(), (err / mag).max().item()
+
+
 def test_fused_policy_rejects_unsupported_shapes():
     n = ctypes.c_int64()
     assert N.lib().mh_policy_packed_size(17, ctypes.byref(n)) == -1

@@ -36,7 +36,7 @@ def main():
     with torch.no_grad():
         ref = net.double()(obs.double())
     err = ((out.double() - ref).abs().max() / ref.abs().max()).item()
-    print(f"policy_forward kernel={os.environ.get('MH_POLICY_KERNEL', 'x6')} E={E}: {ms * 1e3:.2f} us, "
+    print(f"policy_forward kernel={os.environ.get('MH_POLICY_KERNEL', 'x3')} E={E}: {ms * 1e3:.2f} us, "
           f"{flops / ms / 1e9:.1f} TFLOP/s (f32-equivalent), max |err| / max |ref| = {err:.2e}", flush=True)
 
 

@@ -1,16 +1,12 @@
 #!/bin/bash
 # SQ counters of the policy-forward kernels, one PMC pass per kernel variant:
-#   x6 (split-bf16 layer 2, 2 tiles/wave), x6t1 (1 tile/wave), f32 (all-f32 kernel).
+#   x3 (split-f16, default), x6 (split-bf16 layer 2), f32 (all-f32 kernel).
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-for K in ${VARIANTS:-x6 x6t1 f32}; do
+for K in ${VARIANTS:-x3 x6 f32}; do
   rm -rf gpurun_out/pmc_pol_$K
-  case $K in x6) ENVV="MH_POLICY_KERNEL=x6";; x6t1) ENVV="MH_POLICY_TPW=1";; f32) ENVV="MH_POLICY_KERNEL=f32";; esac
-  env $ENVV true
-  export MH_POLICY_KERNEL=x6 MH_POLICY_TPW=2
-  [ "$K" = f32 ] && export MH_POLICY_KERNEL=f32
-  [ "$K" = x6t1 ] && export MH_POLICY_TPW=1
+  export MH_POLICY_KERNEL=$K MH_POLICY_TPW=2
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \
     -d gpurun_out/pmc_pol_$K -o pol --output-format csv -- python3 tools/policy_bench.py 65536 10 > gpurun_out/pmc_pol_$K.log 2>&1 || { echo "pmc $K failed"; tail -5 gpurun_out/pmc_pol_$K.log; exit 1; }
   python3 - "$K" <<'PY'
