@@ -700,23 +700,30 @@ void k_policy_forward_x3(const float* __restrict__ P,
       xl[j] = b;
     }
   };
+  const int wu = __builtin_amdgcn_readfirstlane(w);  // the wave index, in an SGPR
   auto stage = [&](int ib, uint4* dstbuf) {
-    const uint4* src = W2g + (int64_t)ib * PM_X3_FRAGS * 64;
+    // scalar base + lane offset + immediate fragment offset; the laundered base keeps the compiler
+    // from precomputing (and spilling) one 64-bit address per fragment and phase
+    const uint4* src = W2g + ((int64_t)ib * PM_X3_FRAGS + wu * FPW) * 64;
+    asm volatile("" : "+s"(src));
 #pragma unroll
     for (int i = 0; i < FPW; ++i) {
-      const int f = w * FPW + i;
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + f * 64 + lane),
-                                       (void __attribute__((address_space(3)))*)(&dstbuf[f * 64]), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + i * 64 + lane),
+                                       (void __attribute__((address_space(3)))*)(&dstbuf[(wu * FPW + i) * 64]), 16,
+                                       0, 0);
     }
   };
-  // layer 1 of one 32-row block for one tile: 3 MFMAs, then ReLU, rescale to the H1 exponent
-  // and split into the layer-2 B operands (registers 8 s .. 8 s + 7 = k-step s)
-  auto layer1 = [&](const uint4* wf, const f16x8& xh, const f16x8& xl, float rescale, f16x8* ph, f16x8* pl) {
+  // layer 1 of one 32-row block for one tile: 3 MFMAs (l1_mfma), then ReLU, rescale to the H1
+  // exponent and split into the layer-2 B operands, registers 8 s .. 8 s + 7 = k-step s (l1_split)
+  auto l1_mfma = [&](const uint4* wf, const f16x8& xh, const f16x8& xl) {
     const f16x8 wh = __builtin_bit_cast(f16x8, wf[0]), wl = __builtin_bit_cast(f16x8, wf[1]);
     f32x16 h = {};
     h = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh, h, 0, 0, 0);
     h = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl, h, 0, 0, 0);
     h = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh, h, 0, 0, 0);
+    return h;
+  };
+  auto l1_split = [&](const f32x16& h, float rescale, f16x8* ph, f16x8* pl) {
     uint32_t hp[8], lp[8];
 #pragma unroll
     for (int p = 0; p < 8; ++p) {  // rescale (a power of two) commutes with the ReLU
@@ -727,6 +734,9 @@ void k_policy_forward_x3(const float* __restrict__ P,
     ph[1] = __builtin_bit_cast(f16x8, uint4{hp[4], hp[5], hp[6], hp[7]});
     pl[0] = __builtin_bit_cast(f16x8, uint4{lp[0], lp[1], lp[2], lp[3]});
     pl[1] = __builtin_bit_cast(f16x8, uint4{lp[4], lp[5], lp[6], lp[7]});
+  };
+  auto layer1 = [&](const uint4* wf, const f16x8& xh, const f16x8& xl, float rescale, f16x8* ph, f16x8* pl) {
+    l1_split(l1_mfma(wf, xh, xl), rescale, ph, pl);
   };
 
   int64_t t0 = ((int64_t)blockIdx.x * WAVES + w) * NT;
@@ -780,18 +790,18 @@ void k_policy_forward_x3(const float* __restrict__ P,
       uint4* nxt_lds = B ? lds0 : lds1;
       const bool has_next = ib < PM_NB - 1 || more;
       const int nib = (ib + 1) & (PM_NB - 1);
-      if (ib > 0) {
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-          layer1(w1c, xoh[t], xol[t], pm_pow2(ex[t][1] - ex[t][0]) * isw1, xh[t], xl[t]);
-      }
+#ifndef MH_X3_NOBAR  // timing experiments only (tools/ab_libs.sh): parts compiled out
       // LDS DMA completes on vmcnt: drain this wave's share of chunk ib, then the barrier makes
       // the whole chunk (and the fold operands) visible to every wave
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
       __syncthreads();
       if (has_next) stage(nib, nxt_lds);
-      w1c[0] = W1g[(nib * 2 + 0) * 64 + lane];  // a phase ahead
-      w1c[1] = W1g[(nib * 2 + 1) * 64 + lane];
+#endif
+      // layer 1 of block ib + 1 is software-pipelined into this phase's MFMA stream (issued at
+      // step 0, split at step 3, into a second operand set), so no wave idles on it at a barrier
+      const bool pipe = !fold;
+      f32x16 hn[NT];
+      f16x8 xh2[NT][2], xl2[NT][2];
       const uint4* L = cur_lds + lane;
       uint4 ring[3][2];  // W2 fragments read two steps ahead
 #pragma unroll
@@ -807,6 +817,20 @@ void k_policy_forward_x3(const float* __restrict__ P,
           for (int p = 0; p < 2; ++p) ring[(st + 2) % 3][p] = L[((st + 2) * 2 + p) * 64];
         }
         const uint4* cur = ring[st % 3];
+#ifndef MH_X3_NOL1
+        if (pipe && st == 0) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) hn[t] = l1_mfma(w1c, xoh[t], xol[t]);
+          if (ib + 2 < PM_NB) {  // fragments of block ib + 2, a phase ahead
+            w1c[0] = W1g[((ib + 2) * 2 + 0) * 64 + lane];
+            w1c[1] = W1g[((ib + 2) * 2 + 1) * 64 + lane];
+          }
+        }
+        if (pipe && st == 3) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) l1_split(hn[t], pm_pow2(ex[t][1] - ex[t][0]) * isw1, xh2[t], xl2[t]);
+        }
+#endif
         uint4 w3f[4];
         f32x4 b2f[4];
         if (fold && s == 1) {
@@ -833,6 +857,14 @@ void k_policy_forward_x3(const float* __restrict__ P,
             // (powers of two commute with the ReLU and with rounding)
             uint32_t hp[8], lp[8];
             const f32x2 k2 = {k23[t], k23[t]}, s2 = {sc3[t], sc3[t]};
+#ifdef MH_X3_FOLDLITE
+#pragma unroll
+            for (int p = 0; p < 8; ++p) {
+              hp[p] = __float_as_uint(acc[t][ob][2 * p]);
+              lp[p] = __float_as_uint(acc[t][ob][2 * p + 1]);
+            }
+            if (k2.x == 12345.0f)
+#endif
 #pragma unroll
             for (int p = 0; p < 8; ++p) {
               const int r = 2 * p;
@@ -860,6 +892,17 @@ void k_policy_forward_x3(const float* __restrict__ P,
         }
         __builtin_amdgcn_sched_barrier(0);  // one step at a time: bounded live fragments
       }
+#ifndef MH_X3_NOL1
+      if (pipe) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          xh[t][0] = xh2[t][0];
+          xh[t][1] = xh2[t][1];
+          xl[t][0] = xl2[t][0];
+          xl[t][1] = xl2[t][1];
+        }
+      }
+#endif
     };
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, 1>;
@@ -886,6 +929,8 @@ void k_policy_forward_x3(const float* __restrict__ P,
     }
     if (more) {  // the next round's tiles (loaded here, not a round ahead: registers) and their block 0
       uint4 w10[2] = {W1g[lane], W1g[64 + lane]};
+      w1c[0] = W1g[(1 * 2 + 0) * 64 + lane];
+      w1c[1] = W1g[(1 * 2 + 1) * 64 + lane];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         load_split_obs(t0 + per_round + t, xoh[t], xol[t], ex[t]);
