@@ -36,6 +36,8 @@ def parse():
                    help="init: PyTorch default init (SURVEY 8d); hover: action mean [mg,0,0,0], long episodes")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU-baseline leg (1x4 threads, Px1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="serial trainer order (no sampling beside the policy-free updates; A/B)")
     p.add_argument("--graph-segments", action="store_true",
                    help="capture the update as graphs cut at its all-reduces (the world size > 1 path)")
     p.add_argument("--eager-update", action="store_true",
@@ -110,6 +112,8 @@ def main():
         cfg["update_gemm"] = a.update_gemm
     if a.eager_update:
         cfg["alg_use_graph"] = False
+    if a.no_overlap:
+        cfg["trainer_overlap_sampling"] = False
     if a.graph_segments:
         cfg["alg_force_graph_segments"] = True
     if a.policy == "hover":
@@ -131,7 +135,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         one_step()
-    torch.cuda.synchronize()
+    torch.cuda.synchronize()  # every stream: an overlapped sampling still in flight is inside the timed region
     if world > 1:
         torch.distributed.barrier()
     t1 = time.perf_counter()
@@ -139,6 +143,8 @@ def main():
     elapsed = D.max_over_ranks(t1 - t0)
     env_steps_total = world * a.envs * horizon * a.steps
     value = env_steps_total / elapsed
+
+    trainer.finish_pending()
 
     # ---- phase split (diagnostic, after the timed region): sample() vs replay sample + update
     ph_s = ph_u = 0.0

@@ -68,8 +68,8 @@ constexpr int64_t PM_X3_W3_FLOATS = (int64_t)PM_NB * 4 * 64 * 4;
 __host__ __device__ constexpr int64_t pm_off_w2x3(int K1) { return pm_off_w2x6(K1) + PM_X6_FLOATS; }
 __host__ __device__ constexpr int64_t pm_off_w1x3(int K1) { return pm_off_w2x3(K1) + PM_X3_FLOATS; }
 __host__ __device__ constexpr int64_t pm_off_w3x3(int K1) { return pm_off_w1x3(K1) + PM_X3_W1_FLOATS; }
-// scalars: [0..2] sw1, sw2, sw3; [3..5] their inverses; [6] R1 = max_k (sum_j |W1[k][j]| + |b1[k]|),
-// [7] R2 = max_o (sum_k |W2[o][k]| + |b2[o]|): |H1| <= R1 max(1, max |obs|), |H2| <= R2 max(1, |H1|)
+// scalars: the raw layer magnitudes of k_policy_scales (pm_scales() derives sw1..3 and the bounds
+// |H1| <= R1 max(1, max |obs|), |H2| <= R2 max(1, |H1|))
 __host__ __device__ constexpr int64_t pm_off_scal(int K1) { return pm_off_w3x3(K1) + PM_X3_W3_FLOATS; }
 __host__ __device__ constexpr int64_t pm_packed_floats(int K1) { return pm_off_scal(K1) + 64; }
 
@@ -113,6 +113,10 @@ __global__ __launch_bounds__(256) void k_policy_pack(const float* __restrict__ W
     }
     P[q] = v;
   }
+  // the atomic-max slots of k_policy_scales (which runs next) start from zero. Written here, not by a
+  // hipMemsetAsync: captured into a HIP graph, that memset node left the slots dirty from the second
+  // replay on (measured: garbage scales -> logits off by 1e-2 on replays >= 2)
+  if (blockIdx.x == 0 && threadIdx.x < 8) P[pm_off_scal(K1) + threadIdx.x] = 0.0f;
 }
 
 // Exact three-way bf16 split: a = hi + mid + lo with every part a bf16 (round-to-nearest-even
@@ -532,50 +536,60 @@ __device__ __forceinline__ int pm_scale_exp(float bound) {  // 14 - ceil(log2(bo
   return k < -40 ? -40 : (k > 40 ? 40 : k);
 }
 
-// One workgroup: the layer scales and the magnitude bounds R1, R2.
+// The raw magnitudes behind the scales, as float bits combined by atomic max (non-negative floats
+// order like their bit patterns): [0] max |W1, b1|, [1] max |W2|, [2] max |W3|,
+// [3] R1 = max_k (sum_j |W1[k][j]| + |b1[k]|), [4] R2 = max_o (sum_k |W2[o][k]| + |b2[o]|).
+// One workgroup per hidden unit k: row k of W1 and W2, column k of W3.
 __global__ __launch_bounds__(256) void k_policy_scales(const float* __restrict__ W1, const float* __restrict__ b1,
                                                        const float* __restrict__ W2, const float* __restrict__ b2,
                                                        const float* __restrict__ W3, int D, int N3, int K1,
                                                        float* __restrict__ P) {
-  __shared__ float red[5][256];
-  float m1 = 0.0f, m2 = 0.0f, m3 = 0.0f, r1 = 0.0f, r2 = 0.0f;
-  for (int i = threadIdx.x; i < PM_H * PM_H; i += 256) m2 = fmaxf(m2, fabsf(W2[i]));
-  for (int i = threadIdx.x; i < N3 * PM_H; i += 256) m3 = fmaxf(m3, fabsf(W3[i]));
-  for (int k = threadIdx.x; k < PM_H; k += 256) {
-    float a = fabsf(b1[k]);
-    m1 = fmaxf(m1, a);
-    for (int j = 0; j < D; ++j) {
-      const float v = fabsf(W1[(int64_t)k * D + j]);
-      a += v;
-      m1 = fmaxf(m1, v);
-    }
-    r1 = fmaxf(r1, a);
-    float c = fabsf(b2[k]);
-    for (int j = 0; j < PM_H; ++j) c += fabsf(W2[(int64_t)k * PM_H + j]);
-    r2 = fmaxf(r2, c);
-  }
-  red[0][threadIdx.x] = m1;
-  red[1][threadIdx.x] = m2;
-  red[2][threadIdx.x] = m3;
-  red[3][threadIdx.x] = r1;
-  red[4][threadIdx.x] = r2;
+  __shared__ float red[2][256];
+  const int k = blockIdx.x, i = threadIdx.x;
+  const float w2 = fabsf(W2[(int64_t)k * PM_H + i]);
+  red[0][i] = w2;
+  red[1][i] = w2;
   __syncthreads();
   for (int h = 128; h > 0; h >>= 1) {
-    if ((int)threadIdx.x < h)
-      for (int q = 0; q < 5; ++q) red[q][threadIdx.x] = fmaxf(red[q][threadIdx.x], red[q][threadIdx.x + h]);
+    if (i < h) {
+      red[0][i] = fmaxf(red[0][i], red[0][i + h]);
+      red[1][i] = red[1][i] + red[1][i + h];
+    }
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    float* sc = P + pm_off_scal(K1);
-    for (int q = 0; q < 3; ++q) {
-      const int k = pm_scale_exp(red[q][0]);
-      sc[q] = pm_pow2(k);
-      sc[3 + q] = pm_pow2(-k);
+  if (i == 0) {
+    float m1 = fabsf(b1[k]), r1 = m1, m3 = 0.0f;
+    for (int j = 0; j < D; ++j) {
+      const float v = fabsf(W1[(int64_t)k * D + j]);
+      m1 = fmaxf(m1, v);
+      r1 += v;
     }
-    // rounded up so that the f32 bounds stay upper bounds of the true magnitudes
-    sc[6] = red[3][0] * (1.0f + 1.0f / 1024.0f);
-    sc[7] = red[4][0] * (1.0f + 1.0f / 1024.0f);
+    for (int o = 0; o < N3; ++o) m3 = fmaxf(m3, fabsf(W3[(int64_t)o * PM_H + k]));
+    unsigned int* raw = reinterpret_cast<unsigned int*>(P + pm_off_scal(K1));
+    atomicMax(raw + 0, __float_as_uint(m1));
+    atomicMax(raw + 1, __float_as_uint(red[0][0]));
+    atomicMax(raw + 2, __float_as_uint(m3));
+    atomicMax(raw + 3, __float_as_uint(r1));
+    atomicMax(raw + 4, __float_as_uint(red[1][0] + fabsf(b2[k])));
   }
+}
+
+// sw1..3, their inverses, and R1, R2 rounded up (the f32 sums above are upper bounds only up to
+// their own rounding) from the raw magnitudes
+struct PmScales {
+  float sw[3], isw[3], R1, R2;
+};
+__device__ __forceinline__ PmScales pm_scales(const float* scal) {
+  PmScales r;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int e = pm_scale_exp(scal[q]);
+    r.sw[q] = pm_pow2(e);
+    r.isw[q] = pm_pow2(-e);
+  }
+  r.R1 = scal[3] * (1.0f + 1.0f / 1024.0f);
+  r.R2 = scal[4] * (1.0f + 1.0f / 1024.0f);
+  return r;
 }
 
 __device__ __forceinline__ void split2h(float a, _Float16& hi, _Float16& lo) {
@@ -606,8 +620,8 @@ __device__ __forceinline__ float relu_raw(float x) {
 __global__ __launch_bounds__(256) void k_policy_pack_x3(const float* __restrict__ W1, const float* __restrict__ b1,
                                                         const float* __restrict__ W2, const float* __restrict__ W3,
                                                         int D, int N3, int K1, float* __restrict__ P) {
-  const float* sc = P + pm_off_scal(K1);
-  const float sw1 = sc[0], sw2 = sc[1], sw3 = sc[2];
+  const PmScales sc = pm_scales(P + pm_off_scal(K1));
+  const float sw1 = sc.sw[0], sw2 = sc.sw[1], sw3 = sc.sw[2];
   constexpr int64_t n2 = PM_X3_FLOATS * 2, n1 = PM_X3_W1_FLOATS * 2, n3 = PM_X3_W3_FLOATS * 2;
   for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n2 + n1 + n3; q += (int64_t)gridDim.x * 256) {
     float v;
@@ -671,7 +685,8 @@ void k_policy_forward_x3(const float* __restrict__ P,
   const uint4* W2g = reinterpret_cast<const uint4*>(P + pm_off_w2x3(K1));
   const uint4* W1g = reinterpret_cast<const uint4*>(P + pm_off_w1x3(K1));
   const float* scal = P + pm_off_scal(K1);
-  const float isw1 = scal[3], isw2 = scal[4], isw3 = scal[5], R1 = scal[6], R2 = scal[7];
+  const PmScales scs = pm_scales(scal);
+  const float isw1 = scs.isw[0], isw2 = scs.isw[1], isw3 = scs.isw[2], R1 = scs.R1, R2 = scs.R2;
   const float one = 1.0f;
 
   // per lane: the 8 inputs k = 8 (lane >> 5) + j of env column lane & 31 (obs, then the
@@ -952,7 +967,7 @@ hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2,
   if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
   k_policy_pack_x6<<<(int)(PM_X6_FLOATS * 2 / 256), 256, 0, st>>>(W2, K1, P);
   if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
-  k_policy_scales<<<1, 256, 0, st>>>(W1, b1, W2, b2, W3, D, N3, K1, P);
+  k_policy_scales<<<PM_H, 256, 0, st>>>(W1, b1, W2, b2, W3, D, N3, K1, P);
   if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
   k_policy_pack_x3<<<(int)((PM_X3_FLOATS + PM_X3_W1_FLOATS + PM_X3_W3_FLOATS) * 2 / 256), 256, 0, st>>>(
       W1, b1, W2, W3, D, N3, K1, P);

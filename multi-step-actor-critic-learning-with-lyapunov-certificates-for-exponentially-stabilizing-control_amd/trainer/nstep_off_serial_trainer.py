@@ -7,7 +7,14 @@ model_update -> log / save / evaluate. Differences, all at the device boundary:
   * replay batches are already device tensors (no `.cuda()` H2D copy, :87-89);
   * the HIP sampler is bound to the device buffer at construction so windows are emitted in
     place;
-  * tensorboard is optional (in-memory writer when absent).
+  * tensorboard is optional (in-memory writer when absent);
+  * overlapped sampling (`trainer_overlap_sampling`, default on for a device sampler): when the
+    update of iteration k leaves the policy unchanged (k % policy_frequency != 0), the sampling of
+    iteration k + 1 only depends on what precedes that update, so it is enqueued on a second stream
+    right after the replay gather of iteration k and runs concurrently with the update. Same
+    values as the serial order: the sampler reads only the policy (unchanged by that update) and
+    writes only the window store (iteration k's batch was gathered before); the buffer bookkeeping,
+    the next replay gather and every PER tree operation stay on the main stream, in order.
 """
 __all__ = ["NstepOffSerialTrainer"]
 
@@ -64,15 +71,40 @@ class NstepOffSerialTrainer:
                 raise RuntimeError("buffer warm-up did not reach buffer_warm_size: episodes never reach n_step")
         self.sampler_tb_dict = LogData()
         self.use_gpu = kwargs.get("use_gpu", torch.cuda.is_available())
+        dev = torch.device(self.sample_device)
+        self.overlap = (bool(kwargs.get("trainer_overlap_sampling", True)) and dev.type == "cuda"
+                        and hasattr(self.sampler, "bind_store"))
+        self._side = None
+        self._pending = None
         self.start_time = time.time()
+
+    def _sample(self):
+        with ModuleOnDevice(self.networks, self.sample_device):
+            return self.sampler.sample()
+
+    def _overlap_next(self):
+        """Sampling of iteration + 1 may run beside this iteration's update."""
+        return (self.overlap and self.iteration % self.policy_frequency != 0
+                and (self.iteration + 1) % self.sample_interval == 0 and self.iteration + 1 <= self.max_iteration)
 
     def step(self):
         if self.iteration % self.sample_interval == 0:
-            with ModuleOnDevice(self.networks, self.sample_device):
-                sampler_samples, sampler_tb_dict = self.sampler.sample()
+            if self._pending is not None:  # enqueued on the side stream during the last update
+                sampler_samples, sampler_tb_dict = self._pending
+                self._pending = None
+                torch.cuda.current_stream(self._side.device).wait_stream(self._side)
+            else:
+                sampler_samples, sampler_tb_dict = self._sample()
             self.buffer.add_batch(sampler_samples)
             self.sampler_tb_dict.add_average(sampler_tb_dict)
         replay_samples = self.buffer.sample_batch(self.replay_batch_size)
+        if self._overlap_next():
+            if self._side is None:
+                self._side = torch.cuda.Stream(device=torch.device(self.sample_device))
+            main = torch.cuda.current_stream(self._side.device)
+            self._side.wait_stream(main)  # after the replay gather above
+            with torch.cuda.stream(self._side):
+                self._pending = self._sample()
         self.networks.train()
         if self.per_flag:
             alg_tb_dict, idx, new_priority = self.alg.model_update(replay_samples, self.iteration)
@@ -117,10 +149,20 @@ class NstepOffSerialTrainer:
         self.writer.add_scalar(tb_tags["TCS of RL iteration"], cost_std, self.iteration)
         self.writer.add_scalar(tb_tags["TCM of total time"], cost_mean, int(time.time() - self.start_time))
 
+    def finish_pending(self):
+        """Join an overlapped sampling still in flight (its windows join the buffer)."""
+        if self._pending is not None:
+            samples, tb = self._pending
+            self._pending = None
+            torch.cuda.current_stream(self._side.device).wait_stream(self._side)
+            self.buffer.add_batch(samples)
+            self.sampler_tb_dict.add_average(tb)
+
     def train(self):
         while self.iteration <= self.max_iteration:
             self.step()
             self.iteration += 1
+        self.finish_pending()
         if self.is_main:
             self.save_apprfunc()
         self.writer.flush()

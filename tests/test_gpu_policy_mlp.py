@@ -164,3 +164,52 @@ def test_fused_mlp_empty_batch(backend):
             assert p.grad is not None and torch.equal(p.grad, torch.zeros_like(p))
     finally:
         set_gemm_backend(prev)
+
+
+def test_policy_pack_and_forward_replayed_in_a_graph_equal_eager():
+    """mh_policy_pack + mh_policy_forward captured in one HIP graph and replayed several times
+    (the sampler packs at every sample()): every replay equals the eager result bit for bit,
+    including the packed scale slots (they were once zeroed by a memset node that stayed dirty
+    from the second replay on)."""
+    D, A, E = 12, 4, 8192
+    net = _mlp(D, A, seed=3)
+    obs = torch.randn(E, D, device="cuda").contiguous()
+    ref = _fused(net, obs, D, 2 * A)
+    n = ctypes.c_int64()
+    N.check(N.lib().mh_policy_packed_size(D, ctypes.byref(n)), "size")
+    P = torch.full((n.value,), float("nan"), device="cuda")
+    out = torch.empty(E, 2 * A, device="cuda")
+    ps = [p.detach().contiguous() for p in (net[0].weight, net[0].bias, net[2].weight, net[2].bias, net[4].weight,
+                                            net[4].bias)]
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        N.check(N.lib().mh_policy_pack(*[N.ptr(p) for p in ps], D, 256, 256, 2 * A, N.ptr(P), N.stream_of()), "pack")
+        N.check(N.lib().mh_policy_forward(N.ptr(P), N.ptr(obs), E, D, 2 * A, N.ptr(out), N.stream_of()), "fwd")
+    for _ in range(4):
+        P[-64:].fill_(-3.0e38)  # dirty slots between replays must not leak into the scales
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("warm", [0, 3000])
+def test_sampler_graph_replays_equal_eager_sampling(tmp_path, warm):
+    """The n-step sampler's captured horizon (graph replays 1..4) and eager sampling from the same
+    state give bit-identical observations and window stores."""
+    from msacl_amd.utils.config import build_pipeline, default_msacl_args
+
+    def pipe(graph, sub):
+        torch.manual_seed(0)
+        args = default_msacl_args(env_name="DuctedFan", env_num=4096, buffer_warm_size=warm, buffer_max_size=200000,
+                                  max_iteration=0, eval_interval=10 ** 6, save_folder=str(tmp_path / sub), seed=0,
+                                  num_eval_episode=1, sampler_use_graph=graph)
+        return build_pipeline(args)
+    A, B = pipe(True, "a"), pipe(False, "b")
+    for _ in range(4):
+        A[3].add_batch(A[2].sample()[0])
+        B[3].add_batch(B[2].sample()[0])
+        torch.cuda.synchronize()
+        assert torch.equal(A[2].obs, B[2].obs)
+        assert torch.equal(A[3].cursor, B[3].cursor)
+        for k in A[3].n_step_buf:
+            assert torch.equal(A[3].n_step_buf[k], B[3].n_step_buf[k]), k

@@ -108,3 +108,41 @@ def test_evaluator_matches_reference(tmp_path, name):
     ev1.networks.to(ev1.device)
     seq = ev1.run_n_episodes(3, 0, initial_states=g["seq_init"])
     np.testing.assert_allclose(seq, g["sequential"], rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("buffer_name", ["nstep_replay_buffer", "prioritized_replay_buffer"])
+def test_overlapped_sampling_equals_serial_order(tmp_path, buffer_name):
+    """trainer_overlap_sampling (sampling of k + 1 beside the policy-free update of k on a second
+    stream) gives bit-identical networks, window store and sampler state to the serial order.
+    rocBLAS may use atomics in split-K GEMMs (run-to-run ulp noise), so both runs use PyTorch's
+    deterministic mode, which turns them off."""
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    try:
+        _overlap_vs_serial(tmp_path, buffer_name)
+    finally:
+        torch.use_deterministic_algorithms(prev)
+
+
+def _overlap_vs_serial(tmp_path, buffer_name):
+    def run(overlap, sub):
+        torch.manual_seed(0)
+        args = default_msacl_args(env_name="DuctedFan", env_num=4096, buffer_name=buffer_name, buffer_warm_size=3000,
+                                  buffer_max_size=60000, max_iteration=7, eval_interval=10 ** 6,
+                                  log_save_interval=10 ** 6, apprfunc_save_interval=10 ** 6,
+                                  save_folder=str(tmp_path / sub), seed=0, num_eval_episode=1,
+                                  trainer_overlap_sampling=overlap)
+        args, alg, sampler, buffer, evaluator, trainer = build_pipeline(args)
+        assert trainer.overlap == overlap
+        trainer.train()
+        torch.cuda.synchronize()
+        sd = {k: v.detach().cpu().clone() for k, v in alg.networks.state_dict().items()}
+        store = {k: v.cpu().clone() for k, v in buffer.n_step_buf.items()}
+        return sd, store, buffer.cursor.cpu().clone(), sampler.obs.cpu().clone()
+    a = run(True, "a")
+    b = run(False, "b")
+    for k in a[0]:
+        assert torch.equal(a[0][k], b[0][k]), k
+    for k in a[1]:
+        assert torch.equal(a[1][k], b[1][k]), k
+    assert torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
