@@ -36,8 +36,8 @@ def parse():
                    help="init: PyTorch default init (SURVEY 8d); hover: action mean [mg,0,0,0], long episodes")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU-baseline leg (1x4 threads, Px1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-overlap", action="store_true",
-                   help="serial trainer order (no sampling beside the policy-free updates; A/B)")
+    p.add_argument("--overlap", action="store_true",
+                   help="trainer_overlap_sampling: sampling beside the policy-free updates (A/B; off by default)")
     p.add_argument("--graph-segments", action="store_true",
                    help="capture the update as graphs cut at its all-reduces (the world size > 1 path)")
     p.add_argument("--eager-update", action="store_true",
@@ -112,8 +112,8 @@ def main():
         cfg["update_gemm"] = a.update_gemm
     if a.eager_update:
         cfg["alg_use_graph"] = False
-    if a.no_overlap:
-        cfg["trainer_overlap_sampling"] = False
+    if a.overlap:
+        cfg["trainer_overlap_sampling"] = True
     if a.graph_segments:
         cfg["alg_force_graph_segments"] = True
     if a.policy == "hover":

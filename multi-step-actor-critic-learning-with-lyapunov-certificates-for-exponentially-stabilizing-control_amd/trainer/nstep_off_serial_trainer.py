@@ -8,13 +8,16 @@ model_update -> log / save / evaluate. Differences, all at the device boundary:
   * the HIP sampler is bound to the device buffer at construction so windows are emitted in
     place;
   * tensorboard is optional (in-memory writer when absent);
-  * overlapped sampling (`trainer_overlap_sampling`, default on for a device sampler): when the
+  * overlapped sampling (`trainer_overlap_sampling`, off by default): when the
     update of iteration k leaves the policy unchanged (k % policy_frequency != 0), the sampling of
     iteration k + 1 only depends on what precedes that update, so it is enqueued on a second stream
     right after the replay gather of iteration k and runs concurrently with the update. Same
     values as the serial order: the sampler reads only the policy (unchanged by that update) and
     writes only the window store (iteration k's batch was gathered before); the buffer bookkeeping,
     the next replay gather and every PER tree operation stay on the main stream, in order.
+    Measured on one MI355X at the bench config: 567-571 M env-steps/s with it vs 578-587 M
+    without (tools/overlap_ab.sh) — the persistent policy kernel takes every CU, so sharing the
+    chip with the update's kernels only delays it; hence off by default.
 """
 __all__ = ["NstepOffSerialTrainer"]
 
@@ -72,7 +75,7 @@ class NstepOffSerialTrainer:
         self.sampler_tb_dict = LogData()
         self.use_gpu = kwargs.get("use_gpu", torch.cuda.is_available())
         dev = torch.device(self.sample_device)
-        self.overlap = (bool(kwargs.get("trainer_overlap_sampling", True)) and dev.type == "cuda"
+        self.overlap = (bool(kwargs.get("trainer_overlap_sampling", False)) and dev.type == "cuda"
                         and hasattr(self.sampler, "bind_store"))
         self._side = None
         self._pending = None
