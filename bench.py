@@ -36,6 +36,8 @@ def parse():
                    help="init: PyTorch default init (SURVEY 8d); hover: action mean [mg,0,0,0], long episodes")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU-baseline leg (1x4 threads, Px1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-twin-streams", action="store_true",
+                   help="alg_twin_streams off: q1 / q2 branches of the update on one stream (A/B)")
     p.add_argument("--overlap", action="store_true",
                    help="trainer_overlap_sampling: sampling beside the policy-free updates (A/B; off by default)")
     p.add_argument("--graph-segments", action="store_true",
@@ -114,6 +116,8 @@ def main():
         cfg["alg_use_graph"] = False
     if a.overlap:
         cfg["trainer_overlap_sampling"] = True
+    if a.no_twin_streams:
+        cfg["alg_twin_streams"] = False
     if a.graph_segments:
         cfg["alg_force_graph_segments"] = True
     if a.policy == "hover":
