@@ -181,6 +181,11 @@ int mh_env_create(int32_t env_id, int64_t num_envs, uint64_t seed, mh_env_t* out
     const int rows = mh::MAX_STEP + 1;
     double* host = new double[(size_t)rows * mh::QT_ROW];
     mh::quad_fill_table(host, rows);
+    if (!mh::quad_row0_matches(host)) {  // resets use the constant row 0 (QuadTracking::row0)
+      delete[] host;
+      free_handle(h);
+      return fail(MH_EHIP, "mh_env_create: desired-trajectory row 0 differs from QuadTracking::row0");
+    }
     e = hipMalloc(&h->tab, sizeof(double) * rows * mh::QT_ROW);
     if (e == hipSuccess) e = hipMemcpy(h->tab, host, sizeof(double) * rows * mh::QT_ROW, hipMemcpyHostToDevice);
     delete[] host;

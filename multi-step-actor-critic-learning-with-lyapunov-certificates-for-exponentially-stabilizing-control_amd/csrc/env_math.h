@@ -203,6 +203,7 @@ MH_HD float quad_reward(const float* s, const float* Q, const float* u, const fl
 // RL/env/VanderPol.py:23-129. x'' = mu (1 - x^2) x' - x + u, mu = 1, K = 5, dt = 0.01.
 struct VanderPol {
   static constexpr int D = 2, A = 1, S = 2, XS = 0, RS = 2, K = 5;
+  static constexpr int ROWN = 0;  // no per-step table row
   MH_HD static float obs_lo(int i) { (void)i; return -10.0f; }
   MH_HD static float obs_hi(int i) { (void)i; return 10.0f; }
   MH_HD static float act_lo(int i) { (void)i; return -5.0f; }
@@ -229,6 +230,7 @@ struct VanderPol {
 // RL/env/Pendulum.py:22-137. theta'' = (m g L sin th - b th' + u) / (m L^2).
 struct Pendulum {
   static constexpr int D = 2, A = 1, S = 2, XS = 0, RS = 2, K = 5;
+  static constexpr int ROWN = 0;  // no per-step table row
   MH_HD static float obs_lo(int i) { return i == 0 ? -3.14159274101257324f : -10.0f; }
   MH_HD static float obs_hi(int i) { return i == 0 ? 3.14159274101257324f : 10.0f; }
   MH_HD static float act_lo(int i) { (void)i; return -5.0f; }
@@ -257,6 +259,7 @@ struct Pendulum {
 // RL/env/DuctedFan.py:24-147, planar ducted fan, m=8.5 g=9.81 r=0.26 d=0.95 J=0.048.
 struct DuctedFan {
   static constexpr int D = 6, A = 2, S = 6, XS = 0, RS = 6, K = 5;
+  static constexpr int ROWN = 0;  // no per-step table row
   MH_HD static float obs_lo(int i) { return i == 2 ? -1.57079637050628662f : -5.0f; }
   MH_HD static float obs_hi(int i) { return i == 2 ? 1.57079637050628662f : 5.0f; }
   MH_HD static float act_lo(int i) { (void)i; return -5.0f; }
@@ -293,6 +296,7 @@ struct DuctedFan {
 // (M and C are float64 arrays, G float32), LU solve with partial pivoting (LAPACK getrf/getrs).
 struct TwoLink {
   static constexpr int D = 4, A = 2, S = 4, XS = 0, RS = 4, K = 5;
+  static constexpr int ROWN = 0;  // no per-step table row
   MH_HD static float obs_lo(int i) { return i < 2 ? -1.57079637050628662f : -20.0f; }
   MH_HD static float obs_hi(int i) { return i < 2 ? 1.57079637050628662f : 20.0f; }
   MH_HD static float act_lo(int i) { (void)i; return -20.0f; }
@@ -389,6 +393,7 @@ struct CarConst {
 
 struct SingleTrackCar {
   static constexpr int D = 7, A = 2, S = 7, XS = 0, RS = 7, K = 5;
+  static constexpr int ROWN = 0;  // no per-step table row
   MH_HD static float obs_lo(int i) {
     const float lo[7] = {-1.0f, -1.0f, -1.06599998474121094f, -1.0f, -1.57079637050628662f,
                          -1.57079637050628662f, -1.04719758033752441f};
@@ -758,6 +763,7 @@ MH_HD double norm3(const double* a) { return sqrt(fma(a[2], a[2], fma(a[1], a[1]
 struct QuadTracking {
   // state floats: x[0:3] v[3:6] R[6:15] W[15:18]; xstate doubles: Rd_last[9]
   static constexpr int D = 12, A = 4, S = 18, XS = 9, RS = 18, K = 4;
+  static constexpr int ROWN = QT_ROW;  // desired-trajectory row of the step (load_row)
   MH_HD static float obs_lo(int i) { (void)i; return -10.0f; }
   MH_HD static float obs_hi(int i) { (void)i; return 10.0f; }
   MH_HD static float act_lo(int i) { return i == 0 ? 0.0f : -10.0f; }
@@ -847,20 +853,28 @@ struct QuadTracking {
     obs[8] = eR2 * 0.5f;
   }
 
+  // The desired-trajectory row of a step from k (steps since reset): the rollout kernel issues
+  // it as soon as the step counter arrives, so its latency hides behind the action sampling and
+  // the substeps instead of stalling desired_and_obs.
+  MH_HD static void load_row(const double* tab, int k, double* rowv) {
+    const double* rp = tab + (size_t)(k + 1) * QT_ROW;
+    for (int i = 2; i < QT_ROW; ++i) rowv[i] = rp[i];
+  }
+
   // One env.step (QuadTracking.py:205-285); k = steps since reset before this step.
   MH_HD static void step(float* s, double* xs, int k, const float* a, const double* tab,
                          float* obs, float* rew) {
+    double rowv[QT_ROW];
+    load_row(tab, k, rowv);
+    step_row(s, xs, rowv, a, obs, rew);
+  }
+
+  // env.step on a preloaded row (load_row)
+  MH_HD static void step_row(float* s, double* xs, const double* rowv, const float* a, float* obs, float* rew) {
     using Q = QuadConst;
     const float f = a[0];
     const float* M = a + 1;
     const float mf = (float)Q::m;
-    // the desired-trajectory row of this step, loaded before the substeps (its latency hides
-    // behind them instead of stalling desired_and_obs)
-    double rowv[QT_ROW];
-    {
-      const double* rp = tab + (size_t)(k + 1) * QT_ROW;
-      for (int i = 2; i < QT_ROW; ++i) rowv[i] = rp[i];
-    }
 #ifdef MH_EXP_NO_SUBSTEPS  // cost-attribution experiment only
     for (int it = 0; it < 0; ++it) {
 #else
@@ -920,14 +934,53 @@ struct QuadTracking {
     *rew = r;
   }
 
+  // Row 0 of the desired-trajectory table (t = 0: quad_fill_table's expressions with sin 0 = 0,
+  // cos 0 = 1, signed zeros kept) as constants, so a reset reads no memory; mh_env_create and
+  // the host engine compare it with the filled table (quad_row0_matches).
+  MH_HD static double row0(int i) {
+    switch (i) {
+      case 0: return 0.0;                   // t
+      case 1: return 1e-6;                  // safe_time_diff(0, 0)
+      case 2: return 0.4 * 0.0;             // x_d = (0.4 t, 0.4 sin t, 0.6 cos t)
+      case 3: return 0.4 * 0.0;
+      case 4: return 0.6 * 1.0;
+      case 5: return 1.0;                   // b1_d = (cos t, sin t, 0)
+      case 6: return 0.0;
+      case 7: return 0.0;
+      case 8: return (double)(float)0.4;    // v_d (float32 values)
+      case 9: return (double)(float)(0.4 * 1.0);
+      case 10: return (double)(float)(-0.6 * 0.0);
+      case 11: return (double)(float)0.0;   // a_d (float32 values)
+      case 12: return (double)(float)(-0.4 * 0.0);
+      case 13: return (double)(float)(-0.6 * 1.0);
+      case 14: return 0.0;
+      default: return 1.0 / 1e-6;
+    }
+  }
+
   // reset tail (QuadTracking.py:188-202) from drawn x, v, R, W
   MH_HD static void reset_from(const float* rs, float* s, double* xs, const double* tab, float* obs) {
+    (void)tab;
     for (int i = 0; i < 18; ++i) s[i] = rs[i];
+    double row[QT_ROW];
+    for (int i = 0; i < QT_ROW; ++i) row[i] = row0(i);
     double Rd[9];
-    desired_and_obs(s, tab, false, nullptr, Rd, obs);
+    desired_and_obs(s, row, false, nullptr, Rd, obs);
     for (int i = 0; i < 9; ++i) xs[i] = Rd[i];
   }
 };
+
+// Row 0 of a filled table equals QuadTracking::row0 bit for bit (signed zeros included).
+inline bool quad_row0_matches(const double* tab) {
+  for (int i = 0; i < QT_ROW; ++i) {
+    const double c = QuadTracking::row0(i);
+    uint64_t a, b;
+    __builtin_memcpy(&a, tab + i, 8);
+    __builtin_memcpy(&b, &c, 8);
+    if (a != b) return false;
+  }
+  return true;
+}
 
 // Host-side fill of the desired-trajectory table (QuadTracking.py:29-36, 229):
 // current_time accumulates += dt * control_step in float64; row k is the time after k steps.

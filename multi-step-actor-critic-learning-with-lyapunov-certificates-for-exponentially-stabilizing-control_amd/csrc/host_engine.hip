@@ -183,6 +183,10 @@ int mhh_env_create(int32_t env_id, int64_t num_envs, uint64_t seed, mhh_env_t* o
   if (env_id == MH_ENV_QUADTRACKING) {
     h->tab.assign((size_t)(mh::MAX_STEP + 1) * mh::QT_ROW, 0.0);
     mh::quad_fill_table(h->tab.data(), mh::MAX_STEP + 1);
+    if (!mh::quad_row0_matches(h->tab.data())) {  // resets use the constant row 0
+      delete h;
+      return fail(MH_ESTATE, "mhh_env_create: desired-trajectory row 0 differs from QuadTracking::row0");
+    }
   }
   *out = h;
   return MH_OK;

@@ -23,6 +23,41 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t soa_rsrc(const void* p, uint32
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
+// Zero-sized resource for an absent optional input: buffer loads from it return 0.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t opt_rsrc(const void* p, int64_t bytes) {
+  return soa_rsrc(p, p ? (uint32_t)bytes : 0u);
+}
+
+// One env's row of a row-major [E][N] float tensor (byte offset off) as the widest aligned
+// buffer loads (row offsets are multiples of N floats: 16-byte loads when N % 4 == 0, 8-byte
+// loads when N is even; launch_rollout_t checks the base alignment).
+template <int N>
+__device__ __forceinline__ void load_row_buf(__amdgpu_buffer_rsrc_t r, int off, float* out) {
+  // The whole load result is bit-cast to a float vector before any element is read: with this
+  // toolchain (ROCm 7.2 clang, -O3) element extracts from an integer-vector b64/b128 buffer load
+  // are miscompiled (the load shrinks to one dword and every element reads element 0).
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  if constexpr (N % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < N / 4; ++i) {
+      const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 16 * i, 0));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out[4 * i + j] = v[j];
+    }
+  } else if constexpr (N % 2 == 0) {
+#pragma unroll
+    for (int i = 0; i < N / 2; ++i) {
+      const f32x2 v = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 8 * i, 0));
+      out[2 * i] = v[0];
+      out[2 * i + 1] = v[1];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 4 * i, 0));
+  }
+}
+
 // --------------------------------------------------------------- fused lockstep step
 template <class Env>
 #ifndef MH_ROLLOUT_MIN_WAVES
@@ -36,6 +71,8 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
   const bool live = e < E;
   bool emit = false;
   int emit_pos = 0;  // ring slot of the window's oldest record (the position after this push)
+  float rec[F];      // this step's ring record (stored transposed through LDS, below)
+  int wpos = 0;      // the ring slot it goes to
   // store-cursor snapshot for the emission kernel, loaded up front by one thread (the grid
   // finishes with its slowest wave: three dependent round trips at the end would be exposed)
   const bool snap = a.ring && a.cursor && blockIdx.x == 0 && threadIdx.x == 0;
@@ -46,6 +83,29 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
     cur2 = a.cursor[2];
   }
   if (live) {
+    // ---- every per-env input is issued up front, in dependency order: the step counter first
+    // (the QuadTracking desired-trajectory row is addressed by it), then the sampler's inputs
+    // (logits, Philox counter, exploration noise), the ring cursor, the pre-step observation and
+    // the state. The sampling then starts while the state is still in flight, and no load waits
+    // behind a store it cannot be proven disjoint from (one round trip per action component and
+    // one for the ring cursor after the stores, before).
+    // Every load is a raw buffer load, unconditional: an absent optional input is a zero-sized
+    // resource (reads return 0), so there is no branch around a load and the compiler's vmcnt
+    // bookkeeping stays exact (a join after an optional load made it wait for everything).
+    const int vo4 = (int)(e * 4), vo8 = (int)(e * 8);
+    const __amdgpu_buffer_rsrc_t rs_i32 = soa_rsrc(a.steps, (uint32_t)(E * 4));
+    const int k = (int)__builtin_amdgcn_raw_buffer_load_b32(rs_i32, vo4, 0, 0);
+    asm volatile("" ::: "memory");  // issue order pinned (compiler-only barriers: no instruction, no wait)
+    const uint32_t ctr = __builtin_amdgcn_raw_buffer_load_b32(opt_rsrc(a.ctr, E * 4), vo4, 0, 0);
+    float lgt[2 * A], inj[A];
+    load_row_buf<2 * A>(opt_rsrc(a.act_in ? nullptr : a.logits, E * 2 * A * 4), (int)(e * 2 * A * 4), lgt);
+    load_row_buf<A>(opt_rsrc(a.act_in, E * A * 4), (int)(e * A * 4), inj);
+    const float logp_inj =
+        __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(opt_rsrc(a.logp_in, E * 4), vo4, 0, 0));
+    const float noise =
+        __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(opt_rsrc(a.act_noise, 4), 0, 0, 0));
+    float obs0[D];
+    load_row_buf<D>(opt_rsrc((a.ring || a.traj_obs) ? a.obs : nullptr, E * D * 4), (int)(e * D * 4), obs0);
     float s[S];
     double xs[XS > 0 ? XS : 1];
     // SoA state through buffer resources: one VGPR byte offset per env plus a scalar offset per
@@ -53,37 +113,48 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
     // (mh_env_create bounds E so every byte offset fits in 31 bits)
     const __amdgpu_buffer_rsrc_t rs_state = soa_rsrc(a.state, (uint32_t)(S * E * 4));
     const __amdgpu_buffer_rsrc_t rs_xstate = soa_rsrc(a.xstate, (uint32_t)(XS * E * 8));
-    const int vo4 = (int)(e * 4), vo8 = (int)(e * 8);
 #pragma unroll
     for (int i = 0; i < S; ++i)
       s[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs_state, vo4, (int)(i * E * 4), 0));
 #pragma unroll
     for (int i = 0; i < XS; ++i)
       xs[i] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs_xstate, vo8, (int)(i * E * 8), 0));
-    const int k = a.steps[e];
-    const uint32_t ctr = a.ctr[e];  // per-env counter: graph replays need no host RNG state
+    int len = (int)__builtin_amdgcn_raw_buffer_load_b32(opt_rsrc(a.ring_len, E * 4), vo4, 0, 0);
+    int pos = (int)__builtin_amdgcn_raw_buffer_load_b32(opt_rsrc(a.ring_pos, E * 4), vo4, 0, 0);
+    asm volatile("" ::: "memory");  // the table row, which waits for k, is issued after all of the above
+    double rowv[Env::ROWN > 0 ? Env::ROWN : 1];
+    if constexpr (Env::ROWN > 0) {  // Env::load_row as buffer loads (table rows 0..MAX_STEP)
+      typedef double f64x2 __attribute__((ext_vector_type(2)));  // whole-vector cast: see load_row_buf
+      const __amdgpu_buffer_rsrc_t rt = soa_rsrc(a.tab, (uint32_t)((MAX_STEP + 1) * Env::ROWN * 8));
+#ifdef MH_EXP_ROW_CONST  // cost-attribution experiment only: every env reads row 1
+      const int ro = (0 * k + 1) * Env::ROWN * 8;
+#else
+      const int ro = (k + 1) * Env::ROWN * 8;
+#endif
+      static_assert(Env::ROWN % 2 == 0, "rows are read as 16-byte pairs from column 2");
+#pragma unroll
+      for (int i = 2; i < Env::ROWN; i += 2) {
+        const f64x2 v = __builtin_bit_cast(f64x2, __builtin_amdgcn_raw_buffer_load_b128(rt, ro, 8 * i, 0));
+        rowv[i] = v[0];
+        rowv[i + 1] = v[1];
+      }
+    }
+    // compiler-only barrier (no instruction, no wait): the loads above stay issued here instead
+    // of being sunk, split per component, into the branches that consume them (the sampling
+    // branch read one logit per round trip)
+    asm volatile("" ::: "memory");
     const Rng rng = make_rng(a.seed, (uint64_t)e, ctr);
 
-    float obs0[D];
-    if (a.ring || a.traj_obs) {
-#pragma unroll
-      for (int i = 0; i < D; ++i) obs0[i] = a.obs[e * D + i];
-    }
-    // ---- action: injected, or TanhGaussDistribution.sample() + clip
+    // ---- action: TanhGaussDistribution.sample() + clip, or the injected action (selected
+    // after the sampling, which runs either way: no branch merges pending loads into u)
     float u[A];
-    float logp = 0.0f;
-    if (a.act_in) {
-#pragma unroll
-      for (int i = 0; i < A; ++i) u[i] = a.act_in[e * A + i];
-      if (a.logp_in) logp = a.logp_in[e];
-    } else {
+    float logp;
+    {
 #ifdef MH_EXP_NO_SAMPLE  // cost-attribution experiment only
 #pragma unroll
-      for (int i = 0; i < A; ++i) u[i] = fminf(fmaxf(a.logits[e * 2 * A + i], Env::act_lo(i)), Env::act_hi(i));
-      if (false) {
+      for (int i = 0; i < A; ++i) u[i] = fminf(fmaxf(lgt[i], Env::act_lo(i)), Env::act_hi(i));
+      logp = 0.0f;
 #else
-      {
-#endif
       float nz[4];
       rng.normal4f_fast(0, nz);
       // TanhGaussDistribution.sample (act_distribution_cls.py:45-57): z = mu + std * eps,
@@ -92,8 +163,8 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
       float lg = -0.0f, lt = -0.0f;
 #pragma unroll
       for (int i = 0; i < A; ++i) {
-        const float mu = a.logits[e * 2 * A + i];
-        const float raw = a.logits[e * 2 * A + A + i];
+        const float mu = lgt[i];
+        const float raw = lgt[A + i];
         float sd, log_sd;
         if (a.raw_log_std) {  // std = clamp(log_std, lo, hi).exp(): log(std) is the clamped value
           const float c = fminf(fmaxf(raw, a.log_std_lo), a.log_std_hi);
@@ -113,13 +184,18 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
         const float lo = Env::act_lo(i), hi = Env::act_hi(i);
         const float half = (hi - lo) / 2.0f, mid = (hi + lo) / 2.0f;
         float act = half * th + mid;
-        if (a.act_noise) act = act + a.act_noise[0];  // GaussNoise: one scalar per lockstep step
+        if (a.act_noise) act = act + noise;  // GaussNoise: one scalar per lockstep step
         act = fminf(fmaxf(act, lo), hi);  // actions.clip(low, high)
         u[i] = act;
       }
       const float ls = a.log_half_sum;
       logp = (lg - lt) - ls;
-      }
+#endif
+    }
+    if (a.act_in) {  // injected action (and its log-prob when given)
+#pragma unroll
+      for (int i = 0; i < A; ++i) u[i] = inj[i];
+      logp = a.logp_in ? logp_inj : 0.0f;
     }
     if (a.act_out) {
 #pragma unroll
@@ -129,7 +205,10 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
 
     // ---- env.step
     float obs2[D], r;
-    Env::step(s, xs, k, u, a.tab, obs2, &r);
+    if constexpr (Env::ROWN > 0)
+      Env::step_row(s, xs, rowv, u, obs2, &r);
+    else
+      Env::step(s, xs, k, u, a.tab, obs2, &r);
     bool term = false;
 #pragma unroll
     for (int i = 0; i < D; ++i) term = term || (obs2[i] < Env::obs_lo(i)) || (obs2[i] > Env::obs_hi(i));
@@ -203,9 +282,9 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
       a.traj_logp[c] = logp;
     }
 
-    // ---- n-step deque push (base.py:180-217)
+    // ---- n-step deque push (base.py:180-217): the record is built here and stored below,
+    // transposed through LDS with the rest of the wave's records
     if (a.ring) {
-      float rec[F];
 #pragma unroll
       for (int i = 0; i < D; ++i) rec[i] = obs0[i];
 #pragma unroll
@@ -219,10 +298,7 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
 #pragma unroll
       for (int i = 2 * D + A + 4; i < F; ++i) rec[i] = 0.0f;
       const int n = a.n;
-      int len = a.ring_len[e], pos = a.ring_pos[e];
-      float4* dst = reinterpret_cast<float4*>(a.ring + (e * n + pos) * F);
-#pragma unroll
-      for (int i = 0; i < F / 4; ++i) dst[i] = make_float4(rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
+      wpos = pos;
       pos = pos + 1 == n ? 0 : pos + 1;
       len = len + 1 < n ? len + 1 : n;
       emit = (len == n);
@@ -231,6 +307,43 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
       a.ring_len[e] = len;
       a.ring_pos[e] = pos;
     }
+  }
+  if (a.ring) {
+    // Ring records (F floats, one 128-byte line for QuadTracking) written as the wave's
+    // records transposed through LDS: in each store instruction 8 consecutive lanes write one
+    // record's contiguous chunks, so an instruction touches 64 / (F / 4) records' lines instead
+    // of 64 (one record per lane took 3.4 us of the 17.4 us QuadTracking step at E = 65,536:
+    // tools/exp_variants.sh, MH_EXP_NO_RING).
+    constexpr int C = F / 4, CP = C + 1;  // float4 chunks per record; padded LDS record stride
+    __shared__ float4 stage[BLK / 64][64 * CP];
+    __shared__ int spos[BLK / 64][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float4* sw = stage[wave];
+#pragma unroll
+    for (int i = 0; i < C; ++i) sw[lane * CP + i] = make_float4(rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
+    spos[wave][lane] = wpos;
+    __builtin_amdgcn_wave_barrier();
+    const int64_t e0 = (int64_t)blockIdx.x * BLK + wave * 64;
+    const int n = a.n;
+    // the wave's slice of the ring as a buffer resource: records of envs >= E fall outside it
+    // and are dropped by the hardware, so the loop has no branch and its LDS reads batch up
+    const int64_t nrec = e0 < E ? (E - e0 < 64 ? E - e0 : 64) : 0;
+    const __amdgpu_buffer_rsrc_t rr = soa_rsrc(a.ring + e0 * n * F, (uint32_t)(nrec * n * F * 4));
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+#ifndef MH_EXP_NO_RING  // cost-attribution experiment only: no ring record store
+    float4 v[C];
+    int off[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) {  // every LDS read first (one wait), then the stores
+      const int c = j * 64 + lane;
+      const int r = c / C, q = c % C;
+      v[j] = sw[r * CP + q];
+      off[j] = ((r * n + spos[wave][r]) * F + 4 * q) * 4;
+    }
+#pragma unroll
+    for (int j = 0; j < C; ++j) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, v[j]), rr, off[j], 0, 0);
+#endif
+    (void)rr;
   }
   if (a.ring) {
     // block-local exclusive rank of emitters (wave ballot + LDS), env-index order
@@ -561,6 +674,14 @@ __global__ __launch_bounds__(256) void k_aos_to_soa(const T* src, T* dst, int W,
 // --------------------------------------------------------------- launchers
 template <class Env>
 hipError_t launch_rollout_t(const StepArgs& a, hipStream_t st) {
+  // logits / obs rows are read as float4 / float2 vectors (load_row_f32): the tensors must be
+  // aligned to their row vector width (torch allocations are 256-byte aligned)
+  auto aligned = [](const void* p, int n) {
+    const uintptr_t w = n % 4 == 0 ? 16 : (n % 2 == 0 ? 8 : 4);
+    return p == nullptr || (reinterpret_cast<uintptr_t>(p) % w) == 0;
+  };
+  if (!aligned(a.act_in ? nullptr : a.logits, 2 * Env::A) || !aligned(a.act_in, Env::A) || !aligned(a.obs, Env::D))
+    return hipErrorInvalidValue;
   const int grid = (int)((a.E + BLK - 1) / BLK);
   k_rollout<Env><<<grid, BLK, 0, st>>>(a);
   return hipGetLastError();
