@@ -72,6 +72,7 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
   bool emit = false;
   int emit_pos = 0;  // ring slot of the window's oldest record (the position after this push)
   float rec[F];      // this step's ring record (stored transposed through LDS, below)
+  float oout[D];     // next observation row (D % 4 == 0: stored transposed through LDS, below)
   int wpos = 0;      // the ring slot it goes to
   // store-cursor snapshot for the emission kernel, loaded up front by one thread (the grid
   // finishes with its slowest wave: three dependent round trips at the end would be exposed)
@@ -255,7 +256,10 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, xs[i]), rs_xstate, vo8, (int)(i * E * 8), 0);
     a.steps[e] = k1;
     a.ctr[e] = ctr + 1u;
-    if (a.obs) {
+    if constexpr (D % 4 == 0) {  // stored below, transposed through LDS with the wave's rows
+#pragma unroll
+      for (int i = 0; i < D; ++i) oout[i] = obsn[i];
+    } else if (a.obs) {
 #pragma unroll
       for (int i = 0; i < D; ++i) a.obs[e * D + i] = obsn[i];
     }
@@ -344,6 +348,28 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
     for (int j = 0; j < C; ++j) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, v[j]), rr, off[j], 0, 0);
 #endif
     (void)rr;
+  }
+  if constexpr (D % 4 == 0) {
+    if (a.obs) {
+      // next observations, [E][D] rows: the wave's 64 rows are one contiguous 64 * D * 4-byte
+      // range, written as consecutive 16-byte chunks per lane after an LDS transpose
+      __shared__ float4 ostage[BLK / 64][16 * D];
+      const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+      float4* so = ostage[wave];
+#pragma unroll
+      for (int i = 0; i < D / 4; ++i) so[lane * (D / 4) + i] = make_float4(oout[4 * i], oout[4 * i + 1], oout[4 * i + 2], oout[4 * i + 3]);
+      __builtin_amdgcn_wave_barrier();
+      const int64_t e0 = (int64_t)blockIdx.x * BLK + wave * 64;
+      const int64_t nrow = e0 < E ? (E - e0 < 64 ? E - e0 : 64) : 0;
+      const __amdgpu_buffer_rsrc_t ro = soa_rsrc(a.obs + e0 * D, (uint32_t)(nrow * D * 4));
+      typedef float f32x4 __attribute__((ext_vector_type(4)));
+      float4 v[D / 4];
+#pragma unroll
+      for (int j = 0; j < D / 4; ++j) v[j] = so[j * 64 + lane];
+#pragma unroll
+      for (int j = 0; j < D / 4; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, v[j]), ro, (j * 64 + lane) * 16, 0, 0);
+    }
   }
   if (a.ring) {
     // block-local exclusive rank of emitters (wave ballot + LDS), env-index order
