@@ -130,6 +130,20 @@ int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const 
                     const float* reset_states, float* obs, const mh_window_store_t* store,
                     float* act_out, float* logp_out, void* stream);
 
+/* mh_rollout_step with the emission deferred by one step (same arguments; store required):
+ * the windows that become full in this step are copied into `store` by the NEXT deferred step
+ * of the same handle — by extra emitter waves of each block, while the env waves step — or by
+ * mh_rollout_flush. A horizon of deferred steps followed by mh_rollout_flush leaves the store
+ * rows, cursor and ring state identical to the same steps through mh_rollout_step. Every other
+ * call that steps, resets or re-attaches the handle flushes a pending emission first. Falls
+ * back to the immediate emission when num_envs > 1M or num_envs > store->capacity. */
+int mh_rollout_step_deferred(mh_env_t h, const float* logits, const float* act_in, const float* logp_in,
+                             const float* reset_states, float* obs, const mh_window_store_t* store,
+                             float* act_out, float* logp_out, void* stream);
+
+/* Emit the pending windows of the last mh_rollout_step_deferred call (no-op when none). */
+int mh_rollout_flush(mh_env_t h, void* stream);
+
 /* rew_plus_cost scales (RL/utils/rew_plus_cost.py:18-21) used by every sampler step; also set
  * by mh_nstep_attach. Default 1, 1. */
 int mh_env_set_reward_cost_scale(mh_env_t h, float reward_scale, float cost_scale);

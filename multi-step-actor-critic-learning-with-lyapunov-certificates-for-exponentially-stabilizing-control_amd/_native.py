@@ -76,6 +76,9 @@ _PROTOS = {
     "mh_env_set_state": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mh_nstep_attach": (ctypes.c_int, [c_vp, c_i32, c_f32, c_f32]),
     "mh_rollout_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(WindowStore), c_vp, c_vp, c_vp]),
+    "mh_rollout_step_deferred": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(WindowStore), c_vp, c_vp,
+                                                c_vp]),
+    "mh_rollout_flush": (ctypes.c_int, [c_vp, c_vp]),
     "mh_nstep_set_log_std_clamp": (ctypes.c_int, [c_vp, c_i32, c_f32, c_f32]),
     "mh_env_set_reward_cost_scale": (ctypes.c_int, [c_vp, c_f32, c_f32]),
     "mh_env_set_action_noise": (ctypes.c_int, [c_vp, c_vp]),

@@ -69,7 +69,11 @@ struct mh_env_s {
   int32_t* emit_rank = nullptr;
   int32_t* block_count = nullptr;
   int32_t* block_offset = nullptr;
-  int32_t* emit_list = nullptr;
+  int32_t* emit_list = nullptr;     // [2][grid * BLK]: halves alternate between deferred steps
+  // deferred emission (mh_rollout_step_deferred): the last step's windows are not yet emitted
+  bool pending = false;
+  int parity = 0;                   // half of block_count / emit_list the next step writes
+  mh_window_store_t pstore{};       // store the pending windows go to
 
   // optional per-kernel HIP-event timing of mh_rollout_step (bench.py's live roofline)
   bool timing = false;
@@ -128,6 +132,8 @@ static void free_handle(mh_env_s* h) {
 }
 
 extern "C" {
+
+static int flush_pending(mh_env_t h, void* stream);
 
 int mh_abi_version(void) { return MH_ABI_VERSION; }
 
@@ -207,6 +213,7 @@ int mh_env_destroy(mh_env_t h) {
 int mh_nstep_attach(mh_env_t h, int32_t n_step, float reward_scale, float cost_scale) {
   if (!h) return fail(MH_EINVAL, "mh_nstep_attach: null handle");
   if (n_step <= 0 || n_step > 4096) return fail(MH_EINVAL, "mh_nstep_attach: n_step out of range");
+  if (int rc = flush_pending(h, nullptr)) return rc;
   if (h->ring) {
     (void)hipFree(h->ring); (void)hipFree(h->ring_len); (void)hipFree(h->ring_pos);
     (void)hipFree(h->emit_rank); (void)hipFree(h->block_count); (void)hipFree(h->block_offset);
@@ -223,9 +230,11 @@ int mh_nstep_attach(mh_env_t h, int32_t n_step, float reward_scale, float cost_s
   MH_HIP(hipMalloc(&h->ring_len, sizeof(int32_t) * E));
   MH_HIP(hipMalloc(&h->ring_pos, sizeof(int32_t) * E));
   MH_HIP(hipMalloc(&h->emit_rank, sizeof(int32_t) * E));
-  MH_HIP(hipMalloc(&h->block_count, sizeof(int32_t) * h->grid()));
+  MH_HIP(hipMalloc(&h->block_count, sizeof(int32_t) * 2 * h->grid()));
   MH_HIP(hipMalloc(&h->block_offset, sizeof(int32_t) * h->grid()));
-  MH_HIP(hipMalloc(&h->emit_list, sizeof(int32_t) * (size_t)h->grid() * mh::BLK));
+  MH_HIP(hipMalloc(&h->emit_list, sizeof(int32_t) * 2 * (size_t)h->grid() * mh::BLK));
+  h->pending = false;
+  h->parity = 0;
   MH_HIP(hipMemset(h->ring_len, 0, sizeof(int32_t) * E));
   MH_HIP(hipMemset(h->ring_pos, 0, sizeof(int32_t) * E));
   MH_HIP(hipMemset(h->ring, 0, sizeof(float) * E * n_step * F));
@@ -234,6 +243,7 @@ int mh_nstep_attach(mh_env_t h, int32_t n_step, float reward_scale, float cost_s
 
 int mh_env_reset(mh_env_t h, const float* reset_states, float* obs, void* stream) {
   if (!h) return fail(MH_EINVAL, "mh_env_reset: null handle");
+  if (int rc = flush_pending(h, stream)) return rc;
   hipStream_t st = (hipStream_t)stream;
   mh::StepArgs a = h->base_args();
   a.reset_in = reset_states;
@@ -249,6 +259,7 @@ int mh_env_step(mh_env_t h, const float* act, const float* reset_states, float* 
                 float* real_next_obs, float* reward, uint8_t* terminated, uint8_t* truncated,
                 void* stream) {
   if (!h) return fail(MH_EINVAL, "mh_env_step: null handle");
+  if (int rc = flush_pending(h, stream)) return rc;
   if (!act) return fail(MH_EINVAL, "mh_env_step: null actions");
   hipStream_t st = (hipStream_t)stream;
   mh::StepArgs a = h->base_args();
@@ -278,6 +289,7 @@ int mh_env_get_state(mh_env_t h, float* state, double* xstate, int32_t* steps, v
 int mh_env_set_state(mh_env_t h, const float* state, const double* xstate, const int32_t* steps,
                      void* stream) {
   if (!h) return fail(MH_EINVAL, "mh_env_set_state: null handle");
+  if (int rc = flush_pending(h, stream)) return rc;
   hipStream_t st = (hipStream_t)stream;
   if (state) MH_HIP(mh::launch_transpose_f32(state, h->state, h->info.state_dim, h->E, false, st));
   if (xstate && h->info.xstate_dim > 0)
@@ -286,10 +298,9 @@ int mh_env_set_state(mh_env_t h, const float* state, const double* xstate, const
   return MH_OK;
 }
 
-int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const float* logp_in,
-                    const float* reset_states, float* obs, const mh_window_store_t* store,
-                    float* act_out, float* logp_out, void* stream) {
-  if (!h) return fail(MH_EINVAL, "mh_rollout_step: null handle");
+static int rollout_impl(mh_env_t h, const float* logits, const float* act_in, const float* logp_in,
+                        const float* reset_states, float* obs, const mh_window_store_t* store,
+                        float* act_out, float* logp_out, void* stream, bool defer) {
   if (!h->ring) return fail(MH_ESTATE, "mh_rollout_step: call mh_nstep_attach first");
   if (!obs) return fail(MH_EINVAL, "mh_rollout_step: null obs");
   if (!logits && !act_in) return fail(MH_EINVAL, "mh_rollout_step: need logits or act_in");
@@ -316,12 +327,44 @@ int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const 
     a.emit_list = h->emit_list;
     a.cursor = store->cursor;
   }
+  if (defer) {  // this step's counts / lists go to half `parity`; the pending ones are in the other
+    const int p = h->parity;
+    const size_t nb = (size_t)h->grid();
+    a.defer = 1;
+    a.parity = p;
+    a.block_count = h->block_count + p * nb;
+    a.emit_list = h->emit_list + p * nb * mh::BLK;
+    if (h->pending) {
+      a.prev_count = h->block_count + (1 - p) * nb;
+      a.prev_list = h->emit_list + (1 - p) * nb * mh::BLK;
+    }
+    a.w_obs = store->obs;
+    a.w_act = store->act;
+    a.w_rew = store->rew;
+    a.w_cost = store->cost;
+    a.w_obs2 = store->obs2;
+    a.w_done = store->done;
+    a.w_logp = store->logp;
+    a.capacity = store->capacity;
+    a.cursor = store->cursor;
+  }
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   if (h->timing)
     for (int i = 0; i < 4; ++i) ev[i] = h->take_event();
   if (ev[0]) MH_HIP(hipEventRecord(ev[0], st));
   MH_HIP(mh::launch_rollout(h->env_id, a, st));
   if (ev[1]) MH_HIP(hipEventRecord(ev[1], st));
+  if (defer) {  // the emission of this step's windows is left to the next step or the flush
+    h->pending = true;
+    h->pstore = *store;
+    h->parity = 1 - h->parity;
+    if (ev[3]) {
+      MH_HIP(hipEventRecord(ev[2], st));
+      MH_HIP(hipEventRecord(ev[3], st));
+      for (int i = 0; i < 4; ++i) h->ev_pending.push_back(ev[i]);
+    }
+    return MH_OK;
+  }
   if (store && !fused)
     MH_HIP(mh::launch_finalize(h->block_count, store ? h->grid() : 0, h->block_offset, h->meta,
                                store ? store->cursor : nullptr, store ? store->capacity : 1, st));
@@ -380,6 +423,68 @@ int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const 
   return MH_OK;
 }
 
+
+// Emission of the pending deferred step's windows (k_emit_fused on the half of the double
+// buffer that step wrote; the cursor snapshot in meta was written by its emitter waves).
+static int flush_pending(mh_env_t h, void* stream) {
+  if (!h->pending) return MH_OK;
+  h->pending = false;
+  const int pp = 1 - h->parity;  // half written by the pending step
+  const size_t nb = (size_t)h->grid();
+  const mh_window_store_t* store = &h->pstore;
+  mh::EmitArgs ea;
+  std::memset(&ea, 0, sizeof(ea));
+  ea.E = h->E;
+  ea.ring = h->ring;
+  ea.ring_pos = h->ring_pos;
+  ea.meta = h->meta;
+  ea.meta_rw = h->meta;
+  ea.capacity = store->capacity;
+  ea.n = h->n;
+  ea.F = h->info.record_floats;
+  ea.D = h->info.obs_dim;
+  ea.A = h->info.act_dim;
+  ea.obs = store->obs;
+  ea.act = store->act;
+  ea.rew = store->rew;
+  ea.cost = store->cost;
+  ea.obs2 = store->obs2;
+  ea.done = store->done;
+  ea.logp = store->logp;
+  ea.block_count = h->block_count + pp * nb;
+  ea.emit_list = h->emit_list + pp * nb * mh::BLK;
+  ea.nb = (int32_t)nb;
+  ea.cursor = store->cursor;
+  MH_HIP(mh::launch_emit_fused(h->env_id, ea, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_rollout_step(mh_env_t h, const float* logits, const float* act_in, const float* logp_in,
+                    const float* reset_states, float* obs, const mh_window_store_t* store,
+                    float* act_out, float* logp_out, void* stream) {
+  if (!h) return fail(MH_EINVAL, "mh_rollout_step: null handle");
+  if (int rc = flush_pending(h, stream)) return rc;
+  return rollout_impl(h, logits, act_in, logp_in, reset_states, obs, store, act_out, logp_out, stream, false);
+}
+
+int mh_rollout_step_deferred(mh_env_t h, const float* logits, const float* act_in, const float* logp_in,
+                             const float* reset_states, float* obs, const mh_window_store_t* store,
+                             float* act_out, float* logp_out, void* stream) {
+  if (!h) return fail(MH_EINVAL, "mh_rollout_step_deferred: null handle");
+  if (!store) return fail(MH_EINVAL, "mh_rollout_step_deferred: null store (use mh_rollout_step)");
+  // deferral needs the fused emission (E <= 1M envs) and at most `capacity` windows per step
+  const bool ok = h->grid() <= mh::EMIT_FUSED_MAX_NB && h->E <= store->capacity;
+  const bool same = h->pending && std::memcmp(&h->pstore, store, sizeof(*store)) == 0;
+  if (h->pending && (!ok || !same))
+    if (int rc = flush_pending(h, stream)) return rc;
+  return rollout_impl(h, logits, act_in, logp_in, reset_states, obs, store, act_out, logp_out, stream, ok);
+}
+
+int mh_rollout_flush(mh_env_t h, void* stream) {
+  if (!h) return fail(MH_EINVAL, "mh_rollout_flush: null handle");
+  return flush_pending(h, stream);
+}
+
 int mh_env_set_reward_cost_scale(mh_env_t h, float reward_scale, float cost_scale) {
   if (!h) return fail(MH_EINVAL, "mh_env_set_reward_cost_scale: null handle");
   h->reward_scale = reward_scale;
@@ -397,6 +502,7 @@ int mh_rollout_traj_step(mh_env_t h, const float* logits, const float* act_in, c
                          const float* reset_states, float* obs, const mh_traj_store_t* traj, int32_t t,
                          float* act_out, float* logp_out, void* stream) {
   if (!h) return fail(MH_EINVAL, "mh_rollout_traj_step: null handle");
+  if (int rc = flush_pending(h, stream)) return rc;
   if (!obs) return fail(MH_EINVAL, "mh_rollout_traj_step: null obs");
   if (!logits && !act_in) return fail(MH_EINVAL, "mh_rollout_traj_step: need logits or act_in");
   if (!traj || !traj->obs || !traj->act || !traj->rew || !traj->cost || !traj->obs2 || !traj->done ||

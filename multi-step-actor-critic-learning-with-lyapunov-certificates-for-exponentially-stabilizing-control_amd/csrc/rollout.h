@@ -54,10 +54,23 @@ struct StepArgs {
   float *traj_obs, *traj_act, *traj_rew, *traj_cost, *traj_obs2, *traj_logp;
   uint8_t* traj_done;
   int traj_H, traj_t;
+  // deferred emission (mh_rollout_step_deferred): each block has EMIT_WAVES extra waves that
+  // copy the PREVIOUS step's full windows (prev_count / prev_list: its block counts and emitter
+  // lists) into the window store while the env waves step; this step's counts / lists go to
+  // block_count / emit_list (the other half of the double buffer)
+  int defer;                  // 1: deferred mode (blockDim = BLK + 64 * EMIT_WAVES)
+  int parity;                 // meta[META_ACC0 + parity] receives the windows emitted so far
+  const int32_t* prev_count;  // null: nothing pending (first step of a horizon)
+  const int32_t* prev_list;
+  float *w_obs, *w_act, *w_rew, *w_cost, *w_obs2, *w_done, *w_logp;  // window store arrays
+  int64_t capacity;
 };
 
-// meta[] slots (device int64[8])
-constexpr int META_BASE = 1, META_TOTAL = 2, META_SIZE = 3, META_GTOTAL = 4;
+constexpr int EMIT_WAVES = 4;  // emitter waves per block in deferred mode
+
+// meta[] slots (device int64[8]); META_ACC0/1: windows emitted by the deferred steps of the
+// current horizon before the pending step (double-buffered by step parity)
+constexpr int META_BASE = 1, META_TOTAL = 2, META_SIZE = 3, META_GTOTAL = 4, META_ACC0 = 5;
 
 struct EmitArgs {
   int64_t E;

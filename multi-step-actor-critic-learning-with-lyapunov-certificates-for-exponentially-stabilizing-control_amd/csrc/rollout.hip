@@ -58,17 +58,89 @@ __device__ __forceinline__ void load_row_buf(__amdgpu_buffer_rsrc_t r, int off, 
   }
 }
 
+template <int W>
+__device__ __forceinline__ void store_vec(float* dst, const float* v);
+
+// Deferred emission (emitter waves w = 0..EMIT_WAVES-1 of a block in mh_rollout_step_deferred):
+// the previous step's full windows of THIS block's envs, in env-index order, into the window
+// store rows after every earlier block's and every earlier deferred step's windows (the same
+// rows and values as k_emit_fused would have written right after that step:
+// RL/trainer/sampler/base.py:178-217, nstep_replay_buffer.py:122-125). The ring slots read
+// here are overwritten by this launch's env waves only after the block barrier that follows.
+template <int D, int A>
+__device__ void deferred_emit(const StepArgs& a, int w, int lane) {
+  constexpr int F = rec_floats(D, A);
+  const int nb = gridDim.x, blk = blockIdx.x, n = a.n;
+  int pre = 0, tot = 0;  // windows of the blocks before this one / of all blocks
+  if (a.prev_count) {
+    for (int i = lane; i < nb; i += 64) {
+      const int c = a.prev_count[i];
+      tot += c;
+      pre += i < blk ? c : 0;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      pre += __shfl_xor(pre, off, 64);
+      tot += __shfl_xor(tot, off, 64);
+    }
+  }
+  const int64_t M = a.capacity;
+  const int64_t acc = a.prev_count ? a.meta[META_ACC0 + (a.parity ^ 1)] : 0;
+  const int64_t c0 = a.cursor[0];
+  if (a.prev_count) {
+    const int mine = a.prev_count[blk];
+    const int64_t base = (c0 + acc + pre) % M;  // store row of this block's first window
+    for (int q = w * 64 + lane; q < mine * n; q += EMIT_WAVES * 64) {
+      const int r = q / n, j = q - r * n;
+      const int packed = a.prev_list[(int64_t)blk * BLK + r];
+      const int64_t env = (int64_t)blk * BLK + (packed & (BLK - 1));
+      int slot = (packed >> 8) + j;
+      slot = slot >= n ? slot - n : slot;
+      float rec[F];
+      const float4* src = reinterpret_cast<const float4*>(a.ring + (env * n + slot) * (int64_t)F);
+#pragma unroll
+      for (int i = 0; i < F / 4; ++i) {
+        const float4 v = src[i];
+        rec[4 * i] = v.x;
+        rec[4 * i + 1] = v.y;
+        rec[4 * i + 2] = v.z;
+        rec[4 * i + 3] = v.w;
+      }
+      int64_t row = base + r;
+      if (row >= M) row %= M;
+      const int64_t o = row * n + j;
+      store_vec<D>(a.w_obs + o * D, rec);
+      store_vec<A>(a.w_act + o * A, rec + D);
+      store_vec<D>(a.w_obs2 + o * D, rec + D + A);
+      a.w_rew[o] = rec[2 * D + A];
+      a.w_cost[o] = rec[2 * D + A + 1];
+      a.w_done[o] = rec[2 * D + A + 2];
+      a.w_logp[o] = rec[2 * D + A + 3];
+    }
+  }
+  if (blk == 0 && w == 0 && lane == 0) {
+    // windows emitted by this horizon's deferred steps so far, and the cursor snapshot the
+    // flush (k_emit_fused) starts from when this launch's own windows are the last pending ones
+    const int64_t acc1 = acc + tot;
+    a.meta[META_ACC0 + a.parity] = acc1;
+    a.meta[META_BASE] = (c0 + acc1) % M;
+    a.meta[META_SIZE] = a.cursor[1] + acc1;
+    a.meta[META_GTOTAL] = a.cursor[2] + acc1;
+  }
+}
+
 // --------------------------------------------------------------- fused lockstep step
 template <class Env>
 #ifndef MH_ROLLOUT_MIN_WAVES
 #define MH_ROLLOUT_MIN_WAVES 2  // <= 256 VGPRs: 2 waves per SIMD once E exceeds one wave per SIMD
 #endif
-__global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs a) {
+__global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs a) {
   constexpr int D = Env::D, A = Env::A, S = Env::S, XS = Env::XS, RS = Env::RS;
   constexpr int F = rec_floats(D, A);
   const int64_t E = a.E;
+  const bool env_thread = threadIdx.x < BLK;  // waves 0-3; waves 4.. are emitter waves (deferred mode)
   const int64_t e = (int64_t)blockIdx.x * BLK + threadIdx.x;
-  const bool live = e < E;
+  const bool live = env_thread && e < E;
   bool emit = false;
   int emit_pos = 0;  // ring slot of the window's oldest record (the position after this push)
   float rec[F];      // this step's ring record (stored transposed through LDS, below)
@@ -76,7 +148,7 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
   int wpos = 0;      // the ring slot it goes to
   // store-cursor snapshot for the emission kernel, loaded up front by one thread (the grid
   // finishes with its slowest wave: three dependent round trips at the end would be exposed)
-  const bool snap = a.ring && a.cursor && blockIdx.x == 0 && threadIdx.x == 0;
+  const bool snap = a.ring && a.cursor && !a.defer && blockIdx.x == 0 && threadIdx.x == 0;
   int64_t cur0 = 0, cur1 = 0, cur2 = 0;
   if (snap) {
     cur0 = a.cursor[0];
@@ -312,45 +384,8 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
       a.ring_pos[e] = pos;
     }
   }
-  if (a.ring) {
-    // Ring records (F floats, one 128-byte line for QuadTracking) written as the wave's
-    // records transposed through LDS: in each store instruction 8 consecutive lanes write one
-    // record's contiguous chunks, so an instruction touches 64 / (F / 4) records' lines instead
-    // of 64 (one record per lane took 3.4 us of the 17.4 us QuadTracking step at E = 65,536:
-    // tools/exp_variants.sh, MH_EXP_NO_RING).
-    constexpr int C = F / 4, CP = C + 1;  // float4 chunks per record; padded LDS record stride
-    __shared__ float4 stage[BLK / 64][64 * CP];
-    __shared__ int spos[BLK / 64][64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    float4* sw = stage[wave];
-#pragma unroll
-    for (int i = 0; i < C; ++i) sw[lane * CP + i] = make_float4(rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
-    spos[wave][lane] = wpos;
-    __builtin_amdgcn_wave_barrier();
-    const int64_t e0 = (int64_t)blockIdx.x * BLK + wave * 64;
-    const int n = a.n;
-    // the wave's slice of the ring as a buffer resource: records of envs >= E fall outside it
-    // and are dropped by the hardware, so the loop has no branch and its LDS reads batch up
-    const int64_t nrec = e0 < E ? (E - e0 < 64 ? E - e0 : 64) : 0;
-    const __amdgpu_buffer_rsrc_t rr = soa_rsrc(a.ring + e0 * n * F, (uint32_t)(nrec * n * F * 4));
-    typedef float f32x4 __attribute__((ext_vector_type(4)));
-#ifndef MH_EXP_NO_RING  // cost-attribution experiment only: no ring record store
-    float4 v[C];
-    int off[C];
-#pragma unroll
-    for (int j = 0; j < C; ++j) {  // every LDS read first (one wait), then the stores
-      const int c = j * 64 + lane;
-      const int r = c / C, q = c % C;
-      v[j] = sw[r * CP + q];
-      off[j] = ((r * n + spos[wave][r]) * F + 4 * q) * 4;
-    }
-#pragma unroll
-    for (int j = 0; j < C; ++j) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, v[j]), rr, off[j], 0, 0);
-#endif
-    (void)rr;
-  }
   if constexpr (D % 4 == 0) {
-    if (a.obs) {
+    if (a.obs && env_thread) {
       // next observations, [E][D] rows: the wave's 64 rows are one contiguous 64 * D * 4-byte
       // range, written as consecutive 16-byte chunks per lane after an LDS transpose
       __shared__ float4 ostage[BLK / 64][16 * D];
@@ -372,32 +407,75 @@ __global__ __launch_bounds__(BLK, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs 
     }
   }
   if (a.ring) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // Ring records (F floats, one 128-byte line for QuadTracking) are written as the wave's
+    // records transposed through LDS: in each store instruction 8 consecutive lanes write one
+    // record's contiguous chunks, so an instruction touches 64 / (F / 4) records' lines instead
+    // of 64 (one record per lane took 3.4 us of the 17.4 us QuadTracking step at E = 65,536:
+    // tools/exp_variants.sh, MH_EXP_NO_RING). Staged here, stored after the block barrier.
+    constexpr int C = F / 4, CP = C + 1;  // float4 chunks per record; padded LDS record stride
+    __shared__ float4 stage[BLK / 64][64 * CP];
+    __shared__ int spos[BLK / 64][64];
+    if (env_thread) {
+      float4* sw = stage[wave];
+#pragma unroll
+      for (int i = 0; i < C; ++i) sw[lane * CP + i] = make_float4(rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
+      spos[wave][lane] = wpos;
+    } else {
+      // emitter waves: the previous step's windows, while the env waves above compute
+      deferred_emit<D, A>(a, wave - BLK / 64, lane);
+    }
     // block-local exclusive rank of emitters (wave ballot + LDS), env-index order
     __shared__ int wcnt[BLK / 64];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const unsigned long long m = __ballot(emit);
-    if (lane == 0) wcnt[wave] = __popcll(m);
+    if (lane == 0 && env_thread) wcnt[wave] = __popcll(m);
+    // the barrier also orders the emitter waves' ring reads before the ring stores below, which
+    // overwrite each emitted window's oldest slot
     __syncthreads();
-    int base = 0, tot = 0;
+    if (env_thread) {
+      int base = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < BLK / 64; ++w) {
-      base += (w < wave) ? wcnt[w] : 0;
-      tot += wcnt[w];
-    }
-    const int rank = emit ? base + __popcll(m & ((1ull << lane) - 1ull)) : -1;
-    if (a.emit_list) {
-      // (block-local env index | oldest ring slot << 8): the emission kernel needs no ring_pos load
-      static_assert(BLK == 256, "emit_list packs the block-local env index into 8 bits");  // n <= 4096
-      if (emit) a.emit_list[(int64_t)blockIdx.x * BLK + rank] = (int32_t)(e - (int64_t)blockIdx.x * BLK) | (emit_pos << 8);
-    } else if (live) {
-      a.emit_rank[e] = rank;
-    }
-    if (threadIdx.x == 0) a.block_count[blockIdx.x] = tot;
-    if (snap) {
-      // snapshot of the store cursor for the emission kernel (which rewrites the cursor)
-      a.meta[META_BASE] = cur0;
-      a.meta[META_SIZE] = cur1;
-      a.meta[META_GTOTAL] = cur2;
+      for (int w = 0; w < BLK / 64; ++w) {
+        base += (w < wave) ? wcnt[w] : 0;
+        tot += wcnt[w];
+      }
+      const int rank = emit ? base + __popcll(m & ((1ull << lane) - 1ull)) : -1;
+      if (a.emit_list) {
+        // (block-local env index | oldest ring slot << 8): the emission needs no ring_pos load
+        static_assert(BLK == 256, "emit_list packs the block-local env index into 8 bits");  // n <= 4096
+        if (emit) a.emit_list[(int64_t)blockIdx.x * BLK + rank] = (int32_t)(e - (int64_t)blockIdx.x * BLK) | (emit_pos << 8);
+      } else if (live) {
+        a.emit_rank[e] = rank;
+      }
+      if (threadIdx.x == 0) a.block_count[blockIdx.x] = tot;
+      if (snap) {
+        // snapshot of the store cursor for the emission kernel (which rewrites the cursor)
+        a.meta[META_BASE] = cur0;
+        a.meta[META_SIZE] = cur1;
+        a.meta[META_GTOTAL] = cur2;
+      }
+      const float4* sw = stage[wave];
+      const int64_t e0 = (int64_t)blockIdx.x * BLK + wave * 64;
+      const int n = a.n;
+      // the wave's slice of the ring as a buffer resource: records of envs >= E fall outside it
+      // and are dropped by the hardware, so the loop has no branch and its LDS reads batch up
+      const int64_t nrec = e0 < E ? (E - e0 < 64 ? E - e0 : 64) : 0;
+      const __amdgpu_buffer_rsrc_t rr = soa_rsrc(a.ring + e0 * n * F, (uint32_t)(nrec * n * F * 4));
+      typedef float f32x4 __attribute__((ext_vector_type(4)));
+#ifndef MH_EXP_NO_RING  // cost-attribution experiment only: no ring record store
+      float4 v[C];
+      int off[C];
+#pragma unroll
+      for (int j = 0; j < C; ++j) {  // every LDS read first (one wait), then the stores
+        const int c = j * 64 + lane;
+        const int r = c / C, q = c % C;
+        v[j] = sw[r * CP + q];
+        off[j] = ((r * n + spos[wave][r]) * F + 4 * q) * 4;
+      }
+#pragma unroll
+      for (int j = 0; j < C; ++j) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, v[j]), rr, off[j], 0, 0);
+#endif
+      (void)rr;
     }
   }
 }
@@ -709,7 +787,7 @@ hipError_t launch_rollout_t(const StepArgs& a, hipStream_t st) {
   if (!aligned(a.act_in ? nullptr : a.logits, 2 * Env::A) || !aligned(a.act_in, Env::A) || !aligned(a.obs, Env::D))
     return hipErrorInvalidValue;
   const int grid = (int)((a.E + BLK - 1) / BLK);
-  k_rollout<Env><<<grid, BLK, 0, st>>>(a);
+  k_rollout<Env><<<grid, a.defer ? BLK + 64 * EMIT_WAVES : BLK, 0, st>>>(a);
   return hipGetLastError();
 }
 template <class Env>

@@ -56,6 +56,9 @@ class HipNstepOffSampler:
         self.td_lambda = kwargs.get("retrace_lambda", 0.95)
         self.sync_timing = bool(kwargs.get("sampler_sync_timing", True))
         self.use_graph = bool(kwargs.get("sampler_use_graph", True))
+        # emission of each lockstep's windows deferred into the next lockstep's kernel
+        # (mh_rollout_step_deferred); False: a separate emission launch after every step
+        self.deferred_emission = bool(kwargs.get("sampler_deferred_emission", True))
         self.use_fused_policy = bool(kwargs.get("sampler_fused_policy", True))
         self._packed = None
         self._h = self.envs.handle()
@@ -181,11 +184,17 @@ class HipNstepOffSampler:
 
     # ------------------------------------------------------------------ one lockstep step
     def _lockstep(self, store, logits=None, act_in=None, logp_in=None, reset_states=None, act_out=None,
-                  logp_out=None):
-        N.check(N.lib().mh_rollout_step(self._h, N.ptr(logits), N.ptr(act_in), N.ptr(logp_in), N.ptr(reset_states),
-                                        N.ptr(self.obs), ctypes.byref(store.ws) if store is not None else None,
-                                        N.ptr(act_out), N.ptr(logp_out), N.stream_of(self.device)),
+                  logp_out=None, deferred=False):
+        """One lockstep step; `deferred`: its windows are emitted by the next deferred step (by
+        emitter waves running beside that step's env waves) or by _flush (mh_rollout_flush)."""
+        fn = N.lib().mh_rollout_step_deferred if (deferred and store is not None) else N.lib().mh_rollout_step
+        N.check(fn(self._h, N.ptr(logits), N.ptr(act_in), N.ptr(logp_in), N.ptr(reset_states),
+                   N.ptr(self.obs), ctypes.byref(store.ws) if store is not None else None,
+                   N.ptr(act_out), N.ptr(logp_out), N.stream_of(self.device)),
                 "mh_rollout_step")
+
+    def _flush(self):
+        N.check(N.lib().mh_rollout_flush(self._h, N.stream_of(self.device)), "mh_rollout_flush")
 
     def _draw_noise(self):
         if self._noise is not None:
@@ -197,12 +206,13 @@ class HipNstepOffSampler:
         pol = self.networks.policy
         N.check(N.lib().mh_nstep_set_log_std_clamp(self._h, int(raw), float(getattr(pol, "min_log_std", -20.0)),
                                                    float(getattr(pol, "max_log_std", 1.0))), "log_std clamp")
-        self._lockstep(store, logits=logits)
+        self._lockstep(store, logits=logits, deferred=self.deferred_emission)
 
     def _horizon(self, store):
         fused = self._pack_policy()
         for _ in range(self.horizon):
             self._policy_step(store, fused)
+        self._flush()  # the last step's windows: the store is complete when sample() returns
 
     def _graph_for(self, store):
         key = (id(store), id(self.networks.policy), tuple(p.data_ptr() for p in self.networks.policy.parameters()),

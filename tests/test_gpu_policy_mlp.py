@@ -213,3 +213,67 @@ def test_sampler_graph_replays_equal_eager_sampling(tmp_path, warm):
         assert torch.equal(A[3].cursor, B[3].cursor)
         for k in A[3].n_step_buf:
             assert torch.equal(A[3].n_step_buf[k], B[3].n_step_buf[k]), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env_name,graph", [("QuadTracking", True), ("DuctedFan", False), ("VanderPol", True)])
+def test_deferred_emission_equals_immediate_emission(tmp_path, env_name, graph):
+    """mh_rollout_step_deferred (each lockstep's windows copied by the next lockstep's emitter
+    waves, the last by mh_rollout_flush) and mh_rollout_step (a separate emission launch per
+    step) leave bit-identical window stores, cursors and observations after every horizon;
+    VanderPol's long episodes make every env emit every step (the heavy-emission case)."""
+    from msacl_amd.utils.config import build_pipeline, default_msacl_args
+
+    def pipe(deferred, sub):
+        torch.manual_seed(0)
+        args = default_msacl_args(env_name=env_name, env_num=4096, buffer_warm_size=0, buffer_max_size=150000,
+                                  max_iteration=0, eval_interval=10 ** 6, save_folder=str(tmp_path / sub), seed=0,
+                                  num_eval_episode=1, sampler_use_graph=graph, sampler_deferred_emission=deferred)
+        return build_pipeline(args)
+    A, B = pipe(True, "a"), pipe(False, "b")
+    for _ in range(4):
+        A[3].add_batch(A[2].sample()[0])
+        B[3].add_batch(B[2].sample()[0])
+        torch.cuda.synchronize()
+        assert torch.equal(A[2].obs, B[2].obs)
+        assert torch.equal(A[3].cursor, B[3].cursor)
+        for k in A[3].n_step_buf:
+            assert torch.equal(A[3].n_step_buf[k], B[3].n_step_buf[k]), k
+    assert int(A[3].cursor[2]) > 0
+
+
+@pytest.mark.gpu
+def test_deferred_steps_interleaved_with_immediate_calls():
+    """A pending deferred emission is flushed by every other call that steps or resets the
+    handle: deferred, immediate and deferred steps, then an env reset, give the same store and
+    cursor as immediate steps throughout (C ABI, injected actions)."""
+    from msacl_amd.trainer.buffer.device_nstep_replay_buffer import DeviceNstepReplayBuffer
+    from msacl_amd.env.hip_vector_env import HipVectorEnv
+    E, n, name = 1000, 4, "TwoLink"
+    dev = torch.device("cuda", 0)
+    runs = []
+    for mode in ("mixed", "immediate"):
+        env = HipVectorEnv(name, E, seed=3)
+        obs = env.reset()[0].contiguous()
+        N.check(N.lib().mh_nstep_attach(env.handle(), n, 1.0, 1.0), "attach")
+        buf = DeviceNstepReplayBuffer(obs_dim=env.obs_dim, act_dim=env.act_dim, buffer_max_size=5000, n_step=n,
+                                      device=dev)
+        g = torch.Generator(device="cpu").manual_seed(0)
+        st = N.stream_of(dev)
+        for t in range(13):
+            act = (torch.rand(E, env.act_dim, generator=g) * 2 - 1).to(dev).contiguous()
+            lp = torch.randn(E, generator=g).to(dev).contiguous()
+            deferred = mode == "mixed" and t not in (5, 6)
+            fn = N.lib().mh_rollout_step_deferred if deferred else N.lib().mh_rollout_step
+            N.check(fn(env.handle(), None, N.ptr(act), N.ptr(lp), None, N.ptr(obs), ctypes.byref(buf.ws), None, None,
+                       st), "step")
+            if t == 9:
+                N.check(N.lib().mh_env_reset(env.handle(), None, N.ptr(obs), st), "reset")
+        N.check(N.lib().mh_rollout_flush(env.handle(), st), "flush")
+        torch.cuda.synchronize()
+        runs.append((obs.clone(), buf.cursor.clone(), {k: v.clone() for k, v in buf.n_step_buf.items()}))
+    (oa, ca, sa), (ob, cb, sb) = runs
+    assert torch.equal(oa, ob) and torch.equal(ca, cb)
+    assert int(ca[2]) > 0
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
