@@ -22,7 +22,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PEAK_F32_MFMA_TFS = 157.3  # MI355X dense f32 matrix peak (v_mfma_f32_*_f32)
-PMC_TRAFFIC = "r01_pmc_traffic_v3.json"  # the PMC summary of the current kernels (tools/pmc.sh)
+PMC_TRAFFIC = "r02_pmc_traffic_v4.json"  # the PMC summary of the current kernels (tools/pmc.sh + tools/pmc_summary.py)
 
 
 def parse():
@@ -194,12 +194,22 @@ def main():
         N.lib().mh_policy_forward(N.ptr(sampler._packed), N.ptr(sampler.obs), a.envs, sampler.envs.obs_dim,
                                   2 * sampler.envs.act_dim, N.ptr(pol_out), st)
 
+    def k_defer():  # the sampler's lockstep kernel: k_rollout<Env> + its emitter waves copying the
+        # previous launch's windows into the replay store (mh_rollout_step_deferred)
+        N.lib().mh_rollout_step_deferred(h, N.ptr(logits), None, None, None, N.ptr(sampler.obs),
+                                         ctypes.byref(buffer.ws), None, None, st)
+
     t_pol = time_launches(k_policy, reps) * 1e-3 if have_fused else None
     t_step = time_launches(k_roll, reps) * 1e-3
     win1 = int(buffer.cursor[2].item())
     t_pair = time_launches(k_pair, reps, warm=0) * 1e-3
     windows = (int(buffer.cursor[2].item()) - win1) / reps
     t_emit = max(t_pair - t_step, 1e-9)
+    win2 = int(buffer.cursor[2].item())
+    t_defer = time_launches(k_defer, reps, warm=0) * 1e-3
+    N.check(N.lib().mh_rollout_flush(h, st), "mh_rollout_flush")
+    torch.cuda.synchronize()
+    windows_defer = (int(buffer.cursor[2].item()) - win2) / reps
 
     # ---- live roofline of the engine's kernels (algorithmic bytes / measured device time)
     info = sampler.envs.info
@@ -207,12 +217,19 @@ def main():
     n = sampler.n_step
     bytes_step_kernel = a.envs * ((S * 4 + XS * 8 + 4 + 2 * A_ * 4 + D_ * 4 + 8)
                                   + (S * 4 + XS * 8 + 4 + D_ * 4 + F * 4 + 8 + 4))
-    bytes_emit = windows * (n * F * 4 + n * (2 * D_ + A_ + 4) * 4)
+    bytes_window = n * F * 4 + n * (2 * D_ + A_ + 4) * 4  # ring records read + 7 store arrays written
+    bytes_emit = windows * bytes_window
+    bytes_defer = bytes_step_kernel + windows_defer * bytes_window
     kernels = {
+        "rollout_emit": {"avg_us": round(t_defer * 1e6, 3), "bytes": round(bytes_defer, 1),
+                         "windows": windows_defer, "GBps": round(bytes_defer / t_defer / 1e9, 1),
+                         "note": "the sampler's lockstep kernel (mh_rollout_step_deferred): the env step of "
+                                 "every env + the previous launch's windows into the replay store"},
         "rollout_step": {"avg_us": round(t_step * 1e6, 3), "bytes": bytes_step_kernel,
                          "GBps": round(bytes_step_kernel / t_step / 1e9, 1)},
         "window_emit": {"avg_us": round(t_emit * 1e6, 3), "bytes": bytes_emit, "windows": windows,
-                        "GBps": round(bytes_emit / t_emit / 1e9, 1)},
+                        "GBps": round(bytes_emit / t_emit / 1e9, 1),
+                        "note": "separate emission launch (mh_rollout_step), not used by the sampler"},
         "method": f"HIP events around {reps} back-to-back launches after a GPU spin; emit = (rollout+emit) - rollout",
     }
     if t_pol is not None:
@@ -222,7 +239,7 @@ def main():
                                      "TFLOPs": round(flops / t_pol / 1e12, 2),
                                      "frac_f32_mfma": round(flops / t_pol / 1e12 / PEAK_F32_MFMA_TFS, 4),
                                      "note": "per lockstep step; f32 MFMA bound, not HBM"}
-    dom = "rollout_step" if t_step >= t_emit else "window_emit"
+    dom = "rollout_emit"
     ach = kernels[dom]["GBps"]
     # HBM bytes per launch: PMC counters cannot be read from inside this process (rocprofv3 --pmc
     # wraps the whole command), so `traffic` is the committed measurement of this same command

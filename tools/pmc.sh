@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 for c in FETCH_SIZE WRITE_SIZE; do
   rm -rf gpurun_out/pmc_$c
   timeout -k 10 900 rocprofv3 --pmc $c -d gpurun_out/pmc_$c -o pmc --output-format csv -- \
-    python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmc_$c.log 2>&1
+    python3 bench.py --steps 3 --warmup 3 --no-cpu-baseline > gpurun_out/pmc_$c.log 2>&1
   rc=$?
   echo "pmc $c rc=$rc"
   [ $rc -ne 0 ] && { tail -20 gpurun_out/pmc_$c.log; exit $rc; }

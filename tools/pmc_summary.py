@@ -14,8 +14,13 @@ import os
 import sys
 from collections import defaultdict
 
-ALIASES = {"rollout_step": "k_rollout<mh::QuadTracking>", "window_emit": "k_emit_fused<12, 4>",
-           "replay_gather": "k_gather", "msacl_lyapunov": "k_lyapunov", "msacl_q_target": "k_q_target"}
+# alias -> (kernel-name pattern, grid size in threads or None): at 65,536 envs k_rollout runs a
+# 65,536-thread grid for a plain step and 131,072 (4 env + 4 emitter waves per block) for the
+# sampler's deferred-emission step (the Workgroup_Size column is the launch-bounds maximum)
+ALIASES = {"rollout_emit": ("k_rollout<mh::QuadTracking>", 131072),
+           "rollout_step": ("k_rollout<mh::QuadTracking>", 65536),
+           "window_emit": ("k_emit_fused<12, 4>", None), "replay_gather": ("k_gather", None),
+           "msacl_lyapunov": ("k_lyapunov", None), "msacl_q_target": ("k_q_target", None)}
 
 
 def load(root, counter):
@@ -24,7 +29,8 @@ def load(root, counter):
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
                 continue
-            vals[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+            g = r.get("Grid_Size") or r.get("Grid_Size_X") or ""
+            vals[f'{r["Kernel_Name"]} [grid {g}]'].append(float(r["Counter_Value"]))
     return vals
 
 
@@ -38,10 +44,10 @@ def main():
         wk = sum(write.get(name, [0])) / max(1, len(write.get(name, [])))
         res["kernels"][name] = {"fetch_kib": fk, "write_kib": wk, "dispatches": len(fetch.get(name, [])),
                                 "bytes_per_launch": 2 * fk * 1024 + wk * 1024}
-    for alias, pat in ALIASES.items():
+    for alias, (pat, wg) in ALIASES.items():
         for name, v in res["kernels"].items():
-            if pat in name:
-                res[alias] = v
+            if pat in name and (wg is None or f"[grid {wg}]" in name):
+                res[alias] = dict(v, kernel=name)
                 break
     json.dump(res, open(out, "w"), indent=1)
     for a in ALIASES:
