@@ -22,8 +22,11 @@ TOL = dict(rtol=1e-5, atol=1e-5)
 TRACES = sorted(glob.glob(os.path.join(G, "nstep_*.npz")))
 
 
-def _run_trace(path, capacity=None, tile=1, check_obs=False):
-    g = np.load(path)
+def _run_trace(path, capacity=None, tile=1, check_obs=False, deferred=False, g=None):
+    """Replay a reference _n_step trace through the fused rollout (injected actions); deferred:
+    through mh_rollout_step_deferred (each step's windows emitted by the next step's emitter
+    waves) and a final mh_rollout_flush. `g` overrides the fixture (a sliced trace)."""
+    g = np.load(path) if g is None else g
     name = os.path.basename(path)[6:-4].replace("_n20", "")
     # TwoLink's upright arm is open-loop unstable: under the trace's recorded (feedback) torques
     # replayed open loop, ulp-level differences grow ~e-fold every few steps (2e-5 by step 12 of
@@ -46,8 +49,9 @@ def _run_trace(path, capacity=None, tile=1, check_obs=False):
         act = torch.as_tensor(tl(g["actions"][t]), device=dev).contiguous()
         lp = torch.as_tensor(tl(g["logp"][t]), device=dev).contiguous()
         rs = torch.as_tensor(tl(g["resets"][t]), device=dev).contiguous()
-        N.check(N.lib().mh_rollout_step(h, None, N.ptr(act), N.ptr(lp), N.ptr(rs), N.ptr(obs), ctypes.byref(buf.ws),
-                                        None, None, N.stream_of(dev)), "rollout")
+        fn = N.lib().mh_rollout_step_deferred if deferred else N.lib().mh_rollout_step
+        N.check(fn(h, None, N.ptr(act), N.ptr(lp), N.ptr(rs), N.ptr(obs), ctypes.byref(buf.ws), None, None,
+                   N.stream_of(dev)), "rollout")
         if tile == 1:
             np.testing.assert_allclose(obs.cpu().numpy(), g["obs_trace"][t + 1], **TOL)
         elif check_obs:
@@ -57,6 +61,7 @@ def _run_trace(path, capacity=None, tile=1, check_obs=False):
             ref = torch.as_tensor(tl(g["obs_trace"][t + 1]), device=dev).contiguous()
             env.set_state(ref)
             obs.copy_(ref)
+    N.check(N.lib().mh_rollout_flush(h, N.stream_of(dev)), "flush")
     torch.cuda.synchronize()
     return g, buf, total, tile
 
@@ -75,18 +80,20 @@ def _expected_windows(g, tile):
     return {k: np.concatenate(v) for k, v in out.items()}
 
 
+@pytest.mark.parametrize("deferred", [False, True], ids=["immediate", "deferred"])
 @pytest.mark.parametrize("path", TRACES, ids=os.path.basename)
-def test_windows_match_reference_sampler(path):
-    g, buf, total, _ = _run_trace(path)
+def test_windows_match_reference_sampler(path, deferred):
+    g, buf, total, _ = _run_trace(path, deferred=deferred)
     assert buf.size == total and int(buf.cursor[2]) == total
     for k in KEYS:
         np.testing.assert_allclose(buf.n_step_buf[k][:total].cpu().numpy(), g["w_" + k], **TOL, err_msg=k)
     assert not buf.n_step_buf["done"][:total, :-1].any()
 
 
+@pytest.mark.parametrize("deferred", [False, True], ids=["immediate", "deferred"])
 @pytest.mark.parametrize("path", TRACES[:2], ids=os.path.basename)
-def test_windows_tiled_to_many_envs(path):
-    g, buf, total, tile = _run_trace(path, tile=256)
+def test_windows_tiled_to_many_envs(path, deferred):
+    g, buf, total, tile = _run_trace(path, tile=256, deferred=deferred)
     exp = _expected_windows(g, tile)
     for k in KEYS:
         np.testing.assert_allclose(buf.n_step_buf[k][:total].cpu().numpy(), exp[k], **TOL, err_msg=k)
@@ -160,3 +167,51 @@ def test_host_and_device_builds_agree(path):
             np.testing.assert_array_equal(h, d, err_msg=k)
         else:
             np.testing.assert_allclose(h, d, **TOL, err_msg=k)
+
+
+@pytest.mark.parametrize("deferred", [False, True], ids=["immediate", "deferred"])
+def test_single_env_vanderpol_windows(deferred):
+    """Config 1's shape on the device (VanderPol, env_num = 1): env 0 of the reference's n = 20
+    trace alone through the fused rollout; its windows equal the oracle's replay of the same
+    single-env trace (the oracle is bit-exact against the reference's full trace,
+    tests/test_oracle_golden.py; envs are independent, so env 0's slice is a valid trace)."""
+    from oracle import sampler as OS
+    path = os.path.join(G, "nstep_VanderPol_n20.npz")
+    full = np.load(path)
+    g = {k: full[k] for k in full.files}
+    for k in ("init_reset", "init_steps"):
+        g[k] = g[k][:1]
+    for k in ("actions", "logp", "resets", "obs_trace"):
+        g[k] = g[k][:, :1]
+    t = {"t": -1}
+    venv = OS.VectorEnv("VanderPol", 1, lambda idx: g["init_reset"][idx] if t["t"] < 0 else g["resets"][t["t"]][idx])
+    ro = OS.NStepRollout(venv, int(g["n_step"]))
+    venv.steps[:] = g["init_steps"]
+    wins, counts = [], []
+    for k in range(g["actions"].shape[0]):
+        t["t"] = k
+        w, _ = ro.step(g["actions"][k], g["logp"][k])
+        counts.append(len(w))
+        wins += w
+    g["counts"] = np.array(counts)
+    assert len(wins) > 0
+    _, buf, total, _ = _run_trace(path, g=g, deferred=deferred)
+    assert total == len(wins) and int(buf.cursor[2]) == total
+    for j, k in enumerate(KEYS):
+        np.testing.assert_array_equal(buf.n_step_buf[k][:total].cpu().numpy(), np.stack([w[j] for w in wins]),
+                                      err_msg=k)
+
+
+def test_single_env_vanderpol_pipeline_trains(tmp_path):
+    """Config 1's plumbing on the device: the unchanged pipeline (create_envs -> create_sampler ->
+    create_buffer -> create_alg -> trainer) with env_num = 1 trains a few MSACL iterations."""
+    from msacl_amd.utils.config import build_pipeline, default_msacl_args
+    args = default_msacl_args(env_name="VanderPol", env_num=1, buffer_warm_size=64, buffer_max_size=10000,
+                              replay_batch_size=32, max_iteration=4, eval_interval=10 ** 6, save_folder=str(tmp_path),
+                              seed=0, num_eval_episode=1)
+    _, alg, sampler, buffer, _, trainer = build_pipeline(args)
+    assert sampler.device.type == "cuda"
+    trainer.train()
+    torch.cuda.synchronize()
+    assert buffer.size >= 64
+    assert all(torch.isfinite(p).all() for p in alg.networks.parameters())

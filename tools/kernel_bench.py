@@ -90,7 +90,9 @@ def bench_rollout(name, E, reps, dev, n=20):
     try:
         N.check(N.lib().mh_nstep_attach(h, n, 100.0, 100.0), "attach")
         N.check(N.lib().mh_nstep_set_log_std_clamp(h, 1, -20.0, 1.0), "clamp")
-        buf = DeviceNstepReplayBuffer(obs_dim=D, act_dim=A, buffer_max_size=1_000_000, n_step=n, device=dev)
+        store = E <= 1_000_000  # the window store path (fused / deferred emission) at <= 1M envs
+        buf = DeviceNstepReplayBuffer(obs_dim=D, act_dim=A, buffer_max_size=1_000_000, n_step=n, device=dev) \
+            if store else None
         obs = torch.empty(E, D, device=dev)
         st = N.stream_of(dev)
         N.check(N.lib().mh_env_reset(h, None, N.ptr(obs), st), "reset")
@@ -98,8 +100,8 @@ def bench_rollout(name, E, reps, dev, n=20):
         logits[:, A:] = -1.0  # log std
         # warm the rings so windows are emitted every step
         for _ in range(n):
-            N.check(N.lib().mh_rollout_step(h, N.ptr(logits), None, None, None, N.ptr(obs), ctypes.byref(buf.ws),
-                                            None, None, st), "rollout")
+            N.check(N.lib().mh_rollout_step(h, N.ptr(logits), None, None, None, N.ptr(obs),
+                                            ctypes.byref(buf.ws) if store else None, None, None, st), "rollout")
 
         def fn_roll():
             N.lib().mh_rollout_step(h, N.ptr(logits), None, None, None, N.ptr(obs), None, None, None, st)
@@ -107,17 +109,30 @@ def bench_rollout(name, E, reps, dev, n=20):
         def fn_pair():
             N.lib().mh_rollout_step(h, N.ptr(logits), None, None, None, N.ptr(obs), ctypes.byref(buf.ws), None, None, st)
 
+        def fn_defer():
+            N.lib().mh_rollout_step_deferred(h, N.ptr(logits), None, None, None, N.ptr(obs), ctypes.byref(buf.ws),
+                                             None, None, st)
+
         ms_roll = time_launches(fn_roll, reps)
+        b_roll = (S * 4 + XS * 8 + 4 + 2 * A * 4 + D * 4 + 8) + (S * 4 + XS * 8 + 4 + D * 4 + F * 4 + 8 + 4)
+        out.append(row("rollout_step", name, E, "env_steps", b_roll, ms_roll))
+        if not store:
+            return out
         w0 = int(buf.cursor[2].item())
         ms_pair = time_launches(fn_pair, reps, warm=0)
         wins = (int(buf.cursor[2].item()) - w0) / reps
-        b_roll = (S * 4 + XS * 8 + 4 + 2 * A * 4 + D * 4 + 8) + (S * 4 + XS * 8 + 4 + D * 4 + F * 4 + 8 + 4)
-        out.append(row("rollout_step", name, E, "env_steps", b_roll, ms_roll))
         ms_emit = max(ms_pair - ms_roll, 1e-6)
         b_win = n * F * 4 + n * (2 * D + A + 4) * 4
         out.append(row("window_emit(pair-minus-rollout)", name, round(wins, 1), "windows", b_win, ms_emit,
                        pair_us=round(ms_pair * 1e3, 3)))
-        del buf
+        w1 = int(buf.cursor[2].item())
+        ms_defer = time_launches(fn_defer, reps, warm=0)
+        N.check(N.lib().mh_rollout_flush(h, st), "flush")
+        torch.cuda.synchronize()
+        wd = (int(buf.cursor[2].item()) - w1) / reps
+        # per env-step bytes of the deferred kernel: the step + its share of the windows it emits
+        out.append(row("rollout_emit(deferred)", name, E, "env_steps", b_roll + wd * b_win / E, ms_defer,
+                       windows=round(wd, 1)))
         return out
     finally:
         torch.cuda.synchronize()
@@ -270,7 +285,8 @@ def main():
                 rows.append(bench_env_step(name, E, a.reps, dev))
     if "rollout" not in skip:
         for name in a.envs.split(","):
-            rows += bench_rollout(name, 65536, a.reps, dev)
+            for E in sizes:
+                rows += bench_rollout(name, E, a.reps, dev)
     if "gather" not in skip:
         for B in (256, 65536):
             rows.append(bench_gather("QuadTracking", B, a.reps, dev))
