@@ -341,8 +341,8 @@ class MSACL:
             # data parallel: the policy and alpha gradients share one all-reduce (the alpha loss
             # reads the policy forward's entropy, not the stepped policy), then both steps
             merge = self._segmented() and self.auto_alpha
-            for _ in range(self.policy_frequency):
-                loss_policy, entropy = self._policy_update(data=data, defer_step=merge)
+            for k in range(self.policy_frequency):
+                loss_policy, entropy = self._policy_update(data=data, defer_step=merge, reuse_adv=k > 0)
                 if self.auto_alpha:
                     self._alpha_update(entropy=entropy, defer_step=merge)
                 if merge:
@@ -458,10 +458,42 @@ class MSACL:
             self.networks.lyapunov_optimizer.step()
         return s.loss_lya[0]  # a view of the scratch (no allocation on the side stream)
 
-    def _policy_update(self, data, defer_step=False):
+    def _stability_advantage(self, data, s):
+        """V(obs_0), V(obs2) and the raw stability advantage with its (sum, sum of squares)
+        statistics into the scratch (msacl.py:392-400); the (Σ, Σ²) all-reduce makes them the
+        global batch's under data parallelism."""
+        obs, obs2, old_logp = data["obs"], data["obs2"], data["logp"]
+        B, n = old_logp.shape
+        with torch.no_grad():
+            # V(obs_0) and V(obs2) as one batch (msacl.py:395-396)
+            D_ = obs.shape[-1]
+            V_all = self.networks.lyapunov(torch.cat([obs[:, 0], obs2.reshape(-1, D_)], 0))
+            V0 = V_all[:B].contiguous()
+            V2 = V_all[B:].reshape(B, n).contiguous()
+        _engine("msacl_stability_adv", self.device, N.ptr(V0), N.ptr(V2), N.ptr(self.lya_diff_coef),
+                N.ptr(self.start_lya_coef), B, n, N.ptr(s.adv_raw), N.ptr(s.stats))
+        D.allreduce_(s.stats)
+
+    def _policy_update(self, data, defer_step=False, reuse_adv=False):
+        """One policy step (msacl.py:340-405). reuse_adv: a later step of the same update (the
+        policy_frequency loop): the Lyapunov network and the batch are unchanged since the first
+        step, so its stability advantage and statistics, still in the scratch, are the values a
+        recomputation would produce (deterministic kernels), and are not recomputed. The first
+        step computes them on the side stream, beside the policy / critic forward chain (joined
+        before the clip)."""
         obs, old_act, obs2, old_logp = data["obs"], data["act"], data["obs2"], data["logp"]
         B, n = old_logp.shape
         s = self._buf(B, n)
+        side = None
+        if not reuse_adv:
+            side = self._side_stream()
+            if side is not None:
+                main = torch.cuda.current_stream(self.device)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    self._stability_advantage(data, s)
+            else:
+                self._stability_advantage(data, s)
         for p in list(self.networks.q1.parameters()) + list(self.networks.q2.parameters()):
             p.requires_grad = False
         dist = self.networks.create_action_distributions(self.networks.policy(obs))
@@ -472,15 +504,8 @@ class MSACL:
         loss_policy_q, entropy = _PolicyQLoss.apply(q1.contiguous(), q2.contiguous(), new_act_logp.contiguous(),
                                                     self.networks.log_alpha.detach())
         is_ratio = _Ratio0.apply(dist.log_prob(old_act).contiguous(), old_logp.contiguous())
-        with torch.no_grad():
-            # V(obs_0) and V(obs2) as one batch (msacl.py:395-396)
-            D_ = obs.shape[-1]
-            V_all = self.networks.lyapunov(torch.cat([obs[:, 0], obs2.reshape(-1, D_)], 0))
-            V0 = V_all[:B].contiguous()
-            V2 = V_all[B:].reshape(B, n).contiguous()
-        _engine("msacl_stability_adv", self.device, N.ptr(V0), N.ptr(V2), N.ptr(self.lya_diff_coef),
-                N.ptr(self.start_lya_coef), B, n, N.ptr(s.adv_raw), N.ptr(s.stats))
-        D.allreduce_(s.stats)
+        if side is not None:
+            main.wait_stream(side)  # the side branch wrote only the scratch's adv_raw / stats
         n_total = float(B * D.world_size())
         r_det = is_ratio.detach().contiguous()
         _engine("msacl_ppo_clip", self.device, N.ptr(r_det), N.ptr(s.adv_raw), N.ptr(s.stats), n_total,
