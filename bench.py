@@ -159,7 +159,7 @@ def main():
         buffer.add_batch(samples)
         torch.cuda.synchronize()
         tb_ = time.perf_counter()
-        rs = buffer.sample_batch(trainer.replay_batch_size)
+        rs = trainer._replay_batch()  # as the trainer does (into the update graph's static inputs)
         alg.model_update(rs, trainer.iteration)
         trainer.iteration += 1
         torch.cuda.synchronize()

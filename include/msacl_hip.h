@@ -370,6 +370,14 @@ int mh_msacl_ratio0(const float* logp_new, const float* old_logp, int32_t B, int
                     void* stream);
 int mh_msacl_ratio0_backward(const float* ratio, const float* g_ratio, int32_t B, int32_t n, float* d_logp_new,
                              void* stream);
+/* loss_policy = -loss_q - loss_ppo (msacl.py:401-405, device scalars) and neg_d_ratio = -d_ratio
+ * (the is_ratio backward seed of loss_policy) in one launch. */
+int mh_msacl_policy_combine(const float* loss_q, const float* loss_ppo, const float* d_ratio, int32_t B,
+                            float* loss_policy, float* neg_d_ratio, void* stream);
+/* grad = (entropy - target_entropy) * exp(log_alpha): the log_alpha gradient of the alpha loss
+ * (msacl.py:429-437, replaces its 6-kernel autograd chain; the Adam step follows). */
+int mh_msacl_alpha_grad(const float* log_alpha, const float* entropy, float target_entropy, float* grad,
+                        void* stream);
 
 /* ---- prioritized replay (new: the reference trainer expects buffer.update_batch(idx, prio),
  * RL/trainer/nstep_off_serial_trainer.py:93-95, but ships no prioritized buffer) ---- */

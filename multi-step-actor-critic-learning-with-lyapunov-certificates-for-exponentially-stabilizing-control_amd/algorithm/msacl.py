@@ -135,6 +135,7 @@ class _Scratch:
         self.dV_both = f(2 * B, n)
         self.dV, self.dV2 = self.dV_both[:B], self.dV_both[B:]
         self.adv_raw, self.adv, self.loss_ppo, self.d_ratio = f(B), f(B), f(1), f(B)
+        self.loss_policy, self.neg_d_ratio = f(1), f(B)
         self.stats = torch.empty(2, dtype=torch.float64, device=device)
 
 
@@ -186,6 +187,7 @@ class MSACL:
         self._scratch = {}
         self.last_priority = None
         self._neg_one = torch.tensor(-1.0, device=self.device)
+        self._alpha_grad = None
         self.use_graph = bool(kwargs.get("alg_use_graph", True))
         # the Lyapunov update shares no parameter with the critic update (both only read the
         # policy and the batch): on one GPU it runs on a second stream, concurrently
@@ -306,7 +308,7 @@ class MSACL:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 loss_lya = self._lyapunov_update(data)
-            loss_q, q1_mean, q2_mean = self._q_update(data)
+            loss_q, q1_mean, q2_mean = self._q_update(data, stats=do_policy)
             if do_target:
                 self._target_update()
             main.wait_stream(side)
@@ -321,7 +323,7 @@ class MSACL:
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 loss_lya = self._lyapunov_update(data, defer_step=True)
-            loss_q, q1_mean, q2_mean = self._q_update(data, defer_step=True)
+            loss_q, q1_mean, q2_mean = self._q_update(data, defer_step=True, stats=do_policy)
             main.wait_stream(side)
             nets = self.networks
             D.allreduce_grads(list(nets.q1.parameters()) + list(nets.q2.parameters()) +
@@ -332,7 +334,7 @@ class MSACL:
             if do_target:
                 self._target_update()
         else:
-            loss_q, q1_mean, q2_mean = self._q_update(data)
+            loss_q, q1_mean, q2_mean = self._q_update(data, stats=do_policy)
             if do_target:
                 self._target_update()
             loss_lya = self._lyapunov_update(data)
@@ -361,6 +363,16 @@ class MSACL:
         """World size > 1 (or the test switch): the graph is cut at every collective
         (utils/dist.py GraphSegments) instead of capturing the update as one graph."""
         return D.graph_segments_wanted() or self.force_graph_segments
+
+    def replay_inputs(self, batch_size: int):
+        """The replayed update's static input tensors, for the replay buffer to gather the next
+        batch straight into (DeviceNstepReplayBuffer.sample_batch(out=...)): the replay then
+        needs no copy of the batch. None until the first graph-mode update has created them (or
+        when the update does not replay graphs, or the batch size differs)."""
+        st = self._static
+        if st is None or not self._graphable() or st["rew"].shape[0] != batch_size:
+            return None
+        return st
 
     def _graph_update(self, data, flags):
         """Replay the whole update (~250 launches) as one HIP graph (with data parallelism: a
@@ -396,7 +408,7 @@ class MSACL:
         self.last_priority = prio
         return outs
 
-    def _q_update(self, data, defer_step=False):
+    def _q_update(self, data, defer_step=False, stats=True):
         obs, act, rew, obs2, done = data["obs"], data["act"], data["rew"], data["obs2"], data["done"]
         B, n = rew.shape
         s = self._buf(B, n)
@@ -430,8 +442,12 @@ class MSACL:
             D.allreduce_grads(list(self.networks.q1.parameters()) + list(self.networks.q2.parameters()))
             self.networks.q1_optimizer.step()
             self.networks.q2_optimizer.step()
-        self.last_priority = s.abs_td.clone()
-        return s.loss_q[0].clone(), q1.detach().mean(), q2.detach().mean()
+        if self.per_flag:
+            self.last_priority = s.abs_td.clone()
+        if not stats:  # iterations without a policy step log nothing (model_update returns None)
+            return s.loss_q[0], None, None
+        # views of the scratch / fresh means, read by model_update right after the update
+        return s.loss_q[0], q1.detach().mean(), q2.detach().mean()
 
     def _lyapunov_update(self, data, defer_step=False):
         obs, obs2, act, old_logp = data["obs"], data["obs2"], data["act"], data["logp"]
@@ -510,9 +526,16 @@ class MSACL:
         r_det = is_ratio.detach().contiguous()
         _engine("msacl_ppo_clip", self.device, N.ptr(r_det), N.ptr(s.adv_raw), N.ptr(s.stats), n_total,
                 float(self.clip_coef), B, N.ptr(s.adv), N.ptr(s.loss_ppo), N.ptr(s.d_ratio))
-        loss_policy = -loss_policy_q.detach() - s.loss_ppo[0]
+        if self.device.type == "cuda":
+            # the logged total and the ratio seed -d_ratio in one launch (a view of the scratch,
+            # read by model_update right after the update)
+            _engine("msacl_policy_combine", self.device, N.ptr(loss_policy_q.detach()), N.ptr(s.loss_ppo),
+                    N.ptr(s.d_ratio), B, N.ptr(s.loss_policy), N.ptr(s.neg_d_ratio))
+            loss_policy, seed = s.loss_policy[0], s.neg_d_ratio
+        else:
+            loss_policy, seed = -loss_policy_q.detach() - s.loss_ppo[0], -s.d_ratio
         self.networks.policy_optimizer.zero_grad()
-        torch.autograd.backward([loss_policy_q, is_ratio], [self._neg_one, -s.d_ratio])
+        torch.autograd.backward([loss_policy_q, is_ratio], [self._neg_one, seed])
         if not defer_step:
             D.allreduce_grads(list(self.networks.policy.parameters()))
             self.networks.policy_optimizer.step()
@@ -522,10 +545,21 @@ class MSACL:
         return loss_policy.detach(), entropy
 
     def _alpha_update(self, entropy, defer_step=False):
-        alpha = self._get_alpha(requires_grad=True)
-        loss_alpha = alpha * (entropy - self.target_entropy)
-        self.networks.alpha_optimizer.zero_grad()
-        loss_alpha.backward()
+        """msacl.py:429-441. On the device the gradient of alpha * (entropy - target_entropy)
+        w.r.t. log_alpha is formed by one kernel (mh_msacl_alpha_grad, autograd's own product)
+        into a persistent .grad (the zero_grad + backward it replaces write the same value)."""
+        la = self.networks.log_alpha
+        if self.device.type == "cuda":
+            if self._alpha_grad is None:
+                self._alpha_grad = torch.zeros_like(la)
+            la.grad = self._alpha_grad
+            _engine("msacl_alpha_grad", self.device, N.ptr(la.detach()), N.ptr(entropy.contiguous()),
+                    float(self.target_entropy), N.ptr(self._alpha_grad))
+        else:
+            alpha = self._get_alpha(requires_grad=True)
+            loss_alpha = alpha * (entropy - self.target_entropy)
+            self.networks.alpha_optimizer.zero_grad()
+            loss_alpha.backward()
         if not defer_step:
             D.allreduce_grads([self.networks.log_alpha])
             self._alpha_step()

@@ -368,6 +368,23 @@ __global__ __launch_bounds__(256) void k_ratio0_bwd(const float* ratio, const fl
   dlp[i] = (i - b * n) == 0 ? g[b] * ratio[b] : 0.0f;
 }
 
+// loss_policy = -loss_policy_q - loss_policy_lya (msacl.py:401-405, the logged total) and the
+// seed -d_ratio of the is_ratio backward, in one launch (instead of a negation, a subtraction and
+// a second negation)
+__global__ __launch_bounds__(256) void k_policy_combine(const float* loss_q, const float* loss_ppo,
+                                                        const float* d_ratio, int B, float* loss_policy,
+                                                        float* neg_d_ratio) {
+  const int b = blockIdx.x * 256 + threadIdx.x;
+  if (b < B) neg_d_ratio[b] = -d_ratio[b];
+  if (b == 0) loss_policy[0] = (-loss_q[0]) - loss_ppo[0];
+}
+// d/dlog_alpha of loss_alpha = exp(log_alpha) * (entropy - target_entropy) (msacl.py:429-437) as
+// autograd forms it: mul's backward gives 1 * (entropy - target), exp's multiplies by its result
+__global__ __launch_bounds__(64) void k_alpha_grad(const float* log_alpha, const float* entropy, float target,
+                                                   float* grad) {
+  if (threadIdx.x == 0) grad[0] = (entropy[0] - target) * expf(log_alpha[0]);
+}
+
 thread_local std::string g_merr;
 
 }  // namespace
@@ -463,6 +480,23 @@ int mh_msacl_ratio0_backward(const float* ratio, const float* g_ratio, int32_t B
   const int64_t total = (int64_t)B * n;
   k_ratio0_bwd<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(ratio, g_ratio, B, n, d_logp_new);
   MH_CHECK_LAUNCH("ratio0_bwd");
+  return MH_OK;
+}
+
+int mh_msacl_policy_combine(const float* loss_q, const float* loss_ppo, const float* d_ratio, int32_t B,
+                            float* loss_policy, float* neg_d_ratio, void* stream) {
+  if (!loss_q || !loss_ppo || !d_ratio || !loss_policy || !neg_d_ratio || B <= 0) return MH_EINVAL;
+  k_policy_combine<<<(unsigned)((B + 255) / 256), 256, 0, (hipStream_t)stream>>>(loss_q, loss_ppo, d_ratio, B,
+                                                                                 loss_policy, neg_d_ratio);
+  MH_CHECK_LAUNCH("policy_combine");
+  return MH_OK;
+}
+
+int mh_msacl_alpha_grad(const float* log_alpha, const float* entropy, float target_entropy, float* grad,
+                        void* stream) {
+  if (!log_alpha || !entropy || !grad) return MH_EINVAL;
+  k_alpha_grad<<<1, 64, 0, (hipStream_t)stream>>>(log_alpha, entropy, target_entropy, grad);
+  MH_CHECK_LAUNCH("alpha_grad");
   return MH_OK;
 }
 

@@ -536,41 +536,57 @@ __device__ __forceinline__ int pm_scale_exp(float bound) {  // 14 - ceil(log2(bo
   return k < -40 ? -40 : (k > 40 ? 40 : k);
 }
 
-// The raw magnitudes behind the scales, as float bits combined by atomic max (non-negative floats
-// order like their bit patterns): [0] max |W1, b1|, [1] max |W2|, [2] max |W3|,
+// The raw magnitudes behind the scales: [0] max |W1, b1|, [1] max |W2|, [2] max |W3|,
 // [3] R1 = max_k (sum_j |W1[k][j]| + |b1[k]|), [4] R2 = max_o (sum_k |W2[o][k]| + |b2[o]|).
-// One workgroup per hidden unit k: row k of W1 and W2, column k of W3.
-__global__ __launch_bounds__(256) void k_policy_scales(const float* __restrict__ W1, const float* __restrict__ b1,
-                                                       const float* __restrict__ W2, const float* __restrict__ b2,
-                                                       const float* __restrict__ W3, int D, int N3, int K1,
-                                                       float* __restrict__ P) {
-  __shared__ float red[2][256];
-  const int k = blockIdx.x, i = threadIdx.x;
-  const float w2 = fabsf(W2[(int64_t)k * PM_H + i]);
-  red[0][i] = w2;
-  red[1][i] = w2;
-  __syncthreads();
-  for (int h = 128; h > 0; h >>= 1) {
-    if (i < h) {
-      red[0][i] = fmaxf(red[0][i], red[0][i + h]);
-      red[1][i] = red[1][i] + red[1][i + h];
-    }
-    __syncthreads();
+// ONE workgroup of 1024 threads (W2 is 256 KB: ~2 us from L2 for one CU): four lanes per row of
+// W2 (64 columns each, 16-byte loads) combined by shuffles, W1 rows and W3 columns one lane per
+// hidden unit, then a block max. Plain stores: 256 workgroups combining by atomic max on these five
+// words serialised at the L2 (17.5 us per pack).
+__global__ __launch_bounds__(1024) void k_policy_scales(const float* __restrict__ W1, const float* __restrict__ b1,
+                                                        const float* __restrict__ W2, const float* __restrict__ b2,
+                                                        const float* __restrict__ W3, int D, int N3, int K1,
+                                                        float* __restrict__ P) {
+  __shared__ float red[5][16];
+  const int t = threadIdx.x, row = t >> 2, part = t & 3;
+  const float4* w2 = reinterpret_cast<const float4*>(W2 + (int64_t)row * PM_H + part * 64);
+  float m2 = 0.0f, s2 = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float4 v = w2[i];
+    const float a = fabsf(v.x), b = fabsf(v.y), c = fabsf(v.z), d = fabsf(v.w);
+    m2 = fmaxf(m2, fmaxf(fmaxf(a, b), fmaxf(c, d)));
+    s2 += (a + b) + (c + d);
   }
-  if (i == 0) {
-    float m1 = fabsf(b1[k]), r1 = m1, m3 = 0.0f;
+  m2 = fmaxf(m2, __shfl_xor(m2, 1, 64));
+  m2 = fmaxf(m2, __shfl_xor(m2, 2, 64));
+  s2 += __shfl_xor(s2, 1, 64);
+  s2 += __shfl_xor(s2, 2, 64);
+  float r2 = part == 0 ? s2 + fabsf(b2[row]) : 0.0f;
+  float m1 = 0.0f, r1 = 0.0f, m3 = 0.0f;
+  if (t < PM_H) {
+    m1 = fabsf(b1[t]);
+    r1 = m1;
     for (int j = 0; j < D; ++j) {
-      const float v = fabsf(W1[(int64_t)k * D + j]);
+      const float v = fabsf(W1[(int64_t)t * D + j]);
       m1 = fmaxf(m1, v);
       r1 += v;
     }
-    for (int o = 0; o < N3; ++o) m3 = fmaxf(m3, fabsf(W3[(int64_t)o * PM_H + k]));
-    unsigned int* raw = reinterpret_cast<unsigned int*>(P + pm_off_scal(K1));
-    atomicMax(raw + 0, __float_as_uint(m1));
-    atomicMax(raw + 1, __float_as_uint(red[0][0]));
-    atomicMax(raw + 2, __float_as_uint(m3));
-    atomicMax(raw + 3, __float_as_uint(r1));
-    atomicMax(raw + 4, __float_as_uint(red[1][0] + fabsf(b2[k])));
+    for (int o = 0; o < N3; ++o) m3 = fmaxf(m3, fabsf(W3[(int64_t)o * PM_H + t]));
+  }
+  float v[5] = {m1, m2, m3, r1, r2};
+#pragma unroll
+  for (int q = 0; q < 5; ++q)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v[q] = fmaxf(v[q], __shfl_xor(v[q], off, 64));
+  if ((t & 63) == 0) {
+#pragma unroll
+    for (int q = 0; q < 5; ++q) red[q][t >> 6] = v[q];
+  }
+  __syncthreads();
+  if (t < 5) {
+    float m = 0.0f;
+    for (int w = 0; w < 16; ++w) m = fmaxf(m, red[t][w]);
+    P[pm_off_scal(K1) + t] = m;
   }
 }
 
@@ -961,13 +977,14 @@ int64_t policy_packed_floats(int D) { return pm_packed_floats(D / 2 + 1); }
 hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
                               const float* b3, int D, int N3, float* P, hipStream_t st) {
   const int K1 = D / 2 + 1;  // ceil((D + 1) / 2): observation + the bias input
+  if (reinterpret_cast<uintptr_t>(W2) & 15) return hipErrorInvalidValue;  // k_policy_scales: 16-byte rows
   const int64_t total = pm_off_w2x6(K1);
   const int grid = (int)((total + 255) / 256 < 1024 ? (total + 255) / 256 : 1024);
   k_policy_pack<<<grid, 256, 0, st>>>(W1, b1, W2, b2, W3, b3, D, N3, K1, P);
   if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
   k_policy_pack_x6<<<(int)(PM_X6_FLOATS * 2 / 256), 256, 0, st>>>(W2, K1, P);
   if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
-  k_policy_scales<<<PM_H, 256, 0, st>>>(W1, b1, W2, b2, W3, D, N3, K1, P);
+  k_policy_scales<<<1, 1024, 0, st>>>(W1, b1, W2, b2, W3, D, N3, K1, P);
   if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
   k_policy_pack_x3<<<(int)((PM_X3_FLOATS + PM_X3_W1_FLOATS + PM_X3_W3_FLOATS) * 2 / 256), 256, 0, st>>>(
       W1, b1, W2, W3, D, N3, K1, P);

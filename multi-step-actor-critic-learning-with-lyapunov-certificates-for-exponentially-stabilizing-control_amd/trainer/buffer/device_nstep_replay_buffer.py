@@ -131,16 +131,39 @@ class DeviceNstepReplayBuffer:
         self._draws += 1
         return idx
 
-    def gather(self, idx):
+    def _fits(self, out, B):
+        """`out` can receive a gather of B windows: every key, float32, contiguous, this device,
+        the batch's shapes."""
+        if out is None:
+            return False
+        n, D, A = self.n_step, self.obsv_dim, self.act_dim
+        shapes = {"obs": (B, n, D), "act": (B, n, A), "rew": (B, n), "cost": (B, n), "obs2": (B, n, D),
+                  "done": (B, n), "logp": (B, n)}
+        for k, shp in shapes.items():
+            t = out.get(k)
+            if (t is None or tuple(t.shape) != shp or t.dtype != torch.float32 or t.device != self.device
+                    or not t.is_contiguous()):
+                return False
+        return True
+
+    def gather(self, idx, out=None):
+        """The windows at `idx` as [B, n, ...] tensors; into `out` (a dict of such tensors, e.g.
+        the update graph's static inputs, so the replayed update needs no copy) when it fits,
+        otherwise into fresh tensors."""
         B = int(idx.numel())
         n, D, A = self.n_step, self.obsv_dim, self.act_dim
-        e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
-        out = {"obs": e(B, n, D), "act": e(B, n, A), "rew": e(B, n), "cost": e(B, n), "obs2": e(B, n, D),
-               "done": e(B, n), "logp": e(B, n)}
+        if self._fits(out, B):
+            out = {k: out[k] for k in KEYS}
+        else:
+            e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
+            out = {"obs": e(B, n, D), "act": e(B, n, A), "rew": e(B, n), "cost": e(B, n), "obs2": e(B, n, D),
+                   "done": e(B, n), "logp": e(B, n)}
         idx = idx.to(self.device, torch.int64).contiguous()
         N.check(N.lib().mh_replay_gather(ctypes.byref(self.ws), n, D, A, N.ptr(idx), B,
                                          *[N.ptr(out[k]) for k in KEYS], N.stream_of(self.device)), "mh_replay_gather")
         return out
 
-    def sample_batch(self, batch_size: int) -> dict:
-        return self.gather(self.sample_indices(batch_size))
+    def sample_batch(self, batch_size: int, out=None) -> dict:
+        """nstep_replay_buffer.py:136-148. `out` (optional): destination tensors (gather)."""
+        idx = self.sample_indices(batch_size)
+        return self.gather(idx, out) if out is not None else self.gather(idx)

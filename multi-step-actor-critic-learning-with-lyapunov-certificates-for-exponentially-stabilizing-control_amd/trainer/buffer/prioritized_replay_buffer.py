@@ -34,14 +34,21 @@ class PrioritizedReplayBuffer(DeviceNstepReplayBuffer):
                                        self.max_size, N.ptr(self.max_prio), N.stream_of(self.device)), "mh_per_set_new")
         self._seen.copy_(self.cursor)
 
-    def sample_batch(self, batch_size: int) -> dict:
-        idx = torch.empty(batch_size, dtype=torch.int64, device=self.device)
-        w = torch.empty(batch_size, dtype=torch.float32, device=self.device)
+    def sample_batch(self, batch_size: int, out=None) -> dict:
+        """Proportional draw + IS weights, then the window gather (into `out` when it fits,
+        DeviceNstepReplayBuffer.gather; its "idx" / "weight" too)."""
+        fits = self._fits(out, batch_size)
+        idx = out.get("idx") if fits else None
+        w = out.get("weight") if fits else None
+        if idx is None or idx.shape != (batch_size,) or idx.dtype != torch.int64:
+            idx = torch.empty(batch_size, dtype=torch.int64, device=self.device)
+        if w is None or w.shape != (batch_size,) or w.dtype != torch.float32:
+            w = torch.empty(batch_size, dtype=torch.float32, device=self.device)
         N.check(N.lib().mh_per_sample(N.ptr(self.tree), self.pow2, N.ptr(self.cursor), self.seed, self._per_draws,
                                       batch_size, self.beta, N.ptr(idx), N.ptr(w), N.stream_of(self.device)),
                 "mh_per_sample")
         self._per_draws += 1
-        out = self.gather(idx)
+        out = self.gather(idx, out)
         out["idx"] = idx
         out["weight"] = w
         return out

@@ -85,6 +85,14 @@ class NstepOffSerialTrainer:
         with ModuleOnDevice(self.networks, self.sample_device):
             return self.sampler.sample()
 
+    def _replay_batch(self):
+        """buffer.sample_batch (:87-89); gathered straight into the update graph's static inputs
+        when the algorithm replays graphs and the buffer takes an `out` (no copy before the replay)."""
+        out = self.alg.replay_inputs(self.replay_batch_size) if hasattr(self.alg, "replay_inputs") else None
+        if out is not None:
+            return self.buffer.sample_batch(self.replay_batch_size, out=out)
+        return self.buffer.sample_batch(self.replay_batch_size)
+
     def _overlap_next(self):
         """Sampling of iteration + 1 may run beside this iteration's update."""
         return (self.overlap and self.iteration % self.policy_frequency != 0
@@ -100,7 +108,7 @@ class NstepOffSerialTrainer:
                 sampler_samples, sampler_tb_dict = self._sample()
             self.buffer.add_batch(sampler_samples)
             self.sampler_tb_dict.add_average(sampler_tb_dict)
-        replay_samples = self.buffer.sample_batch(self.replay_batch_size)
+        replay_samples = self._replay_batch()
         if self._overlap_next():
             if self._side is None:
                 self._side = torch.cuda.Stream(device=torch.device(self.sample_device))

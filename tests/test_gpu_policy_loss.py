@@ -60,3 +60,33 @@ def test_ratio0_matches_torch(B, n):
     torch.autograd.backward([r], [up])
     torch.autograd.backward([ref], [up])
     assert torch.equal(lp.grad, lp2.grad)
+
+
+@pytest.mark.parametrize("B", [256, 1, 300])
+def test_policy_combine_matches_torch(B):
+    """mh_msacl_policy_combine: loss_policy = -loss_q - loss_ppo and -d_ratio, bit-exact with the
+    PyTorch expressions it replaces (msacl.py:401-405)."""
+    import msacl_amd._native as N
+    g = torch.Generator(device="cuda").manual_seed(B)
+    lq = torch.randn(1, device="cuda", generator=g)
+    lppo = torch.randn(1, device="cuda", generator=g)
+    dr = torch.randn(B, device="cuda", generator=g)
+    lp, neg = torch.empty(1, device="cuda"), torch.empty(B, device="cuda")
+    N.check(N.lib().mh_msacl_policy_combine(N.ptr(lq), N.ptr(lppo), N.ptr(dr), B, N.ptr(lp), N.ptr(neg),
+                                            N.stream_of(lq.device)), "mh_msacl_policy_combine")
+    assert torch.equal(lp[0], -lq[0] - lppo[0])
+    assert torch.equal(neg, -dr)
+
+
+@pytest.mark.parametrize("log_alpha,entropy,target", [(1.0, 3.7, -5.0), (-2.3, -6.1, -4.0), (0.0, 0.0, 0.0)])
+def test_alpha_grad_matches_autograd(log_alpha, entropy, target):
+    """mh_msacl_alpha_grad equals autograd's gradient of exp(log_alpha) * (entropy - target)
+    w.r.t. log_alpha (msacl.py:429-437), bit for bit."""
+    import msacl_amd._native as N
+    la = torch.tensor(log_alpha, device="cuda", requires_grad=True)
+    ent = torch.tensor(entropy, device="cuda")
+    (la.exp() * (ent - target)).backward()
+    out = torch.empty((), device="cuda")
+    N.check(N.lib().mh_msacl_alpha_grad(N.ptr(la.detach()), N.ptr(ent), float(target), N.ptr(out),
+                                        N.stream_of(ent.device)), "mh_msacl_alpha_grad")
+    assert torch.equal(out, la.grad)

@@ -146,3 +146,50 @@ def _overlap_vs_serial(tmp_path, buffer_name):
     for k in a[1]:
         assert torch.equal(a[1][k], b[1][k]), k
     assert torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
+
+
+@pytest.mark.parametrize("buffer_name", ["nstep_replay_buffer", "prioritized_replay_buffer"])
+def test_gather_into_update_inputs_equals_copy(tmp_path, monkeypatch, buffer_name):
+    """The trainer gathers each replay batch straight into the replayed update graph's static
+    inputs (MSACL.replay_inputs -> sample_batch(out=...)): bit-identical networks and buffer to
+    gathering into fresh tensors that the update then copies in (deterministic GEMM mode, as
+    above)."""
+    from msacl_amd.algorithm.msacl import MSACL
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+
+    def run(direct, sub):
+        torch.manual_seed(0)
+        args = default_msacl_args(env_name="DuctedFan", env_num=2048, buffer_name=buffer_name, buffer_warm_size=2000,
+                                  buffer_max_size=60000, max_iteration=6, eval_interval=10 ** 6,
+                                  log_save_interval=10 ** 6, apprfunc_save_interval=10 ** 6,
+                                  save_folder=str(tmp_path / sub), seed=0, num_eval_episode=1)
+        args, alg, sampler, buffer, evaluator, trainer = build_pipeline(args)
+        seen = []
+        orig = buffer.sample_batch
+
+        def spy(bs, out=None):
+            r = orig(bs, out=out) if out is not None else orig(bs)
+            seen.append(all(r[k].data_ptr() == alg._static[k].data_ptr() for k in ("obs", "rew"))
+                        if alg._static is not None else False)
+            return r
+        buffer.sample_batch = spy
+        if not direct:
+            monkeypatch.setattr(MSACL, "replay_inputs", lambda self, b: None)
+        trainer.train()
+        monkeypatch.undo()
+        torch.cuda.synchronize()
+        sd = {k: v.detach().cpu().clone() for k, v in alg.networks.state_dict().items()}
+        extra = buffer.tree.cpu().clone() if hasattr(buffer, "tree") else None
+        return sd, extra, seen
+
+    try:
+        a = run(True, "a")
+        b = run(False, "b")
+    finally:
+        torch.use_deterministic_algorithms(prev)
+    assert any(a[2]) and not any(b[2])  # the direct path really gathered into the static inputs
+    for k in a[0]:
+        assert torch.equal(a[0][k], b[0][k]), k
+    if a[1] is not None:
+        assert torch.equal(a[1], b[1])

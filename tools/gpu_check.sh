@@ -14,7 +14,7 @@ run() {  # run <name> <timeout_s> <cmd...>
 STEPS=${STEPS:-"tests smoke bench"}
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 1500 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf ;;
+    tests) run pytest_gpu 840 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf ;;
     smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py --steps ${BENCH_STEPS:-10} --warmup ${BENCH_WARMUP:-3} ;;
     hover) run bench_hover 900 python bench.py --steps ${BENCH_STEPS:-10} --warmup ${BENCH_WARMUP:-3} --policy hover --no-cpu-baseline ;;
