@@ -22,6 +22,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PEAK_F32_MFMA_TFS = 157.3  # MI355X dense f32 matrix peak (v_mfma_f32_*_f32)
+PEAK_F16_MFMA_TFS = 2500.0  # MI355X dense f16 matrix peak (v_mfma_f32_32x32x16_f16), MI355X_MICROARCH.md
 PMC_TRAFFIC = "r02_pmc_traffic_v4.json"  # the PMC summary of the current kernels (tools/pmc.sh + tools/pmc_summary.py)
 
 
@@ -235,10 +236,15 @@ def main():
     if t_pol is not None:
         D0, A2 = sampler.envs.obs_dim, 2 * sampler.envs.act_dim
         flops = 2.0 * a.envs * (D0 * 256 + 256 * 256 + 256 * A2)
+        # split-f16 arithmetic: every f32 product is 3 f16 MFMA products (hi.hi + hi.lo + lo.hi),
+        # so the kernel's own ceiling is the dense f16 peak / 3 in f32-equivalent flop/s
         kernels["policy_forward"] = {"avg_us": round(t_pol * 1e6, 3), "flops": flops,
                                      "TFLOPs": round(flops / t_pol / 1e12, 2),
-                                     "frac_f32_mfma": round(flops / t_pol / 1e12 / PEAK_F32_MFMA_TFS, 4),
-                                     "note": "per lockstep step; f32 MFMA bound, not HBM"}
+                                     "f16_mfma_TFLOPs": round(3 * flops / t_pol / 1e12, 2),
+                                     "frac_f16_mfma_peak": round(3 * flops / t_pol / 1e12 / PEAK_F16_MFMA_TFS, 4),
+                                     "vs_f32_mfma_peak": round(flops / t_pol / 1e12 / PEAK_F32_MFMA_TFS, 4),
+                                     "note": "per lockstep step; f32-accurate split-f16 MFMA (3 products per f32 "
+                                             "product): bound by the f16 MFMA rate, not HBM; flops = f32-equivalent"}
     dom = "rollout_emit"
     ach = kernels[dom]["GBps"]
     # HBM bytes per launch: PMC counters cannot be read from inside this process (rocprofv3 --pmc

@@ -39,6 +39,34 @@ constexpr int MAX_STEP = 1000;  // every env: truncated = current_step >= 1000
 MH_HD float sin32(float x) { return sinf(x); }
 MH_HD float cos32(float x) { return cosf(x); }
 MH_HD float tan32(float x) { return tanf(x); }
+// sin and cos of one argument through one shared range reduction (OCML / glibc sincosf: the same
+// reduction and polynomials as sinf and cosf, so the same values)
+MH_HD void sincos32(float x, float* s, float* c) { sincosf(x, s, c); }
+// a / b for the f32 sites whose reference division is not a bit-exact parity point: on the
+// device the hardware reciprocal and one FMA residual correction (within 1 ulp, correctly rounded
+// almost always; ~5 instructions instead of the IEEE division's scale / fixup sequence), on the
+// host the division itself
+MH_HD float div32(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float r = __builtin_amdgcn_rcpf(b);
+  const float q = a * r;
+  return fmaf(fmaf(-b, q, a), r, q);
+#else
+  return a / b;
+#endif
+}
+// 1.0 / x in float64: on the device the hardware reciprocal refined by two Newton steps (within
+// ~1 ulp), on the host the division
+MH_HD double rcp64(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double d = __builtin_amdgcn_rcp(x);
+  d = d * fma(-x, d, 2.0);
+  d = d * fma(-x, d, 2.0);
+  return d;
+#else
+  return 1.0 / x;
+#endif
+}
 
 // `s ** 2` on a NumPy float32 SCALAR calls the C library's powf (glibc 2.35 e_powf.c, the
 // ARM optimized-routines algorithm: 16-entry log2 table + degree-5 poly, 32-entry exp2 table +
@@ -306,14 +334,14 @@ struct TwoLink {
     const double I2 = I1;
     const float q1 = s[0], q2 = s[1], dq1 = s[2], dq2 = s[3];
     // mass matrix (TwoLink.py:100-107)
-    float c2 = cos32(q2);
+    float s2, c2;
+    sincos32(q2, &s2, &c2);
     float in11 = (float)(1.0 * 1.0 + 0.5 * 0.5) + ((float)((2.0 * 1.0) * 0.5) * c2);
     float M11f = (float)((I1 + I2) + 1.0 * (0.5 * 0.5)) + (1.0f * in11);
     float in12 = (float)(0.5 * 0.5) + ((float)(1.0 * 0.5) * c2);
     float M12f = (float)I2 + (1.0f * in12);
     double M11 = M11f, M12 = M12f, M21 = M12f, M22 = I2 + 1.0 * (0.5 * 0.5);
     // coriolis (TwoLink.py:109-119)
-    float s2 = sin32(q2);
     float h = (float)((-1.0 * 1.0) * 0.5) * s2;
     float C11 = h * dq2, C12 = h * dq2 + h * dq1, C21 = (-h) * dq1;
     // gravity (TwoLink.py:121-129)
@@ -335,11 +363,12 @@ struct TwoLink {
       t = a12; a12 = a22; a22 = t;
       t = b1; b1 = b2; b2 = t;
     }
-    double l21 = a21 * (1.0 / a11);
+    const double i11 = rcp64(a11);
+    double l21 = a21 * i11;
     double u22 = a22 - l21 * a12;
     double y2 = b2 - l21 * b1;
-    double x2 = y2 * (1.0 / u22);
-    double x1 = (b1 - a12 * x2) * (1.0 / a11);
+    double x2 = y2 * rcp64(u22);
+    double x1 = (b1 - a12 * x2) * i11;
     out[0] = dq1; out[1] = dq2; out[2] = x1; out[3] = x2;
   }
   MH_HD static void step(float* s, double*, int, const float* u, const double*, float* obs, float* rew) {
@@ -409,21 +438,23 @@ struct SingleTrackCar {
     float psid = ped + 0.0f;    // omega_ref = 0.0
     double f[7], g5[2] = {0.0, 0.0}, g6[2] = {0.0, 0.0}, g2 = 0.0, g3 = 0.0;
     float pb = pe + beta;
-    f[0] = (double)(((v * cos32(pb)) - 1.0f) + (0.0f * sye));   // SingleTrackCar.py:165
-    f[1] = (double)((v * sin32(pb)) - (0.0f * sxe));            // SingleTrackCar.py:166
+    float spb, cpb;
+    sincos32(pb, &spb, &cpb);
+    f[0] = (double)(((v * cpb) - 1.0f) + (0.0f * sye));   // SingleTrackCar.py:165
+    f[1] = (double)((v * spb) - (0.0f * sxe));            // SingleTrackCar.py:166
     f[3] = -0.0;                                               // -a_ref
     f[2] = 0.0;
     const float lsum = (float)C::lsum;
     if (!(fabsf(v) < 0.1f)) {
       // dynamic model (SingleTrackCar.py:178-196, 243-256)
-      float X = (float)C::P1 / ((v * (float)C::Iz) * lsum);
+      float X = div32((float)C::P1, (v * (float)C::Iz) * lsum);
       float t1 = ((-X) * (float)C::K1) * psid;
       float t2 = (float)(C::Q2 * C::K2) * beta;
       float t3 = (float)(C::Q2 * C::K3) * delta;
       f[4] = (double)ped;
       f[5] = (double)((t1 + t2) + t3);
-      float Y1 = (float)C::mu / (powf2(v) * lsum);
-      float Y2 = (float)C::mu / (v * lsum);
+      float Y1 = div32((float)C::mu, powf2(v) * lsum);
+      float Y2 = div32((float)C::mu, v * lsum);
       float b1 = ((Y1 * (float)C::K4) - 1.0f) * psid;
       float b2 = (Y2 * (float)C::K5) * beta;
       float b3 = (Y2 * (float)C::K6) * delta;

@@ -130,11 +130,26 @@ __device__ void deferred_emit(const StepArgs& a, int w, int lane) {
 }
 
 // --------------------------------------------------------------- fused lockstep step
-template <class Env>
+// Occupancy floor per env (the launch bound's waves per SIMD, i.e. a VGPR budget of 512 / waves):
+// 2 (<= 256 VGPRs) by default; the env-step bound kernels of the mid-weight envs run better with
+// more waves resident to hide their dependent f32/f64 chains (MH_*_WAVES: A/B switches)
 #ifndef MH_ROLLOUT_MIN_WAVES
-#define MH_ROLLOUT_MIN_WAVES 2  // <= 256 VGPRs: 2 waves per SIMD once E exceeds one wave per SIMD
+#define MH_ROLLOUT_MIN_WAVES 2
 #endif
-__global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, MH_ROLLOUT_MIN_WAVES) void k_rollout(StepArgs a) {
+#ifndef MH_CAR_WAVES
+#define MH_CAR_WAVES MH_ROLLOUT_MIN_WAVES
+#endif
+#ifndef MH_TWOLINK_WAVES
+#define MH_TWOLINK_WAVES MH_ROLLOUT_MIN_WAVES
+#endif
+template <class Env> struct RolloutWaves { static constexpr int v = MH_ROLLOUT_MIN_WAVES; };
+template <> struct RolloutWaves<SingleTrackCar> { static constexpr int v = MH_CAR_WAVES; };
+template <> struct RolloutWaves<TwoLink> { static constexpr int v = MH_TWOLINK_WAVES; };
+
+// SAMPLE: actions drawn from the policy logits (the sampler); false: injected actions (a.act_in,
+// the env.step / parity path), whose instantiation carries no sampling code at all.
+template <class Env, bool SAMPLE>
+__global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k_rollout(StepArgs a) {
   constexpr int D = Env::D, A = Env::A, S = Env::S, XS = Env::XS, RS = Env::RS;
   constexpr int F = rec_floats(D, A);
   const int64_t E = a.E;
@@ -171,12 +186,14 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, MH_ROLLOUT_MIN_WAVES) void k
     asm volatile("" ::: "memory");  // issue order pinned (compiler-only barriers: no instruction, no wait)
     const uint32_t ctr = __builtin_amdgcn_raw_buffer_load_b32(opt_rsrc(a.ctr, E * 4), vo4, 0, 0);
     float lgt[2 * A], inj[A];
-    load_row_buf<2 * A>(opt_rsrc(a.act_in ? nullptr : a.logits, E * 2 * A * 4), (int)(e * 2 * A * 4), lgt);
-    load_row_buf<A>(opt_rsrc(a.act_in, E * A * 4), (int)(e * A * 4), inj);
-    const float logp_inj =
-        __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(opt_rsrc(a.logp_in, E * 4), vo4, 0, 0));
-    const float noise =
-        __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(opt_rsrc(a.act_noise, 4), 0, 0, 0));
+    float logp_inj = 0.0f, noise = 0.0f;
+    if constexpr (SAMPLE) {
+      load_row_buf<2 * A>(opt_rsrc(a.logits, E * 2 * A * 4), (int)(e * 2 * A * 4), lgt);
+      noise = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(opt_rsrc(a.act_noise, 4), 0, 0, 0));
+    } else {
+      load_row_buf<A>(opt_rsrc(a.act_in, E * A * 4), (int)(e * A * 4), inj);
+      logp_inj = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(opt_rsrc(a.logp_in, E * 4), vo4, 0, 0));
+    }
     float obs0[D];
     load_row_buf<D>(opt_rsrc((a.ring || a.traj_obs) ? a.obs : nullptr, E * D * 4), (int)(e * D * 4), obs0);
     float s[S];
@@ -221,8 +238,8 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, MH_ROLLOUT_MIN_WAVES) void k
     // ---- action: TanhGaussDistribution.sample() + clip, or the injected action (selected
     // after the sampling, which runs either way: no branch merges pending loads into u)
     float u[A];
-    float logp;
-    {
+    float logp = 0.0f;
+    if constexpr (SAMPLE) {
 #ifdef MH_EXP_NO_SAMPLE  // cost-attribution experiment only
 #pragma unroll
       for (int i = 0; i < A; ++i) u[i] = fminf(fmaxf(lgt[i], Env::act_lo(i)), Env::act_hi(i));
@@ -265,7 +282,7 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, MH_ROLLOUT_MIN_WAVES) void k
       logp = (lg - lt) - ls;
 #endif
     }
-    if (a.act_in) {  // injected action (and its log-prob when given)
+    if constexpr (!SAMPLE) {  // injected action (and its log-prob when given)
 #pragma unroll
       for (int i = 0; i < A; ++i) u[i] = inj[i];
       logp = a.logp_in ? logp_inj : 0.0f;
@@ -787,7 +804,11 @@ hipError_t launch_rollout_t(const StepArgs& a, hipStream_t st) {
   if (!aligned(a.act_in ? nullptr : a.logits, 2 * Env::A) || !aligned(a.act_in, Env::A) || !aligned(a.obs, Env::D))
     return hipErrorInvalidValue;
   const int grid = (int)((a.E + BLK - 1) / BLK);
-  k_rollout<Env><<<grid, a.defer ? BLK + 64 * EMIT_WAVES : BLK, 0, st>>>(a);
+  const int threads = a.defer ? BLK + 64 * EMIT_WAVES : BLK;
+  if (a.act_in)
+    k_rollout<Env, false><<<grid, threads, 0, st>>>(a);
+  else
+    k_rollout<Env, true><<<grid, threads, 0, st>>>(a);
   return hipGetLastError();
 }
 template <class Env>
