@@ -5,10 +5,10 @@ parameters and state_dict keys); on HIP tensors their forward runs each (Linear,
 pair as one autograd Function:
   forward   y = act(x W^T + b): one mh_gemm_f32 launch (csrc/gemm.hip, f32 MFMA) with the bias
             and ReLU / tanh in its epilogue
-  backward  optionally (MSACL_FUSED_BACKWARD=1) for the B x n-row 256-wide layers,
+  backward  by default (MSACL_FUSED_BACKWARD=0: off) for the B x n-row 256-wide layers,
             mh_linear_backward (csrc/gemm.hip): dx = g W and dW = g^T x, db = column sums of g,
             with g = dy * act'(y) formed inside the two GEMMs' operand staging (never written);
-            by default g and the bias gradient in one pass
+            for the other layers g and the bias gradient in one pass
             of mh_act_grad_colsum (csrc/mlp_grad.hip) instead of an elementwise backward kernel
             plus a reduction, then dx = g W and dW = g^T x as two mh_gemm_f32 launches. Each
             output only when autograd needs it (frozen critics in the policy update skip dW / db).
@@ -116,10 +116,11 @@ def gemm(a, b, bias, M, N, K, lda, ldb, ta, tb, act=0):
 
 
 _LB_PLAN = {}
-# Off by default: measured neutral in the MSACL update (A/B on one box, update 1.08-1.12 ms
-# either way: the colsum launch it removes overlaps the other stream's work, while the fused
-# GEMMs carry the act' loads); MSACL_FUSED_BACKWARD=1 turns it on.
-_FUSED_BACKWARD = {"on": os.environ.get("MSACL_FUSED_BACKWARD", "0") == "1"}
+# On by default since round 2: measured neutral in round 1 (update 1.08-1.12 ms either way), but
+# with the update's other launches trimmed the colsum launch it removes is on the critical path:
+# 696-708 vs 674-678 M env-steps/s, 3 alternating pairs on one box
+# (profiles/r02_fused_backward_ab.jsonl); MSACL_FUSED_BACKWARD=0 turns it off.
+_FUSED_BACKWARD = {"on": os.environ.get("MSACL_FUSED_BACKWARD", "1") == "1"}
 
 
 def _linear_backward_fused(dy, y, act, x, weight, need_x, need_w, need_b):
