@@ -122,7 +122,7 @@ class UpdateGraph:
                     outs = self.body(self._static, *key)
             else:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with D.cuda_graph(g):
                     outs = self.body(self._static, *key)
             self._graphs[key] = (g, outs)
         g, outs = self._graphs[key]

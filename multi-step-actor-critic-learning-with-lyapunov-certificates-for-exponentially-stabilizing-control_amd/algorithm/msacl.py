@@ -21,6 +21,7 @@ __all__ = ["ApproxContainer", "MSACL"]
 import math
 import time
 from copy import deepcopy
+from collections.abc import Mapping
 from typing import Any, Dict, Optional
 
 import torch
@@ -77,6 +78,39 @@ class ApproxContainer(nn.Module):
 
     def create_action_distributions(self, logits):
         return self.policy.get_act_dist_cls(logits)
+
+
+class LazyTbInfo(Mapping):
+    """model_update's tb dict (msacl.py:211-222) over a device tensor of its seven scalars: the
+    values are read back (one transfer, a host sync) on first access, alg_time then being the
+    wall time from the update's start to that read (the reference's .item() calls sync inside
+    model_update, so its alg_time includes the device work too)."""
+
+    KEYS = ("MSACL/entropy-RL iter", "MSACL/alpha-RL iter", "MSACL/q1_mean-RL iter", "MSACL/q2_mean-RL iter",
+            tb_tags["loss_critic"], tb_tags["loss_lyapunov"], tb_tags["loss_actor"])
+
+    def __init__(self, vals: torch.Tensor, start: float):
+        self._vals, self._start, self._d = vals, start, None
+
+    def _dict(self):
+        if self._d is None:
+            v = self._vals.tolist()
+            self._d = dict(zip(self.KEYS, v))
+            self._d[tb_tags["alg_time"]] = (time.time() - self._start) * 1000
+            self._vals = None
+        return self._d
+
+    def __getitem__(self, k):
+        return self._dict()[k]
+
+    def __iter__(self):
+        return iter(self._dict())
+
+    def __len__(self):
+        return len(self._dict())
+
+    def __repr__(self):
+        return repr(self._dict())
 
 
 class _PolicyQLoss(torch.autograd.Function):
@@ -233,19 +267,14 @@ class MSACL:
             outs = self._update_body(data, *flags)
         tb_info = None
         if flags[1]:
-            loss_q, q1_mean, q2_mean, loss_lya, loss_policy, entropy = outs
-            vals = torch.stack([entropy, self.networks.log_alpha.detach().exp(), q1_mean, q2_mean, loss_q, loss_lya,
-                                loss_policy]).tolist()  # one device->host transfer instead of seven
-            tb_info = {
-                "MSACL/entropy-RL iter": vals[0],
-                "MSACL/alpha-RL iter": vals[1],
-                "MSACL/q1_mean-RL iter": vals[2],
-                "MSACL/q2_mean-RL iter": vals[3],
-                tb_tags["loss_critic"]: vals[4],
-                tb_tags["loss_lyapunov"]: vals[5],
-                tb_tags["loss_actor"]: vals[6],
-                tb_tags["alg_time"]: (time.time() - start) * 1000,
-            }
+            # the logged scalars (msacl.py:211-222), stacked on the device inside the update and
+            # snapshotted here (the next replay overwrites the graph's output); read back only when
+            # the caller reads the dict (the trainer: on logging iterations), so an update leaves
+            # no host sync behind and the next sampling is enqueued while it still runs
+            tb_info = LazyTbInfo(outs[-1].clone(), start)
+        if self.per_flag:
+            return tb_info, data.get("idx"), self.last_priority
+        return tb_info
         if self.per_flag:
             return tb_info, data.get("idx"), self.last_priority
         return tb_info
@@ -339,6 +368,8 @@ class MSACL:
                 self._target_update()
             loss_lya = self._lyapunov_update(data)
         loss_policy = entropy = None
+        if not do_policy:
+            return loss_q, q1_mean, q2_mean, loss_lya, loss_policy, entropy
         if do_policy:
             # data parallel: the policy and alpha gradients share one all-reduce (the alpha loss
             # reads the policy forward's entropy, not the stepped policy), then both steps
@@ -352,7 +383,9 @@ class MSACL:
                     D.allreduce_grads(list(nets.policy.parameters()) + [nets.log_alpha])
                     nets.policy_optimizer.step()
                     self._alpha_step()
-        return loss_q, q1_mean, q2_mean, loss_lya, loss_policy, entropy
+        tb = torch.stack([entropy, self.networks.log_alpha.detach().exp(), q1_mean, q2_mean, loss_q, loss_lya,
+                          loss_policy])
+        return loss_q, q1_mean, q2_mean, loss_lya, loss_policy, entropy, tb
 
     # ------------------------------------------------------------------ HIP-graph replay
     def _graphable(self):
@@ -399,7 +432,7 @@ class MSACL:
                     prio = self.last_priority
             else:
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with D.cuda_graph(g):
                     outs = self._update_body(self._static, *flags)
                     prio = self.last_priority
             self._graphs[flags] = (g, outs, prio)

@@ -23,6 +23,7 @@ import torch
 import torch.nn as nn
 
 from ... import _native as N
+from ...utils import dist as D
 from ...create_pkg.create_alg import create_approx_contrainer
 from ...env.hip_vector_env import HipVectorEnv
 from ...utils.act_distribution_cls import TanhGaussDistribution
@@ -219,7 +220,7 @@ class HipNstepOffSampler:
                self.obs.data_ptr())
         if self._graph is None or self._graph_key != key:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with D.cuda_graph(g):
                 self._horizon(store)
             self._graph, self._graph_key = g, key
         return self._graph

@@ -22,6 +22,7 @@ import ctypes
 import torch
 
 from ... import _native as N
+from ...utils import dist as D
 from .hip_nstep_off_sampler import HipNstepOffSampler
 
 __all__ = ["OnSampler"]
@@ -77,7 +78,7 @@ class OnSampler(HipNstepOffSampler):
                tuple(p.data_ptr() for p in self.networks.value.parameters()), self.obs.data_ptr())
         if self._graph is None or self._graph_key != key:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with D.cuda_graph(g):
                 self._horizon(None)
             self._graph, self._graph_key = g, key
         return self._graph

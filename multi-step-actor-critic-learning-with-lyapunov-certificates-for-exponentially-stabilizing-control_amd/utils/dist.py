@@ -9,6 +9,8 @@ sizes a ring all-reduce over xGMI is latency-bound, so one call per step beats p
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import os
 
 import torch
@@ -50,6 +52,23 @@ def init_from_env(backend=None):
         kw["device_id"] = torch.device("cuda", local)
     dist.init_process_group(backend=backend, **kw)
     return True
+
+
+@contextlib.contextmanager
+def cuda_graph(g, **kw):
+    """torch.cuda.graph with the cyclic garbage collector paused while the stream captures.
+    torch.cuda.graph collects once before the capture, but an allocation inside the capture can
+    trigger another collection, which may finalise graphs, events or streams of pipelines that
+    died in reference cycles: HIP calls that are illegal during a capture (seen as aborts and a
+    host segfault in a later replay during one full test session)."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        with torch.cuda.graph(g, **kw):
+            yield
+    finally:
+        if was:
+            gc.enable()
 
 
 class GraphSegments:
@@ -102,6 +121,8 @@ class capturing:
         self.seg = seg
 
     def __enter__(self):
+        self._gc = gc.isenabled()
+        gc.disable()  # as cuda_graph: no collection while a segment captures
         _SEG["active"] = self.seg
         self.seg._begin()
         return self.seg
@@ -112,6 +133,8 @@ class capturing:
         finally:
             self.seg._ctx = None
             _SEG["active"] = None
+            if self._gc:
+                gc.enable()
         return False
 
 

@@ -9,6 +9,7 @@ import pytest
 import torch
 
 import msacl_amd  # noqa: F401
+from msacl_amd.utils.dist import cuda_graph
 from msacl_amd.algorithm._update_graph import HipAdam
 
 pytestmark = pytest.mark.gpu
@@ -64,7 +65,7 @@ def test_hip_adam_state_dict_round_trip_and_graph_capture():
         opt.step()
     torch.cuda.current_stream().wait_stream(s)
     gph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(gph):
+    with cuda_graph(gph):
         opt.step()
     for _ in range(3):
         gph.replay()

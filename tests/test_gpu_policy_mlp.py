@@ -10,6 +10,7 @@ import torch
 import torch.nn as nn
 
 import msacl_amd  # noqa: F401
+from msacl_amd.utils.dist import cuda_graph
 import msacl_amd._native as N
 
 pytestmark = pytest.mark.gpu
@@ -182,7 +183,7 @@ def test_policy_pack_and_forward_replayed_in_a_graph_equal_eager():
     ps = [p.detach().contiguous() for p in (net[0].weight, net[0].bias, net[2].weight, net[2].bias, net[4].weight,
                                             net[4].bias)]
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with cuda_graph(g):
         N.check(N.lib().mh_policy_pack(*[N.ptr(p) for p in ps], D, 256, 256, 2 * A, N.ptr(P), N.stream_of()), "pack")
         N.check(N.lib().mh_policy_forward(N.ptr(P), N.ptr(obs), E, D, 2 * A, N.ptr(out), N.stream_of()), "fwd")
     for _ in range(4):
