@@ -232,9 +232,19 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs g) {
   const int64_t MN = g.M * g.N;
   if (g.dbp) {
+    // dbn = splits x column tiles partials per output (64 for a 256 x 256 layer): sixteen loads
+    // in flight per batch, added in partial order (a load-add loop paid one round trip per
+    // partial: 18.8 us for this reduce)
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < g.M; i += (int64_t)gridDim.x * 256) {
-      float v = g.dbp[i];
-      for (int sp = 1; sp < g.dbn; ++sp) v = v + g.dbp[(int64_t)sp * g.M + i];
+      float v = 0.0f;
+      for (int s0 = 0; s0 < g.dbn; s0 += 16) {
+        float x[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) x[u] = s0 + u < g.dbn ? g.dbp[(int64_t)(s0 + u) * g.M + i] : 0.0f;
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (s0 + u < g.dbn) v = (s0 + u == 0) ? x[u] : v + x[u];
+      }
       g.db[i] = v;
     }
   }
@@ -464,7 +474,8 @@ __global__ __launch_bounds__(256) void k_gemm_deep(GemmArgs g, int tiles_m) {
   constexpr int NF = 64 * TK / 4 / 256;  // float4 loads per operand per thread per chunk (4)
   __shared__ float lds[2][2 * TK * DLD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tiles = tiles_m * (int)(g.N / 64);
+  const int ntn = (int)((g.N + 63) / 64);  // column tiles (one, partly used, when N < 64)
+  const int tiles = tiles_m * ntn;
   const int bid = (int)blockIdx.x;
   const int tile = bid % tiles, split = bid / tiles;
   const int m0 = (tile % tiles_m) * 64, n0 = (tile / tiles_m) * 64;
@@ -483,7 +494,8 @@ __global__ __launch_bounds__(256) void k_gemm_deep(GemmArgs g, int tiles_m) {
   for (int s = 0; s < NF; ++s) {
     const int f = tid + 256 * s;
     aoff[s] = (f / 16) * lda * 4 + (m0 + 4 * (f % 16)) * 4;
-    boff[s] = (f / 16) * ldb * 4 + (n0 + 4 * (f % 16)) * 4;
+    // columns past N (a narrow layer, N < 64) read from beyond the buffer: zeros
+    boff[s] = n0 + 4 * (f % 16) < (int)g.N ? (f / 16) * ldb * 4 + (n0 + 4 * (f % 16)) * 4 : (1 << 30);
   }
   f32x4 ra[2][NF], rb[2][NF];
   f32x4 ry[AG ? 2 : 1][AG ? NF : 1];
@@ -532,7 +544,7 @@ __global__ __launch_bounds__(256) void k_gemm_deep(GemmArgs g, int tiles_m) {
   // chunk, so the ntn column tiles share its column sums: tile tn sums the k rows
   // tn, tn + ntn, ... (thread: column tid & 63, every fourth of those rows from tid >> 6), in
   // order, in a register
-  const int ntn = (int)(g.N / 64), tn = tile / tiles_m;
+  const int tn = tile / tiles_m;
   const bool colsum = AG && g.dbp;
   float cs = 0.0f;
   auto mma = [&](int c) {
@@ -594,8 +606,9 @@ __global__ __launch_bounds__(256) void k_gemm_deep(GemmArgs g, int tiles_m) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int f = tid + 256 * s;
-    *reinterpret_cast<f32x4*>(out + (int64_t)(m0 + f / 16) * ld + n0 + 4 * (f % 16)) =
-        *reinterpret_cast<const f32x4*>(Cs + (f / 16) * DLD + 4 * (f % 16));
+    if (n0 + 4 * (f % 16) < (int)g.N)
+      *reinterpret_cast<f32x4*>(out + (int64_t)(m0 + f / 16) * ld + n0 + 4 * (f % 16)) =
+          *reinterpret_cast<const f32x4*>(Cs + (f / 16) * DLD + 4 * (f % 16));
   }
 }
 
@@ -612,7 +625,7 @@ static bool deep_ok(const float* A, const float* B, const float* bias, int64_t M
 
 // K splits: about 256 workgroups, slices of >= 2 chunks
 static int deep_splits(int64_t M, int64_t N, int64_t K) {
-  const int64_t tiles = (M / 64) * (N / 64);
+  const int64_t tiles = (M / 64) * ((N + 63) / 64);
   const int64_t chunks = (K + TK - 1) / TK;
   int64_t S = (256 + tiles - 1) / tiles;
   if (S > chunks / 2) S = chunks / 2;
@@ -784,8 +797,12 @@ static bool lb_dx_ok(int64_t rows, int64_t n_out, int64_t n_in) {
   return rows >= 2048 && n_in % 64 == 0 && n_out % 4 == 0 && n_out >= 64 && rows * n_out * 4 < ((int64_t)1 << 30) &&
          n_out * n_in * 4 < ((int64_t)1 << 30) && n_out * 4 < ((int64_t)1 << 28);
 }
+// n_in below 64 (the first layer's observation / observation+action inputs): one column tile,
+// its columns past n_in read as zeros and not stored (dW and db only: the tall dx kernel needs
+// n_in % 64 == 0)
 static bool lb_dw_ok(int64_t rows, int64_t n_out, int64_t n_in) {
-  return n_out % 64 == 0 && n_in % 64 == 0 && rows >= 1024 && (rows + TK) * n_out * 4 < ((int64_t)1 << 30) &&
+  return n_out % 64 == 0 && (n_in % 64 == 0 || (n_in < 64 && n_in % 4 == 0)) && rows >= 1024 &&
+         (rows + TK) * n_out * 4 < ((int64_t)1 << 30) &&
          (rows + TK) * n_in * 4 < ((int64_t)1 << 30);
 }
 
@@ -796,7 +813,7 @@ bool linear_backward_plan(int64_t rows, int64_t n_out, int64_t n_in, bool dx, bo
   if (dw && !lb_dw_ok(rows, n_out, n_in)) return false;
   if (dw) {
     const int S = deep_splits(n_out, n_in, rows);
-    *ws = (S > 1 ? (int64_t)S * n_out * n_in : 0) + (db ? (int64_t)S * (n_in / 64) * n_out : 0);
+    *ws = (S > 1 ? (int64_t)S * n_out * n_in : 0) + (db ? (int64_t)S * ((n_in + 63) / 64) * n_out : 0);
   }
   return true;
 }
@@ -824,10 +841,11 @@ hipError_t launch_linear_backward(const float* dy, const float* y, int act, cons
     const int64_t chunks = (rows + TK - 1) / TK;
     const int64_t per = (chunks + S - 1) / S;
     float* dbp = db ? workspace + (S > 1 ? (int64_t)S * n_out * n_in : 0) : nullptr;
+    const int ntn = (int)((n_in + 63) / 64);
     GemmArgs g{dy, x, nullptr, dw, n_out, n_in, rows, n_out, n_in, n_in, 0, S, per, workspace, y, act, db, dbp,
-               S * (int)(n_in / 64)};
+               S * ntn};
     const int tiles_m = (int)(n_out / 64);
-    const unsigned grid = (unsigned)(tiles_m * (n_in / 64) * S);
+    const unsigned grid = (unsigned)(tiles_m * ntn * S);
     if (per == 5 && chunks == per * S) k_gemm_deep<5, true><<<grid, 256, 0, st>>>(g, tiles_m);
     else k_gemm_deep<0, true><<<grid, 256, 0, st>>>(g, tiles_m);
     hipError_t e = hipGetLastError();

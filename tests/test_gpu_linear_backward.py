@@ -72,3 +72,31 @@ def test_linear_backward_plan_rejects():
         assert ok.value == 0, args
     assert N.lib().mh_linear_backward_plan(5120, 256, 256, 1, 1, 1, ctypes.byref(ok), ctypes.byref(ws)) == 0
     assert ok.value == 1 and ws.value == 16 * 256 * 256 + 16 * 4 * 256  # dW partials + bias partials per split x column tile
+
+
+@pytest.mark.parametrize("rows,n_in", [(5120, 12), (5120, 16), (10240, 12), (3001, 4), (5120, 60)])
+@pytest.mark.parametrize("act", [1, 2])
+def test_linear_backward_narrow_input_dw_db(rows, n_in, act):
+    """First layers (n_in < 64: the observation / observation + action inputs): dW and db through
+    the deep kernel's single, partly used column tile (its columns past n_in read as zeros and are
+    not stored), against float64; deterministic."""
+    x, w, y, dy = _case(rows, n_in, 256, act, rows + n_in + 11 * act)
+    out = _linear_backward_fused(dy, y, act, x, w, False, True, True)
+    assert out is not None, "fused path not taken"
+    _, dw, db, _ = out
+    yd = y.double()
+    gd = dy.double() * ((yd > 0).double() if act == 1 else (1 - yd * yd))
+    _check(dw, gd.t() @ x.double(), gd.abs().t() @ x.double().abs(), rows)
+    _check(db, gd.sum(0), gd.abs().sum(0), rows)
+    _, dw2, db2, _ = _linear_backward_fused(dy, y, act, x, w, False, True, True)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+
+
+def test_linear_backward_plan_narrow_input():
+    ok, ws = ctypes.c_int32(), ctypes.c_int64()
+    assert N.lib().mh_linear_backward_plan(5120, 256, 12, 0, 1, 1, ctypes.byref(ok), ctypes.byref(ws)) == 0
+    # S splits (about 256 workgroups over the 4 row tiles: 40, two 64-row chunks each) x (dW + one bias tile)
+    assert ok.value == 1 and ws.value == 40 * 256 * 12 + 40 * 1 * 256
+    for args in [(5120, 256, 12, 1, 1, 1), (5120, 256, 6, 0, 1, 1), (5120, 256, 68, 0, 1, 1)]:
+        assert N.lib().mh_linear_backward_plan(*args, ctypes.byref(ok), ctypes.byref(ws)) == 0
+        assert ok.value == 0, args

@@ -17,8 +17,8 @@ from collections import defaultdict
 # alias -> (kernel-name pattern, grid size in threads or None): at 65,536 envs k_rollout runs a
 # 65,536-thread grid for a plain step and 131,072 (4 env + 4 emitter waves per block) for the
 # sampler's deferred-emission step (the Workgroup_Size column is the launch-bounds maximum)
-ALIASES = {"rollout_emit": ("k_rollout<mh::QuadTracking>", 131072),
-           "rollout_step": ("k_rollout<mh::QuadTracking>", 65536),
+ALIASES = {"rollout_emit": ("k_rollout<mh::QuadTracking, true>", 131072),
+           "rollout_step": ("k_rollout<mh::QuadTracking, true>", 65536),
            "window_emit": ("k_emit_fused<12, 4>", None), "replay_gather": ("k_gather", None),
            "msacl_lyapunov": ("k_lyapunov", None), "msacl_q_target": ("k_q_target", None)}
 
