@@ -264,6 +264,14 @@ int mh_gemm_f32(const float* A, const float* B, const float* bias, float* C, int
  * request is supported (tall dx: rows >= 2048, n_in % 64 == 0, n_out % 4 == 0, n_out >= 64; dw/db:
  * n_out and n_in multiples of 64, rows >= 1024) and the workspace floats it needs; matrices
  * contiguous and 16-byte aligned. Otherwise use mh_act_grad_colsum + mh_gemm_f32. */
+/* Backward of a narrow identity output layer y = x W^T + b (W [n_out][n_in], n_out <= 16: the
+ * critic / policy heads of RL/apprfunc/mlp.py:18-30 under autograd): dx = dy W, dW = dy^T x,
+ * db = column sums of dy in one pass over x plus a block-ordered finish (deterministic). Any
+ * output may be NULL (db needs dw); workspace: mh_head_backward_workspace floats when dw is wanted.
+ * Row-major contiguous operands. */
+int mh_head_backward_workspace(int64_t rows, int32_t n_out, int32_t n_in, int64_t* floats_out);
+int mh_head_backward(const float* dy, const float* x, const float* W, int64_t rows, int32_t n_out, int32_t n_in,
+                     float* dx, float* dw, float* db, float* workspace, void* stream);
 int mh_linear_backward_plan(int64_t rows, int64_t n_out, int64_t n_in, int32_t need_dx, int32_t need_dw,
                             int32_t need_db, int32_t* supported, int64_t* workspace_floats);
 int mh_linear_backward(const float* dy, const float* y, int32_t act, const float* x, const float* W, int64_t rows,

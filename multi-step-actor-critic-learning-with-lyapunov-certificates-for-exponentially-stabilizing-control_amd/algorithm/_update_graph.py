@@ -80,6 +80,46 @@ class HipAdam(Adam):
         return loss
 
 
+def adam_steps(*opts):
+    """opt.step() for every optimiser in `opts`, as ONE mh_adam_multi launch when they are all
+    HipAdams with a single parameter group and the same lr / betas / eps whose parameters all
+    take the kernel (the twin critics: one launch instead of two back to back on the update's
+    critical path); each parameter keeps its own step counter, so the result is the separate
+    steps'. Otherwise each optimiser steps on its own."""
+    from .. import _native as N
+    ok = len(opts) > 1 and all(isinstance(o, HipAdam) and len(o.param_groups) == 1 for o in opts)
+    entries = []
+    if ok:
+        g0 = opts[0].param_groups[0]
+        for o in opts:
+            g = o.param_groups[0]
+            if (torch.is_tensor(g["lr"]) or g["lr"] != g0["lr"] or tuple(g["betas"]) != tuple(g0["betas"])
+                    or g["eps"] != g0["eps"]):
+                ok = False
+                break
+            e = o._hip_entries(g)
+            if e is None:
+                ok = False
+                break
+            entries += e
+        ok = ok and len(entries) > 0  # (the C ABI chunks lists longer than its per-launch table)
+    if not ok:
+        for o in opts:
+            o.step()
+        return
+    o0 = opts[0]
+    dev = entries[0][0].device
+    if o0._ticket is None or o0._ticket.device != dev:
+        o0._ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+    b1, b2 = g0["betas"]
+    arr = (N.AdamTensor * len(entries))()
+    for i, (p, g, m, v, stp) in enumerate(entries):
+        arr[i] = N.AdamTensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), stp.data_ptr(), p.numel())
+    with torch.no_grad():
+        N.check(N.lib().mh_adam_multi(arr, len(entries), float(g0["lr"]), float(b1), float(b2), float(g0["eps"]),
+                                      N.ptr(o0._ticket), N.stream_of(dev)), "mh_adam_multi")
+
+
 def fused_adam(params, lr):
     params = list(params)
     try:
@@ -128,6 +168,29 @@ class UpdateGraph:
         g, outs = self._graphs[key]
         g.replay()
         return outs
+
+
+def polyak_pairs(pairs, tau):
+    """polyak_ over several (net, target) pairs in one mh_polyak_multi launch when every tensor
+    qualifies (the twin critics' targets); per pair otherwise."""
+    polyak = 1 - tau
+    with torch.no_grad():
+        tp, sp = [], []
+        for net, target in pairs:
+            tp += [p.data for p in target.parameters()]
+            sp += [p.data for p in net.parameters()]
+        if tp and len(tp) == len(sp) and all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
+                                             and s.is_contiguous() and s.dtype == torch.float32 and t.shape == s.shape
+                                             for t, s in zip(tp, sp)):
+            from .. import _native as N
+            arr = (N.PolyakTensor * len(tp))()
+            for i, (t, s) in enumerate(zip(tp, sp)):
+                arr[i] = N.PolyakTensor(t.data_ptr(), s.data_ptr(), t.numel())
+            N.check(N.lib().mh_polyak_multi(arr, len(tp), float(polyak), N.stream_of(tp[0].device)),
+                    "mh_polyak_multi")
+            return
+    for net, target in pairs:
+        polyak_(net, target, tau)
 
 
 def polyak_(net, target, tau):

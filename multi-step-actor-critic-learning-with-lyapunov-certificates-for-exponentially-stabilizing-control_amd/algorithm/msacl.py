@@ -42,6 +42,11 @@ def _adam(params, lr):
     return fused_adam(params, lr)
 
 
+def adam_steps(*opts):
+    from ._update_graph import adam_steps as _steps
+    _steps(*opts)
+
+
 def _engine(name, device, *args):
     """mh_<name>(*args, stream) on a HIP device; mhh_<name>(*args) of the CPU build on the CPU."""
     if device.type == "cpu":
@@ -357,8 +362,7 @@ class MSACL:
             nets = self.networks
             D.allreduce_grads(list(nets.q1.parameters()) + list(nets.q2.parameters()) +
                               list(nets.lyapunov.parameters()))
-            nets.q1_optimizer.step()
-            nets.q2_optimizer.step()
+            adam_steps(nets.q1_optimizer, nets.q2_optimizer)
             nets.lyapunov_optimizer.step()
             if do_target:
                 self._target_update()
@@ -473,8 +477,7 @@ class MSACL:
         torch.autograd.backward([q1, q2], [s.dq1, s.dq2])
         if not defer_step:  # deferred: the caller all-reduces and steps (data-parallel join)
             D.allreduce_grads(list(self.networks.q1.parameters()) + list(self.networks.q2.parameters()))
-            self.networks.q1_optimizer.step()
-            self.networks.q2_optimizer.step()
+            adam_steps(self.networks.q1_optimizer, self.networks.q2_optimizer)  # one launch for both
         if self.per_flag:
             self.last_priority = s.abs_td.clone()
         if not stats:  # iterations without a policy step log nothing (model_update returns None)
@@ -604,7 +607,7 @@ class MSACL:
                 self.networks.log_alpha.clamp_(max=math.log(self.alpha_bound))
 
     def _target_update(self):
-        """Polyak averaging (msacl.py:445-460): one mh_polyak_multi launch per net."""
-        from ._update_graph import polyak_
-        for net, targ in ((self.networks.q1, self.networks.q1_target), (self.networks.q2, self.networks.q2_target)):
-            polyak_(net, targ, self.tau)
+        """Polyak averaging (msacl.py:445-460): one mh_polyak_multi launch for both target nets."""
+        from ._update_graph import polyak_pairs
+        polyak_pairs(((self.networks.q1, self.networks.q1_target), (self.networks.q2, self.networks.q2_target)),
+                     self.tau)

@@ -158,6 +158,37 @@ def _linear_backward_fused(dy, y, act, x, weight, need_x, need_w, need_b):
     return dx, dw, db, None
 
 
+_HEAD_WS = {}
+_HEAD_BACKWARD = {"on": os.environ.get("MSACL_HEAD_BACKWARD", "1") == "1"}  # A/B switch
+
+
+def _head_backward(dy, x, weight, need_x, need_w, need_b):
+    """Backward of a narrow identity output layer (n_out <= 16, the critic / policy heads) as
+    mh_head_backward (csrc/mlp_grad.hip): dx = dy W, dW = dy^T x and db in one pass over x + a
+    block-ordered finish; None when the request does not qualify."""
+    rows, n_out = dy.shape
+    n_in = x.shape[1]
+    if (need_b and not need_w) or not (need_x or need_w) or rows < 1024 or n_out > 16:
+        return None
+    N = _native()
+    dev = dy.device
+    key = (rows, n_out, n_in)
+    ws = _HEAD_WS.get(key)
+    if ws is None:
+        wf = ctypes.c_int64()
+        N.check(N.lib().mh_head_backward_workspace(rows, n_out, n_in, ctypes.byref(wf)), "mh_head_backward_workspace")
+        ws = _HEAD_WS[key] = wf.value
+    xc = x.contiguous()
+    w = weight.contiguous()
+    dx = torch.empty(rows, n_in, dtype=dy.dtype, device=dev) if need_x else None
+    dw = torch.empty(n_out, n_in, dtype=dy.dtype, device=dev) if need_w else None
+    db = torch.empty(n_out, dtype=dy.dtype, device=dev) if need_b else None
+    work = torch.empty(ws, dtype=torch.float32, device=dev) if need_w else None
+    N.check(N.lib().mh_head_backward(N.ptr(dy), N.ptr(xc), N.ptr(w), rows, n_out, n_in, N.ptr(dx), N.ptr(dw), N.ptr(db),
+                                     N.ptr(work), N.stream_of(dev)), "mh_head_backward")
+    return dx, dw, db, None
+
+
 class LinearAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, act):
@@ -181,6 +212,10 @@ class LinearAct(torch.autograd.Function):
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
         act = ctx.act
         dy = dy.contiguous()
+        if act == 0 and _HEAD_BACKWARD["on"] and _GEMM_BACKEND["name"] != "blas":
+            head = _head_backward(dy, x, weight, need_x, need_w, need_b)
+            if head is not None:
+                return head
         if _FUSED_BACKWARD["on"]:
             fused = _linear_backward_fused(dy, y, act, x, weight, need_x, need_w, need_b)
             if fused is not None:

@@ -583,6 +583,22 @@ int mh_act_grad_colsum(const float* dy, const float* y, int64_t rows, int32_t co
   return MH_OK;
 }
 
+int mh_head_backward_workspace(int64_t rows, int32_t n_out, int32_t n_in, int64_t* floats_out) {
+  if (!floats_out || rows < 0 || n_out <= 0 || n_out > 16 || n_in <= 0)
+    return fail(MH_EINVAL, "mh_head_backward_workspace: bad argument");
+  *floats_out = mh::head_backward_workspace(rows, n_out, n_in);
+  return MH_OK;
+}
+
+int mh_head_backward(const float* dy, const float* x, const float* W, int64_t rows, int32_t n_out, int32_t n_in,
+                     float* dx, float* dw, float* db, float* workspace, void* stream) {
+  if (rows <= 0 || n_out <= 0 || n_out > 16 || n_in <= 0) return fail(MH_EINVAL, "mh_head_backward: bad shape");
+  if (!dy || (dx && !W) || ((dw || db) && !workspace) || (dw && !x) || (db && !dw))
+    return fail(MH_EINVAL, "mh_head_backward: null pointer");
+  MH_HIP(mh::launch_head_backward(dy, x, W, rows, n_out, n_in, dx, dw, db, workspace, (hipStream_t)stream));
+  return MH_OK;
+}
+
 int mh_adam_multi(const mh_adam_tensor_t* tensors, int32_t n, double lr, double beta1, double beta2, double eps,
                   uint32_t* ticket, void* stream) {
   if (n < 0 || (n > 0 && (!tensors || !ticket))) return fail(MH_EINVAL, "mh_adam_multi: bad argument");

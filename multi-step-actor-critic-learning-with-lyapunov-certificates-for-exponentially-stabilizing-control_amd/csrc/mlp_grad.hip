@@ -137,6 +137,119 @@ __global__ __launch_bounds__(256) void k_colsum_finish(const float* __restrict__
   if (ty == 0 && n < N) db[n] = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
 }
 
+// ------------------------------------------------------------------ output-layer backward
+// The identity-activation output layer of a narrow head (n_out <= HB_MAX_OUT: the critics' 1,
+// the policy's 2A) over many rows: dx = dy W (the gradient handed to the hidden layer below),
+// dW = dy^T x and db = column sums of dy, in one pass over x instead of a bias-gradient kernel,
+// an input-gradient GEMM and a weight-gradient GEMM with its split-K finish. Workgroup = HB_ROWS
+// rows; its dy rows are staged in LDS; thread = input column j (and j + 256, ...):
+// x[r][j] is read once (row-contiguous across the workgroup) and feeds both the dx element
+// (W column j in registers) and the n_out dW partial sums; per-workgroup partials [blk][n_out][n_in]
+// and [blk][n_out] are summed in block order by k_head_finish (deterministic).
+constexpr int HB_MAX_OUT = 16;
+constexpr int HB_ROWS = 64;
+
+template <int NO>
+__global__ __launch_bounds__(256) void k_head_backward(const float* __restrict__ dy, const float* __restrict__ x,
+                                                       const float* __restrict__ W, int64_t M, int n_in,
+                                                       float* __restrict__ dx, float* __restrict__ pdw,
+                                                       float* __restrict__ pdb) {
+  __shared__ float sdy[HB_ROWS][NO];
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * HB_ROWS;
+  const int nr = M - r0 < HB_ROWS ? (int)(M - r0) : HB_ROWS;
+  for (int q = tid; q < HB_ROWS * NO; q += 256) {
+    const int r = q / NO, o = q - r * NO;
+    sdy[r][o] = r < nr ? dy[(r0 + r) * NO + o] : 0.0f;
+  }
+  __syncthreads();
+  if (pdb && tid < NO) {  // bias partial: this block's rows in order
+    float s = 0.0f;
+    for (int r = 0; r < nr; ++r) s = s + sdy[r][tid];
+    pdb[(int64_t)blockIdx.x * NO + tid] = s;
+  }
+  for (int j = tid; j < n_in; j += 256) {
+    float w[NO], acc[NO];
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      w[o] = W[(int64_t)o * n_in + j];
+      acc[o] = 0.0f;
+    }
+    for (int rb = 0; rb < nr; rb += 16) {
+      float xv[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) xv[u] = rb + u < nr ? x[(r0 + rb + u) * n_in + j] : 0.0f;  // 16 in flight
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        if (rb + u >= nr) break;
+        float d = 0.0f;
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+          const float g = sdy[rb + u][o];
+          d = o == 0 ? g * w[0] : d + g * w[o];  // dy[r] . W[:, j], o ascending
+          acc[o] = acc[o] + g * xv[u];
+        }
+        if (dx) dx[(r0 + rb + u) * n_in + j] = d;
+      }
+    }
+    if (pdw) {
+#pragma unroll
+      for (int o = 0; o < NO; ++o) pdw[((int64_t)blockIdx.x * NO + o) * n_in + j] = acc[o];
+    }
+  }
+}
+
+// dW[o][j] = sum over blocks of pdw[b][o][j] (and db[o] of pdb[b][o]), blocks in order, sixteen
+// loads in flight per batch
+__global__ __launch_bounds__(256) void k_head_finish(const float* __restrict__ pdw, const float* __restrict__ pdb,
+                                                     int nblk, int n_out, int n_in, float* __restrict__ dw,
+                                                     float* __restrict__ db) {
+  const int64_t nw = (int64_t)n_out * n_in;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nw + (db ? n_out : 0); i += (int64_t)gridDim.x * 256) {
+    const bool isw = i < nw;
+    const float* src = isw ? pdw + i : pdb + (i - nw);
+    const int64_t stride = isw ? nw : n_out;
+    float v = 0.0f;
+    for (int b0 = 0; b0 < nblk; b0 += 16) {
+      float t[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) t[u] = b0 + u < nblk ? src[(int64_t)(b0 + u) * stride] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (b0 + u < nblk) v = (b0 + u == 0) ? t[u] : v + t[u];
+    }
+    if (isw) dw[i] = v;
+    else db[i - nw] = v;
+  }
+}
+
+int64_t head_backward_workspace(int64_t M, int n_out, int n_in) {
+  const int64_t nblk = (M + HB_ROWS - 1) / HB_ROWS;
+  return nblk * n_out * (int64_t)n_in + nblk * n_out;
+}
+
+hipError_t launch_head_backward(const float* dy, const float* x, const float* W, int64_t M, int n_out, int n_in,
+                                float* dx, float* dw, float* db, float* workspace, hipStream_t st) {
+  if (M <= 0 || n_out <= 0 || n_out > HB_MAX_OUT || n_in <= 0) return hipErrorInvalidValue;
+  const int64_t nblk = (M + HB_ROWS - 1) / HB_ROWS;
+  float* pdw = dw ? workspace : nullptr;
+  float* pdb = db ? workspace + nblk * n_out * (int64_t)n_in : nullptr;
+  const unsigned grid = (unsigned)nblk;
+#define HB_CASE(K)                                                                                     \
+  case K: k_head_backward<K><<<grid, 256, 0, st>>>(dy, x, W, M, n_in, dx, pdw, pdb); break;
+  switch (n_out) {
+    HB_CASE(1) HB_CASE(2) HB_CASE(3) HB_CASE(4) HB_CASE(5) HB_CASE(6) HB_CASE(7) HB_CASE(8)
+    HB_CASE(9) HB_CASE(10) HB_CASE(11) HB_CASE(12) HB_CASE(13) HB_CASE(14) HB_CASE(15) HB_CASE(16)
+  }
+#undef HB_CASE
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || (!dw && !db)) return e;
+  const int64_t outs = (int64_t)n_out * n_in + n_out;
+  const int64_t want = (outs + 255) / 256;
+  k_head_finish<<<(unsigned)(want < 1024 ? want : 1024), 256, 0, st>>>(pdw, pdb, (int)nblk, n_out, n_in, dw, db);
+  return hipGetLastError();
+}
+
 int act_grad_chunks(int64_t M) { return (int)((M + AG_ROWS - 1) / AG_ROWS); }
 
 int act_grad_tickets(int N) { return (N + AG_COLS - 1) / AG_COLS; }

@@ -131,6 +131,9 @@ hipError_t launch_tg_log_prob_bwd(const float* logits, const float* a, const flo
 hipError_t launch_act_grad_colsum(const float* dy, const float* y, int64_t M, int N, int act, float* g, float* db,
                                   float* partial, uint32_t* tickets, hipStream_t st);
 int act_grad_tickets(int N);
+int64_t head_backward_workspace(int64_t M, int n_out, int n_in);
+hipError_t launch_head_backward(const float* dy, const float* x, const float* W, int64_t M, int n_out, int n_in,
+                                float* dx, float* dw, float* db, float* workspace, hipStream_t st);
 constexpr int ADAM_MAX_TENSORS = 32;
 struct AdamList {  // one optimiser's tensors, passed by value in the kernel arguments
   float* p[ADAM_MAX_TENSORS];

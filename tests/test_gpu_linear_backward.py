@@ -100,3 +100,27 @@ def test_linear_backward_plan_narrow_input():
     for args in [(5120, 256, 12, 1, 1, 1), (5120, 256, 6, 0, 1, 1), (5120, 256, 68, 0, 1, 1)]:
         assert N.lib().mh_linear_backward_plan(*args, ctypes.byref(ok), ctypes.byref(ws)) == 0
         assert ok.value == 0, args
+
+
+@pytest.mark.parametrize("rows,n_out,n_in", [(5120, 1, 256), (5120, 8, 256), (10240, 16, 256), (3001, 3, 128),
+                                             (1024, 8, 300)])
+@pytest.mark.parametrize("need", [(True, True, True), (True, False, False), (False, True, True)])
+def test_head_backward_matches_float64(rows, n_out, n_in, need):
+    """mh_head_backward (the identity output layer of a narrow head, n_out <= 16): dx = dy W,
+    dW = dy^T x, db = column sums of dy, against float64; deterministic; each output only when
+    requested."""
+    from msacl_amd.apprfunc._fused import _head_backward
+    x, w, _, dy = _case(rows, n_in, n_out, 0, rows + 7 * n_out + n_in)
+    out = _head_backward(dy, x, w, *need)
+    assert out is not None
+    for got, wanted in zip(out[:3], need):
+        assert (got is not None) == wanted
+    dd = dy.double()
+    if need[0]:
+        _check(out[0], dd @ w.double(), dd.abs() @ w.double().abs(), n_out)
+    if need[1]:
+        _check(out[1], dd.t() @ x.double(), dd.abs().t() @ x.double().abs(), rows)
+        _check(out[2], dd.sum(0), dd.abs().sum(0), rows)
+    again = _head_backward(dy, x, w, *need)
+    for a, b in zip(out[:3], again[:3]):
+        assert a is None or torch.equal(a, b)
