@@ -264,6 +264,19 @@ int mh_gemm_f32(const float* A, const float* B, const float* bias, float* C, int
  * request is supported (tall dx: rows >= 2048, n_in % 64 == 0, n_out % 4 == 0, n_out >= 64; dw/db:
  * n_out and n_in multiples of 64, rows >= 1024) and the workspace floats it needs; matrices
  * contiguous and 16-byte aligned. Otherwise use mh_act_grad_colsum + mh_gemm_f32. */
+/* The MSACL update's policy head on B*n rows of the StochaPolicy MLP's raw [mean | log_std]
+ * (msacl.py:242-251, 270-273, 340-394; mlp.py:132-136; act_distribution_cls.py:39-62): std =
+ * exp(clamp(log_std, lo, hi)); with eps: the TanhGauss reparameterised sample written into the
+ * critic input rows xq = [obs | act] (D + A columns) and its log-prob new_logp; with old_act:
+ * log_prob(old_act) into old_logp. Its backward gives d_raw from d_xq (the action columns),
+ * d_new_logp and d_old_logp (each nullable), as autograd accumulates them. A <= 8. */
+int mh_policy_head(const float* raw, const float* eps, const float* obs, const float* old_act, const float* high,
+                   const float* low, int64_t rows, int32_t A, int32_t D, float log_std_lo, float log_std_hi, float* xq,
+                   float* new_logp, float* old_logp, void* stream);
+int mh_policy_head_backward(const float* raw, const float* eps, const float* old_act, const float* high,
+                            const float* low, const float* d_xq, const float* d_new_logp, const float* d_old_logp,
+                            int64_t rows, int32_t A, int32_t D, float log_std_lo, float log_std_hi, float* d_raw,
+                            void* stream);
 /* Backward of a narrow identity output layer y = x W^T + b (W [n_out][n_in], n_out <= 16: the
  * critic / policy heads of RL/apprfunc/mlp.py:18-30 under autograd): dx = dy W, dW = dy^T x,
  * db = column sums of dy in one pass over x plus a block-ordered finish (deterministic). Any

@@ -89,6 +89,10 @@ _PROTOS = {
     "mh_policy_forward": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "mh_act_grad_chunks": (ctypes.c_int, [c_i64, ctypes.POINTER(c_i32)]),
     "mh_act_grad_colsum": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mh_policy_head": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_f32, c_f32, c_vp,
+                                      c_vp, c_vp, c_vp]),
+    "mh_policy_head_backward": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32,
+                                               c_f32, c_f32, c_vp, c_vp]),
     "mh_head_backward_workspace": (ctypes.c_int, [c_i64, c_i32, c_i32, ctypes.POINTER(c_i64)]),
     "mh_head_backward": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mh_linear_backward_plan": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp]),

@@ -25,6 +25,7 @@ from collections.abc import Mapping
 from typing import Any, Dict, Optional
 
 import torch
+import torch.distributions.normal as tdn
 import torch.nn as nn
 from torch.optim import Adam
 
@@ -141,6 +142,36 @@ class _PolicyQLoss(torch.autograd.Function):
         return dq1, dq2, dlogp, None
 
 
+class _PolicyHead(torch.autograd.Function):
+    """The policy step's head (msacl.py:340-394): StochaPolicy's [mean | exp(clamp(log_std))] of the
+    MLP's raw rows, the TanhGauss reparameterised sample written into the critic input
+    xq = [obs | act] (ActionValue's concat), its log-prob, and log_prob(old_act), as one launch
+    forward (mh_policy_head) and one backward (mh_policy_head_backward) instead of StochaHead +
+    rsample + two concats + log_prob forward and their four backward kernels + gradient adds."""
+
+    @staticmethod
+    def forward(ctx, raw, eps, obs, old_act, high, low, lo, hi):
+        R, A, D = raw.shape[0], raw.shape[1] // 2, obs.shape[1]
+        xq = torch.empty(R, D + A, dtype=raw.dtype, device=raw.device)
+        new_logp = torch.empty(R, dtype=raw.dtype, device=raw.device)
+        old_logp = torch.empty(R, dtype=raw.dtype, device=raw.device)
+        _engine("policy_head", raw.device, N.ptr(raw), N.ptr(eps), N.ptr(obs), N.ptr(old_act), N.ptr(high), N.ptr(low),
+                R, A, D, lo, hi, N.ptr(xq), N.ptr(new_logp), N.ptr(old_logp))
+        ctx.save_for_backward(raw, eps, old_act, high, low)
+        ctx.dims = (R, A, D, lo, hi)
+        return xq, new_logp, old_logp
+
+    @staticmethod
+    def backward(ctx, d_xq, d_new_logp, d_old_logp):
+        raw, eps, old_act, high, low = ctx.saved_tensors
+        R, A, D, lo, hi = ctx.dims
+        d_raw = torch.empty_like(raw)
+        c = lambda t: None if t is None else t.contiguous()  # noqa: E731
+        _engine("policy_head_backward", raw.device, N.ptr(raw), N.ptr(eps), N.ptr(old_act), N.ptr(high), N.ptr(low),
+                N.ptr(c(d_xq)), N.ptr(c(d_new_logp)), N.ptr(c(d_old_logp)), R, A, D, lo, hi, N.ptr(d_raw))
+        return d_raw, None, None, None, None, None, None, None
+
+
 class _Ratio0(torch.autograd.Function):
     """exp(logp_new - old_logp)[:, 0] (msacl.py:392-394) and its backward, one launch each."""
 
@@ -243,6 +274,32 @@ class MSACL:
     @property
     def adjustable_parameters(self):
         return ("gamma", "tau", "auto_alpha", "alpha", "target_entropy", "policy_frequency", "target_network_frequency")
+
+    def _head(self):
+        """(high, low, log_std lo, hi) when the fused policy head applies (HIP float32 StochaPolicy
+        MLP + TanhGaussDistribution with A <= 8, ActionValue critics), else None."""
+        if getattr(self, "_head_cache", 0) != 0:
+            return self._head_cache
+        from ..apprfunc.mlp import ActionValue, StochaPolicy
+        from ..utils.act_distribution_cls import TanhGaussDistribution
+        nets, h = self.networks, None
+        pol = nets.policy
+        if (self.device.type == "cuda" and isinstance(pol, StochaPolicy)
+                and pol.action_distribution_cls is TanhGaussDistribution
+                and all(isinstance(q, ActionValue) for q in (nets.q1, nets.q2, nets.q1_target, nets.q2_target))):
+            hi, lo = pol.act_high_lim, pol.act_low_lim
+            A = hi.numel()
+            if (0 < A <= 8 and hi.shape == (A,) and lo.shape == (A,) and hi.dtype == torch.float32
+                    and lo.dtype == torch.float32 and hi.device == self.device and lo.device == self.device):
+                h = (hi.contiguous(), lo.contiguous(), float(pol.min_log_std), float(pol.max_log_std))
+        self._head_cache = h
+        return h
+
+    def _noise(self, raw):
+        """The rsample noise, drawn where TanhGaussDistribution.rsample draws it (same generator
+        call, same shape: the tests' recorded-noise injection sees the same sequence)."""
+        shape = raw.shape[:-1] + (raw.shape[-1] // 2,)
+        return tdn._standard_normal(shape, dtype=raw.dtype, device=raw.device)
 
     def _buf(self, B, n):
         key = (B, n)
@@ -449,20 +506,39 @@ class MSACL:
         obs, act, rew, obs2, done = data["obs"], data["act"], data["rew"], data["obs2"], data["done"]
         B, n = rew.shape
         s = self._buf(B, n)
-        with torch.no_grad():
-            dist = self.networks.create_action_distributions(self.networks.policy(obs2))
-            next_act, next_logp = dist.rsample()
         nets = self.networks
+        head = self._head()
+        if head is not None:
+            # policy(obs2) -> head + rsample written straight into the target critics' input
+            # [obs2 | next_act] (one launch); the batch's [obs | act] concatenated once for both
+            hi, lo, lsl, lsh = head
+            A, Dd = hi.numel(), obs.shape[-1]
+            with torch.no_grad():
+                raw = nets.policy.policy(obs2)
+                eps = self._noise(raw)
+                xq2 = torch.empty(B, n, Dd + A, dtype=torch.float32, device=self.device)
+                next_logp = torch.empty(B, n, dtype=torch.float32, device=self.device)
+                _engine("policy_head", self.device, N.ptr(raw.contiguous()), N.ptr(eps.contiguous()), N.ptr(obs2), None,
+                        N.ptr(hi), N.ptr(lo), B * n, A, Dd, lsl, lsh, N.ptr(xq2), N.ptr(next_logp), None)
+            xa = torch.cat([obs, act], dim=-1)
+            q_in = lambda q: q.q(xa).squeeze(-1)  # noqa: E731  (ActionValue.forward on the shared concat)
+            qt_in = lambda q: q.q(xq2).squeeze(-1)  # noqa: E731
+        else:
+            with torch.no_grad():
+                dist = nets.create_action_distributions(nets.policy(obs2))
+                next_act, next_logp = dist.rsample()
+            q_in = lambda q: q(obs, act)  # noqa: E731
+            qt_in = lambda q: q(obs2, next_act)  # noqa: E731
 
         def critic1():
-            q = nets.q1(obs, act)
+            q = q_in(nets.q1)
             with torch.no_grad():
-                return q, nets.q1_target(obs2, next_act).contiguous()
+                return q, qt_in(nets.q1_target).contiguous()
 
         def critic2():
-            q = nets.q2(obs, act)
+            q = q_in(nets.q2)
             with torch.no_grad():
-                return q, nets.q2_target(obs2, next_act).contiguous()
+                return q, qt_in(nets.q2_target).contiguous()
 
         (q1, q1t), (q2, q2t) = self._twin_pair(critic1, critic2)
         weight = data.get("weight") if self.per_flag else None
@@ -489,9 +565,17 @@ class MSACL:
         obs, obs2, act, old_logp = data["obs"], data["obs2"], data["act"], data["logp"]
         B, n = old_logp.shape
         s = self._buf(B, n)
+        head = self._head()
         with torch.no_grad():
-            dist = self.networks.create_action_distributions(self.networks.policy(obs))
-            logp = dist.log_prob(act).contiguous()
+            if head is not None:  # policy(obs) -> head + log_prob(act) in one launch
+                hi, lo, lsl, lsh = head
+                raw = self.networks.policy.policy(obs).contiguous()
+                logp = torch.empty(B, n, dtype=torch.float32, device=self.device)
+                _engine("policy_head", self.device, N.ptr(raw), None, None, N.ptr(act), N.ptr(hi), N.ptr(lo), B * n,
+                        hi.numel(), 0, lsl, lsh, None, None, N.ptr(logp))
+            else:
+                dist = self.networks.create_action_distributions(self.networks.policy(obs))
+                logp = dist.log_prob(act).contiguous()
         # V(obs) and V(obs2) (msacl.py:275-276) as ONE batch through the network: one forward and
         # one backward instead of two each (the weight gradients sum the same 2 B n rows)
         V_both = self.networks.lyapunov(torch.cat([obs, obs2], 0))
@@ -548,14 +632,31 @@ class MSACL:
                 self._stability_advantage(data, s)
         for p in list(self.networks.q1.parameters()) + list(self.networks.q2.parameters()):
             p.requires_grad = False
-        dist = self.networks.create_action_distributions(self.networks.policy(obs))
-        new_act, new_act_logp = dist.rsample()
-        q1, q2 = self._twin_pair(lambda: self.networks.q1(obs, new_act), lambda: self.networks.q2(obs, new_act))
+        nets = self.networks
+        head = self._head()
+        if head is not None:
+            hi, lo, lsl, lsh = head
+            A, Dd = hi.numel(), obs.shape[-1]
+            raw = nets.policy.policy(obs)
+            eps = self._noise(raw)
+            xq, new_act_logp, old_lp = _PolicyHead.apply(raw.reshape(B * n, 2 * A).contiguous(),
+                                                         eps.reshape(B * n, A).contiguous(), obs.reshape(B * n, Dd),
+                                                         old_act.reshape(B * n, A), hi, lo, lsl, lsh)
+            xq = xq.reshape(B, n, Dd + A)
+            new_act_logp, old_lp = new_act_logp.reshape(B, n), old_lp.reshape(B, n)
+            q1, q2 = self._twin_pair(lambda: nets.q1.q(xq).squeeze(-1), lambda: nets.q2.q(xq).squeeze(-1))
+        else:
+            dist = nets.create_action_distributions(nets.policy(obs))
+            new_act, new_act_logp = dist.rsample()
+            q1, q2 = self._twin_pair(lambda: nets.q1(obs, new_act), lambda: nets.q2(obs, new_act))
+            old_lp = None
         # (min(q1, q2) - alpha logp).mean() with alpha = exp(log_alpha) read on the device (the
         # reference's alpha.item() float has the same f32 value), and the entropy, in one kernel
         loss_policy_q, entropy = _PolicyQLoss.apply(q1.contiguous(), q2.contiguous(), new_act_logp.contiguous(),
                                                     self.networks.log_alpha.detach())
-        is_ratio = _Ratio0.apply(dist.log_prob(old_act).contiguous(), old_logp.contiguous())
+        if old_lp is None:
+            old_lp = dist.log_prob(old_act)
+        is_ratio = _Ratio0.apply(old_lp.contiguous(), old_logp.contiguous())
         if side is not None:
             main.wait_stream(side)  # the side branch wrote only the scratch's adv_raw / stats
         n_total = float(B * D.world_size())

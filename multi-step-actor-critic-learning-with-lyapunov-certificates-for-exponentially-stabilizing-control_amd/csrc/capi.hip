@@ -583,6 +583,29 @@ int mh_act_grad_colsum(const float* dy, const float* y, int64_t rows, int32_t co
   return MH_OK;
 }
 
+int mh_policy_head(const float* raw, const float* eps, const float* obs, const float* old_act, const float* high,
+                   const float* low, int64_t rows, int32_t A, int32_t D, float log_std_lo, float log_std_hi, float* xq,
+                   float* new_logp, float* old_logp, void* stream) {
+  if (rows < 0 || A <= 0 || A > 8 || D < 0) return fail(MH_EINVAL, "mh_policy_head: bad shape");
+  if (!raw || ((eps || old_act) && (!high || !low)) || (eps && !xq && !new_logp) || (xq && !obs && D > 0))
+    return fail(MH_EINVAL, "mh_policy_head: null pointer");
+  MH_HIP(mh::launch_policy_head(raw, eps, obs, old_act, high, low, rows, A, D, log_std_lo, log_std_hi, xq, new_logp,
+                                old_logp, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_policy_head_backward(const float* raw, const float* eps, const float* old_act, const float* high,
+                            const float* low, const float* d_xq, const float* d_new_logp, const float* d_old_logp,
+                            int64_t rows, int32_t A, int32_t D, float log_std_lo, float log_std_hi, float* d_raw,
+                            void* stream) {
+  if (rows < 0 || A <= 0 || A > 8 || D < 0) return fail(MH_EINVAL, "mh_policy_head_backward: bad shape");
+  if (!raw || !d_raw || !high || !low || ((d_xq || d_new_logp) && !eps) || (d_old_logp && !old_act))
+    return fail(MH_EINVAL, "mh_policy_head_backward: null pointer");
+  MH_HIP(mh::launch_policy_head_bwd(raw, eps, old_act, high, low, d_xq, d_new_logp, d_old_logp, rows, A, D,
+                                    log_std_lo, log_std_hi, d_raw, (hipStream_t)stream));
+  return MH_OK;
+}
+
 int mh_head_backward_workspace(int64_t rows, int32_t n_out, int32_t n_in, int64_t* floats_out) {
   if (!floats_out || rows < 0 || n_out <= 0 || n_out > 16 || n_in <= 0)
     return fail(MH_EINVAL, "mh_head_backward_workspace: bad argument");

@@ -974,6 +974,17 @@ void k_policy_forward_x3(const float* __restrict__ P,
 
 int64_t policy_packed_floats(int D) { return pm_packed_floats(D / 2 + 1); }
 
+// MH_POLICY_KERNEL (A/B measurements): f32 = the all-f32 kernel (0), x6 = split-bf16 layer 2 (1);
+// default split-f16 (x3, 2)
+static int policy_mode() {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* m = getenv("MH_POLICY_KERNEL");
+    mode = (m && m[0] == 'f') ? 0 : ((m && m[0] == 'x' && m[1] == '6') ? 1 : 2);
+  }
+  return mode;
+}
+
 hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
                               const float* b3, int D, int N3, float* P, hipStream_t st) {
   const int K1 = D / 2 + 1;  // ceil((D + 1) / 2): observation + the bias input
@@ -982,8 +993,10 @@ hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2,
   const int grid = (int)((total + 255) / 256 < 1024 ? (total + 255) / 256 : 1024);
   k_policy_pack<<<grid, 256, 0, st>>>(W1, b1, W2, b2, W3, b3, D, N3, K1, P);
   if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
-  k_policy_pack_x6<<<(int)(PM_X6_FLOATS * 2 / 256), 256, 0, st>>>(W2, K1, P);
-  if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
+  if (policy_mode() == 1) {  // the split-bf16 copy of W2 only for that (A/B) kernel
+    k_policy_pack_x6<<<(int)(PM_X6_FLOATS * 2 / 256), 256, 0, st>>>(W2, K1, P);
+    if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
+  }
   k_policy_scales<<<1, 1024, 0, st>>>(W1, b1, W2, b2, W3, D, N3, K1, P);
   if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
   k_policy_pack_x3<<<(int)((PM_X3_FLOATS + PM_X3_W1_FLOATS + PM_X3_W3_FLOATS) * 2 / 256), 256, 0, st>>>(
@@ -1005,13 +1018,7 @@ static hipError_t launch_fwd_t(const float* P, const float* obs, int64_t E, int 
   }
   const int64_t want = (tiles + 3) / 4;
   const int grid = (int)(want < cus ? want : cus);
-  // MH_POLICY_KERNEL (A/B measurements): f32 = the all-f32 kernel, x6 = split-bf16 layer 2;
-  // default split-f16 layer 2 (x3)
-  static int mode = -1;
-  if (mode < 0) {
-    const char* m = getenv("MH_POLICY_KERNEL");
-    mode = (m && m[0] == 'f') ? 0 : ((m && m[0] == 'x' && m[1] == '6') ? 1 : 2);
-  }
+  const int mode = policy_mode();
   if (D <= 15 && mode == 2) {  // K = 16 holds the observation and the bias input
     static int w8 = -1;  // MH_POLICY_WAVES=4: one wave per SIMD with 2 tiles (A/B); default 8
     if (w8 < 0) {

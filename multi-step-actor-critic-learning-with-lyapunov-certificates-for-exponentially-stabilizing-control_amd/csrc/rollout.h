@@ -131,6 +131,13 @@ hipError_t launch_tg_log_prob_bwd(const float* logits, const float* a, const flo
 hipError_t launch_act_grad_colsum(const float* dy, const float* y, int64_t M, int N, int act, float* g, float* db,
                                   float* partial, uint32_t* tickets, hipStream_t st);
 int act_grad_tickets(int N);
+hipError_t launch_policy_head(const float* raw, const float* eps, const float* obs, const float* old_act,
+                              const float* high, const float* low, int64_t M, int A, int D, float lo, float hi,
+                              float* xq, float* new_logp, float* old_logp, hipStream_t st);
+hipError_t launch_policy_head_bwd(const float* raw, const float* eps, const float* old_act, const float* high,
+                                  const float* low, const float* d_xq, const float* d_new_logp,
+                                  const float* d_old_logp, int64_t M, int A, int D, float lo, float hi, float* d_raw,
+                                  hipStream_t st);
 int64_t head_backward_workspace(int64_t M, int n_out, int n_in);
 hipError_t launch_head_backward(const float* dy, const float* x, const float* W, int64_t M, int n_out, int n_in,
                                 float* dx, float* dw, float* db, float* workspace, hipStream_t st);

@@ -181,3 +181,50 @@ def test_stocha_head_matches_torch():
     (y2 * w).sum().backward()
     torch.testing.assert_close(r1.grad, r2.grad, rtol=5e-7, atol=0)
     assert float(r1.grad[0, 6]) == 0.0 and float(r1.grad[0, 7]) == 0.0 and float(r1.grad[0, 4]) != 0.0
+
+
+@pytest.mark.parametrize("R,A,D", [(5120, 4, 12), (257, 1, 3), (1000, 8, 9)])
+def test_policy_head_equals_separate_kernels(R, A, D):
+    """mh_policy_head (MSACL's policy step head: StochaPolicy std + TanhGauss rsample into the
+    critic input [obs | act] + its log-prob + log_prob(old_act)) and its backward equal the
+    separate StochaHead / rsample / concat / log_prob autograd chain bit for bit, with log-stds on
+    both sides of the clamp bounds."""
+    from msacl_amd.algorithm.msacl import _PolicyHead
+    from msacl_amd.apprfunc._fused import StochaHead
+    from msacl_amd.utils.act_distribution_cls import TanhGaussDistribution
+    g = torch.Generator(device="cuda").manual_seed(R + A + D)
+    raw = torch.randn(R, 2 * A, device="cuda", generator=g)
+    raw[:, A:] = raw[:, A:] * 3.0 - 1.0
+    raw[::7, A] = 1.5   # above max_log_std = 1 (clamped: no gradient)
+    raw[::11, A] = -25.0  # below min_log_std = -20
+    eps = torch.randn(R, A, device="cuda", generator=g)
+    obs = torch.randn(R, D, device="cuda", generator=g)
+    hi = torch.linspace(1.0, 3.0, A, device="cuda")
+    lo = -hi * 0.5
+    old_act = lo + (hi - lo) * torch.rand(R, A, device="cuda", generator=g)
+    d_xq = torch.randn(R, D + A, device="cuda", generator=g)
+    d_new = torch.randn(R, device="cuda", generator=g)
+    d_old = torch.randn(R, device="cuda", generator=g)
+
+    r1 = raw.clone().requires_grad_(True)
+    xq, new_lp, old_lp = _PolicyHead.apply(r1, eps, obs, old_act, hi, lo, -20.0, 1.0)
+    torch.autograd.backward([xq, new_lp, old_lp], [d_xq, d_new, d_old])
+
+    r2 = raw.clone().requires_grad_(True)
+    logits = StochaHead.apply(r2, -20.0, 1.0)
+    dist = TanhGaussDistribution(logits)
+    dist.act_high_lim, dist.act_low_lim = hi, lo
+    import torch.distributions.normal as tdn
+    orig = tdn._standard_normal
+    tdn._standard_normal = lambda shape, dtype, device: eps.reshape(shape)
+    try:
+        act, lp = dist.rsample()
+    finally:
+        tdn._standard_normal = orig
+    xq_ref = torch.cat([obs, act], -1)
+    olp_ref = dist.log_prob(old_act)
+    torch.autograd.backward([xq_ref, lp, olp_ref], [d_xq, d_new, d_old])
+    assert torch.equal(xq, xq_ref)
+    assert torch.equal(new_lp, lp)
+    assert torch.equal(old_lp, olp_ref)
+    torch.testing.assert_close(r1.grad, r2.grad, rtol=0, atol=0)
