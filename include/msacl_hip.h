@@ -391,6 +391,19 @@ int mh_msacl_ratio0(const float* logp_new, const float* old_logp, int32_t B, int
                     void* stream);
 int mh_msacl_ratio0_backward(const float* ratio, const float* g_ratio, int32_t B, int32_t n, float* d_logp_new,
                              void* stream);
+/* A policy step's whole objective (msacl.py:379-405) in one single-workgroup launch: mh_msacl_policy_loss
+ * (loss_q, entropy over B*n), mh_msacl_ratio0 (ratio [B] from lp_new = log_prob(old act) under the
+ * current policy), mh_msacl_ppo_clip (adv, loss_ppo, d_ratio) and loss_policy = -loss_q - loss_ppo,
+ * bit-identical to those launches; its backward for a device upstream g of loss_policy gives
+ * dq1, dq2, dlogp [B*n] and dlp_new [B*n] (step 0 only). */
+int mh_msacl_policy_objective(const float* q1, const float* q2, const float* logp, const float* log_alpha,
+                              const float* lp_new, const float* old_logp, const float* adv_raw, const double* stats,
+                              double n_total, float clip_eps, int32_t B, int32_t n, float* loss_q, float* entropy,
+                              float* ratio, float* adv, float* loss_ppo, float* d_ratio, float* loss_policy,
+                              void* stream);
+int mh_msacl_policy_objective_backward(const float* q1, const float* q2, const float* log_alpha, const float* ratio,
+                                       const float* d_ratio, const float* g_loss, int32_t B, int32_t n, float* dq1,
+                                       float* dq2, float* dlogp, float* dlp_new, void* stream);
 /* loss_policy = -loss_q - loss_ppo (msacl.py:401-405, device scalars) and neg_d_ratio = -d_ratio
  * (the is_ratio backward seed of loss_policy) in one launch. */
 int mh_msacl_policy_combine(const float* loss_q, const float* loss_ppo, const float* d_ratio, int32_t B,

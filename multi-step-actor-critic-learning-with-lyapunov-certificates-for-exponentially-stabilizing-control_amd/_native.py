@@ -102,6 +102,10 @@ _PROTOS = {
     "mh_msacl_policy_loss_backward": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_vp, c_vp, c_vp, c_vp]),
     "mh_msacl_ratio0": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "mh_msacl_ratio0_backward": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
+    "mh_msacl_policy_objective": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f64, c_f32, c_i32,
+                                                 c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mh_msacl_policy_objective_backward": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
+                                                          c_vp, c_vp, c_vp, c_vp]),
     "mh_msacl_policy_combine": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp]),
     "mh_msacl_alpha_grad": (ctypes.c_int, [c_vp, c_vp, c_f32, c_vp, c_vp]),
     "mh_polyak_multi": (ctypes.c_int, [c_vp, c_i32, ctypes.c_double, c_vp]),

@@ -172,6 +172,39 @@ class _PolicyHead(torch.autograd.Function):
         return d_raw, None, None, None, None, None, None, None
 
 
+class _PolicyObjective(torch.autograd.Function):
+    """loss_policy = -(min(q1, q2) - alpha logp).mean() - PPO-clip(exp(lp_new - old_logp)[:, 0],
+    normalised stability advantage) (msacl.py:379-405) and the entropy, as one single-workgroup
+    launch (mh_msacl_policy_objective: the policy-loss, ratio, clip and total kernels' own
+    expressions, writing ratio / adv / loss_ppo / d_ratio into the scratch) and one backward
+    launch; bit-identical to those kernels and their autograd seeds (-1, -d_ratio)."""
+
+    @staticmethod
+    def forward(ctx, q1, q2, logp, lp_new, old_logp, log_alpha, s, n_total, clip):
+        B, n = lp_new.shape
+        out = torch.empty(3, dtype=torch.float32, device=q1.device)  # loss_q, entropy, loss_policy
+        _engine("msacl_policy_objective", q1.device, N.ptr(q1), N.ptr(q2), N.ptr(logp), N.ptr(log_alpha),
+                N.ptr(lp_new), N.ptr(old_logp), N.ptr(s.adv_raw), N.ptr(s.stats), n_total, clip, B, n,
+                N.ptr(out[0:1]), N.ptr(out[1:2]), N.ptr(s.ratio), N.ptr(s.adv), N.ptr(s.loss_ppo), N.ptr(s.d_ratio),
+                N.ptr(out[2:3]))
+        ctx.save_for_backward(q1, q2, log_alpha)
+        ctx.s, ctx.shape = s, (B, n)
+        entropy = out[1]
+        ctx.mark_non_differentiable(entropy)
+        return out[2], entropy
+
+    @staticmethod
+    def backward(ctx, g_loss, g_entropy):
+        q1, q2, log_alpha = ctx.saved_tensors
+        s = ctx.s
+        B, n = ctx.shape
+        dq1, dq2, dlogp = torch.empty_like(q1), torch.empty_like(q2), torch.empty_like(q1)
+        dlp = torch.empty(B, n, dtype=torch.float32, device=q1.device)
+        _engine("msacl_policy_objective_backward", q1.device, N.ptr(q1), N.ptr(q2), N.ptr(log_alpha), N.ptr(s.ratio),
+                N.ptr(s.d_ratio), N.ptr(g_loss.contiguous()), B, n, N.ptr(dq1), N.ptr(dq2), N.ptr(dlogp), N.ptr(dlp))
+        return dq1, dq2, dlogp, dlp, None, None, None, None, None
+
+
 class _Ratio0(torch.autograd.Function):
     """exp(logp_new - old_logp)[:, 0] (msacl.py:392-394) and its backward, one launch each."""
 
@@ -205,7 +238,7 @@ class _Scratch:
         self.dV_both = f(2 * B, n)
         self.dV, self.dV2 = self.dV_both[:B], self.dV_both[B:]
         self.adv_raw, self.adv, self.loss_ppo, self.d_ratio = f(B), f(B), f(1), f(B)
-        self.loss_policy, self.neg_d_ratio = f(1), f(B)
+        self.loss_policy, self.neg_d_ratio, self.ratio = f(1), f(B), f(B)
         self.stats = torch.empty(2, dtype=torch.float64, device=device)
 
 
@@ -257,6 +290,7 @@ class MSACL:
         self._scratch = {}
         self.last_priority = None
         self._neg_one = torch.tensor(-1.0, device=self.device)
+        self._one = torch.tensor(1.0, device=self.device)
         self._alpha_grad = None
         self.use_graph = bool(kwargs.get("alg_use_graph", True))
         # the Lyapunov update shares no parameter with the critic update (both only read the
@@ -652,6 +686,23 @@ class MSACL:
             old_lp = None
         # (min(q1, q2) - alpha logp).mean() with alpha = exp(log_alpha) read on the device (the
         # reference's alpha.item() float has the same f32 value), and the entropy, in one kernel
+        if head is not None:
+            # the whole objective (policy loss, step-0 ratio, PPO clip on the stability advantage,
+            # the total) in one launch forward and one backward (mh_msacl_policy_objective)
+            if side is not None:
+                main.wait_stream(side)  # the side branch wrote only the scratch's adv_raw / stats
+            loss_policy, entropy = _PolicyObjective.apply(
+                q1.contiguous(), q2.contiguous(), new_act_logp.contiguous(), old_lp.contiguous(),
+                old_logp.contiguous(), self.networks.log_alpha.detach(), s, float(B * D.world_size()),
+                float(self.clip_coef))
+            self.networks.policy_optimizer.zero_grad()
+            torch.autograd.backward([loss_policy], [self._one])
+            if not defer_step:
+                D.allreduce_grads(list(self.networks.policy.parameters()))
+                self.networks.policy_optimizer.step()
+            for p in list(self.networks.q1.parameters()) + list(self.networks.q2.parameters()):
+                p.requires_grad = True
+            return loss_policy.detach(), entropy.detach()
         loss_policy_q, entropy = _PolicyQLoss.apply(q1.contiguous(), q2.contiguous(), new_act_logp.contiguous(),
                                                     self.networks.log_alpha.detach())
         if old_lp is None:

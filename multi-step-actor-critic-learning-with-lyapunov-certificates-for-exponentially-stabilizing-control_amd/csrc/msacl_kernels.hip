@@ -283,10 +283,9 @@ __global__ __launch_bounds__(TPB) void k_stab_adv(const float* V0, const float* 
 }
 
 // --------------------------------------------------- PPO clip on the advantage (msacl.py:400-405)
-__global__ __launch_bounds__(TPB) void k_ppo_clip(const float* ratio, const float* adv_raw, const double* stats,
-                                                  double n_total, float eps, int B, float* adv, float* loss_out,
-                                                  float* d_ratio) {
-  __shared__ double sh[TPB];
+__device__ __forceinline__ void ppo_clip_body(const float* ratio, const float* adv_raw, const double* stats,
+                                              double n_total, float eps, int B, float* adv, float* loss_out,
+                                              float* d_ratio, double* sh) {
   const double mean = stats[0] / n_total;
   double var = (stats[1] - n_total * mean * mean) / (n_total - 1.0);
   var = var > 0.0 ? var : 0.0;
@@ -314,6 +313,12 @@ __global__ __launch_bounds__(TPB) void k_ppo_clip(const float* ratio, const floa
   const double t = block_sum(acc, sh);
   if (threadIdx.x == 0) loss_out[0] = (float)(t / (double)B);
 }
+__global__ __launch_bounds__(TPB) void k_ppo_clip(const float* ratio, const float* adv_raw, const double* stats,
+                                                  double n_total, float eps, int B, float* adv, float* loss_out,
+                                                  float* d_ratio) {
+  __shared__ double sh[TPB];
+  ppo_clip_body(ratio, adv_raw, stats, n_total, eps, B, adv, loss_out, d_ratio, sh);
+}
 
 // --------------------------------------------------- policy loss pieces (msacl.py:383-405)
 // loss_policy_q = (min(q1, q2) - alpha * logp).mean(), alpha = exp(log_alpha) (the reference's
@@ -321,10 +326,9 @@ __global__ __launch_bounds__(TPB) void k_ppo_clip(const float* ratio, const floa
 __device__ __forceinline__ float torch_min(float a, float b) {
   return (a != a || b != b) ? __builtin_nanf("") : (a < b ? a : b);  // torch.min propagates NaN
 }
-__global__ __launch_bounds__(TPB) void k_policy_loss(const float* q1, const float* q2, const float* logp,
-                                                     const float* log_alpha, int64_t N, float* loss,
-                                                     float* entropy) {
-  __shared__ double sh[TPB];
+__device__ __forceinline__ void policy_loss_body(const float* q1, const float* q2, const float* logp,
+                                                 const float* log_alpha, int64_t N, float* loss, float* entropy,
+                                                 double* sh) {
   const float alpha = expf(*log_alpha);
   double a = 0.0, b = 0.0;
   for (int64_t i = threadIdx.x; i < N; i += TPB) {
@@ -339,6 +343,12 @@ __global__ __launch_bounds__(TPB) void k_policy_loss(const float* q1, const floa
     loss[0] = (float)(ta / (double)N);
     entropy[0] = -(float)(tb / (double)N);
   }
+}
+__global__ __launch_bounds__(TPB) void k_policy_loss(const float* q1, const float* q2, const float* logp,
+                                                     const float* log_alpha, int64_t N, float* loss,
+                                                     float* entropy) {
+  __shared__ double sh[TPB];
+  policy_loss_body(q1, q2, logp, log_alpha, N, loss, entropy, sh);
 }
 // autograd's backward of that expression for an upstream gradient g (device scalar):
 // mean -> g / N; sub -> (+, -); mul by alpha; minimum -> the smaller input (ties: half each)
@@ -383,6 +393,47 @@ __global__ __launch_bounds__(256) void k_policy_combine(const float* loss_q, con
 __global__ __launch_bounds__(64) void k_alpha_grad(const float* log_alpha, const float* entropy, float target,
                                                    float* grad) {
   if (threadIdx.x == 0) grad[0] = (entropy[0] - target) * expf(log_alpha[0]);
+}
+
+// The whole policy objective of a policy step (msacl.py:379-405) in ONE single-workgroup launch:
+// loss_q = (min(q1, q2) - alpha logp).mean() and the entropy (k_policy_loss's body), the step-0
+// importance ratio exp(lp_new - old_logp)[:, 0] (k_ratio0's), the normalised stability advantage
+// with the PPO clip and its d_ratio (k_ppo_clip's body) and loss_policy = -loss_q - loss_ppo
+// (k_policy_combine's): the same expressions in the same order, so the same bits as the four
+// launches it replaces. Each thread's ratios are read back by the same thread (b = tid + k TPB).
+__global__ __launch_bounds__(TPB) void k_policy_objective(const float* q1, const float* q2, const float* logp,
+                                                          const float* log_alpha, const float* lp_new,
+                                                          const float* old_logp, const float* adv_raw,
+                                                          const double* stats, double n_total, float clip_eps, int B,
+                                                          int n, float* loss_q, float* entropy, float* ratio,
+                                                          float* adv, float* loss_ppo, float* d_ratio,
+                                                          float* loss_policy) {
+  __shared__ double sh[TPB];
+  policy_loss_body(q1, q2, logp, log_alpha, (int64_t)B * n, loss_q, entropy, sh);
+  for (int b = threadIdx.x; b < B; b += TPB) ratio[b] = expf(lp_new[(int64_t)b * n] - old_logp[(int64_t)b * n]);
+  __syncthreads();
+  ppo_clip_body(ratio, adv_raw, stats, n_total, clip_eps, B, adv, loss_ppo, d_ratio, sh);
+  if (threadIdx.x == 0) loss_policy[0] = (-loss_q[0]) - loss_ppo[0];
+}
+// Its backward for an upstream gradient g of loss_policy (device scalar): d loss_q = -g through
+// k_policy_loss_bwd's expressions (dq1, dq2, dlogp), d is_ratio = -g d_ratio through k_ratio0_bwd's
+// (d lp_new: step 0 only). With g = 1 the same bits as the separate backward launches.
+__global__ __launch_bounds__(256) void k_policy_objective_bwd(const float* q1, const float* q2,
+                                                              const float* log_alpha, const float* ratio,
+                                                              const float* d_ratio, const float* g, int B, int n,
+                                                              float* dq1, float* dq2, float* dlogp, float* dlp_new) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t N = (int64_t)B * n;
+  if (i >= N) return;
+  const float alpha = expf(*log_alpha);
+  const float gq = -*g;
+  const float gg = gq * (1.0f / (float)N);
+  const float a = q1[i], bq = q2[i];
+  dq1[i] = a == bq ? gg / 2.0f : (a > bq ? 0.0f : gg);
+  dq2[i] = a == bq ? gg / 2.0f : (a < bq ? 0.0f : gg);
+  dlogp[i] = (-gg) * alpha;
+  const int64_t b = i / n;
+  dlp_new[i] = (i - b * n) == 0 ? (-(*g * d_ratio[b])) * ratio[b] : 0.0f;
 }
 
 thread_local std::string g_merr;
@@ -480,6 +531,34 @@ int mh_msacl_ratio0_backward(const float* ratio, const float* g_ratio, int32_t B
   const int64_t total = (int64_t)B * n;
   k_ratio0_bwd<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(ratio, g_ratio, B, n, d_logp_new);
   MH_CHECK_LAUNCH("ratio0_bwd");
+  return MH_OK;
+}
+
+int mh_msacl_policy_objective(const float* q1, const float* q2, const float* logp, const float* log_alpha,
+                              const float* lp_new, const float* old_logp, const float* adv_raw, const double* stats,
+                              double n_total, float clip_eps, int32_t B, int32_t n, float* loss_q, float* entropy,
+                              float* ratio, float* adv, float* loss_ppo, float* d_ratio, float* loss_policy,
+                              void* stream) {
+  if (!q1 || !q2 || !logp || !log_alpha || !lp_new || !old_logp || !adv_raw || !stats || !loss_q || !entropy ||
+      !ratio || !adv || !loss_ppo || !d_ratio || !loss_policy || B <= 0 || n <= 0)
+    return MH_EINVAL;
+  k_policy_objective<<<1, TPB, 0, (hipStream_t)stream>>>(q1, q2, logp, log_alpha, lp_new, old_logp, adv_raw, stats,
+                                                         n_total, clip_eps, B, n, loss_q, entropy, ratio, adv,
+                                                         loss_ppo, d_ratio, loss_policy);
+  MH_CHECK_LAUNCH("policy_objective");
+  return MH_OK;
+}
+
+int mh_msacl_policy_objective_backward(const float* q1, const float* q2, const float* log_alpha, const float* ratio,
+                                       const float* d_ratio, const float* g_loss, int32_t B, int32_t n, float* dq1,
+                                       float* dq2, float* dlogp, float* dlp_new, void* stream) {
+  if (!q1 || !q2 || !log_alpha || !ratio || !d_ratio || !g_loss || !dq1 || !dq2 || !dlogp || !dlp_new || B <= 0 ||
+      n <= 0)
+    return MH_EINVAL;
+  const int64_t N = (int64_t)B * n;
+  k_policy_objective_bwd<<<(unsigned)((N + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      q1, q2, log_alpha, ratio, d_ratio, g_loss, B, n, dq1, dq2, dlogp, dlp_new);
+  MH_CHECK_LAUNCH("policy_objective_bwd");
   return MH_OK;
 }
 

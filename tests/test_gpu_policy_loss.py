@@ -90,3 +90,45 @@ def test_alpha_grad_matches_autograd(log_alpha, entropy, target):
     N.check(N.lib().mh_msacl_alpha_grad(N.ptr(la.detach()), N.ptr(ent), float(target), N.ptr(out),
                                         N.stream_of(ent.device)), "mh_msacl_alpha_grad")
     assert torch.equal(out, la.grad)
+
+
+@pytest.mark.parametrize("B,n", [(256, 20), (3, 5), (1100, 2)])
+def test_policy_objective_equals_separate_kernels(B, n):
+    """mh_msacl_policy_objective[_backward] (the policy step's whole objective in one launch each way)
+    equals the policy-loss, ratio, PPO-clip and combine kernels with their autograd seeds (-1 and
+    -d_ratio) bit for bit: loss, entropy, advantage, d_ratio and every input gradient."""
+    import msacl_amd._native as N
+    from msacl_amd.algorithm.msacl import _PolicyObjective, _Scratch
+    g = torch.Generator(device="cuda").manual_seed(B * 7 + n)
+    q1 = torch.randn(B, n, device="cuda", generator=g)
+    q2 = torch.randn(B, n, device="cuda", generator=g)
+    q2[:, ::3] = q1[:, ::3]
+    lp = torch.randn(B, n, device="cuda", generator=g)
+    lp_new = torch.randn(B, n, device="cuda", generator=g) * 0.1
+    old = lp_new + torch.randn(B, n, device="cuda", generator=g) * 0.1
+    log_alpha = torch.tensor(0.3, device="cuda")
+    adv_raw = torch.randn(B, device="cuda", generator=g)
+    stats = torch.stack([adv_raw.double().sum(), (adv_raw.double() ** 2).sum()])
+    st = N.stream_of(q1.device)
+
+    s = _Scratch(B, n, q1.device)
+    s.adv_raw.copy_(adv_raw)
+    s.stats.copy_(stats)
+    a = [t.clone().requires_grad_(True) for t in (q1, q2, lp, lp_new)]
+    loss, ent = _PolicyObjective.apply(a[0], a[1], a[2], a[3], old, log_alpha, s, float(B), 0.1)
+    torch.autograd.backward([loss], [torch.tensor(1.0, device="cuda")])
+
+    b = [t.clone().requires_grad_(True) for t in (q1, q2, lp, lp_new)]
+    lq, ent2 = _PolicyQLoss.apply(b[0], b[1], b[2], log_alpha)
+    ratio = _Ratio0.apply(b[3], old)
+    adv, lppo, dr = torch.empty(B, device="cuda"), torch.empty(1, device="cuda"), torch.empty(B, device="cuda")
+    N.check(N.lib().mh_msacl_ppo_clip(N.ptr(ratio.detach().contiguous()), N.ptr(adv_raw), N.ptr(stats), float(B), 0.1, B,
+                                      N.ptr(adv), N.ptr(lppo), N.ptr(dr), st), "ppo_clip")
+    lpol, neg = torch.empty(1, device="cuda"), torch.empty(B, device="cuda")
+    N.check(N.lib().mh_msacl_policy_combine(N.ptr(lq.detach()), N.ptr(lppo), N.ptr(dr), B, N.ptr(lpol), N.ptr(neg), st),
+            "combine")
+    torch.autograd.backward([lq, ratio], [torch.tensor(-1.0, device="cuda"), neg])
+    assert torch.equal(loss.detach(), lpol[0]) and torch.equal(ent, ent2)
+    assert torch.equal(s.adv, adv) and torch.equal(s.d_ratio, dr) and torch.equal(s.loss_ppo, lppo)
+    for x, y in zip(a, b):
+        assert torch.equal(x.grad, y.grad)
