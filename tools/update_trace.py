@@ -32,6 +32,13 @@ def run(reps=6):
         trainer.step()
         trainer.iteration += 1
     torch.cuda.synchronize()
+    if os.environ.get("TRACE_WHAT") == "sample":  # sampler.sample() bursts instead of updates
+        for _ in range(12):
+            time.sleep(0.02)
+            sampler.sample()
+            torch.cuda.synchronize()
+        print("done", flush=True)
+        return
     batch = buffer.sample_batch(256)
     for it in (0, 1):
         for _ in range(reps):
