@@ -728,6 +728,35 @@ int64_t gemm_workspace_floats(int64_t M, int64_t N, int64_t K) {
   return S > 1 ? S * M * N : 0;
 }
 
+// One-output products C[M][1] = act(A[M][K] . b + bias) (the critics' / value nets' last layer:
+// 5,120 x 256 in the MSACL update): one wave per row, each lane a float4 of every 256-wide K chunk
+// in order, the 64 lane sums added by a butterfly; no split-K partials or finishing launch
+// (k_gemm + k_gemm_reduce took 9 + 4 us for this shape).
+__global__ __launch_bounds__(256) void k_gemv_n1(GemmArgs g, int64_t bstride) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= g.M) return;
+  const float* a = g.A + row * g.lda;
+  float acc = 0.0f;
+  for (int64_t k0 = 0; k0 < g.K; k0 += 256) {
+    const int64_t k = k0 + 4 * lane;
+    if (k + 3 < g.K && bstride == 1) {
+      const float4 av = *reinterpret_cast<const float4*>(a + k);
+      const float4 bv = *reinterpret_cast<const float4*>(g.B + k);
+      acc = acc + av.x * bv.x;
+      acc = acc + av.y * bv.y;
+      acc = acc + av.z * bv.z;
+      acc = acc + av.w * bv.w;
+    } else {
+      for (int u = 0; u < 4; ++u)
+        if (k + u < g.K) acc = acc + a[k + u] * g.B[(k + u) * bstride];
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
+  if (lane == 0) g.C[row * g.ldc] = gemm_act(g.bias ? acc + g.bias[0] : acc, g.act);
+}
+
 template <int WM, int WN>
 static hipError_t launch_gemm_cfg(const GemmArgs& g, int64_t grid, bool ta, bool tb, hipStream_t st) {
   if (!ta && !tb) k_gemm<WM, WN, false, false><<<(unsigned)grid, 256, 0, st>>>(g);
@@ -773,6 +802,11 @@ hipError_t launch_gemm(const float* A, const float* B, const float* bias, float*
       case 7: return launch_tall<7>(g, tb, st);
       default: return launch_tall<8>(g, tb, st);
     }
+  }
+  if (N == 1 && !ta && M >= 256 && K > 0 && lda % 4 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0) {
+    GemmArgs g{A, B, bias, C, M, N, K, lda, ldb, ldc, act, 1, 0, nullptr, nullptr, -1, nullptr, nullptr};
+    k_gemv_n1<<<(unsigned)((M + 3) / 4), 256, 0, st>>>(g, tb ? 1 : ldb);
+    return hipGetLastError();
   }
   const GemmPlan p = gemm_plan(M, N, K > 0 ? K : 1);
   GemmArgs g{A, B, bias, C, M, N, K, lda, ldb, ldc, act, p.S, p.kc_per, workspace, nullptr, -1, nullptr, nullptr};

@@ -37,7 +37,7 @@ def _ref(a, b, bias, ta, tb, act):
 SHAPES = [  # (M, N, K)
     (5120, 256, 16), (5120, 256, 256), (5120, 1, 256), (5120, 8, 256), (256, 256, 256), (256, 256, 12),
     (256, 8, 256), (256, 256, 5120), (8, 256, 5120), (1, 256, 5120), (16, 256, 5120), (256, 16, 5120),
-    (333, 77, 45), (1, 1, 1), (65, 33, 129), (7, 300, 1000),
+    (333, 77, 45), (1, 1, 1), (65, 33, 129), (7, 300, 1000), (4097, 1, 300), (256, 1, 1000), (2048, 1, 3),
     # tall products (k_gemm_tall when op(A) is A: M >= 2,048, N % 64 == 0, K % 4 == 0)
     (5120, 256, 12), (5120, 64, 4), (3001, 128, 20), (2048, 192, 36), (4100, 256, 256),
 ]
