@@ -77,7 +77,9 @@ def _tall(rows, n, k):
 def _hip_forward(rows, out_features, act=0, in_features=0):
     b = _GEMM_BACKEND["name"]
     # tanh layers with a short K: the epilogue saves the library path's separate tanh launch
+    # (first layers, K <= 32 over >= 256 rows: mh_gemm_f32's short-K kernel)
     return b == "hip" or (b == "auto" and (rows <= 1024 or out_features == 1 or (act == 2 and in_features <= 64)
+                                           or (in_features <= 32 and out_features >= 64)
                                            or _tall(rows, out_features, in_features)))
 
 

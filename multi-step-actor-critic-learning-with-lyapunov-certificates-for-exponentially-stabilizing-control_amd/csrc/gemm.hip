@@ -757,6 +757,43 @@ __global__ __launch_bounds__(256) void k_gemv_n1(GemmArgs g, int64_t bstride) {
   if (lane == 0) g.C[row * g.ldc] = gemm_act(g.bias ? acc + g.bias[0] : acc, g.act);
 }
 
+// Short-K products C[M][N] = act(A[M][K] B[N][K]^T + bias), K <= 32 (the first layers of the
+// update's MLPs: observations / observation + action, K = 12 or 16, into 256 hidden units over
+// 5,120-10,240 rows): write-bound, not MFMA-bound. Workgroup = 32 rows x 64 columns with both
+// operand tiles in LDS; thread = one column x 8 rows, the K products summed in k order, bias and
+// activation applied, 64 consecutive columns per store instruction (k_gemm_tall's 64-deep chunk
+// and the library's tile both took 7-14 us for these shapes).
+constexpr int SK_MAX = 32;
+__global__ __launch_bounds__(256) void k_gemm_shortk(GemmArgs g) {
+  __shared__ float As[32][SK_MAX + 1];
+  __shared__ float Bs[64][SK_MAX + 1];
+  const int tid = threadIdx.x, tx = tid & 63, ty = tid >> 6;
+  const int tiles_n = (int)((g.N + 63) / 64);
+  const int64_t m0 = (int64_t)(blockIdx.x / tiles_n) * 32;
+  const int64_t n0 = (int64_t)(blockIdx.x % tiles_n) * 64;
+  const int K = (int)g.K;
+  for (int q = tid; q < 32 * K; q += 256) {
+    const int r = q / K, k = q - r * K;
+    As[r][k] = m0 + r < g.M ? g.A[(m0 + r) * g.lda + k] : 0.0f;
+  }
+  for (int q = tid; q < 64 * K; q += 256) {
+    const int c = q / K, k = q - c * K;
+    Bs[c][k] = n0 + c < g.N ? g.B[(n0 + c) * g.ldb + k] : 0.0f;
+  }
+  __syncthreads();
+  const int64_t col = n0 + tx;
+  if (col >= g.N) return;
+  const float bv = g.bias ? g.bias[col] : 0.0f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = ty + 4 * i;
+    if (m0 + r >= g.M) break;
+    float acc = As[r][0] * Bs[tx][0];
+    for (int k = 1; k < K; ++k) acc = acc + As[r][k] * Bs[tx][k];
+    g.C[(m0 + r) * g.ldc + col] = gemm_act(g.bias ? acc + bv : acc, g.act);
+  }
+}
+
 template <int WM, int WN>
 static hipError_t launch_gemm_cfg(const GemmArgs& g, int64_t grid, bool ta, bool tb, hipStream_t st) {
   if (!ta && !tb) k_gemm<WM, WN, false, false><<<(unsigned)grid, 256, 0, st>>>(g);
@@ -788,6 +825,12 @@ hipError_t launch_gemm(const float* A, const float* B, const float* bias, float*
     if (e != hipSuccess || S == 1) return e;
     const int64_t want = (M * N + 255) / 256;
     k_gemm_reduce<<<(unsigned)(want < 2048 ? want : 2048), 256, 0, st>>>(g);
+    return hipGetLastError();
+  }
+  if (!ta && tb && K >= 1 && K <= SK_MAX && M >= 256 && N >= 64) {
+    GemmArgs g{A, B, bias, C, M, N, K, lda, ldb, ldc, act, 1, 0, nullptr, nullptr, -1, nullptr, nullptr};
+    const int64_t grid = ((M + 31) / 32) * ((N + 63) / 64);
+    k_gemm_shortk<<<(unsigned)grid, 256, 0, st>>>(g);
     return hipGetLastError();
   }
   if (tall_ok(A, B, bias, C, M, N, K, lda, ldb, ldc, ta) && (tb ? N : K) * ldb * 4 < ((int64_t)1 << 30)) {

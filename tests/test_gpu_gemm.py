@@ -40,6 +40,8 @@ SHAPES = [  # (M, N, K)
     (333, 77, 45), (1, 1, 1), (65, 33, 129), (7, 300, 1000), (4097, 1, 300), (256, 1, 1000), (2048, 1, 3),
     # tall products (k_gemm_tall when op(A) is A: M >= 2,048, N % 64 == 0, K % 4 == 0)
     (5120, 256, 12), (5120, 64, 4), (3001, 128, 20), (2048, 192, 36), (4100, 256, 256),
+    # short-K products (k_gemm_shortk: op(A) = A, op(B) = B^T, K <= 32)
+    (10240, 256, 12), (5376, 256, 16), (300, 100, 32), (257, 64, 1), (1000, 130, 7),
 ]
 
 
