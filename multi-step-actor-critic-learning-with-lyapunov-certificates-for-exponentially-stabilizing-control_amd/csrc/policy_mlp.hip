@@ -538,56 +538,73 @@ __device__ __forceinline__ int pm_scale_exp(float bound) {  // 14 - ceil(log2(bo
 
 // The raw magnitudes behind the scales: [0] max |W1, b1|, [1] max |W2|, [2] max |W3|,
 // [3] R1 = max_k (sum_j |W1[k][j]| + |b1[k]|), [4] R2 = max_o (sum_k |W2[o][k]| + |b2[o]|).
-// ONE workgroup of 1024 threads (W2 is 256 KB: ~2 us from L2 for one CU): four lanes per row of
-// W2 (64 columns each, 16-byte loads) combined by shuffles, W1 rows and W3 columns one lane per
-// hidden unit, then a block max. Plain stores: 256 workgroups combining by atomic max on these five
-// words serialised at the L2 (17.5 us per pack).
+// PM_SC_WG workgroups of 16 waves, one row of W2 per wave and pass (a float4 per lane, wave
+// max / sum by butterflies), W1 row / W3 column of the same hidden unit on its lane 0; each
+// workgroup stores its five maxima to the partial slots scal[8 + 5 wg + q] with plain stores
+// (no atomics: 256 workgroups combining by atomic max on five words serialised at the L2, 17.5
+// us; one workgroup alone took 11 us); k_policy_pack_x3 reduces the partials.
+constexpr int PM_SC_WG = 8;
 __global__ __launch_bounds__(1024) void k_policy_scales(const float* __restrict__ W1, const float* __restrict__ b1,
                                                         const float* __restrict__ W2, const float* __restrict__ b2,
                                                         const float* __restrict__ W3, int D, int N3, int K1,
                                                         float* __restrict__ P) {
   __shared__ float red[5][16];
-  const int t = threadIdx.x, row = t >> 2, part = t & 3;
-  const float4* w2 = reinterpret_cast<const float4*>(W2 + (int64_t)row * PM_H + part * 64);
-  float m2 = 0.0f, s2 = 0.0f;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float v[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  for (int row = blockIdx.x * (PM_H / PM_SC_WG) + wv; row < (blockIdx.x + 1) * (PM_H / PM_SC_WG); row += 16) {
+    const float4 x = reinterpret_cast<const float4*>(W2 + (int64_t)row * PM_H)[lane];
+    const float a = fabsf(x.x), b = fabsf(x.y), c = fabsf(x.z), d = fabsf(x.w);
+    float m2 = fmaxf(fmaxf(a, b), fmaxf(c, d)), s2 = (a + b) + (c + d);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const float4 v = w2[i];
-    const float a = fabsf(v.x), b = fabsf(v.y), c = fabsf(v.z), d = fabsf(v.w);
-    m2 = fmaxf(m2, fmaxf(fmaxf(a, b), fmaxf(c, d)));
-    s2 += (a + b) + (c + d);
-  }
-  m2 = fmaxf(m2, __shfl_xor(m2, 1, 64));
-  m2 = fmaxf(m2, __shfl_xor(m2, 2, 64));
-  s2 += __shfl_xor(s2, 1, 64);
-  s2 += __shfl_xor(s2, 2, 64);
-  float r2 = part == 0 ? s2 + fabsf(b2[row]) : 0.0f;
-  float m1 = 0.0f, r1 = 0.0f, m3 = 0.0f;
-  if (t < PM_H) {
-    m1 = fabsf(b1[t]);
-    r1 = m1;
-    for (int j = 0; j < D; ++j) {
-      const float v = fabsf(W1[(int64_t)t * D + j]);
-      m1 = fmaxf(m1, v);
-      r1 += v;
+    for (int off = 32; off > 0; off >>= 1) {
+      m2 = fmaxf(m2, __shfl_xor(m2, off, 64));
+      s2 += __shfl_xor(s2, off, 64);
     }
-    for (int o = 0; o < N3; ++o) m3 = fmaxf(m3, fabsf(W3[(int64_t)o * PM_H + t]));
+    v[1] = fmaxf(v[1], m2);
+    v[4] = fmaxf(v[4], s2 + fabsf(b2[row]));
+    if (lane == 0) {  // hidden unit `row`: row of W1 (+ b1) and column of W3
+      float m1 = fabsf(b1[row]), r1 = m1, m3 = 0.0f;
+      for (int j = 0; j < D; ++j) {
+        const float u = fabsf(W1[(int64_t)row * D + j]);
+        m1 = fmaxf(m1, u);
+        r1 += u;
+      }
+      for (int o = 0; o < N3; ++o) m3 = fmaxf(m3, fabsf(W3[(int64_t)o * PM_H + row]));
+      v[0] = fmaxf(v[0], m1);
+      v[2] = fmaxf(v[2], m3);
+      v[3] = fmaxf(v[3], r1);
+    }
   }
-  float v[5] = {m1, m2, m3, r1, r2};
 #pragma unroll
   for (int q = 0; q < 5; ++q)
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v[q] = fmaxf(v[q], __shfl_xor(v[q], off, 64));
-  if ((t & 63) == 0) {
+  if (lane == 0) {
 #pragma unroll
-    for (int q = 0; q < 5; ++q) red[q][t >> 6] = v[q];
+    for (int q = 0; q < 5; ++q) red[q][wv] = v[q];
   }
   __syncthreads();
-  if (t < 5) {
+  if (threadIdx.x < 5) {
     float m = 0.0f;
-    for (int w = 0; w < 16; ++w) m = fmaxf(m, red[t][w]);
-    P[pm_off_scal(K1) + t] = m;
+    for (int w = 0; w < 16; ++w) m = fmaxf(m, red[threadIdx.x][w]);
+    P[pm_off_scal(K1) + 8 + 5 * blockIdx.x + threadIdx.x] = m;
   }
+}
+
+// The final magnitudes from k_policy_scales' partials (every workgroup of k_policy_pack_x3 forms
+// them; its workgroup 0 stores them to scal[0..4] for the forward kernel)
+__device__ __forceinline__ void pm_reduce_scales(float* P, int K1, float* out5) {
+  __shared__ float s5[5];
+  float* scal = P + pm_off_scal(K1);
+  if (threadIdx.x < 5) {
+    float m = 0.0f;
+    for (int w = 0; w < PM_SC_WG; ++w) m = fmaxf(m, scal[8 + 5 * w + threadIdx.x]);
+    s5[threadIdx.x] = m;
+    if (blockIdx.x == 0) scal[threadIdx.x] = m;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 5; ++q) out5[q] = s5[q];
 }
 
 // sw1..3, their inverses, and R1, R2 rounded up (the f32 sums above are upper bounds only up to
@@ -633,12 +650,29 @@ __device__ __forceinline__ float relu_raw(float x) {
 }
 
 // One thread per packed f16 of W2x3, W1x3 and W3x3.
+// with_bias: also the f32 layer-2 / layer-3 bias regions the split-f16 forward reads (k_policy_pack's
+// layout), so the default kernel needs no f32 pack launch
 __global__ __launch_bounds__(256) void k_policy_pack_x3(const float* __restrict__ W1, const float* __restrict__ b1,
-                                                        const float* __restrict__ W2, const float* __restrict__ W3,
-                                                        int D, int N3, int K1, float* __restrict__ P) {
-  const PmScales sc = pm_scales(P + pm_off_scal(K1));
+                                                        const float* __restrict__ W2, const float* __restrict__ b2,
+                                                        const float* __restrict__ W3, const float* __restrict__ b3,
+                                                        int D, int N3, int K1, int with_bias, float* __restrict__ P) {
+  float raw5[5];
+  pm_reduce_scales(P, K1, raw5);
+  const PmScales sc = pm_scales(raw5);
   const float sw1 = sc.sw[0], sw2 = sc.sw[1], sw3 = sc.sw[2];
   constexpr int64_t n2 = PM_X3_FLOATS * 2, n1 = PM_X3_W1_FLOATS * 2, n3 = PM_X3_W3_FLOATS * 2;
+  if (with_bias) {  // b2 as [blk][lane][16] (pm_row order) and b3 (N3 values, zero padded)
+    const int64_t nb2 = pm_off_w3(K1) - pm_off_b2(K1);
+    for (int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x; o < nb2 + 32; o += (int64_t)gridDim.x * 256) {
+      if (o < nb2) {
+        const int r = (int)(o % 16), l = (int)((o / 16) % 64), blk = (int)(o / (16 * 64));
+        P[pm_off_b2(K1) + o] = b2[blk * 32 + pm_row(r, l)];
+      } else {
+        const int i = (int)(o - nb2);
+        P[pm_off_b3(K1) + i] = i < N3 ? b3[i] : 0.0f;
+      }
+    }
+  }
   for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n2 + n1 + n3; q += (int64_t)gridDim.x * 256) {
     float v;
     int64_t r;
@@ -991,16 +1025,19 @@ hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2,
   if (reinterpret_cast<uintptr_t>(W2) & 15) return hipErrorInvalidValue;  // k_policy_scales: 16-byte rows
   const int64_t total = pm_off_w2x6(K1);
   const int grid = (int)((total + 255) / 256 < 1024 ? (total + 255) / 256 : 1024);
-  k_policy_pack<<<grid, 256, 0, st>>>(W1, b1, W2, b2, W3, b3, D, N3, K1, P);
-  if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
+  const bool split_only = policy_mode() == 2 && D <= 15;  // the default kernel reads only b2 / b3 in f32
+  if (!split_only) {
+    k_policy_pack<<<grid, 256, 0, st>>>(W1, b1, W2, b2, W3, b3, D, N3, K1, P);
+    if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
+  }
   if (policy_mode() == 1) {  // the split-bf16 copy of W2 only for that (A/B) kernel
     k_policy_pack_x6<<<(int)(PM_X6_FLOATS * 2 / 256), 256, 0, st>>>(W2, K1, P);
     if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
   }
-  k_policy_scales<<<1, 1024, 0, st>>>(W1, b1, W2, b2, W3, D, N3, K1, P);
+  k_policy_scales<<<PM_SC_WG, 1024, 0, st>>>(W1, b1, W2, b2, W3, D, N3, K1, P);
   if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
   k_policy_pack_x3<<<(int)((PM_X3_FLOATS + PM_X3_W1_FLOATS + PM_X3_W3_FLOATS) * 2 / 256), 256, 0, st>>>(
-      W1, b1, W2, W3, D, N3, K1, P);
+      W1, b1, W2, b2, W3, b3, D, N3, K1, split_only ? 1 : 0, P);
   return hipGetLastError();
 }
 
