@@ -65,7 +65,9 @@ def _compare_params(alg, g, prefix):
         ref = g[k]
         got = mine[k[len(prefix):]].detach().cpu().numpy()
         bad = ~np.isclose(got, ref, rtol=1e-4, atol=3e-5)
-        assert bad.mean() < 2e-3, (k, int(bad.sum()), float(np.abs(got - ref).max()))
+        # every element (round 1 allowed 0.2 % outliers per tensor; measured on the MI355X: none
+        # in any tensor of SAC / LAC / PPO / POLYC / MSACL, max |diff| ~1e-8)
+        assert not bad.any(), (k, int(bad.sum()), float(np.abs(got - ref).max()))
         n += 1
     assert n > 0
 
