@@ -277,6 +277,10 @@ int mh_policy_head_backward(const float* raw, const float* eps, const float* old
                             const float* low, const float* d_xq, const float* d_new_logp, const float* d_old_logp,
                             int64_t rows, int32_t A, int32_t D, float log_std_lo, float log_std_hi, float* d_raw,
                             void* stream);
+/* LyapunovValue's V = sum_j y[r][j]^2 per row (RL/apprfunc/mlp.py, torch.pow(y, 2).sum(-1)) and its
+ * backward dy = g[r] * (2 y) (the pow backward's bits). Row-major contiguous y [rows][cols]. */
+int mh_square_sum(const float* y, int64_t rows, int32_t cols, float* out, void* stream);
+int mh_square_sum_backward(const float* y, const float* g, int64_t rows, int32_t cols, float* dy, void* stream);
 /* Backward of a narrow identity output layer y = x W^T + b (W [n_out][n_in], n_out <= 16: the
  * critic / policy heads of RL/apprfunc/mlp.py:18-30 under autograd): dx = dy W, dW = dy^T x,
  * db = column sums of dy in one pass over x plus a block-ordered finish (deterministic). Any

@@ -86,6 +86,16 @@ class ApproxContainer(nn.Module):
         return self.policy.get_act_dist_cls(logits)
 
 
+def _stacked(a, b):
+    """torch.cat([a, b], 0), as a view when b directly follows a in one buffer (the replayed
+    update's static inputs)."""
+    if (a.is_contiguous() and b.is_contiguous() and a.shape == b.shape and a.dtype == b.dtype
+            and a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
+            and b.data_ptr() == a.data_ptr() + a.numel() * a.element_size()):
+        return a.as_strided((2 * a.shape[0],) + tuple(a.shape[1:]), a.stride())
+    return torch.cat([a, b], 0)
+
+
 class LazyTbInfo(Mapping):
     """model_update's tb dict (msacl.py:211-222) over a device tensor of its seven scalars: the
     values are read back (one transfer, a host sync) on first access, alg_time then being the
@@ -510,6 +520,14 @@ class MSACL:
         shapes = tuple((k, tuple(v.shape)) for k, v in sorted(data.items()) if torch.is_tensor(v))
         if self._static is None or self._static_shapes != shapes:
             self._static = {k: v.clone() for k, v in data.items() if torch.is_tensor(v)}
+            o, o2 = self._static.get("obs"), self._static.get("obs2")
+            if o is not None and o2 is not None and o.shape == o2.shape and o.dtype == o2.dtype:
+                # obs and obs2 as the two halves of one buffer: the Lyapunov step's batch of both
+                # (msacl.py:275-276) is then a view, not a concatenation per update
+                joint = torch.empty((2,) + tuple(o.shape), dtype=o.dtype, device=o.device)
+                joint[0].copy_(o)
+                joint[1].copy_(o2)
+                self._static["obs"], self._static["obs2"] = joint[0], joint[1]
             self._static_shapes = shapes
             self._graphs = {}
             self._warm = set()
@@ -612,7 +630,7 @@ class MSACL:
                 logp = dist.log_prob(act).contiguous()
         # V(obs) and V(obs2) (msacl.py:275-276) as ONE batch through the network: one forward and
         # one backward instead of two each (the weight gradients sum the same 2 B n rows)
-        V_both = self.networks.lyapunov(torch.cat([obs, obs2], 0))
+        V_both = self.networks.lyapunov(_stacked(obs, obs2))
         V, V2 = V_both[:B], V_both[B:]
         _engine(
             "msacl_lyapunov", self.device,

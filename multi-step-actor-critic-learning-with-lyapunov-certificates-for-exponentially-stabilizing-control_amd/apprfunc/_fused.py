@@ -247,6 +247,33 @@ class LinearAct(torch.autograd.Function):
         return dx, dw, db, None
 
 
+class SquareSum(torch.autograd.Function):
+    """torch.pow(y, 2).sum(-1) over the last dimension (LyapunovValue.forward) as one launch
+    forward and one backward (mh_square_sum[_backward]); the backward's bits are pow's."""
+
+    @staticmethod
+    def forward(ctx, y):
+        N = _native()
+        cols = y.shape[-1]
+        yc = y.contiguous()
+        rows = yc.numel() // cols
+        out = torch.empty(y.shape[:-1], dtype=y.dtype, device=y.device)
+        N.check(N.lib().mh_square_sum(N.ptr(yc), rows, cols, N.ptr(out), N.stream_of(y.device)), "mh_square_sum")
+        ctx.save_for_backward(yc)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        N = _native()
+        cols = y.shape[-1]
+        rows = y.numel() // cols
+        dy = torch.empty_like(y)
+        N.check(N.lib().mh_square_sum_backward(N.ptr(y), N.ptr(g.contiguous()), rows, cols, N.ptr(dy),
+                                               N.stream_of(y.device)), "mh_square_sum_backward")
+        return dy
+
+
 class StochaHead(torch.autograd.Function):
     """[mean | log_std] -> [mean | exp(clamp(log_std, lo, hi))] (StochaPolicy.forward, mlp.py:132-136)
     as one launch forward and one backward (mh_stocha_head[_backward], csrc/dist_kernels.hip)."""

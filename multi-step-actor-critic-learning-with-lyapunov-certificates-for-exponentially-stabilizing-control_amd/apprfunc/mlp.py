@@ -8,7 +8,7 @@ import torch.nn as nn
 
 from ..utils.act_distribution_cls import Action_Distribution_Cls
 from ..utils.common_utils import get_activation_func
-from ._fused import MLP, StochaHead
+from ._fused import MLP, SquareSum, StochaHead
 
 
 def mlp(sizes, activation, output_activation=nn.Identity):
@@ -56,7 +56,10 @@ class LyapunovValue(nn.Module):
         self.lya = mlp([kw["input_dim"]] + list(kw["hidden_sizes"]) + [kw["output_dim"]], *_acts(kw))
 
     def forward(self, input_obs):
-        return torch.pow(self.lya(input_obs), 2).sum(dim=-1, keepdim=True).squeeze(-1)
+        y = self.lya(input_obs)
+        if y.is_cuda and y.dtype == torch.float32:
+            return SquareSum.apply(y)  # one launch each way (apprfunc/_fused.py)
+        return torch.pow(y, 2).sum(dim=-1, keepdim=True).squeeze(-1)
 
 
 class ActionValueDistri(nn.Module):

@@ -606,6 +606,19 @@ int mh_policy_head_backward(const float* raw, const float* eps, const float* old
   return MH_OK;
 }
 
+int mh_square_sum(const float* y, int64_t rows, int32_t cols, float* out, void* stream) {
+  if (rows < 0 || cols <= 0 || (rows > 0 && (!y || !out))) return fail(MH_EINVAL, "mh_square_sum: bad argument");
+  MH_HIP(mh::launch_square_sum(y, rows, cols, out, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_square_sum_backward(const float* y, const float* g, int64_t rows, int32_t cols, float* dy, void* stream) {
+  if (rows < 0 || cols <= 0 || (rows > 0 && (!y || !g || !dy)))
+    return fail(MH_EINVAL, "mh_square_sum_backward: bad argument");
+  MH_HIP(mh::launch_square_sum_bwd(y, g, rows, cols, dy, (hipStream_t)stream));
+  return MH_OK;
+}
+
 int mh_head_backward_workspace(int64_t rows, int32_t n_out, int32_t n_in, int64_t* floats_out) {
   if (!floats_out || rows < 0 || n_out <= 0 || n_out > 16 || n_in <= 0)
     return fail(MH_EINVAL, "mh_head_backward_workspace: bad argument");

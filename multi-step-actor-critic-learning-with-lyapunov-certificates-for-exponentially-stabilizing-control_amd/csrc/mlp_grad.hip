@@ -250,6 +250,53 @@ hipError_t launch_head_backward(const float* dy, const float* x, const float* W,
   return hipGetLastError();
 }
 
+// LyapunovValue's V = sum_j y_j^2 over each row (RL/apprfunc/mlp.py: torch.pow(y, 2).sum(-1)) and
+// its backward dy = g * (2 y) (pow's backward, bit for bit): one wave per row, a float4 per lane
+// per 256-wide chunk, butterfly sum (replaces the pow and reduce launches and their two
+// backward launches).
+__global__ __launch_bounds__(256) void k_square_sum(const float* __restrict__ y, int64_t rows, int cols,
+                                                    float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float* yr = y + r * cols;
+  float acc = 0.0f;
+  for (int c0 = 0; c0 < cols; c0 += 256) {
+    const int c = c0 + 4 * lane;
+    if (c + 3 < cols && (cols & 3) == 0) {
+      const float4 v = *reinterpret_cast<const float4*>(yr + c);
+      acc = acc + v.x * v.x;
+      acc = acc + v.y * v.y;
+      acc = acc + v.z * v.z;
+      acc = acc + v.w * v.w;
+    } else {
+      for (int u = 0; u < 4; ++u)
+        if (c + u < cols) acc = acc + yr[c + u] * yr[c + u];
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
+  if (lane == 0) out[r] = acc;
+}
+__global__ __launch_bounds__(256) void k_square_sum_bwd(const float* __restrict__ y, const float* __restrict__ g,
+                                                        int64_t rows, int cols, float* __restrict__ dy) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * cols) return;
+  dy[i] = g[i / cols] * (2.0f * y[i]);
+}
+
+hipError_t launch_square_sum(const float* y, int64_t rows, int cols, float* out, hipStream_t st) {
+  if (rows <= 0) return hipSuccess;
+  k_square_sum<<<(unsigned)((rows + 3) / 4), 256, 0, st>>>(y, rows, cols, out);
+  return hipGetLastError();
+}
+hipError_t launch_square_sum_bwd(const float* y, const float* g, int64_t rows, int cols, float* dy, hipStream_t st) {
+  const int64_t n = rows * cols;
+  if (n <= 0) return hipSuccess;
+  k_square_sum_bwd<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(y, g, rows, cols, dy);
+  return hipGetLastError();
+}
+
 int act_grad_chunks(int64_t M) { return (int)((M + AG_ROWS - 1) / AG_ROWS); }
 
 int act_grad_tickets(int N) { return (N + AG_COLS - 1) / AG_COLS; }

@@ -124,3 +124,21 @@ def test_head_backward_matches_float64(rows, n_out, n_in, need):
     again = _head_backward(dy, x, w, *need)
     for a, b in zip(out[:3], again[:3]):
         assert a is None or torch.equal(a, b)
+
+
+@pytest.mark.parametrize("rows,cols", [(10240, 256), (5376, 256), (77, 33), (1, 4)])
+def test_square_sum_matches_torch(rows, cols):
+    """mh_square_sum[_backward] (LyapunovValue's torch.pow(y, 2).sum(-1)): the value within f32
+    summation-order rounding of torch's, the gradient bit-identical to pow's backward."""
+    from msacl_amd.apprfunc._fused import SquareSum
+    g = torch.Generator(device="cuda").manual_seed(rows + cols)
+    y = torch.randn(rows, cols, device="cuda", generator=g)
+    up = torch.randn(rows, device="cuda", generator=g)
+    a, b = y.clone().requires_grad_(True), y.clone().requires_grad_(True)
+    out = SquareSum.apply(a)
+    ref = torch.pow(b, 2).sum(dim=-1, keepdim=True).squeeze(-1)
+    _check(out, (y.double() ** 2).sum(-1), (y.double() ** 2).sum(-1), cols)
+    torch.testing.assert_close(out, ref, rtol=1e-6, atol=1e-6)
+    out.backward(up)
+    ref.backward(up)
+    assert torch.equal(a.grad, b.grad)
