@@ -37,6 +37,7 @@ def parse():
                    help="init: PyTorch default init (SURVEY 8d); hover: action mean [mg,0,0,0], long episodes")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="per CPU-baseline leg (1x4 threads, Px1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-4m", action="store_true", help="skip the 4,194,304-env lockstep-kernel measurement")
     p.add_argument("--no-twin-streams", action="store_true",
                    help="alg_twin_streams off: q1 / q2 branches of the update on one stream (A/B)")
     p.add_argument("--overlap", action="store_true",
@@ -245,6 +246,22 @@ def main():
                                      "vs_f32_mfma_peak": round(flops / t_pol / 1e12 / PEAK_F32_MFMA_TFS, 4),
                                      "note": "per lockstep step; f32-accurate split-f16 MFMA (3 products per f32 "
                                              "product): bound by the f16 MFMA rate, not HBM; flops = f32-equivalent"}
+    # the same lockstep kernel over 4,194,304 envs (SURVEY 8(d)'s second size): its 2.4 GB of state,
+    # observations and ring records exceed the 256 MB Infinity Cache, so this fraction is HBM's
+    # (at 65,536 envs the 37 MB working set is cache-resident)
+    if not a.no_4m and a.env == "QuadTracking" and world == 1:
+        import contextlib
+        import io
+        from tools.kernel_bench import bench_rollout
+        with contextlib.redirect_stdout(io.StringIO()):  # (kernel_bench prints its rows)
+            rows4 = bench_rollout(a.env, 4_194_304, reps, dev)
+        r4 = [r for r in rows4 if r["kernel"] == "rollout_step"]
+        if r4:
+            r4 = r4[0]
+            kernels["rollout_step_4m"] = {"avg_us": r4["avg_us"], "env_steps": r4["env_steps"],
+                                          "bytes": r4["env_steps"] * r4["bytes_per_unit"], "GBps": r4["GBps"],
+                                          "frac": r4["frac"],
+                                          "note": "k_rollout<QuadTracking> at 4,194,304 envs (beyond the Infinity Cache)"}
     dom = "rollout_emit"
     ach = kernels[dom]["GBps"]
     # HBM bytes per launch: PMC counters cannot be read from inside this process (rocprofv3 --pmc
@@ -262,6 +279,8 @@ def main():
             traffic = None
     roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_source": traffic_src}
+    if "rollout_step_4m" in kernels:
+        roof["frac_4m_envs"] = kernels["rollout_step_4m"]["frac"]
 
     out = {
         "metric": "env steps/sec (whole node), QuadrotorTracking 65536 envs, 1/2/4/8 MI355X",
