@@ -86,6 +86,9 @@ class ApproxContainer(nn.Module):
         return self.policy.get_act_dist_cls(logits)
 
 
+_UNSET = object()
+
+
 def _stacked(a, b):
     """torch.cat([a, b], 0), as a view when b directly follows a in one buffer (the replayed
     update's static inputs)."""
@@ -300,6 +303,7 @@ class MSACL:
         self._scratch = {}
         self.last_priority = None
         self._neg_one = torch.tensor(-1.0, device=self.device)
+        self._head_cache = _UNSET
         self._one = torch.tensor(1.0, device=self.device)
         self._alpha_grad = None
         self.use_graph = bool(kwargs.get("alg_use_graph", True))
@@ -322,7 +326,7 @@ class MSACL:
     def _head(self):
         """(high, low, log_std lo, hi) when the fused policy head applies (HIP float32 StochaPolicy
         MLP + TanhGaussDistribution with A <= 8, ActionValue critics), else None."""
-        if getattr(self, "_head_cache", 0) != 0:
+        if self._head_cache is not _UNSET:
             return self._head_cache
         from ..apprfunc.mlp import ActionValue, StochaPolicy
         from ..utils.act_distribution_cls import TanhGaussDistribution
@@ -475,19 +479,19 @@ class MSACL:
         loss_policy = entropy = None
         if not do_policy:
             return loss_q, q1_mean, q2_mean, loss_lya, loss_policy, entropy
-        if do_policy:
-            # data parallel: the policy and alpha gradients share one all-reduce (the alpha loss
-            # reads the policy forward's entropy, not the stepped policy), then both steps
-            merge = self._segmented() and self.auto_alpha
-            for k in range(self.policy_frequency):
-                loss_policy, entropy = self._policy_update(data=data, defer_step=merge, reuse_adv=k > 0)
-                if self.auto_alpha:
-                    self._alpha_update(entropy=entropy, defer_step=merge)
-                if merge:
-                    nets = self.networks
-                    D.allreduce_grads(list(nets.policy.parameters()) + [nets.log_alpha])
-                    nets.policy_optimizer.step()
-                    self._alpha_step()
+        # data parallel: the policy and alpha gradients share one all-reduce (the alpha loss reads
+        # the policy forward's entropy, not the stepped policy), then both steps
+        merge = self._segmented() and self.auto_alpha
+        for k in range(self.policy_frequency):
+            loss_policy, entropy = self._policy_update(data=data, defer_step=merge, reuse_adv=k > 0)
+            if self.auto_alpha:
+                self._alpha_update(entropy=entropy, defer_step=merge)
+            if merge:
+                nets = self.networks
+                D.allreduce_grads(list(nets.policy.parameters()) + [nets.log_alpha])
+                nets.policy_optimizer.step()
+                self._alpha_step()
+        # the logged scalars (msacl.py:211-222), stacked inside the update (model_update snapshots them)
         tb = torch.stack([entropy, self.networks.log_alpha.detach().exp(), q1_mean, q2_mean, loss_q, loss_lya,
                           loss_policy])
         return loss_q, q1_mean, q2_mean, loss_lya, loss_policy, entropy, tb
