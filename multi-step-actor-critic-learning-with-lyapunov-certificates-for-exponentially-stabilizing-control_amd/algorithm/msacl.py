@@ -204,6 +204,7 @@ class _PolicyObjective(torch.autograd.Function):
         ctx.s, ctx.shape = s, (B, n)
         entropy = out[1]
         ctx.mark_non_differentiable(entropy)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the entropy (a fill launch)
         return out[2], entropy
 
     @staticmethod

@@ -46,15 +46,29 @@ _GEMM_BACKEND = {"name": "auto"}
 _COLSUM_TICKETS = {}
 
 
+_TICKET_POOL = {}
+
+
 def _colsum_tickets(dev, cols):
     """Arrival counters of mh_act_grad_colsum's in-launch bias-gradient finish, one set per
     (device, stream): zeroed once, left zero by every launch, never shared by launches that can
-    run concurrently (the MSACL update runs two streams)."""
+    run concurrently (the MSACL update runs several streams). Sets are slices of one per-device
+    pool zeroed at its first use, so a stream first seen inside a graph capture (torch captures
+    on its own stream) adds no zero-fill node to the replayed graph."""
     need = (cols + 63) // 64
     key = (dev, torch.cuda.current_stream(dev).cuda_stream)
     t = _COLSUM_TICKETS.get(key)
     if t is None or t.numel() < need:
-        t = torch.zeros(max(need, 64), dtype=torch.int32, device=dev)
+        width = max(need, 64)
+        pool = _TICKET_POOL.get(dev)
+        if pool is None:
+            pool = _TICKET_POOL[dev] = [torch.zeros(64 * 256, dtype=torch.int32, device=dev), 0]
+        buf, used = pool
+        if used + width <= buf.numel():
+            t = buf[used:used + width]
+            pool[1] = used + width
+        else:  # pool exhausted (many streams or very wide layers): a set of its own
+            t = torch.zeros(width, dtype=torch.int32, device=dev)
         _COLSUM_TICKETS[key] = t
     return t
 _WS = {}
