@@ -277,6 +277,11 @@ int mh_policy_head_backward(const float* raw, const float* eps, const float* old
                             const float* low, const float* d_xq, const float* d_new_logp, const float* d_old_logp,
                             int64_t rows, int32_t A, int32_t D, float log_std_lo, float log_std_hi, float* d_raw,
                             void* stream);
+/* Input gradient of y = act(x W^T + b) for a narrow input (n_in <= 32, n_out <= 1024) when no
+ * weight / bias gradient is wanted (a frozen critic's first layer): dx = (dy * act'(y)) W with the
+ * activation derivative formed on the fly. Row-major contiguous dy, y [rows][n_out], W [n_out][n_in]. */
+int mh_dx_narrow(const float* dy, const float* y, int32_t act, const float* W, int64_t rows, int32_t n_out,
+                 int32_t n_in, float* dx, void* stream);
 /* LyapunovValue's V = sum_j y[r][j]^2 per row (RL/apprfunc/mlp.py, torch.pow(y, 2).sum(-1)) and its
  * backward dy = g[r] * (2 y) (the pow backward's bits). Row-major contiguous y [rows][cols]. */
 int mh_square_sum(const float* y, int64_t rows, int32_t cols, float* out, void* stream);

@@ -232,6 +232,16 @@ class LinearAct(torch.autograd.Function):
             head = _head_backward(dy, x, weight, need_x, need_w, need_b)
             if head is not None:
                 return head
+        if (need_x and not need_w and not need_b and _FUSED_BACKWARD["on"] and _GEMM_BACKEND["name"] != "blas"
+                and x.shape[1] <= 32 and dy.shape[0] >= 1024 and dy.shape[1] <= 1024):
+            # narrow input, input gradient only (a frozen critic's first layer): one launch
+            N = _native()
+            rows, n_out = dy.shape
+            dx = torch.empty(rows, x.shape[1], dtype=dy.dtype, device=dy.device)
+            N.check(N.lib().mh_dx_narrow(N.ptr(dy), N.ptr(y.contiguous()) if act else None, act,
+                                         N.ptr(weight.contiguous()), rows, n_out, x.shape[1], N.ptr(dx),
+                                         N.stream_of(dy.device)), "mh_dx_narrow")
+            return dx, None, None, None
         if _FUSED_BACKWARD["on"]:
             fused = _linear_backward_fused(dy, y, act, x, weight, need_x, need_w, need_b)
             if fused is not None:

@@ -606,6 +606,15 @@ int mh_policy_head_backward(const float* raw, const float* eps, const float* old
   return MH_OK;
 }
 
+int mh_dx_narrow(const float* dy, const float* y, int32_t act, const float* W, int64_t rows, int32_t n_out,
+                 int32_t n_in, float* dx, void* stream) {
+  if (act < 0 || act > 2 || rows < 0 || n_out <= 0 || n_out > 1024 || n_in <= 0 || n_in > 32)
+    return fail(MH_EINVAL, "mh_dx_narrow: bad shape");
+  if (rows > 0 && (!dy || !W || !dx || (act != 0 && !y))) return fail(MH_EINVAL, "mh_dx_narrow: null pointer");
+  MH_HIP(mh::launch_dx_narrow(dy, y, act, W, rows, n_out, n_in, dx, (hipStream_t)stream));
+  return MH_OK;
+}
+
 int mh_square_sum(const float* y, int64_t rows, int32_t cols, float* out, void* stream) {
   if (rows < 0 || cols <= 0 || (rows > 0 && (!y || !out))) return fail(MH_EINVAL, "mh_square_sum: bad argument");
   MH_HIP(mh::launch_square_sum(y, rows, cols, out, (hipStream_t)stream));

@@ -297,6 +297,54 @@ hipError_t launch_square_sum_bwd(const float* y, const float* g, int64_t rows, i
   return hipGetLastError();
 }
 
+// Input gradient of a layer with a narrow input (n_in <= DN_MAX_IN: the MLPs' first layers, e.g.
+// a frozen critic's [obs | act] input in the policy step) when no weight / bias gradient is wanted:
+// dx[r][c] = sum_j dy[r][j] act'(y[r][j]) W[j][c], act' formed on the fly (replaces the colsum
+// pass writing g and the library GEMM reading it back). Workgroup = DN_ROWS rows: g rows and W
+// staged in LDS (16-byte loads), thread = (row, input column), the n_out products summed in j order.
+constexpr int DN_MAX_IN = 32;
+constexpr int DN_ROWS = 16;
+__global__ __launch_bounds__(256) void k_dx_narrow(const float* __restrict__ dy, const float* __restrict__ y,
+                                                   int act, const float* __restrict__ W, int64_t M, int n_out,
+                                                   int n_in, float* __restrict__ dx) {
+  extern __shared__ float sm[];
+  float* sg = sm;                    // [DN_ROWS][n_out]
+  float* sw = sm + DN_ROWS * n_out;  // [n_out][n_in]
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * DN_ROWS;
+  const int nr = M - r0 < DN_ROWS ? (int)(M - r0) : DN_ROWS;
+  for (int q = tid; q < DN_ROWS * n_out; q += 256) {
+    const int r = q / n_out;
+    float g = 0.0f;
+    if (r < nr) {
+      const int64_t i = r0 * n_out + q;
+      const float d = dy[i];
+      g = d;
+      if (act == 1) g = y[i] > 0.0f ? d : 0.0f;
+      else if (act == 2) { const float t = y[i]; g = d * (1.0f - t * t); }
+    }
+    sg[q] = g;
+  }
+  for (int q = tid; q < n_out * n_in; q += 256) sw[q] = W[q];
+  __syncthreads();
+  for (int q = tid; q < nr * n_in; q += 256) {
+    const int r = q / n_in, c = q - r * n_in;
+    const float* gr = sg + r * n_out;
+    float acc = gr[0] * sw[c];
+    for (int j = 1; j < n_out; ++j) acc = acc + gr[j] * sw[j * n_in + c];
+    dx[(r0 + r) * n_in + c] = acc;
+  }
+}
+
+hipError_t launch_dx_narrow(const float* dy, const float* y, int act, const float* W, int64_t M, int n_out,
+                            int n_in, float* dx, hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (n_in <= 0 || n_in > DN_MAX_IN || n_out <= 0 || n_out > 1024) return hipErrorInvalidValue;
+  const size_t shm = sizeof(float) * ((size_t)DN_ROWS * n_out + (size_t)n_out * n_in);
+  k_dx_narrow<<<(unsigned)((M + DN_ROWS - 1) / DN_ROWS), 256, shm, st>>>(dy, y, act, W, M, n_out, n_in, dx);
+  return hipGetLastError();
+}
+
 int act_grad_chunks(int64_t M) { return (int)((M + AG_ROWS - 1) / AG_ROWS); }
 
 int act_grad_tickets(int N) { return (N + AG_COLS - 1) / AG_COLS; }

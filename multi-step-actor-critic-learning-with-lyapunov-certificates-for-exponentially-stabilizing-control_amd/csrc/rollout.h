@@ -140,6 +140,8 @@ hipError_t launch_policy_head_bwd(const float* raw, const float* eps, const floa
                                   hipStream_t st);
 int64_t head_backward_workspace(int64_t M, int n_out, int n_in);
 hipError_t launch_square_sum(const float* y, int64_t rows, int cols, float* out, hipStream_t st);
+hipError_t launch_dx_narrow(const float* dy, const float* y, int act, const float* W, int64_t M, int n_out,
+                            int n_in, float* dx, hipStream_t st);
 hipError_t launch_square_sum_bwd(const float* y, const float* g, int64_t rows, int cols, float* dy, hipStream_t st);
 hipError_t launch_head_backward(const float* dy, const float* x, const float* W, int64_t M, int n_out, int n_in,
                                 float* dx, float* dw, float* db, float* workspace, hipStream_t st);

@@ -142,3 +142,16 @@ def test_square_sum_matches_torch(rows, cols):
     out.backward(up)
     ref.backward(up)
     assert torch.equal(a.grad, b.grad)
+
+
+@pytest.mark.parametrize("rows,n_in,n_out", [(5120, 16, 256), (5120, 12, 256), (1031, 32, 100), (2048, 1, 7)])
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_dx_narrow_matches_float64(rows, n_in, n_out, act):
+    """mh_dx_narrow (input gradient only of a narrow-input layer, act' on the fly) against float64."""
+    x, w, y, dy = _case(rows, n_in, n_out, act, rows + n_in + n_out + act)
+    dx = torch.empty(rows, n_in, device="cuda")
+    N.check(N.lib().mh_dx_narrow(N.ptr(dy), N.ptr(y), act, N.ptr(w), rows, n_out, n_in, N.ptr(dx),
+                                 N.stream_of(dy.device)), "mh_dx_narrow")
+    yd = y.double()
+    gd = dy.double() * ((yd > 0).double() if act == 1 else (1 - yd * yd) if act == 2 else 1.0)
+    _check(dx, gd @ w.double(), gd.abs() @ w.double().abs(), n_out)
