@@ -90,10 +90,10 @@ def _tall(rows, n, k):
 
 def _hip_forward(rows, out_features, act=0, in_features=0):
     b = _GEMM_BACKEND["name"]
-    # tanh layers with a short K: the epilogue saves the library path's separate tanh launch
-    # (first layers, K <= 32 over >= 256 rows: mh_gemm_f32's short-K kernel)
+    # tanh layers with a short K: the epilogue saves the library path's separate tanh launch.
+    # ReLU first layers (K <= 32) stay on the library: its fused addmm+relu beats mh_gemm_f32's
+    # short-K kernel there (5.1 vs 9.0 us at 5,120 x 256 x 16, tools/gemm_shapes.py)
     return b == "hip" or (b == "auto" and (rows <= 1024 or out_features == 1 or (act == 2 and in_features <= 64)
-                                           or (in_features <= 32 and out_features >= 64)
                                            or _tall(rows, out_features, in_features)))
 
 
