@@ -555,25 +555,27 @@ __global__ __launch_bounds__(1024) void k_policy_scales(const float* __restrict_
     const float4 x = reinterpret_cast<const float4*>(W2 + (int64_t)row * PM_H)[lane];
     const float a = fabsf(x.x), b = fabsf(x.y), c = fabsf(x.z), d = fabsf(x.w);
     float m2 = fmaxf(fmaxf(a, b), fmaxf(c, d)), s2 = (a + b) + (c + d);
+    // hidden unit `row`: its W1 row on lanes j < D, its W3 column on lanes 32 + o, o < N3 — one
+    // load per lane, all in flight together (a serial per-element loop on one lane waited out
+    // ~40 L2 latencies per wave: 12 us for the kernel)
+    const int j = lane & 31;
+    const float u1 = lane < 32 && j < D ? fabsf(W1[(int64_t)row * D + j]) : 0.0f;
+    const float u3 = lane >= 32 && j < N3 ? fabsf(W3[(int64_t)j * PM_H + row]) : 0.0f;
+    float m1 = u1, r1 = u1, m3 = u3;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       m2 = fmaxf(m2, __shfl_xor(m2, off, 64));
       s2 += __shfl_xor(s2, off, 64);
+      m1 = fmaxf(m1, __shfl_xor(m1, off, 64));
+      r1 += __shfl_xor(r1, off, 64);
+      m3 = fmaxf(m3, __shfl_xor(m3, off, 64));
     }
+    const float bb = fabsf(b1[row]);
+    v[0] = fmaxf(v[0], fmaxf(m1, bb));
     v[1] = fmaxf(v[1], m2);
+    v[2] = fmaxf(v[2], m3);
+    v[3] = fmaxf(v[3], r1 + bb);
     v[4] = fmaxf(v[4], s2 + fabsf(b2[row]));
-    if (lane == 0) {  // hidden unit `row`: row of W1 (+ b1) and column of W3
-      float m1 = fabsf(b1[row]), r1 = m1, m3 = 0.0f;
-      for (int j = 0; j < D; ++j) {
-        const float u = fabsf(W1[(int64_t)row * D + j]);
-        m1 = fmaxf(m1, u);
-        r1 += u;
-      }
-      for (int o = 0; o < N3; ++o) m3 = fmaxf(m3, fabsf(W3[(int64_t)o * PM_H + row]));
-      v[0] = fmaxf(v[0], m1);
-      v[2] = fmaxf(v[2], m3);
-      v[3] = fmaxf(v[3], r1);
-    }
   }
 #pragma unroll
   for (int q = 0; q < 5; ++q)

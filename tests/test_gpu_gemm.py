@@ -42,6 +42,8 @@ SHAPES = [  # (M, N, K)
     (5120, 256, 12), (5120, 64, 4), (3001, 128, 20), (2048, 192, 36), (4100, 256, 256),
     # short-K products (k_gemm_shortk: op(A) = A, op(B) = B^T, K <= 32)
     (10240, 256, 12), (5376, 256, 16), (300, 100, 32), (257, 64, 1), (1000, 130, 7),
+    # more short-K shapes: several 64-column tiles, ragged last tile
+    (700, 300, 20), (3000, 512, 5), (9000, 256, 28),
 ]
 
 
@@ -60,6 +62,22 @@ def test_gemm_matches_f64(M, N, K, ta, tb):
     err = (c.double() - ref).abs()
     tol = 2e-6 * (K ** 0.5) * mag + 1e-6
     assert bool((err <= tol).all()), f"max err {float(err.max()):.3e}"
+
+
+@pytest.mark.parametrize("lda_pad,a_off,act", [(0, 0, 2), (4, 0, 1), (3, 0, 0), (0, 1, 2), (4, 4, 2)])
+def test_shortk_strided_and_offset_operands(lda_pad, a_off, act):
+    """Short-K path (K <= 32, op(B) = B^T) on views: padded leading dimensions (float4 row loads
+    only when lda % 4 == 0 and A is 16-byte aligned) and a misaligned start."""
+    g = torch.Generator(device="cuda").manual_seed(17 + lda_pad + 5 * a_off + act)
+    M, N, K = 5120, 256, 12
+    abuf = torch.randn(M * (K + lda_pad) + a_off, device="cuda", generator=g)
+    a = abuf[a_off:].reshape(M, K + lda_pad)[:, :K]
+    b = torch.randn(N, K, device="cuda", generator=g)
+    bias = torch.randn(N, device="cuda", generator=g)
+    c = gemm(abuf[a_off:], b, bias, M, N, K, K + lda_pad, K, 0, 1, act)  # pointer + lda (a 1-D view)
+    ref, mag = _ref(a.contiguous(), b, bias, 0, 1, act)
+    err = (c.double() - ref).abs()
+    assert bool((err <= 2e-6 * (K ** 0.5) * mag + 1e-6).all()), f"max err {float(err.max()):.3e}"
 
 
 def test_gemm_weight_gradient_form_is_deterministic():
