@@ -84,7 +84,10 @@ def cpu_baseline(env_name, seconds):
         ratio = float(cal[key]["ratio_reference_over_restatement"])
         out["reference_equivalent_value"] = round(out["value"] * ratio, 1)
         out["calibration"] = {"ratio_reference_over_restatement": ratio, "source": "profiles/r02_cpu_ratio.json",
-                              "measured": f"{cal['env']}, {cal['envs_per_process']} envs/process, {key}, build container"}
+                              "measured": f"{cal['env']}, {cal['envs_per_process']} envs/process, {key}, build container",
+                              "calibration_cpu": cal["host"].get("model"),
+                              "note": "ratio measured on the build container's CPU (the reference cannot run on "
+                                      "the GPU box), applied to this host's CPU: a cross-CPU estimate"}
     except (OSError, ValueError, StopIteration, KeyError):
         out["calibration"] = None
     return out
@@ -272,9 +275,15 @@ def main():
     pmc_path = os.path.join(ROOT, "profiles", PMC_TRAFFIC)
     if a.env == "QuadTracking" and a.envs == 65536 and os.path.exists(pmc_path):
         try:
-            traffic = json.load(open(pmc_path)).get(dom, {}).get("bytes_per_launch")
-            traffic = None if traffic is None else round(float(traffic), 1)
-            traffic_src = f"profiles/{PMC_TRAFFIC} (rocprofv3 --pmc passes of this bench command; not measured live)"
+            from tools.kernel_hash import rollout_sources_sha
+            pmc = json.load(open(pmc_path))
+            if pmc.get("rollout_sources_sha") == rollout_sources_sha():
+                traffic = pmc.get(dom, {}).get("bytes_per_launch")
+                traffic = None if traffic is None else round(float(traffic), 1)
+                traffic_src = (f"profiles/{PMC_TRAFFIC} (rocprofv3 --pmc passes of this bench command on the same "
+                               f"kernel sources, sha {pmc['rollout_sources_sha']}; not measured live)")
+            else:  # the kernel changed since the PMC passes: no stale figure
+                traffic_src = f"profiles/{PMC_TRAFFIC} is for other kernel sources (stale): not reported"
         except (OSError, ValueError):
             traffic = None
     roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",

@@ -154,6 +154,16 @@ int mh_env_set_reward_cost_scale(mh_env_t h, float reward_scale, float cost_scal
  * (a device RNG write, capturable). NULL disables. Ignored for injected actions. */
 int mh_env_set_action_noise(mh_env_t h, const float* noise);
 
+/* Per-env step trace of every later mh_rollout_step / mh_rollout_step_deferred of this handle,
+ * in the SAME kernel instantiation the call would run anyway (the sampling one when logits are
+ * given): the pre-reset observation [E][D] (SyncVectorEnv info["final_observation"], the
+ * `real_next_obs` of base.py:156-160), the env's raw float32 reward [E] (before reward_scale),
+ * and terminated / truncated [E] (u8) — the values gymnasium's step returns to
+ * BaseSampler._n_step (base.py:148). DEVICE pointers owned by the caller; any may be NULL;
+ * all NULL switches the trace off. Used by the parity tests of the benchmarked sampler path. */
+int mh_rollout_set_trace(mh_env_t h, float* real_next_obs, float* reward, uint8_t* terminated,
+                         uint8_t* truncated);
+
 /* On-policy trajectory store = OnSampler's mini-batch arrays (RL/trainer/sampler/
  * on_sampler.py:22-41), env-major exactly as the reference's numpy arrays:
  * obs/obs2 [E][horizon][obs_dim], act [E][horizon][act_dim], rew/cost/logp [E][horizon] float32,

@@ -82,6 +82,7 @@ _PROTOS = {
     "mh_nstep_set_log_std_clamp": (ctypes.c_int, [c_vp, c_i32, c_f32, c_f32]),
     "mh_env_set_reward_cost_scale": (ctypes.c_int, [c_vp, c_f32, c_f32]),
     "mh_env_set_action_noise": (ctypes.c_int, [c_vp, c_vp]),
+    "mh_rollout_set_trace": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mh_rollout_traj_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(TrajStore), c_i32,
                                             c_vp, c_vp, c_vp]),
     "mh_policy_packed_size": (ctypes.c_int, [c_i32, ctypes.POINTER(c_i64)]),

@@ -17,6 +17,8 @@ it out of the create_alg registry, RL/create_pkg/create_alg.py:38-47).
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 from torch.optim import Adam
 
@@ -128,13 +130,38 @@ def fused_adam(params, lr):
         return HipAdam(params, lr=lr)
 
 
+def release_graph(g) -> None:
+    """Free a captured update's graph(s) now (torch CUDAGraph or utils/dist.py GraphSegments)."""
+    if g is not None:
+        g.reset()  # CUDAGraph.reset / GraphSegments.reset
+
+
 class UpdateGraph:
     def __init__(self, body, enabled=True):
-        self.body = body
+        # the owner's bound method held weakly: an algorithm and its UpdateGraph form no reference
+        # cycle, so a dropped algorithm frees its graphs at once (refcount), never later inside
+        # the garbage collector (which may run during another pipeline's capture)
+        self._body = weakref.WeakMethod(body) if hasattr(body, "__self__") else (lambda b=body: b)
         self.enabled = enabled
         self._static = None
         self._shapes = None
         self._graphs = {}
+        self._warm = set()
+
+    @property
+    def body(self):
+        b = self._body()
+        if b is None:
+            raise RuntimeError("UpdateGraph: its algorithm was released")
+        return b
+
+    def close(self):
+        """Release every captured graph and the static inputs (idempotent)."""
+        graphs, self._graphs = self._graphs, {}
+        for g, _outs in graphs.values():
+            release_graph(g)
+        self._static = None
+        self._shapes = None
         self._warm = set()
 
     def usable(self):

@@ -320,6 +320,20 @@ class MSACL:
         self._graphs = {}
         self._warm = set()
 
+    def close(self):
+        """Release the captured update graphs, their static inputs, the scratch buffers and the
+        side streams now, deterministically (idempotent). A dropped MSACL is freed by refcount
+        anyway (it sits in no reference cycle); close() also frees it while it is still referenced."""
+        from ._update_graph import release_graph
+        graphs, self._graphs = self._graphs, {}
+        for g, _outs, _prio in graphs.values():
+            release_graph(g)
+        self._static = self._static_shapes = None
+        self._warm = set()
+        self._scratch = {}
+        self.last_priority = None
+        self._twin = self._side = None
+
     @property
     def adjustable_parameters(self):
         return ("gamma", "tau", "auto_alpha", "alpha", "target_entropy", "policy_frequency", "target_network_frequency")
@@ -383,9 +397,6 @@ class MSACL:
             # the caller reads the dict (the trainer: on logging iterations), so an update leaves
             # no host sync behind and the next sampling is enqueued while it still runs
             tb_info = LazyTbInfo(outs[-1].clone(), start)
-        if self.per_flag:
-            return tb_info, data.get("idx"), self.last_priority
-        return tb_info
         if self.per_flag:
             return tb_info, data.get("idx"), self.last_priority
         return tb_info

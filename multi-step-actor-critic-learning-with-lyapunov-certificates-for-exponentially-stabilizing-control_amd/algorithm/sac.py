@@ -72,6 +72,10 @@ class SAC:
         self.target_network_frequency = target_network_frequency
         self._graph = UpdateGraph(self._update_body, enabled=bool(kwargs.get("alg_use_graph", True)))
 
+    def close(self):
+        """Release the captured update graphs deterministically (idempotent)."""
+        self._graph.close()
+
     @property
     def adjustable_parameters(self):
         return ("gamma", "tau", "alpha", "auto_alpha", "target_entropy")

@@ -74,6 +74,11 @@ struct mh_env_s {
   bool pending = false;
   int parity = 0;                   // half of block_count / emit_list the next step writes
   mh_window_store_t pstore{};       // store the pending windows go to
+  // optional step trace (mh_rollout_set_trace): caller-owned device outputs of every rollout step
+  float* tr_real = nullptr;
+  float* tr_reward = nullptr;
+  uint8_t* tr_term = nullptr;
+  uint8_t* tr_trunc = nullptr;
 
   // optional per-kernel HIP-event timing of mh_rollout_step (bench.py's live roofline)
   bool timing = false;
@@ -316,6 +321,10 @@ static int rollout_impl(mh_env_t h, const float* logits, const float* act_in, co
   a.obs = obs;
   a.act_out = act_out;
   a.logp_out = logp_out;
+  a.real_next_obs = h->tr_real;
+  a.reward_out = h->tr_reward;
+  a.term_out = h->tr_term;
+  a.trunc_out = h->tr_trunc;
   a.ring = h->ring;
   a.ring_len = h->ring_len;
   a.ring_pos = h->ring_pos;
@@ -498,6 +507,16 @@ int mh_env_set_action_noise(mh_env_t h, const float* noise) {
   return MH_OK;
 }
 
+int mh_rollout_set_trace(mh_env_t h, float* real_next_obs, float* reward, uint8_t* terminated,
+                         uint8_t* truncated) {
+  if (!h) return fail(MH_EINVAL, "mh_rollout_set_trace: null handle");
+  h->tr_real = real_next_obs;
+  h->tr_reward = reward;
+  h->tr_term = terminated;
+  h->tr_trunc = truncated;
+  return MH_OK;
+}
+
 int mh_rollout_traj_step(mh_env_t h, const float* logits, const float* act_in, const float* logp_in,
                          const float* reset_states, float* obs, const mh_traj_store_t* traj, int32_t t,
                          float* act_out, float* logp_out, void* stream) {
@@ -638,7 +657,8 @@ int mh_head_backward_workspace(int64_t rows, int32_t n_out, int32_t n_in, int64_
 int mh_head_backward(const float* dy, const float* x, const float* W, int64_t rows, int32_t n_out, int32_t n_in,
                      float* dx, float* dw, float* db, float* workspace, void* stream) {
   if (rows <= 0 || n_out <= 0 || n_out > 16 || n_in <= 0) return fail(MH_EINVAL, "mh_head_backward: bad shape");
-  if (!dy || (dx && !W) || ((dw || db) && !workspace) || (dw && !x) || (db && !dw))
+  // the kernel reads x on every path (dx-only calls included), so x is always required
+  if (!dy || !x || (dx && !W) || ((dw || db) && !workspace) || (db && !dw))
     return fail(MH_EINVAL, "mh_head_backward: null pointer");
   MH_HIP(mh::launch_head_backward(dy, x, W, rows, n_out, n_in, dx, dw, db, workspace, (hipStream_t)stream));
   return MH_OK;

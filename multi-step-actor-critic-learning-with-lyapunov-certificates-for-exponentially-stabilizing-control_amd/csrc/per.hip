@@ -7,7 +7,9 @@
 // Work per call is proportional to what changed, never to the capacity:
 //   mh_per_update   B leaves -> leaf-to-root recompute of their ancestors, one workgroup,
 //                   log2(pow2) barrier-separated levels (O(B log N)). Duplicate leaves in one
-//                   batch resolve to the LAST entry (sequential last-write-wins).
+//                   batch resolve to the LAST entry (sequential last-write-wins), found in
+//                   O(B) with the touched leaf slots as owner tags (atomic max of the entry
+//                   index, then a compare-and-swap of the winner's tag for its priority).
 //   mh_per_set_new  the rows the rollout just appended (a contiguous FIFO arc read from the
 //                   device cursors) get the running max priority; only the 1024-leaf subtrees
 //                   the arc touches are rebuilt (in LDS), then the ~pow2/1024 nodes above them
@@ -15,7 +17,8 @@
 //                   so the launch is graph-capturable); untouched workgroups exit at once.
 //   mh_per_sample   stratified proportional draws; the top 11 tree levels are staged in LDS so
 //                   only the lower levels of each descent go to L2/HBM.
-// No atomics: for given inputs the tree, the indices and the weights are bitwise deterministic.
+// For given inputs the tree, the indices and the weights are bitwise deterministic (the update's
+// owner-tag atomics decide only WHICH entry writes a leaf, always the last one).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -38,38 +41,40 @@ __device__ __forceinline__ double leaf_priority(float td, float alpha, float eps
 __global__ __launch_bounds__(UPD) void k_update(double* tree, int64_t pow2, int log2p, const int64_t* idx,
                                                 const float* prio, int64_t count, float alpha, float eps,
                                                 double* max_prio) {
-  __shared__ int64_t tile[UPD];
   __shared__ int64_t leaves[LEAF_CACHE];
   __shared__ double red[UPD];
   const int tid = threadIdx.x;
   double m = 0.0;
+  // last-write-wins (entry i loses if a later entry names the same leaf), O(count): every
+  // touched leaf slot is about to be overwritten, so it serves as its own owner slot first —
+  // cleared, then the largest entry index + 1 naming it is kept by an L2 atomic max, and the
+  // entry whose index it holds is the winner (one workgroup: barriers order the three passes)
+  unsigned long long* owner = reinterpret_cast<unsigned long long*>(tree + pow2);
+  for (int64_t i = tid; i < count; i += UPD) {
+    const int64_t my = idx[i];
+    if (my >= 0 && my < pow2) atomicExch(owner + my, 0ull);
+  }
+  __threadfence();
+  __syncthreads();
+  for (int64_t i = tid; i < count; i += UPD) {
+    const int64_t my = idx[i];
+    if (my >= 0 && my < pow2) atomicMax(owner + my, (unsigned long long)(i + 1));
+  }
+  __threadfence();
+  __syncthreads();
   for (int64_t c0 = 0; c0 < count; c0 += UPD) {
     const int64_t i = c0 + tid;
     const int64_t my = i < count ? idx[i] : -1;
     const bool valid = my >= 0 && my < pow2;
-    bool winner = valid;
-    // last-write-wins: entry i loses if a later entry j > i names the same leaf
-    for (int64_t t0 = c0; t0 < count; t0 += UPD) {
-      __syncthreads();
-      tile[tid] = t0 + tid < count ? idx[t0 + tid] : -2;
-      __syncthreads();
-      if (winner) {
-        const int lim = (int)(count - t0 < UPD ? count - t0 : UPD);
-        for (int k = (t0 == c0 ? tid + 1 : 0); k < lim; ++k) {
-          if (tile[k] == my) {
-            winner = false;
-            break;
-          }
-        }
-      }
-    }
     if (valid) {
       const double p = leaf_priority(prio[i], alpha, eps);
       m = fmax(m, p);
-      if (winner) tree[pow2 + my] = p;
+      // the winner swaps its own tag for the priority; every other entry's swap fails
+      atomicCAS(owner + my, (unsigned long long)(i + 1), __double_as_longlong(p));
     }
     if (i < LEAF_CACHE && i < count) leaves[i] = valid ? my : -1;
   }
+  __threadfence();
   // ancestors, one level per barrier: every node on a touched path is recomputed from its two
   // children, which are final after the previous level (several entries may share a node; they
   // store the same value)

@@ -987,10 +987,26 @@ void k_policy_forward_x3(const float* __restrict__ P,
       const int64_t b = (t0 + t) * 32 + (lane & 31);
       const float iu = isw3 * pm_pow2(-ex[t][2]);
       if (t0 + t < ntiles && b < E) {
+        if ((N3 & 3) == 0) {
+          // registers 4q..4q+3 are the env's consecutive outputs 8q + 4 (lane >> 5) + 0..3: one
+          // 16-byte store each, so a wave writes its 32 rows as whole lines (4-byte stores at the
+          // row stride wrote every line 4 times: PMC WRITE_SIZE 9.5x the logits' bytes)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int oo = pm_row(r, lane);
-          if (oo < N3) logits[b * N3 + oo] = acc[t][0][r] * iu + b3[oo];
+          for (int q = 0; q < 4; ++q) {
+            const int o0 = 8 * q + 4 * (lane >> 5);
+            if (o0 < N3) {
+              const float4 bb = *reinterpret_cast<const float4*>(b3 + o0);
+              *reinterpret_cast<float4*>(logits + b * N3 + o0) =
+                  make_float4(acc[t][0][4 * q] * iu + bb.x, acc[t][0][4 * q + 1] * iu + bb.y,
+                              acc[t][0][4 * q + 2] * iu + bb.z, acc[t][0][4 * q + 3] * iu + bb.w);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int oo = pm_row(r, lane);
+            if (oo < N3) logits[b * N3 + oo] = acc[t][0][r] * iu + b3[oo];
+          }
         }
       }
     }
@@ -1087,6 +1103,9 @@ static hipError_t launch_fwd_t(const float* P, const float* obs, int64_t E, int 
 hipError_t launch_policy_forward(const float* P, const float* obs, int64_t E, int D, int N3, float* logits,
                                  hipStream_t st) {
   if (E <= 0) return hipSuccess;
+  // rows of 4k logits are stored as 16-byte vectors (and b3 read as such from the packed block)
+  if ((N3 & 3) == 0 && ((reinterpret_cast<uintptr_t>(logits) | reinterpret_cast<uintptr_t>(P)) & 15))
+    return hipErrorInvalidValue;
   switch (D / 2 + 1) {
     case 1: return launch_fwd_t<1>(P, obs, E, D, N3, logits, st);
     case 2: return launch_fwd_t<2>(P, obs, E, D, N3, logits, st);

@@ -85,14 +85,29 @@ class HipVectorEnv:
 
     def close(self):
         if self._h is not None:
-            N.lib().mh_env_destroy(self._h)
-            self._h = None
+            h, self._h = self._h, None
+            _destroy_when_safe(h)
 
     def __del__(self):
         try:
             self.close()
         except Exception:
             pass
+
+
+# Handles released while a HIP graph is being captured (a finaliser run by the garbage collector
+# inside someone else's capture): hipFree is illegal there, so their destruction waits for the
+# next release outside a capture.
+_PENDING = []
+
+
+def _destroy_when_safe(h):
+    capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+    _PENDING.append(h)
+    if capturing:
+        return
+    while _PENDING:
+        N.lib().mh_env_destroy(_PENDING.pop())
 
     def _f32(self, x, cols, name):
         if x is None:

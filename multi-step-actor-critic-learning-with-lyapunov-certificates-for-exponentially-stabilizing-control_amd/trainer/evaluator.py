@@ -36,6 +36,12 @@ class Evaluator:
         self.save_folder = kwargs.get("save_folder")
         self.max_eval_steps = int(kwargs.get("max_eval_steps", 1000))
 
+    def close(self):
+        """Release the evaluation envs' device handle (idempotent)."""
+        close = getattr(self.envs, "close", None)
+        if close is not None:
+            close()
+
     def load_state_dict(self, state_dict):
         self.networks.load_state_dict(state_dict)
 

@@ -169,6 +169,18 @@ class NstepOffSerialTrainer:
             self.buffer.add_batch(samples)
             self.sampler_tb_dict.add_average(tb)
 
+    def close(self):
+        """Release the device resources of the pipeline's parts now (sampler graph + env handle,
+        the algorithm's captured update graphs, the evaluator's envs), deterministically instead
+        of whenever their owners are garbage collected. Idempotent."""
+        fin = getattr(self, "finish_pending", None)
+        if fin is not None:
+            fin()
+        for part in (self.sampler, self.alg, self.evaluator):
+            close = getattr(part, "close", None)
+            if close is not None:
+                close()
+
     def train(self):
         while self.iteration <= self.max_iteration:
             self.step()

@@ -86,6 +86,18 @@ class OnSerialTrainer:
         self.writer.add_scalar(tb_tags["TCS of RL iteration"], cost_std, it)
         self.writer.add_scalar(tb_tags["TCM of total time"], cost_mean, now)
 
+    def close(self):
+        """Release the device resources of the pipeline's parts now (sampler graph + env handle,
+        the algorithm's captured update graphs, the evaluator's envs), deterministically instead
+        of whenever their owners are garbage collected. Idempotent."""
+        fin = getattr(self, "finish_pending", None)
+        if fin is not None:
+            fin()
+        for part in (self.sampler, self.alg, self.evaluator):
+            close = getattr(part, "close", None)
+            if close is not None:
+                close()
+
     def train(self):
         while self.global_iteration < self.max_iteration:
             self.step()

@@ -201,13 +201,14 @@ class HipNstepOffSampler:
         if self._noise is not None:
             self._noise.normal_(self._noise_mean, self._noise_std)
 
-    def _policy_step(self, store, fused=False):
+    def _policy_step(self, store, fused=False, act_out=None, logp_out=None):
         self._draw_noise()
         logits, raw = self._policy_fused() if fused else self._policy_raw()
         pol = self.networks.policy
         N.check(N.lib().mh_nstep_set_log_std_clamp(self._h, int(raw), float(getattr(pol, "min_log_std", -20.0)),
                                                    float(getattr(pol, "max_log_std", 1.0))), "log_std clamp")
-        self._lockstep(store, logits=logits, deferred=self.deferred_emission)
+        self._lockstep(store, logits=logits, deferred=self.deferred_emission, act_out=act_out, logp_out=logp_out)
+        return logits
 
     def _horizon(self, store):
         fused = self._pack_policy()
@@ -250,12 +251,53 @@ class HipNstepOffSampler:
         tb = {tb_tags["sampler_time"]: (time.perf_counter() - t0) * 1000}
         return data, tb
 
+    def close(self):
+        """Release the sampler's device resources now: its captured horizon graph, the packed
+        policy, the staging store and the env handle (mh_env_destroy). Idempotent."""
+        g, self._graph, self._graph_key = self._graph, None, None
+        if g is not None:
+            g.reset()
+        self._packed = self._staging = self._bound = None
+        self.envs.close()
+        self._noise = None
+
     def set_kernel_timing(self, enable: bool):
         """Per-kernel HIP-event timing (runs the horizon eagerly while enabled)."""
         self._timing = bool(enable)
         N.check(N.lib().mh_env_set_timing(self._h, int(enable)), "mh_env_set_timing")
 
     # ------------------------------------------------------------------ parity mode
+    def step_traced(self, act_out, logp_out, trace=None):
+        """One lockstep step of the sampling path itself, eagerly: exactly what one iteration of
+        the sampler's horizon runs (policy forward, then the lockstep kernel with in-kernel
+        TanhGauss sampling, clip, in-kernel resets and deferred emission into the bound store),
+        additionally writing the sampled actions [E, A] and log-probs [E] and, when `trace` =
+        (real_next_obs [E, D], reward [E], terminated u8 [E], truncated u8 [E]) device tensors is
+        given, the env step's outputs (mh_rollout_set_trace). Returns the policy logits.
+        Call flush() after the last step to emit its windows."""
+        N.require_device(act_out, "act_out", torch.float32, self.num_envs * self.envs.act_dim, self.device)
+        N.require_device(logp_out, "logp_out", torch.float32, self.num_envs, self.device)
+        ptrs = [None] * 4
+        if trace is not None:
+            real, rew, term, trunc = trace
+            N.require_device(real, "real_next_obs", torch.float32, self.num_envs * self.envs.obs_dim, self.device)
+            N.require_device(rew, "reward", torch.float32, self.num_envs, self.device)
+            N.require_device(term, "terminated", torch.uint8, self.num_envs, self.device)
+            N.require_device(trunc, "truncated", torch.uint8, self.num_envs, self.device)
+            ptrs = [N.ptr(t) for t in trace]
+        if self._bound is None:
+            raise RuntimeError("step_traced: bind_store(buffer) first (windows go to the bound store)")
+        N.check(N.lib().mh_rollout_set_trace(self._h, *ptrs), "mh_rollout_set_trace")
+        try:
+            with torch.no_grad():
+                return self._policy_step(self._bound, self._pack_policy(), act_out=act_out, logp_out=logp_out)
+        finally:
+            N.check(N.lib().mh_rollout_set_trace(self._h, None, None, None, None), "mh_rollout_set_trace")
+
+    def flush(self):
+        """Emit the windows of the last deferred lockstep step (mh_rollout_flush)."""
+        self._flush()
+
     def step_injected(self, actions, logp, reset_states=None, store=None):
         """One lockstep step with injected (already clipped) actions and log-probs."""
         act = torch.as_tensor(actions, dtype=torch.float32, device=self.device).contiguous()

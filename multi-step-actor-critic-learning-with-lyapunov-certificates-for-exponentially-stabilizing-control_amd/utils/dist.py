@@ -95,6 +95,12 @@ class GraphSegments:
         self.ops.append(op)
         self._begin()
 
+    def reset(self):
+        """Free every captured graph now (idempotent)."""
+        graphs, self.graphs, self.ops = self.graphs, [], []
+        for g in graphs:
+            g.reset()
+
     def replay(self):
         for i, g in enumerate(self.graphs):
             g.replay()
@@ -122,9 +128,13 @@ class capturing:
 
     def __enter__(self):
         self._gc = gc.isenabled()
-        gc.disable()  # as cuda_graph: no collection while a segment captures
         _SEG["active"] = self.seg
-        self.seg._begin()
+        try:
+            self.seg._begin()
+        except BaseException:
+            _SEG["active"] = None
+            raise
+        gc.disable()  # as cuda_graph: no collection while a segment captures (only once it began)
         return self.seg
 
     def __exit__(self, *exc):

@@ -103,6 +103,42 @@ class NStepRollout:
         return windows, dict(real_next_obs=real_next_obs, rew=rew, cost=cost, done=dones, next_obs=next_obs)
 
 
+class NStepWindows:
+    """The `_n_step` deque bookkeeping of NStepRollout (base.py:178-217: per env a
+    deque(maxlen=n); append the step's record; a full deque is emitted oldest-first; the deque is
+    cleared when the newest record is done; emission in env-index order) restated over arrays
+    for 65,536-env parity tests: each env's deque is a ring of n records with a length and a
+    write position. Records are given as the 7 per-step arrays (obs[E,D], act[E,A], rew[E],
+    cost[E], obs2[E,D], done[E], logp[E]); `push` returns the step's windows as 7 arrays
+    [W, n, ...] (W = emitting envs) in WindowStore.KEYS order. tests/test_oracle_windows.py pins
+    it to NStepRollout."""
+
+    def __init__(self, num_envs, n_step, obs_dim, act_dim):
+        self.E, self.n, self.D, self.A = num_envs, n_step, obs_dim, act_dim
+        self.F = 2 * obs_dim + act_dim + 4
+        self.ring = np.zeros((num_envs, n_step, self.F), F32)
+        self.len = np.zeros(num_envs, np.int64)
+        self.pos = np.zeros(num_envs, np.int64)
+
+    def push(self, obs, act, rew, cost, obs2, done, logp):
+        E, n, D, A = self.E, self.n, self.D, self.A
+        rec = np.concatenate([np.asarray(obs, F32).reshape(E, D), np.asarray(act, F32).reshape(E, A),
+                              np.asarray(obs2, F32).reshape(E, D), np.asarray(rew, F32).reshape(E, 1),
+                              np.asarray(cost, F32).reshape(E, 1), np.asarray(done, F32).reshape(E, 1),
+                              np.asarray(logp, F32).reshape(E, 1)], axis=1)
+        env = np.arange(E)
+        self.ring[env, self.pos] = rec
+        self.pos = (self.pos + 1) % n
+        self.len = np.minimum(self.len + 1, n)
+        em = np.nonzero(self.len == n)[0]                   # env-index order
+        slots = (self.pos[em, None] + np.arange(n)[None, :]) % n  # oldest first
+        w = self.ring[em[:, None], slots]                    # [W, n, F]
+        self.len[np.asarray(done, bool).reshape(E)] = 0      # deque.clear()
+        s = 2 * D + A
+        return (w[:, :, :D], w[:, :, D:D + A], w[:, :, s], w[:, :, s + 1], w[:, :, D + A:s], w[:, :, s + 2],
+                w[:, :, s + 3])  # KEYS order: obs, act, rew, cost, obs2, done, logp
+
+
 class WindowStore:
     """NstepReplayBuffer storage (nstep_replay_buffer.py:52-125)."""
 

@@ -19,10 +19,13 @@ Compared (reference = RL/algorithm/msacl.py:174-460 run on CPU in the generator)
     i.e. the device's final moments differ from the reference's by more than 1e-3 relative or,
     after some Adam step so far, the reference's first moment is below 1e-3 of the scale its
     summation-order noise has (_noise_scale) — there lr * m / (sqrt(v) + eps) can flip sign and
-    the difference is bounded by Adam's maximum step instead. Elements that actually moved
-    apart must stay below 0.5 % of each tensor (measured: gpurun_out/msacl_bench_parity_*,
-    committed as profiles/r02_msacl_bench_parity.json). The moments themselves (the gradients)
-    are checked for EVERY element.
+    the difference is bounded by Adam's maximum step instead. Bars set from what was measured
+    (profiles/r02_msacl_bench_parity_eager.json, _graph.json, _2rank_segments.json; each run
+    writes gpurun_out/msacl_bench_parity_*.json): elements that actually moved apart at most
+    max(1, 1e-4 x numel) per tensor (measured: one element of 65,536, 1.5e-5); the small-moment
+    class at most 15 % of a tensor (measured up to 9.8 %, in first-layer biases: ReLU units whose
+    gradient sums cancel to the GEMM noise level). The moments themselves (the gradients) are
+    checked for EVERY element.
 """
 import json
 import os
@@ -181,7 +184,10 @@ def _check_params(alg, g, it, tag):
                                                 "flipped_frac": flipped, "numel": int(d.size)}
             assert not bad_c.any(), (key, int(bad_c.sum()), float(d[cond].max()))
             assert not bad_u.any() and not bad_0.any(), key
-            assert flipped < 5e-3, (key, flipped)
+            n_flip = int((d > tol_c).sum())
+            assert n_flip <= max(1, int(1e-4 * d.size)), (key, n_flip, d.size)
+            small = float((~cond & ~unchanged).mean())
+            assert small <= 0.15, (key, small)
     # Polyak targets t <- (1 - tau) t + tau q after each critic step: a target element inherits
     # tau times its critic element's difference from every update so far; log_alpha: allclose
     sd = nets.state_dict()

@@ -85,7 +85,7 @@ def test_fifo_insertion_matches_oracle(capacity):
     assert not got[d.pow2 + capacity:].any()  # rows past the capacity never gain mass
 
 
-@pytest.mark.parametrize("capacity,batch", [(1000, 256), (1 << 20, 256), (50_000, 3000)])
+@pytest.mark.parametrize("capacity,batch", [(1000, 256), (1 << 20, 256), (50_000, 3000), (4096, 65536)])
 def test_update_leaf_to_root_matches_oracle(capacity, batch):
     """update_batch: p = (|td| + eps)^alpha in f64, duplicates keep the last entry, ancestors
     recomputed; the full tree (2 x pow2 nodes) equals the oracle's bit for bit."""

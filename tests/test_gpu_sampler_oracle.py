@@ -1,0 +1,174 @@
+"""GPU parity of the BENCHMARKED sampler instantiation against the oracle.
+
+The headline runs `k_rollout<Env, true>` (csrc/rollout.hip): in-kernel TanhGauss sampling and
+clip (RL/utils/act_distribution_cls.py:45-57, RL/trainer/sampler/base.py:127-143), the env
+step, rew_plus_cost, in-kernel Philox resets (gymnasium SyncVectorEnv autoreset) and the
+deferred n-step window emission (base.py:178-217). The other parity tests drive the injected-
+action instantiation `k_rollout<Env, false>`. Here the sampler itself runs, lockstep by
+lockstep, eagerly (HipNstepOffSampler.step_traced: the same policy forward + lockstep launch as
+one iteration of the sampler's graph-captured horizon) at the configs' 65,536 envs with
+n = 20, writing its own sampled actions / log-probs and the env step's outputs
+(mh_rollout_set_trace). Before each lockstep the env state is snapshotted, and the oracle
+replays the kernel's OWN actions from that snapshot:
+
+* next observation (final_observation), raw reward, terminated, truncated at rtol = atol = 1e-5
+  (QuadTracking against the float64-polar path, and the as-is path within 1e-5 plus the
+  reference's own float32-SVD deviation: see tests/test_gpu_env.py);
+* the next state of every continuing env, its steps counter (k + 1, or 0 after a reset);
+* every reset row: the stored state is a draw of the env's reset distribution and the returned
+  observation (and QuadTracking's Rd_last) equals oracle.env_reset_from(stored state);
+* the log-prob the kernel emitted equals the float64 TanhGauss log-prob of the pre-tanh sample
+  recovered from its action and the logits the policy kernel produced;
+* the replay store filled by the deferred emitter waves (+ the final flush) equals the windows
+  oracle.sampler.NStepWindows assembles from the oracle's per-step records, row for row.
+
+1/16 of the envs start 985-999 steps into their episode so truncation happens inside the run.
+"""
+import numpy as np
+import pytest
+import torch
+
+import msacl_amd  # noqa: F401
+from msacl_amd.create_pkg.create_buffer import create_buffer
+from msacl_amd.create_pkg.create_envs import create_envs
+from msacl_amd.create_pkg.create_sampler import create_sampler
+from msacl_amd.trainer.buffer.device_nstep_replay_buffer import KEYS
+from msacl_amd.utils.config import default_msacl_args
+from msacl_amd.utils.init_args import init_args
+from oracle import envs as OE
+from oracle import sampler as OS
+
+pytestmark = pytest.mark.gpu
+TOL = dict(rtol=1e-5, atol=1e-5)
+E, NSTEP = 65536, 20
+# locksteps per env: windows need 20 consecutive steps; QuadTracking's oracle (batched 3x3 SVDs
+# twice per substep) is the slow one
+STEPS = {"QuadTracking": 27}
+
+
+def _near_bound(cls, obs, eps=1e-4):
+    return np.any((np.abs(obs - cls.obs_low) < eps) | (np.abs(obs - cls.obs_high) < eps), axis=1)
+
+
+def _reset_box_ok(name, st):
+    if name == "VanderPol":
+        return np.abs(st).max(initial=0) <= 5.0
+    if name == "Pendulum":
+        return np.all(st >= OE.Pendulum.obs_low) and np.all(st <= OE.Pendulum.obs_high)
+    if name == "QuadTracking":
+        n = st.shape[0]
+        R = st[:, 6:15].reshape(n, 3, 3).astype(np.float64)
+        orth = np.abs(np.matmul(R, np.transpose(R, (0, 2, 1))) - np.eye(3)).max(initial=0) < 1e-6
+        return np.abs(st[:, np.r_[0:6, 15:18]]).max(initial=0) <= 0.01 and orth
+    return np.abs(st).max(initial=0) <= 0.5
+
+
+def _sampler(name, tmp_path, noise=None):
+    args = default_msacl_args(env_name=name, env_num=E, n_step=NSTEP, seed=0, env_seed=5, buffer_max_size=400_000,
+                              buffer_warm_size=0, save_folder=str(tmp_path), noise_params=noise)
+    args = init_args(create_envs(**args), **args)
+    sampler, buffer = create_sampler(**args), create_buffer(**args)
+    sampler.bind_store(buffer)
+    return sampler, buffer
+
+
+@pytest.mark.parametrize("name,noise", [(n, None) for n in OE.ENVS] + [("DuctedFan", {"mean": 0.0, "std": 0.2})],
+                         ids=list(OE.ENVS) + ["DuctedFan-gauss-noise"])
+def test_sampled_lockstep_kernel_matches_oracle(name, noise, tmp_path):
+    cls = OE.ENVS[name]
+    quad = name == "QuadTracking"
+    sampler, buffer = _sampler(name, tmp_path, noise)
+    env, dev = sampler.envs, sampler.device
+    D, A = env.obs_dim, env.act_dim
+    rng = np.random.default_rng(3)
+    k0 = np.zeros(E, np.int32)
+    late = rng.choice(E, E // 16, replace=False)
+    k0[late] = rng.integers(985, 1000, size=late.size)
+    env.set_state(None, None, k0)
+    lo, hi = cls.act_low.astype(np.float64), cls.act_high.astype(np.float64)
+    act, logp = torch.empty(E, A, device=dev), torch.empty(E, device=dev)
+    real, rew = torch.empty(E, D, device=dev), torch.empty(E, device=dev)
+    term, trunc = torch.empty(E, dtype=torch.uint8, device=dev), torch.empty(E, dtype=torch.uint8, device=dev)
+    windows = OS.NStepWindows(E, NSTEP, D, A)
+    expect = {k: [] for k in KEYS}
+
+    st, xs, k = env.get_state()
+    st = st.cpu().numpy()
+    xs = xs.cpu().numpy() if xs is not None else None
+    k = k.cpu().numpy().astype(np.int64)
+    assert _reset_box_ok(name, st)
+    _, xs_r, obs_o = OE.env_reset_from(name, st)  # the oracle's view of the current observation
+    np.testing.assert_allclose(sampler.obs.cpu().numpy(), obs_o, **TOL)
+    if quad:
+        np.testing.assert_allclose(xs, xs_r, rtol=0, atol=1e-12)
+    n_reset = n_trunc = n_lp = 0
+    for t in range(STEPS.get(name, 40)):
+        logits = sampler.step_traced(act, logp, trace=(real, rew, term, trunc))
+        a_np, lp_np, lg = act.cpu().numpy(), logp.cpu().numpy(), logits.cpu().numpy().astype(np.float64)
+        got_real, got_rew = real.cpu().numpy(), rew.cpu().numpy()
+        got_term, got_trunc = term.cpu().numpy().astype(bool), trunc.cpu().numpy().astype(bool)
+        st2, xs2, k2 = env.get_state()
+        st2, k2 = st2.cpu().numpy(), k2.cpu().numpy().astype(np.int64)
+        xs2 = xs2.cpu().numpy() if xs2 is not None else None
+        obs_next = sampler.obs.cpu().numpy()
+
+        # ---- the action: in the box; its log-prob from the policy logits (no-noise runs)
+        assert np.all((a_np >= cls.act_low) & (a_np <= cls.act_high))
+        if noise is None:
+            mu, sd = lg[:, :A], np.exp(np.clip(lg[:, A:], -20, 1))
+            th = (2 * a_np.astype(np.float64) - (hi + lo)) / (hi - lo)
+            ok = np.all(np.abs(th) < 0.95, axis=1)
+            z = np.arctanh(np.clip(th, -0.95, 0.95))
+            lp = (-((z - mu) ** 2) / (2 * sd ** 2) - np.log(sd) - 0.5 * np.log(2 * np.pi)).sum(1)
+            lp = lp - np.log(1 + 1e-6 - np.tanh(z) ** 2).sum(1) - np.log((hi - lo) / 2).sum()
+            np.testing.assert_allclose(lp_np[ok], lp[ok], rtol=1e-4, atol=5e-3)
+            n_lp += int(ok.sum())
+
+        # ---- the env step from the snapshot, with the kernel's own actions
+        s_o, xs_o, o2, r2, te, tr = OE.env_step(name, st, a_np, xs, k, polar64=quad)
+        np.testing.assert_allclose(got_real, o2, **TOL)
+        np.testing.assert_allclose(got_rew, r2, **TOL)
+        if quad:  # the reference as-is (float32 SVD) on a slice: within 1e-5 + its own SVD noise
+            sl = slice(0, 4096)
+            _, _, o32, _, _, _ = OE.env_step(name, st[sl], a_np[sl], xs[sl], k[sl])
+            dev32 = np.abs(o32.astype(np.float64) - o2[sl])
+            assert np.all(np.abs(got_real[sl] - o32) <= 1e-5 + 1e-5 * np.abs(o32) + dev32)
+        nb = _near_bound(cls, o2)
+        np.testing.assert_array_equal(got_term[~nb], te[~nb])
+        np.testing.assert_array_equal(got_trunc, tr)
+        done = got_term | got_trunc  # the kernel's flags (they differ from te only at the bound)
+        n_reset += int(done.sum())
+        n_trunc += int(got_trunc.sum())
+
+        # ---- continuing envs: next state, Rd_last, counter, observation
+        np.testing.assert_array_equal(k2, np.where(done, 0, k + 1))
+        np.testing.assert_allclose(st2[~done], s_o[~done], **TOL)
+        if quad:
+            np.testing.assert_allclose(xs2[~done], xs_o[~done], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(obs_next[~done], o2[~done], **TOL)
+        # ---- reset rows: a reset-distribution draw, and obs / Rd_last = env_reset_from(state)
+        obs_new = o2.copy()
+        if done.any():
+            assert _reset_box_ok(name, st2[done])
+            _, xr, orr = OE.env_reset_from(name, st2[done])
+            np.testing.assert_allclose(obs_next[done], orr, **TOL)
+            if quad:
+                np.testing.assert_allclose(xs2[done], xr, rtol=0, atol=1e-12)
+            obs_new[done] = orr
+
+        # ---- the oracle's n-step records (rew_plus_cost.py:18-21 with the reference's scales)
+        r_s, c_s = OS.rew_plus_cost(o2, r2.astype(np.float32), 100.0, 100.0)
+        for key, w in zip(KEYS, windows.push(obs_o, a_np, r_s, c_s, o2, done, lp_np)):
+            expect[key].append(w)
+        st, xs, k, obs_o = st2, xs2, k2, obs_new
+
+    sampler.flush()
+    torch.cuda.synchronize()
+    exp = {key: np.concatenate(v) for key, v in expect.items()}
+    total = exp["obs"].shape[0]
+    assert total > 500 and n_reset > 0 and n_trunc > 0, (total, n_reset, n_trunc)
+    assert noise is not None or n_lp > 1000
+    assert int(buffer.cursor[2]) == total and total < buffer.max_size
+    for key in KEYS:
+        np.testing.assert_allclose(buffer.n_step_buf[key][:total].cpu().numpy(), exp[key], **TOL, err_msg=key)
+    assert not buffer.n_step_buf["done"][:total, :-1].any()

@@ -111,15 +111,30 @@ def measure(env_name="QuadTracking", seconds=6.0, n_envs=64, procs=None, box_sha
         cand = [c for c in (topo.get("physical_cores"), topo.get("affinity"), box_share) if c]
         procs = max(1, min(cand))
     sp, tp = _run(ctx, env_name, n_envs, seconds, 1, procs)
+    s11, t11 = _run(ctx, env_name, n_envs, seconds, 1, 1)
     single = s1 / t1
     agg = sp / tp
+    one = s11 / t11
+    phys = topo.get("physical_cores")
+    proj = None
+    if phys and phys > procs:
+        # SURVEY 8(d) asks for P = the physical cores; the pool caps a GPU box's worker pools at
+        # its per-GPU CPU share (16 of the host's cores are this GPU's), so the physical-core
+        # figure is the measured per-process rate times the core count, with the measured
+        # P-process efficiency (aggregate / (P x the 1-process rate)) shown beside it
+        proj = {"cores": phys, "value": round(agg / procs * phys, 1),
+                "method": (f"measured {procs}-process per-process rate x {phys} physical cores (linear; "
+                           f"not run: the pool limits a one-GPU box's worker pools to its {box_share}-CPU share)"),
+                "efficiency_at_measured_procs": round(agg / (procs * one), 3)}
     return {
         "value": round(agg, 1), "unit": "env_steps/s", "cores": procs, "kind": "port",
         "sample": (f"{env_name}: oracle restatement of the reference CPU sampler (per-env SyncVectorEnv loop + "
                    f"_n_step deques + NumPy 256x256 StochaPolicy), {procs} processes x 1 thread x {n_envs} envs, "
                    f"{seconds:.0f} s each, started together; value = node aggregate"),
         "one_process_4_threads": round(single, 1),
+        "one_process_1_thread": round(one, 1),
         "per_process": round(agg / procs, 1),
+        "projected_physical_cores": proj,
         "host": topo,
         "procs_rule": "min(physical cores, CPU affinity, the box's per-GPU CPU share of 16)",
     }

@@ -20,7 +20,8 @@ from collections import defaultdict
 ALIASES = {"rollout_emit": ("k_rollout<mh::QuadTracking, true>", 131072),
            "rollout_step": ("k_rollout<mh::QuadTracking, true>", 65536),
            "window_emit": ("k_emit_fused<12, 4>", None), "replay_gather": ("k_gather", None),
-           "msacl_lyapunov": ("k_lyapunov", None), "msacl_q_target": ("k_q_target", None)}
+           "msacl_lyapunov": ("k_lyapunov", None), "msacl_q_target": ("k_q_target", None),
+           "policy_forward": ("k_policy_forward_x3", None)}
 
 
 def load(root, counter):
@@ -37,8 +38,10 @@ def load(root, counter):
 def main():
     root, out = sys.argv[1], sys.argv[2]
     fetch, write = load(root, "FETCH_SIZE"), load(root, "WRITE_SIZE")
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from tools.kernel_hash import rollout_sources_sha
     res = {"units": "bytes per launch (mean over dispatches); FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE",
-           "kernels": {}}
+           "rollout_sources_sha": rollout_sources_sha(), "kernels": {}}
     for name in sorted(set(fetch) | set(write)):
         fk = sum(fetch.get(name, [0])) / max(1, len(fetch.get(name, [])))
         wk = sum(write.get(name, [0])) / max(1, len(write.get(name, [])))
