@@ -154,6 +154,36 @@ int mh_env_set_reward_cost_scale(mh_env_t h, float reward_scale, float cost_scal
  * (a device RNG write, capturable). NULL disables. Ignored for injected actions. */
 int mh_env_set_action_noise(mh_env_t h, const float* noise);
 
+/* Grow each env's n-step ring to `ring_slots` (>= n_step) records, so that windows stay readable
+ * for ring_slots - n_step further steps after they become full (the fused horizon sampler,
+ * mh_sample_horizon, emits a whole horizon's windows after it: ring_slots >= n_step + H - 1).
+ * Every deque restarts empty (call before sampling); a no-op when the size is unchanged.
+ * Needs num_envs <= 1M when ring_slots > n_step. Reference: the per-env deque(maxlen=n) of
+ * BaseSampler._n_step (base.py:180-188) — the extra slots only delay the reads. */
+int mh_nstep_reserve(mh_env_t h, int32_t ring_slots);
+
+/* A whole horizon of BaseSampler._n_step (RL/trainer/sampler/base.py:118-222, `horizon` lockstep
+ * steps of policy -> TanhGauss sample -> clip -> env step -> autoreset -> rew_plus_cost -> deque
+ * push) in ONE persistent kernel, followed by one emission launch that copies every window
+ * completed in the horizon into `store` in the reference's order (lockstep major, env index
+ * within a lockstep; base.py:178-213, nstep_replay_buffer.py:122-125) and advances its cursor.
+ * The default StochaPolicy shape only (D -> 256 -> 256 -> 2A, ReLU; obs_dim <= 15): the policy
+ * is `packed_policy` as built by mh_policy_pack, with the SAME split-f16 arithmetic as
+ * mh_policy_forward, and the env step is mh_rollout_step's, so a horizon gives the same rows,
+ * observations and env state bit for bit as `horizon` x (mh_policy_forward +
+ * mh_rollout_step_deferred) + mh_rollout_flush with the same noise. Requires the rings reserved
+ * for it: mh_nstep_reserve(h, n_step + horizon - 1).
+ *   obs        [E][obs_dim] in: current observation; out: the observation after the horizon
+ *   act_noise  DEVICE float[horizon] (GaussNoise, one scalar per lockstep) or NULL
+ *   act_out / logp_out  optional [horizon][E][act_dim] / [horizon][E]: the sampled actions */
+int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, int32_t n_out, float* obs,
+                      int32_t horizon, const mh_window_store_t* store, const float* act_noise, float* act_out,
+                      float* logp_out, void* stream);
+
+/* Diagnostics of mh_sample_horizon: copies the handle's device error word (the number of bounded
+ * intra-workgroup waits that timed out since mh_env_create; 0 when healthy) to DEVICE int64 `out`. */
+int mh_sample_horizon_errors(mh_env_t h, int64_t* out, void* stream);
+
 /* Per-env step trace of every later mh_rollout_step / mh_rollout_step_deferred of this handle,
  * in the SAME kernel instantiation the call would run anyway (the sampling one when logits are
  * given): the pre-reset observation [E][D] (SyncVectorEnv info["final_observation"], the

@@ -6,6 +6,7 @@
 
 #include "msacl_hip.h"
 #include "rollout.h"
+#include "sample_fused.h"
 
 namespace {
 
@@ -59,6 +60,7 @@ struct mh_env_s {
   uint32_t* ctr = nullptr;
   // n-step
   int n = 0;
+  int R = 0;  // ring slots per env (n, or more after mh_nstep_reserve)
   float reward_scale = 1.0f, cost_scale = 1.0f;
   int raw_log_std = 0;
   float log_std_lo = -20.0f, log_std_hi = 1.0f;
@@ -70,6 +72,11 @@ struct mh_env_s {
   int32_t* block_count = nullptr;
   int32_t* block_offset = nullptr;
   int32_t* emit_list = nullptr;     // [2][grid * BLK]: halves alternate between deferred steps
+  // fused horizon sampler (mh_sample_horizon): per-(lockstep, wave) window counts / lists for up
+  // to hcap locksteps (sized by mh_nstep_reserve: hcap = ring slots - n + 1)
+  int hcap = 0;
+  int32_t* h_count = nullptr;       // [hcap][ceil(E / 64)]
+  int32_t* h_list = nullptr;        // [hcap][E]
   // deferred emission (mh_rollout_step_deferred): the last step's windows are not yet emitted
   bool pending = false;
   int parity = 0;                   // half of block_count / emit_list the next step writes
@@ -110,6 +117,7 @@ struct mh_env_s {
     a.ctr = ctr;
     a.seed = seed;
     a.n = n;
+    a.ring_slots = R;
     a.reward_scale = reward_scale;
     a.cost_scale = cost_scale;
     a.raw_log_std = raw_log_std;
@@ -130,7 +138,8 @@ static void free_handle(mh_env_s* h) {
   for (hipEvent_t e : h->ev_free) (void)hipEventDestroy(e);
   for (hipEvent_t e : h->ev_pending) (void)hipEventDestroy(e);
   void* ptrs[] = {h->state, h->xstate, h->steps, h->tab, h->meta, h->ctr, h->ring, h->ring_len,
-                  h->ring_pos, h->emit_rank, h->block_count, h->block_offset, h->emit_list};
+                  h->ring_pos, h->emit_rank, h->block_count, h->block_offset, h->emit_list, h->h_count,
+                  h->h_list};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete h;
@@ -227,6 +236,7 @@ int mh_nstep_attach(mh_env_t h, int32_t n_step, float reward_scale, float cost_s
     h->ring = nullptr;
   }
   h->n = n_step;
+  h->R = n_step;
   h->reward_scale = reward_scale;
   h->cost_scale = cost_scale;
   const int64_t E = h->E;
@@ -243,6 +253,113 @@ int mh_nstep_attach(mh_env_t h, int32_t n_step, float reward_scale, float cost_s
   MH_HIP(hipMemset(h->ring_len, 0, sizeof(int32_t) * E));
   MH_HIP(hipMemset(h->ring_pos, 0, sizeof(int32_t) * E));
   MH_HIP(hipMemset(h->ring, 0, sizeof(float) * E * n_step * F));
+  return MH_OK;
+}
+
+int mh_nstep_reserve(mh_env_t h, int32_t ring_slots) {
+  if (!h) return fail(MH_EINVAL, "mh_nstep_reserve: null handle");
+  if (!h->ring) return fail(MH_ESTATE, "mh_nstep_reserve: call mh_nstep_attach first");
+  if (ring_slots < h->n || ring_slots > 8192) return fail(MH_EINVAL, "mh_nstep_reserve: ring_slots outside [n_step, 8192]");
+  // the legacy per-env emission stages a whole ring in LDS: only grids the fused emission covers
+  if (ring_slots != h->n && h->grid() > mh::EMIT_FUSED_MAX_NB)
+    return fail(MH_EINVAL, "mh_nstep_reserve: more ring slots than n_step need num_envs <= 1M");
+  if (ring_slots == h->R) return MH_OK;
+  if (int rc = flush_pending(h, nullptr)) return rc;
+  MH_HIP(hipDeviceSynchronize());
+  const int64_t E = h->E;
+  const int F = h->info.record_floats;
+  float* ring = nullptr;
+  MH_HIP(hipMalloc(&ring, sizeof(float) * E * ring_slots * F));
+  (void)hipFree(h->ring);
+  h->ring = ring;
+  h->R = ring_slots;
+  // the fused horizon's window lists, for horizons up to ring_slots - n + 1 locksteps
+  (void)hipFree(h->h_count);
+  (void)hipFree(h->h_list);
+  h->h_count = h->h_list = nullptr;
+  h->hcap = ring_slots - h->n + 1;
+  MH_HIP(hipMalloc(&h->h_count, sizeof(int32_t) * h->hcap * ((E + 63) / 64)));
+  MH_HIP(hipMalloc(&h->h_list, sizeof(int32_t) * h->hcap * E));
+  MH_HIP(hipMemset(h->ring, 0, sizeof(float) * E * ring_slots * F));
+  MH_HIP(hipMemset(h->ring_len, 0, sizeof(int32_t) * E));
+  MH_HIP(hipMemset(h->ring_pos, 0, sizeof(int32_t) * E));
+  return MH_OK;
+}
+
+int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, int32_t n_out, float* obs,
+                      int32_t horizon, const mh_window_store_t* store, const float* act_noise, float* act_out,
+                      float* logp_out, void* stream) {
+  if (!h) return fail(MH_EINVAL, "mh_sample_horizon: null handle");
+  if (!h->ring) return fail(MH_ESTATE, "mh_sample_horizon: call mh_nstep_attach first");
+  if (!packed_policy || !obs) return fail(MH_EINVAL, "mh_sample_horizon: null policy / obs");
+  if (obs_dim != h->info.obs_dim || n_out != 2 * h->info.act_dim || obs_dim > 15)
+    return fail(MH_EINVAL, "mh_sample_horizon: policy shape does not match the env (or obs_dim > 15)");
+  if (horizon <= 0 || horizon > h->hcap || h->R < h->n + horizon - 1)
+    return fail(MH_ESTATE, "mh_sample_horizon: horizon exceeds the reserved ring (mh_nstep_reserve(n + H - 1))");
+  if (store && (store->capacity <= 0 || !store->cursor || !store->obs || !store->act || !store->rew ||
+                !store->cost || !store->obs2 || !store->done || !store->logp))
+    return fail(MH_EINVAL, "mh_sample_horizon: incomplete window store");
+  if (store && mh::fused_emit_cells(h->E, horizon) + 1 > 12288)
+    return fail(MH_EINVAL, "mh_sample_horizon: horizon x blocks exceeds the emission scan (12288 cells)");
+  if (int rc = flush_pending(h, stream)) return rc;
+  mh::FusedArgs a;
+  std::memset(&a, 0, sizeof(a));
+  const mh::StepArgs b = h->base_args();
+  a.E = h->E;
+  a.state = h->state;
+  a.xstate = h->xstate;
+  a.steps = h->steps;
+  a.tab = h->tab;
+  a.ctr = h->ctr;
+  a.seed = h->seed;
+  a.obs = obs;
+  a.P = packed_policy;
+  a.K1 = obs_dim / 2 + 1;
+  a.N3 = n_out;
+  a.H = horizon;
+  a.ring = h->ring;
+  a.ring_len = h->ring_len;
+  a.ring_pos = h->ring_pos;
+  a.n = h->n;
+  a.R = h->R;
+  a.reward_scale = h->reward_scale;
+  a.cost_scale = h->cost_scale;
+  a.log_std_lo = h->log_std_lo;
+  a.log_std_hi = h->log_std_hi;
+  a.log_half_sum = b.log_half_sum;
+  a.act_noise = act_noise;
+  a.emit_count = h->h_count;
+  a.emit_list = h->h_list;
+  a.act_out = act_out;
+  a.logp_out = logp_out;
+  a.err = h->meta + 7;  // meta[7]: the fused kernel's error word
+  mh::HorizonEmitArgs ea;
+  std::memset(&ea, 0, sizeof(ea));
+  ea.E = h->E;
+  ea.H = horizon;
+  ea.n = h->n;
+  ea.R = h->R;
+  ea.ring = h->ring;
+  ea.emit_count = h->h_count;
+  ea.emit_list = h->h_list;
+  if (store) {
+    ea.obs = store->obs;
+    ea.act = store->act;
+    ea.rew = store->rew;
+    ea.cost = store->cost;
+    ea.obs2 = store->obs2;
+    ea.done = store->done;
+    ea.logp = store->logp;
+    ea.capacity = store->capacity;
+    ea.cursor = store->cursor;
+  }
+  MH_HIP(mh::launch_sample_fused(h->env_id, a, ea, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_sample_horizon_errors(mh_env_t h, int64_t* out, void* stream) {
+  if (!h || !out) return fail(MH_EINVAL, "mh_sample_horizon_errors: null argument");
+  MH_HIP(hipMemcpyAsync(out, h->meta + 7, sizeof(int64_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return MH_OK;
 }
 
@@ -388,6 +505,7 @@ static int rollout_impl(mh_env_t h, const float* logits, const float* act_in, co
     ea.meta_rw = h->meta;
     ea.capacity = store->capacity;
     ea.n = h->n;
+    ea.R = h->R;
     ea.F = h->info.record_floats;
     ea.D = h->info.obs_dim;
     ea.A = h->info.act_dim;
@@ -413,6 +531,7 @@ static int rollout_impl(mh_env_t h, const float* logits, const float* act_in, co
     ea.meta = h->meta;
     ea.capacity = store->capacity;
     ea.n = h->n;
+    ea.R = h->R;
     ea.F = h->info.record_floats;
     ea.D = h->info.obs_dim;
     ea.A = h->info.act_dim;
@@ -450,6 +569,7 @@ static int flush_pending(mh_env_t h, void* stream) {
   ea.meta_rw = h->meta;
   ea.capacity = store->capacity;
   ea.n = h->n;
+  ea.R = h->R;
   ea.F = h->info.record_floats;
   ea.D = h->info.obs_dim;
   ea.A = h->info.act_dim;

@@ -43,6 +43,7 @@ struct StepArgs {
   int32_t* emit_list;         // [grid*BLK] block-compacted emitter env ids (rank order)
   const int64_t* cursor;      // store cursor, snapshotted into meta[1], meta[3], meta[4]
   int n;
+  int ring_slots;             // R >= n ring slots per env (n unless mh_nstep_reserve grew it)
   float reward_scale, cost_scale;
   int raw_log_std;               // logits second half is log_std: std = exp(clamp(., lo, hi))
   float log_std_lo, log_std_hi;  // StochaPolicy min/max_log_std (mlp.py:125-136)
@@ -81,6 +82,7 @@ struct EmitArgs {
   const int64_t* meta;
   int64_t capacity;
   int n, F, D, A;
+  int R;                      // ring slots per env (>= n)
   float *obs, *act, *rew, *cost, *obs2, *done, *logp;
   // fused scan + persistent emission (k_emit_fused)
   const int32_t* block_count;

@@ -70,7 +70,7 @@ __device__ __forceinline__ void store_vec(float* dst, const float* v);
 template <int D, int A>
 __device__ void deferred_emit(const StepArgs& a, int w, int lane) {
   constexpr int F = rec_floats(D, A);
-  const int nb = gridDim.x, blk = blockIdx.x, n = a.n;
+  const int nb = gridDim.x, blk = blockIdx.x, n = a.n, R = a.ring_slots;
   int pre = 0, tot = 0;  // windows of the blocks before this one / of all blocks
   if (a.prev_count) {
     for (int i = lane; i < nb; i += 64) {
@@ -95,9 +95,9 @@ __device__ void deferred_emit(const StepArgs& a, int w, int lane) {
       const int packed = a.prev_list[(int64_t)blk * BLK + r];
       const int64_t env = (int64_t)blk * BLK + (packed & (BLK - 1));
       int slot = (packed >> 8) + j;
-      slot = slot >= n ? slot - n : slot;
+      slot = slot >= R ? slot - R : slot;
       float rec[F];
-      const float4* src = reinterpret_cast<const float4*>(a.ring + (env * n + slot) * (int64_t)F);
+      const float4* src = reinterpret_cast<const float4*>(a.ring + (env * R + slot) * (int64_t)F);
 #pragma unroll
       for (int i = 0; i < F / 4; ++i) {
         const float4 v = src[i];
@@ -390,12 +390,12 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
       rec[2 * D + A + 3] = logp;
 #pragma unroll
       for (int i = 2 * D + A + 4; i < F; ++i) rec[i] = 0.0f;
-      const int n = a.n;
+      const int n = a.n, R = a.ring_slots;
       wpos = pos;
-      pos = pos + 1 == n ? 0 : pos + 1;
+      pos = pos + 1 == R ? 0 : pos + 1;
       len = len + 1 < n ? len + 1 : n;
       emit = (len == n);
-      emit_pos = pos;
+      emit_pos = pos - n < 0 ? pos - n + R : pos - n;  // the window's oldest slot (pos when R == n)
       if (done) len = 0;  // deque.clear() when the newest item is done
       a.ring_len[e] = len;
       a.ring_pos[e] = pos;
@@ -473,11 +473,11 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
       }
       const float4* sw = stage[wave];
       const int64_t e0 = (int64_t)blockIdx.x * BLK + wave * 64;
-      const int n = a.n;
+      const int R = a.ring_slots;
       // the wave's slice of the ring as a buffer resource: records of envs >= E fall outside it
       // and are dropped by the hardware, so the loop has no branch and its LDS reads batch up
       const int64_t nrec = e0 < E ? (E - e0 < 64 ? E - e0 : 64) : 0;
-      const __amdgpu_buffer_rsrc_t rr = soa_rsrc(a.ring + e0 * n * F, (uint32_t)(nrec * n * F * 4));
+      const __amdgpu_buffer_rsrc_t rr = soa_rsrc(a.ring + e0 * R * F, (uint32_t)(nrec * R * F * 4));
       typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef MH_EXP_NO_RING  // cost-attribution experiment only: no ring record store
       float4 v[C];
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
         const int c = j * 64 + lane;
         const int r = c / C, q = c % C;
         v[j] = sw[r * CP + q];
-        off[j] = ((r * n + spos[wave][r]) * F + 4 * q) * 4;
+        off[j] = ((r * R + spos[wave][r]) * F + 4 * q) * 4;
       }
 #pragma unroll
       for (int j = 0; j < C; ++j) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, v[j]), rr, off[j], 0, 0);
@@ -587,15 +587,15 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
   const int64_t M = a.capacity;
   if (g < total - M) return;  // overwritten later in this same step (FIFO order)
   const int64_t row = (a.meta[1] + g) % M;
-  const int n = a.n, F = a.F, D = a.D, A = a.A;
-  float* buf = lds + wave * n * F;
-  const float4* src = reinterpret_cast<const float4*>(a.ring + e * (int64_t)n * F);
+  const int n = a.n, F = a.F, D = a.D, A = a.A, R = a.R;
+  float* buf = lds + wave * R * F;
+  const float4* src = reinterpret_cast<const float4*>(a.ring + e * (int64_t)R * F);
   float4* b4 = reinterpret_cast<float4*>(buf);
-  for (int i = lane; i < (n * F) / 4; i += 64) b4[i] = src[i];
+  for (int i = lane; i < (R * F) / 4; i += 64) b4[i] = src[i];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int pos = a.ring_pos[e];  // oldest record of a full deque
+  const int pos = a.ring_pos[e] - n < 0 ? a.ring_pos[e] - n + R : a.ring_pos[e] - n;  // oldest record
   struct Field {
     float* dst;
     int off, width;
@@ -610,7 +610,7 @@ __global__ __launch_bounds__(256) void k_emit(EmitArgs a) {
     for (int idx = lane; idx < n * W; idx += 64) {
       const int j = idx / W, d = idx - j * W;
       int slot = pos + j;
-      slot = slot >= n ? slot - n : slot;
+      slot = slot >= R ? slot - R : slot;
       dst[idx] = buf[slot * F + off + d];
     }
   }
@@ -698,9 +698,9 @@ __global__ __launch_bounds__(256) void k_emit_fused(EmitArgs a) {
     const int packed = a.emit_list[(int64_t)bl * BLK + r];
     const int64_t e = (int64_t)bl * BLK + (packed & (BLK - 1));
     int slot = (packed >> 8) + j;
-    slot = slot >= n ? slot - n : slot;
+    slot = slot >= a.R ? slot - a.R : slot;
     float rec[F];
-    const float4* src = reinterpret_cast<const float4*>(a.ring + (e * n + slot) * (int64_t)F);
+    const float4* src = reinterpret_cast<const float4*>(a.ring + (e * a.R + slot) * (int64_t)F);
 #pragma unroll
     for (int i = 0; i < F / 4; ++i) {
       const float4 v = src[i];
@@ -847,7 +847,7 @@ hipError_t launch_finalize(const int32_t* block_count, int32_t nb, int32_t* bloc
 }
 hipError_t launch_emit(const EmitArgs& a, hipStream_t st) {
   const int grid = (int)((a.E + 3) / 4);
-  const size_t shm = (size_t)4 * a.n * a.F * sizeof(float);
+  const size_t shm = (size_t)4 * a.R * a.F * sizeof(float);
   k_emit<<<grid, 256, shm, st>>>(a);
   return hipGetLastError();
 }

@@ -1,0 +1,53 @@
+// sample_fused.h — argument blocks of the fused horizon sampler (sample_fused.hip), shared with
+// the C ABI (capi.hip: mh_sample_horizon).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mh {
+
+struct FusedArgs {
+  int64_t E;
+  float* state;       // [S][E]
+  double* xstate;     // [XS][E]
+  int32_t* steps;     // [E]
+  const double* tab;  // QuadTracking desired-trajectory table or null
+  uint32_t* ctr;      // [E] per-env Philox counter
+  uint64_t seed;
+  float* obs;         // [E][D] in: current observation, out: the observation after the horizon
+  const float* P;     // packed policy parameters (k_policy_pack_x3 layout)
+  int K1, N3, H;
+  float* ring;        // [E][R][F]
+  int32_t* ring_len;
+  int32_t* ring_pos;
+  int n, R;
+  float reward_scale, cost_scale;
+  float log_std_lo, log_std_hi, log_half_sum;
+  const float* act_noise;  // [H] GaussNoise scalars (one per lockstep) or null
+  int32_t* emit_count;     // [H][NW] windows completed per (lockstep, 64-env wave)
+  int32_t* emit_list;      // [H][E] per wave, rank-ordered (lane | oldest slot << 6)
+  float* act_out;          // [H][E][A] or null
+  float* logp_out;         // [H][E] or null
+  int64_t* err;            // device error word: policy-wave waits that timed out (0 when healthy)
+};
+
+constexpr int FUSED_ENVS = 256;   // envs per workgroup (one workgroup per CU)
+constexpr int FUSED_THREADS = 512;
+// (lockstep, 256-env block) cells the horizon emission scans in LDS
+inline int64_t fused_emit_cells(int64_t E, int H) { return (int64_t)H * ((E + FUSED_ENVS - 1) / FUSED_ENVS); }
+
+struct HorizonEmitArgs {
+  int64_t E;
+  int H, n, R;
+  const float* ring;
+  const int32_t* emit_count;  // [H][NW]
+  const int32_t* emit_list;   // [H][E]
+  float *obs, *act, *rew, *cost, *obs2, *done, *logp;
+  int64_t capacity;
+  int64_t* cursor;  // {ptr, size, total, last}
+};
+
+
+hipError_t launch_sample_fused(int env_id, const FusedArgs& a, const HorizonEmitArgs& ea, hipStream_t st);
+
+}  // namespace mh

@@ -1,0 +1,707 @@
+// sample_fused.hip — the sampler's whole horizon (RL/trainer/sampler/base.py:118-222 run for
+// `sample_batch_size` lockstep steps) as ONE persistent kernel per sample(), for the default
+// StochaPolicy shape (256 x 256, D <= 15) and num_envs <= 256 x the CU count.
+//
+// Why: the two-kernel lockstep (k_policy_forward_x3, MFMA-bound, then k_rollout, latency-bound
+// at one wave per SIMD) alternates two phases that each leave the other unit of every SIMD idle,
+// and every lockstep re-reads and re-writes the env state through the cache hierarchy. Here each
+// workgroup owns 256 envs for the whole horizon, one workgroup per CU, 8 waves:
+//   waves 0-3  policy waves: the split-f16 MLP (policy_x3.h, the same MFMA sequence as
+//              k_policy_forward_x3, so the same logits bit for bit), one 32-env tile per wave
+//              per pass, W2 streamed through LDS by LDS-DMA and shared by the four policy waves
+//              (they synchronise among themselves through an LDS counter, not s_barrier, so the
+//              env waves never wait on the policy's chunk handoffs);
+//   waves 4-7  env waves: one env per lane, the env's state (state, Rd_last, steps, Philox
+//              counter, deque length / position) kept in REGISTERS across the horizon; each
+//              lockstep samples the TanhGauss action, steps the env, autoresets and pushes the
+//              ring record exactly as k_rollout<Env, true> does.
+// The 256 envs are two halves H0 (env waves 4, 5) and H1 (6, 7), pipelined so MFMA and VALU
+// work of the same CU overlap (the policy waves and the env waves share each SIMD):
+//   phase A(t): policy(H0, obs after t-1)  ||  env step t of H1 (logits from B(t-1))
+//   phase B(t): policy(H1, obs after t)    ||  env step t of H0 (logits from A(t))
+// with one workgroup barrier between phases; observations and logits pass through LDS only.
+// Windows: every full deque of lockstep t is recorded as (lane | oldest slot << 6) in a per-wave,
+// rank-ordered list; the rings hold n + H - 1 records (mh_nstep_reserve) so every window of the
+// horizon is still intact when k_emit_horizon copies them, in the reference's order (lockstep
+// major, env index within a lockstep: base.py:178-213), into the replay store after the kernel.
+#include <type_traits>
+
+#include "policy_x3.h"
+#include "reset_draw.h"
+#include "rollout.h"
+#include "sample_fused.h"
+
+#ifndef MH_FUSED_STATE_IN_REGS
+#define MH_FUSED_STATE_IN_REGS 1
+#endif
+
+namespace mh {
+
+// ------------------------------------------------------------------ policy waves
+struct PolicyLds {
+  uint4* c0;            // W2 chunk buffers (PM_X3_FRAGS * 64 records each)
+  uint4* c1;
+  const uint4* w3;      // fold operands [ob][s][split][lane]
+  const float* b2;      // layer-2 bias, [256]
+  const float* obs;     // [256][D] observations of the workgroup's envs
+  float* lgt;           // [256][N3] logits out
+  uint32_t* bar;        // policy-wave barrier counter
+  int64_t* err;         // device error word (bounded waits that timed out)
+};
+
+// the four policy waves' barrier: own LDS-DMA landed (vmcnt(0)), arrive, wait for all four. The
+// wait is bounded (~1e9 cycles): a wave that gives up records it in *err (read by the tests
+// through mh_sample_horizon_errors) instead of hanging the device
+__device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_t* err) {
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  target += 4;
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  uint32_t spins = 0;
+  while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins == (1u << 24)) {
+      if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(err, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+}
+
+// One pass: the 32-env tile `row0 .. row0 + 31` (workgroup-local rows) of policy wave pw through
+// all three layers; k_policy_forward_x3<1, 8>'s per-tile sequence with the observation rows and
+// the logits in LDS. `next`: stage chunk 0 of the following pass during the last phase.
+template <int D>
+__device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int row0, bool next, uint32_t& target) {
+  typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+  constexpr int FPW = PM_X3_FRAGS / 4;  // W2 fragments each policy wave stages per chunk
+  const int lane = threadIdx.x & 63;
+  const int K1 = a.K1, N3 = a.N3;
+  const float* P = a.P;
+  const float* b3 = P + pm_off_b3(K1);
+  const uint4* W2g = reinterpret_cast<const uint4*>(P + pm_off_w2x3(K1));
+  const uint4* W1g = reinterpret_cast<const uint4*>(P + pm_off_w1x3(K1));
+  const PmScales scs = pm_scales(P + pm_off_scal(K1));
+  const float isw1 = scs.isw[0], isw2 = scs.isw[1], isw3 = scs.isw[2], R1 = scs.R1, R2 = scs.R2;
+  const float one = 1.0f;
+
+  auto stage = [&](int ib, uint4* dstbuf) {
+    const uint4* src = W2g + ((int64_t)ib * PM_X3_FRAGS + pw * FPW) * 64;
+    asm volatile("" : "+s"(src));
+#pragma unroll
+    for (int i = 0; i < FPW; ++i)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + i * 64 + lane),
+                                       (void __attribute__((address_space(3)))*)(&dstbuf[(pw * FPW + i) * 64]), 16, 0, 0);
+  };
+  auto l1_mfma = [&](const uint4* wf, const f16x8& xh, const f16x8& xl) {
+    const f16x8 wh = __builtin_bit_cast(f16x8, wf[0]), wl = __builtin_bit_cast(f16x8, wf[1]);
+    f32x16 h = {};
+    h = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh, h, 0, 0, 0);
+    h = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl, h, 0, 0, 0);
+    h = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh, h, 0, 0, 0);
+    return h;
+  };
+  auto l1_split = [&](const f32x16& h, float rescale, f16x8* ph, f16x8* pl) {
+    uint32_t hp[8], lp[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const f32x2 y = f32x2{h[2 * p], h[2 * p + 1]} * f32x2{rescale, rescale};
+      split2h_pair(relu_raw(y.x), relu_raw(y.y), one, hp[p], lp[p]);
+    }
+    ph[0] = __builtin_bit_cast(f16x8, uint4{hp[0], hp[1], hp[2], hp[3]});
+    ph[1] = __builtin_bit_cast(f16x8, uint4{hp[4], hp[5], hp[6], hp[7]});
+    pl[0] = __builtin_bit_cast(f16x8, uint4{lp[0], lp[1], lp[2], lp[3]});
+    pl[1] = __builtin_bit_cast(f16x8, uint4{lp[4], lp[5], lp[6], lp[7]});
+  };
+
+  // observations of env column lane & 31 (inputs k = 8 (lane >> 5) + j; the constant-1 bias input
+  // at k = D), scaled by 2^ex[0] and split (load_split_obs of k_policy_forward_x3)
+  f16x8 xoh, xol;
+  int ex[3];
+  {
+    const int row = row0 + (lane & 31);
+    float x[8];
+    float m = 1.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * (lane >> 5) + j;
+      x[j] = k < D ? L.obs[row * D + k] : (k == D ? 1.0f : 0.0f);
+      m = fmaxf(m, fabsf(x[j]));
+    }
+    m = fmaxf(m, __shfl_xor(m, 32));
+    ex[0] = pm_scale_exp(m);
+    const float b1v = R1 * m;
+    ex[1] = pm_scale_exp(b1v);
+    ex[2] = pm_scale_exp(R2 * fmaxf(1.0f, b1v));
+    const float sx = pm_pow2(ex[0]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      _Float16 hi, lo;
+      split2h(x[j] * sx, hi, lo);
+      xoh[j] = hi;
+      xol[j] = lo;
+    }
+  }
+  f16x8 xh[2], xl[2];
+  uint4 w1c[2];
+  {
+    const uint4 w10[2] = {W1g[lane], W1g[64 + lane]};
+    w1c[0] = W1g[(1 * 2 + 0) * 64 + lane];
+    w1c[1] = W1g[(1 * 2 + 1) * 64 + lane];
+    l1_split(l1_mfma(w10, xoh, xol), pm_pow2(ex[1] - ex[0]) * isw1, xh, xl);
+  }
+  const float k23 = isw2 * pm_pow2(ex[2] - ex[1]), sc3 = pm_pow2(ex[2]);
+  f32x16 acc[PM_NB];
+#pragma unroll
+  for (int ob = 0; ob < PM_NB; ++ob) acc[ob] = f32x16{};
+
+  auto phase = [&](auto bufc, int ib, bool fold) {
+    constexpr int B = decltype(bufc)::value;
+    uint4* cur_lds = B ? L.c1 : L.c0;
+    uint4* nxt_lds = B ? L.c0 : L.c1;
+    const bool has_next = ib < PM_NB - 1 || next;
+    const int nib = (ib + 1) & (PM_NB - 1);
+    pol_sync(L.bar, target, L.err);  // chunk ib landed in every policy wave's share
+    if (has_next) stage(nib, nxt_lds);
+    const bool pipe = !fold;
+    f32x16 hn;
+    f16x8 xh2[2], xl2[2];
+    const uint4* Lc = cur_lds + lane;
+    uint4 ring[3][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      ring[0][p] = Lc[p * 64];
+      ring[1][p] = Lc[(2 + p) * 64];
+    }
+#pragma unroll
+    for (int st = 0; st < 2 * PM_NB; ++st) {
+      const int ob = st >> 1, s = st & 1;
+      if (st + 2 < 2 * PM_NB) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) ring[(st + 2) % 3][p] = Lc[((st + 2) * 2 + p) * 64];
+      }
+      const uint4* cur = ring[st % 3];
+      if (pipe && st == 0) {
+        hn = l1_mfma(w1c, xoh, xol);
+        if (ib + 2 < PM_NB) {
+          w1c[0] = W1g[((ib + 2) * 2 + 0) * 64 + lane];
+          w1c[1] = W1g[((ib + 2) * 2 + 1) * 64 + lane];
+        }
+      }
+      if (pipe && st == 3) l1_split(hn, pm_pow2(ex[1] - ex[0]) * isw1, xh2, xl2);
+      uint4 w3f[4];
+      f32x4 b2f[4];
+      if (fold && s == 1) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          w3f[q] = L.w3[(ob * 4 + q) * 64 + lane];
+          // registers 4q .. 4q + 3 of block ob hold hidden units ob*32 + 8q + 4 (lane >> 5) + 0..3
+          b2f[q] = *reinterpret_cast<const f32x4*>(L.b2 + ob * 32 + 8 * q + 4 * (lane >> 5));
+        }
+      }
+      const f16x8 wh = __builtin_bit_cast(f16x8, cur[0]);
+      const f16x8 wl = __builtin_bit_cast(f16x8, cur[1]);
+      {
+        f32x16 acc_ob = acc[ob];
+        acc_ob = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh[s], acc_ob, 0, 0, 0);
+        acc_ob = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl[s], acc_ob, 0, 0, 0);
+        acc_ob = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh[s], acc_ob, 0, 0, 0);
+        acc[ob] = acc_ob;
+      }
+      if (fold && s == 1) {  // H2 block ob final: bias, ReLU, rescale, split, layer 3
+        uint32_t hp[8], lp[8];
+        const f32x2 k2 = {k23, k23}, s2 = {sc3, sc3};
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+          const int r = 2 * p;
+          const f32x2 bs = f32x2{b2f[r >> 2][r & 3], b2f[r >> 2][(r & 3) + 1]} * s2;
+          const f32x2 y = __builtin_elementwise_fma(f32x2{acc[ob][r], acc[ob][r + 1]}, k2, bs);
+          split2h_pair(relu_raw(y.x), relu_raw(y.y), one, hp[p], lp[p]);
+        }
+        const f16x8 hh[2] = {__builtin_bit_cast(f16x8, uint4{hp[0], hp[1], hp[2], hp[3]}),
+                             __builtin_bit_cast(f16x8, uint4{hp[4], hp[5], hp[6], hp[7]})};
+        const f16x8 hl[2] = {__builtin_bit_cast(f16x8, uint4{lp[0], lp[1], lp[2], lp[3]}),
+                             __builtin_bit_cast(f16x8, uint4{lp[4], lp[5], lp[6], lp[7]})};
+        f32x16 o = ob == 0 ? f32x16{} : acc[0];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const f16x8 vh = __builtin_bit_cast(f16x8, w3f[2 * ks]);
+          const f16x8 vl = __builtin_bit_cast(f16x8, w3f[2 * ks + 1]);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, hh[ks], o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, hl[ks], o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, hh[ks], o, 0, 0, 0);
+        }
+        acc[0] = o;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (pipe) {
+      xh[0] = xh2[0];
+      xh[1] = xh2[1];
+      xl[0] = xl2[0];
+      xl[1] = xl2[1];
+    }
+  };
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+#pragma unroll 1
+  for (int ib = 0; ib < PM_NB - 2; ib += 2) {
+    phase(B0{}, ib, false);
+    phase(B1{}, ib + 1, false);
+  }
+  phase(B0{}, PM_NB - 2, false);
+  phase(B1{}, PM_NB - 1, true);
+  // logits rows (registers r hold output pm_row(r, lane) of env column lane & 31), the same
+  // expression as k_policy_forward_x3's store
+  const float iu = isw3 * pm_pow2(-ex[2]);
+  const int row = row0 + (lane & 31);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int oo = pm_row(r, lane);
+    if (oo < N3) L.lgt[row * N3 + oo] = acc[0][r] * iu + b3[oo];
+  }
+}
+
+// ------------------------------------------------------------------ env waves
+template <class Env>
+struct EnvLane {  // one env's persistent state, held in registers across the horizon
+  float s[Env::S];
+  double xs[Env::XS > 0 ? Env::XS : 1];
+  int k, len, pos;
+  uint32_t ctr;
+};
+
+// One lockstep of one env (lane) — k_rollout<Env, true>'s arithmetic: TanhGauss sample from the
+// logits in LDS, clip, env step, term/trunc, rew_plus_cost, autoreset, ring record.
+template <class Env>
+__device__ __forceinline__ void env_lockstep(const FusedArgs& a, EnvLane<Env>& v, int64_t e, bool live, int t,
+                                             const float* lg_row, float* obs_row, float4* stage, int* spos,
+                                             bool& emit, int& emit_pos) {
+  constexpr int D = Env::D, A = Env::A, RS = Env::RS;
+  constexpr int F = rec_floats(D, A);
+  const int lane = threadIdx.x & 63;
+  float rec[F];  // [0, D) unused: the stage holds obs0
+  emit = false;
+  emit_pos = 0;
+  int wpos = 0;
+  constexpr int C = F / 4, CP = C + 1;
+  float* srec = reinterpret_cast<float*>(stage + lane * CP);  // this lane's record in the stage
+  if (live) {
+    float lgt[2 * A];
+#pragma unroll
+    for (int i = 0; i < 2 * A; ++i) lgt[i] = lg_row[i];
+    // the record's pre-step observation goes to the stage now: not held across the env step
+#pragma unroll
+    for (int i = 0; i < D; ++i) srec[i] = obs_row[i];
+    const float noise = a.act_noise ? a.act_noise[t] : 0.0f;
+    double rowv[Env::ROWN > 0 ? Env::ROWN : 1];
+    if constexpr (Env::ROWN > 0) {
+      typedef double f64x2 __attribute__((ext_vector_type(2)));
+      const f64x2* rp = reinterpret_cast<const f64x2*>(a.tab + (int64_t)(v.k + 1) * Env::ROWN);
+#pragma unroll
+      for (int i = 2; i < Env::ROWN; i += 2) {
+        const f64x2 q = rp[i / 2];
+        rowv[i] = q[0];
+        rowv[i + 1] = q[1];
+      }
+    }
+    const Rng rng = make_rng(a.seed, (uint64_t)e, v.ctr);
+    float u[A];
+    float logp;
+    {
+      float nz[4];
+      rng.normal4f_fast(0, nz);
+      float lg = -0.0f, lt = -0.0f;
+#pragma unroll
+      for (int i = 0; i < A; ++i) {
+        const float mu = lgt[i];
+        const float c = fminf(fmaxf(lgt[A + i], a.log_std_lo), a.log_std_hi);
+        const float sd = __builtin_amdgcn_exp2f(c * 1.44269504088896341f);
+        const float log_sd = c;
+        const float z = mu + sd * nz[i];
+        const float df = z - mu;
+        lg = lg + ((-(df * df) * __builtin_amdgcn_rcpf(2.0f * (sd * sd)) - log_sd) - 0.918938533204672742f);
+        const float tt = __builtin_amdgcn_exp2f(-2.88539008177792682f * fabsf(z));
+        const float th = copysignf((1.0f - tt) * __builtin_amdgcn_rcpf(1.0f + tt), z);
+        lt = lt + __builtin_amdgcn_logf(1.000001f - th * th) * 0.693147180559945309f;
+        const float lo = Env::act_lo(i), hi = Env::act_hi(i);
+        const float half = (hi - lo) / 2.0f, mid = (hi + lo) / 2.0f;
+        float act = half * th + mid;
+        if (a.act_noise) act = act + noise;
+        act = fminf(fmaxf(act, lo), hi);
+        u[i] = act;
+      }
+      logp = (lg - lt) - a.log_half_sum;
+    }
+#ifndef MH_FUSED_EXP_NO_TRACE
+    if (a.act_out) {
+#pragma unroll
+      for (int i = 0; i < A; ++i) a.act_out[((int64_t)t * a.E + e) * A + i] = u[i];
+    }
+    if (a.logp_out) a.logp_out[(int64_t)t * a.E + e] = logp;
+#endif
+    float obs2[D], r;
+    if constexpr (Env::ROWN > 0)
+      Env::step_row(v.s, v.xs, rowv, u, obs2, &r);
+    else
+      Env::step(v.s, v.xs, v.k, u, a.tab, obs2, &r);
+    bool term = false;
+#pragma unroll
+    for (int i = 0; i < D; ++i) term = term || (obs2[i] < Env::obs_lo(i)) || (obs2[i] > Env::obs_hi(i));
+    int k1 = v.k + 1;
+    const bool trunc = k1 >= MAX_STEP;
+    const bool done = term || trunc;
+    float sq[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) sq[i] = obs2[i] * obs2[i];
+    const float cost = np_sum<D>(sq) * a.cost_scale;
+    const float rew = r * a.reward_scale;
+    float obsn[D];
+    if (done) {
+      float rs[RS];
+      ResetDraw<Env>::draw(rng, rs);
+      Env::reset_from(rs, v.s, v.xs, a.tab, obsn);
+      k1 = 0;
+    } else {
+#pragma unroll
+      for (int i = 0; i < D; ++i) obsn[i] = obs2[i];
+    }
+    v.k = k1;
+    v.ctr = v.ctr + 1u;
+#pragma unroll
+    for (int i = 0; i < D; ++i) obs_row[i] = obsn[i];
+#pragma unroll
+    for (int i = 0; i < A; ++i) rec[D + i] = u[i];
+#pragma unroll
+    for (int i = 0; i < D; ++i) rec[D + A + i] = obs2[i];
+    rec[2 * D + A + 0] = rew;
+    rec[2 * D + A + 1] = cost;
+    rec[2 * D + A + 2] = done ? 1.0f : 0.0f;
+    rec[2 * D + A + 3] = logp;
+#pragma unroll
+    for (int i = 2 * D + A + 4; i < F; ++i) rec[i] = 0.0f;
+    const int n = a.n, R = a.R;
+    wpos = v.pos;
+    v.pos = v.pos + 1 == R ? 0 : v.pos + 1;
+    v.len = v.len + 1 < n ? v.len + 1 : n;
+    emit = (v.len == n);
+    emit_pos = v.pos - n < 0 ? v.pos - n + R : v.pos - n;
+    if (done) v.len = 0;
+  }
+  // ring record: transposed through this wave's LDS staging so each store instruction writes
+  // whole records (k_rollout's ring store); its first D floats (obs0) are already there
+#pragma unroll
+  for (int i = D; i < F; ++i) srec[i] = rec[i];
+  spos[lane] = wpos;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int64_t e0 = e - lane;
+  const int64_t nrec = e0 < a.E ? (a.E - e0 < 64 ? a.E - e0 : 64) : 0;
+  const int R = a.R;
+  const __amdgpu_buffer_rsrc_t rr =
+      __builtin_amdgcn_make_buffer_rsrc(a.ring + e0 * R * F, (short)0, (int)(nrec * R * F * 4), 0x00020000);
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  float4 vv[C];
+  int off[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) {
+    const int c = j * 64 + lane;
+    const int rr_ = c / C, q = c % C;
+    vv[j] = stage[rr_ * CP + q];
+    off[j] = ((rr_ * R + spos[rr_]) * F + 4 * q) * 4;
+  }
+#pragma unroll
+  for (int j = 0; j < C; ++j) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4v, vv[j]), rr, off[j], 0, 0);
+  // the stage is rewritten by the next lockstep of a wave sharing it only after a workgroup
+  // barrier; within this wave the reads above complete before its next writes (in order)
+}
+
+// ------------------------------------------------------------------ the kernel
+template <class Env>
+__global__ __launch_bounds__(FUSED_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k_sample_fused(FusedArgs a) {
+  constexpr int D = Env::D, A = Env::A, S = Env::S, XS = Env::XS;
+  constexpr int N3C = 2 * A;
+  constexpr int F = rec_floats(D, A), CP = F / 4 + 1;
+  __shared__ uint4 lds0[PM_X3_FRAGS * 64];
+  __shared__ uint4 lds1[PM_X3_FRAGS * 64];
+  __shared__ uint4 lds_w3[PM_NB * 4 * 64];
+  __shared__ float lds_b2[PM_H];
+  __shared__ float s_obs[FUSED_ENVS * D];
+  __shared__ float s_lgt[FUSED_ENVS * N3C];
+  __shared__ float4 s_stage[2][64 * CP];
+  __shared__ int s_spos[2][64];
+  __shared__ uint32_t s_bar;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t E = a.E;
+  const int64_t base = (int64_t)blockIdx.x * FUSED_ENVS;
+  const int H = a.H;
+
+  // ---- prologue: the workgroup's observations into LDS (rows past E: zeros), the policy's
+  // fold operands and layer-2 bias, chunk 0 of W2
+  for (int i = threadIdx.x; i < FUSED_ENVS * D; i += FUSED_THREADS) {
+    const int64_t g = base * D + i;
+    s_obs[i] = g < E * D ? a.obs[g] : 0.0f;
+  }
+  if (threadIdx.x == 0) s_bar = 0u;
+  const bool pol = w < 4;
+  if (pol) {
+    const uint4* w3g = reinterpret_cast<const uint4*>(a.P + pm_off_w3x3(a.K1));
+    constexpr int FOPW = PM_NB * 4 / 4;
+#pragma unroll
+    for (int i = 0; i < FOPW; ++i) {
+      const int r = w * FOPW + i;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(w3g + r * 64 + lane),
+                                       (void __attribute__((address_space(3)))*)(&lds_w3[r * 64]), 16, 0, 0);
+    }
+    // compact b2 from the packed [ob][lane][16] copy: lanes 0 and 32 of each block hold all 32 rows
+    const float* b2p = a.P + pm_off_b2(a.K1);
+    for (int q = threadIdx.x; q < PM_NB * 2 * 16; q += 256) {
+      const int r = q & 15, l = ((q >> 4) & 1) * 32, ob = q >> 5;
+      lds_b2[ob * 32 + pm_row(r, l)] = b2p[((int64_t)ob * 64 + l) * 16 + r];
+    }
+    const uint4* W2g = reinterpret_cast<const uint4*>(a.P + pm_off_w2x3(a.K1));
+    constexpr int FPW = PM_X3_FRAGS / 4;
+#pragma unroll
+    for (int i = 0; i < FPW; ++i)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(W2g + (w * FPW + i) * 64 + lane),
+                                       (void __attribute__((address_space(3)))*)(&lds0[(w * FPW + i) * 64]), 16, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's fold operands landed before the barrier
+  }
+  __syncthreads();
+
+#ifdef MH_FUSED_EXP_NO_POLICY  // cost-attribution experiment only
+  if (false) {
+#else
+  if (pol) {
+#endif
+    // ================= policy waves: 2H passes (H1 first, then H0 / H1 alternating)
+    PolicyLds L{lds0, lds1, lds_w3, lds_b2, s_obs, s_lgt, &s_bar, a.err};
+    uint32_t target = 0;
+    const int total = 2 * H;
+    int pass = 0;
+    policy_pass<D>(a, L, w, FUSED_ENVS / 2 + w * 32, ++pass < total, target);
+    __syncthreads();
+    for (int t = 0; t < H; ++t) {
+      policy_pass<D>(a, L, w, w * 32, ++pass < total, target);  // A(t): H0
+      __syncthreads();
+      if (t < H - 1) policy_pass<D>(a, L, w, FUSED_ENVS / 2 + w * 32, ++pass < total, target);  // B(t): H1
+      __syncthreads();
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+  } else {
+#ifdef MH_FUSED_EXP_NO_ENV  // cost-attribution experiment only
+    if (false)
+#endif
+    {
+    // ================= env waves: one env per lane, state in registers across the horizon
+    const int ew = w - 4;             // 0, 1: half H0; 2, 3: half H1
+    const int half = ew >> 1;
+    const int row = ew * 64 + lane;   // workgroup-local env row
+    const int64_t e = base + row;
+    const bool live = e < E;
+    EnvLane<Env> v;
+    if (MH_FUSED_STATE_IN_REGS && live) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) v.s[i] = a.state[(int64_t)i * E + e];
+#pragma unroll
+      for (int i = 0; i < XS; ++i) v.xs[i] = a.xstate[(int64_t)i * E + e];
+      v.k = a.steps[e];
+      v.ctr = a.ctr[e];
+      v.len = a.ring_len[e];
+      v.pos = a.ring_pos[e];
+    }
+    const int NW = (int)((E + 63) / 64);
+    const int gw = (int)(e / 64);
+    float4* stage = s_stage[ew & 1];
+    int* spos = s_spos[ew & 1];
+    auto step = [&](int t) {
+      bool emit;
+      int emit_pos;
+#if !MH_FUSED_STATE_IN_REGS
+      // the env's state through the cache hierarchy each lockstep (what k_rollout does): held in
+      // registers across the horizon instead, the Quad step's live set spills
+      if (live) {
+#pragma unroll
+        for (int i = 0; i < S; ++i) v.s[i] = a.state[(int64_t)i * E + e];
+#pragma unroll
+        for (int i = 0; i < XS; ++i) v.xs[i] = a.xstate[(int64_t)i * E + e];
+        v.k = a.steps[e];
+        v.ctr = a.ctr[e];
+        v.len = a.ring_len[e];
+        v.pos = a.ring_pos[e];
+      }
+#endif
+      env_lockstep<Env>(a, v, e, live, t, s_lgt + row * N3C, s_obs + row * D, stage, spos, emit, emit_pos);
+#if !MH_FUSED_STATE_IN_REGS
+      if (live) {
+#pragma unroll
+        for (int i = 0; i < S; ++i) a.state[(int64_t)i * E + e] = v.s[i];
+#pragma unroll
+        for (int i = 0; i < XS; ++i) a.xstate[(int64_t)i * E + e] = v.xs[i];
+        a.steps[e] = v.k;
+        a.ctr[e] = v.ctr;
+        a.ring_len[e] = v.len;
+        a.ring_pos[e] = v.pos;
+      }
+#endif
+      const unsigned long long m = __ballot(emit);
+      if (base + ew * 64 < E) {
+        if (lane == 0) a.emit_count[(int64_t)t * NW + gw] = __popcll(m);
+        if (emit) a.emit_list[(int64_t)t * E + (int64_t)gw * 64 + __popcll(m & ((1ull << lane) - 1ull))] =
+            lane | (emit_pos << 6);
+      }
+    };
+    __syncthreads();  // the policy's first pass (H1)
+    // phases A(t) (half H1 steps) and B(t) (half H0 steps), one call site for the step's body
+    for (int ph = 0; ph < 2 * H; ++ph) {
+      if ((ph & 1) == (half ^ 1)) step(ph >> 1);
+      __syncthreads();
+    }
+    if (MH_FUSED_STATE_IN_REGS && live) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) a.state[(int64_t)i * E + e] = v.s[i];
+#pragma unroll
+      for (int i = 0; i < XS; ++i) a.xstate[(int64_t)i * E + e] = v.xs[i];
+      a.steps[e] = v.k;
+      a.ctr[e] = v.ctr;
+      a.ring_len[e] = v.len;
+      a.ring_pos[e] = v.pos;
+    }
+    }
+  }
+  // ---- epilogue: the observations after the horizon (both halves final after the last B phase)
+  for (int i = threadIdx.x; i < FUSED_ENVS * D; i += FUSED_THREADS) {
+    const int64_t g = base * D + i;
+    if (g < E * D) a.obs[g] = s_obs[i];
+  }
+}
+
+// ------------------------------------------------------------------ horizon emission
+// Every window of the horizon, in the reference's order (lockstep major; env index within a
+// lockstep), into the store rows after the cursor (FIFO wrap; windows older than the last
+// `capacity` of this horizon are skipped as overwritten): one thread per (window, slot) record,
+// like k_emit_fused. The (lockstep, wave) counts are scanned by every workgroup in LDS.
+template <int D, int A>
+__global__ __launch_bounds__(256) void k_emit_horizon(HorizonEmitArgs a) {
+  constexpr int F = rec_floats(D, A);
+  extern __shared__ int offs[];  // [H * NBK + 1] exclusive prefix over (lockstep, 256-env block)
+  const int NW = (int)((a.E + 63) / 64);
+  const int NBK = (NW + 3) / 4;
+  const int NC = a.H * NBK;
+  __shared__ int wsum[4];
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  auto cell_count = [&](int c) {
+    const int ts = c / NBK, b = c - ts * NBK;
+    const int32_t* cnt = a.emit_count + (int64_t)ts * NW;
+    int s = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s += 4 * b + q < NW ? cnt[4 * b + q] : 0;
+    return s;
+  };
+  const int per = (NC + 255) / 256;
+  const int lo = min(NC, t * per), hi = min(NC, lo + per);
+  int local = 0;
+  for (int i = lo; i < hi; ++i) local += cell_count(i);
+  int incl = local;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int v = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += v;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  int wbase = 0, all = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    wbase += q < wave ? wsum[q] : 0;
+    all += wsum[q];
+  }
+  int run = wbase + incl - local;
+  for (int i = lo; i < hi; ++i) {
+    offs[i] = run;
+    run += cell_count(i);
+  }
+  if (t == 0) offs[NC] = all;
+  __syncthreads();
+  const int64_t total = offs[NC];
+  const int64_t M = a.capacity;
+  const int64_t c0 = a.cursor[0];
+  const int64_t start = total > M ? total - M : 0;  // older windows are overwritten this horizon
+  const int n = a.n, R = a.R;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + t; q < (total - start) * n; q += (int64_t)gridDim.x * 256) {
+    const int64_t gl = q / n;
+    const int j = (int)(q - gl * n);
+    const int64_t g = start + gl;
+    int bl = 0, bh = NC - 1;  // the (lockstep, block) cell holding window g: largest offs <= g
+    while (bl < bh) {
+      const int mid = (bl + bh + 1) >> 1;
+      if ((int64_t)offs[mid] <= g) bl = mid; else bh = mid - 1;
+    }
+    const int ts = bl / NBK, b = bl - ts * NBK;
+    int r = (int)(g - offs[bl]);
+    int gw = 4 * b;  // the block's wave holding it (waves in env order)
+    const int32_t* cnt = a.emit_count + (int64_t)ts * NW;
+    while (gw + 1 < NW && gw + 1 < 4 * b + 4 && r >= cnt[gw]) r -= cnt[gw++];
+    const int packed = a.emit_list[(int64_t)ts * a.E + (int64_t)gw * 64 + r];
+    const int64_t e = (int64_t)gw * 64 + (packed & 63);
+    int slot = (packed >> 6) + j;
+    slot = slot >= R ? slot - R : slot;
+    float rec[F];
+    const float4* src = reinterpret_cast<const float4*>(a.ring + (e * R + slot) * (int64_t)F);
+#pragma unroll
+    for (int i = 0; i < F / 4; ++i) {
+      const float4 v = src[i];
+      rec[4 * i] = v.x;
+      rec[4 * i + 1] = v.y;
+      rec[4 * i + 2] = v.z;
+      rec[4 * i + 3] = v.w;
+    }
+    const int64_t o = ((c0 + g) % M) * n + j;
+#pragma unroll
+    for (int i = 0; i < D; ++i) a.obs[o * D + i] = rec[i];
+#pragma unroll
+    for (int i = 0; i < A; ++i) a.act[o * A + i] = rec[D + i];
+#pragma unroll
+    for (int i = 0; i < D; ++i) a.obs2[o * D + i] = rec[D + A + i];
+    a.rew[o] = rec[2 * D + A];
+    a.cost[o] = rec[2 * D + A + 1];
+    a.done[o] = rec[2 * D + A + 2];
+    a.logp[o] = rec[2 * D + A + 3];
+  }
+  if (blockIdx.x == 0 && t == 0) {
+    a.cursor[0] = (c0 + total) % M;
+    const int64_t sz = a.cursor[1] + total;
+    a.cursor[1] = sz < M ? sz : M;
+    a.cursor[2] += total;
+    a.cursor[3] = total;
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+template <class Env>
+static hipError_t launch_fused_t(const FusedArgs& a, const HorizonEmitArgs& ea, hipStream_t st) {
+  const int grid = (int)((a.E + FUSED_ENVS - 1) / FUSED_ENVS);
+  k_sample_fused<Env><<<grid, FUSED_THREADS, 0, st>>>(a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || ea.obs == nullptr) return e;
+  const int64_t want = (a.E * a.n + 255) / 256;
+  const int eg = (int)(want < 1 ? 1 : (want > 2048 ? 2048 : want));
+  const size_t shm = (size_t)(fused_emit_cells(a.E, a.H) + 1) * sizeof(int);
+  k_emit_horizon<Env::D, Env::A><<<eg, 256, shm, st>>>(ea);
+  return hipGetLastError();
+}
+
+hipError_t launch_sample_fused(int env_id, const FusedArgs& a, const HorizonEmitArgs& ea, hipStream_t st) {
+  switch (env_id) {
+    case ENV_VANDERPOL: return launch_fused_t<VanderPol>(a, ea, st);
+    case ENV_PENDULUM: return launch_fused_t<Pendulum>(a, ea, st);
+    case ENV_DUCTEDFAN: return launch_fused_t<DuctedFan>(a, ea, st);
+    case ENV_TWOLINK: return launch_fused_t<TwoLink>(a, ea, st);
+    case ENV_SINGLETRACKCAR: return launch_fused_t<SingleTrackCar>(a, ea, st);
+    case ENV_QUADTRACKING: return launch_fused_t<QuadTracking>(a, ea, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace mh

@@ -94,21 +94,6 @@ class HipVectorEnv:
         except Exception:
             pass
 
-
-# Handles released while a HIP graph is being captured (a finaliser run by the garbage collector
-# inside someone else's capture): hipFree is illegal there, so their destruction waits for the
-# next release outside a capture.
-_PENDING = []
-
-
-def _destroy_when_safe(h):
-    capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
-    _PENDING.append(h)
-    if capturing:
-        return
-    while _PENDING:
-        N.lib().mh_env_destroy(_PENDING.pop())
-
     def _f32(self, x, cols, name):
         if x is None:
             return None
@@ -162,6 +147,21 @@ def _destroy_when_safe(h):
             sp = torch.as_tensor(steps, dtype=torch.int32, device=dev).contiguous()
             N.require_device(sp, "steps", torch.int32, self.num_envs, dev)
         N.check(N.lib().mh_env_set_state(h, N.ptr(st), N.ptr(xs), N.ptr(sp), N.stream_of(dev)), "mh_env_set_state")
+
+
+# Handles released while a HIP graph is being captured (a finaliser run by the garbage collector
+# inside someone else's capture): hipFree is illegal there, so their destruction waits for the
+# next release outside a capture.
+_PENDING = []
+
+
+def _destroy_when_safe(h):
+    capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+    _PENDING.append(h)
+    if capturing:
+        return
+    while _PENDING:
+        N.lib().mh_env_destroy(_PENDING.pop())
 
 
 def make_env(env_id, seed, idx, capture_video=False, run_name=""):

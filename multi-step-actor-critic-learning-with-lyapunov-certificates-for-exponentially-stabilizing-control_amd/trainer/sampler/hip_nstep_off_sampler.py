@@ -61,17 +61,27 @@ class HipNstepOffSampler:
         # (mh_rollout_step_deferred); False: a separate emission launch after every step
         self.deferred_emission = bool(kwargs.get("sampler_deferred_emission", True))
         self.use_fused_policy = bool(kwargs.get("sampler_fused_policy", True))
+        # the whole horizon as one persistent kernel (mh_sample_horizon) when the fused policy
+        # applies; False: per lockstep, policy kernel + lockstep kernel (the same values)
+        self.fused_horizon = bool(kwargs.get("sampler_fused_horizon", True)) and self.use_fused_policy
         self._packed = None
         self._h = self.envs.handle()
         N.check(N.lib().mh_nstep_attach(self._h, self.n_step, self.reward_scale, self.cost_scale), "mh_nstep_attach")
+        if self.fused_horizon:
+            # rings long enough that a horizon's windows are intact until its emission launch
+            rc = N.lib().mh_nstep_reserve(self._h, self.n_step + self.horizon - 1)
+            if rc != 0:
+                self.fused_horizon = False
         # GaussNoise (explore_noise.py:3-9; base.py:83-88,136-137): ONE scalar
         # np.random.normal(mean, std) per lockstep step, added to every action before the clip.
         # Drawn on the device into a 1-float tensor (capturable), read by the rollout kernel.
+        # One scalar per lockstep: the horizon's H values are drawn at its start into a device
+        # tensor (capturable); lockstep t reads element t.
         self._noise = None
         if self.noise_params is not None:
             self._noise_mean = float(self.noise_params["mean"])
             self._noise_std = float(self.noise_params["std"])
-            self._noise = torch.zeros(1, dtype=torch.float32, device=self.device)
+            self._noise = torch.zeros(max(1, self.horizon), dtype=torch.float32, device=self.device)
             N.check(N.lib().mh_env_set_action_noise(self._h, N.ptr(self._noise)), "mh_env_set_action_noise")
         self.obs, _ = self.envs.reset(seed=None)
         self._bound = None
@@ -201,8 +211,12 @@ class HipNstepOffSampler:
         if self._noise is not None:
             self._noise.normal_(self._noise_mean, self._noise_std)
 
-    def _policy_step(self, store, fused=False, act_out=None, logp_out=None):
-        self._draw_noise()
+    def _noise_at(self, t):
+        if self._noise is not None:
+            N.check(N.lib().mh_env_set_action_noise(self._h, N.ptr(self._noise[t:t + 1])), "mh_env_set_action_noise")
+
+    def _policy_step(self, store, fused=False, act_out=None, logp_out=None, t=0):
+        self._noise_at(t)
         logits, raw = self._policy_fused() if fused else self._policy_raw()
         pol = self.networks.policy
         N.check(N.lib().mh_nstep_set_log_std_clamp(self._h, int(raw), float(getattr(pol, "min_log_std", -20.0)),
@@ -210,10 +224,25 @@ class HipNstepOffSampler:
         self._lockstep(store, logits=logits, deferred=self.deferred_emission, act_out=act_out, logp_out=logp_out)
         return logits
 
-    def _horizon(self, store):
+    def _fused_horizon_ok(self, fused):
+        return fused and self.fused_horizon and self.envs.obs_dim <= 15
+
+    def _horizon(self, store, act_out=None, logp_out=None):
         fused = self._pack_policy()
-        for _ in range(self.horizon):
-            self._policy_step(store, fused)
+        self._draw_noise()
+        if self._fused_horizon_ok(fused):
+            # policy -> sample -> env step -> ring push for every lockstep in ONE persistent
+            # kernel, then one launch emits the horizon's windows (csrc/sample_fused.hip)
+            pol = self.networks.policy
+            N.check(N.lib().mh_nstep_set_log_std_clamp(self._h, 1, float(getattr(pol, "min_log_std", -20.0)),
+                                                       float(getattr(pol, "max_log_std", 1.0))), "log_std clamp")
+            N.check(N.lib().mh_sample_horizon(self._h, N.ptr(self._packed), self.envs.obs_dim, 2 * self.envs.act_dim,
+                                              N.ptr(self.obs), self.horizon, ctypes.byref(store.ws), N.ptr(self._noise),
+                                              N.ptr(act_out), N.ptr(logp_out), N.stream_of(self.device)),
+                    "mh_sample_horizon")
+            return
+        for t in range(self.horizon):
+            self._policy_step(store, fused, t=t)
         self._flush()  # the last step's windows: the store is complete when sample() returns
 
     def _graph_for(self, store):
@@ -290,6 +319,7 @@ class HipNstepOffSampler:
         N.check(N.lib().mh_rollout_set_trace(self._h, *ptrs), "mh_rollout_set_trace")
         try:
             with torch.no_grad():
+                self._draw_noise()
                 return self._policy_step(self._bound, self._pack_policy(), act_out=act_out, logp_out=logp_out)
         finally:
             N.check(N.lib().mh_rollout_set_trace(self._h, None, None, None, None), "mh_rollout_set_trace")

@@ -32,6 +32,7 @@ class OnSampler(HipNstepOffSampler):
     def __init__(self, **kwargs):
         kw = dict(kwargs)
         kw["n_step"] = 1  # no n-step deques on this path (the rings stay unused)
+        kw["sampler_fused_horizon"] = False  # trajectory columns, not windows: its own horizon loop
         super().__init__(**kw)
         self.gamma = kwargs["gamma"]
         self.gae_lambda = kwargs["gae_lambda"]

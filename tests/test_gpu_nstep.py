@@ -22,7 +22,7 @@ TOL = dict(rtol=1e-5, atol=1e-5)
 TRACES = sorted(glob.glob(os.path.join(G, "nstep_*.npz")))
 
 
-def _run_trace(path, capacity=None, tile=1, check_obs=False, deferred=False, g=None):
+def _run_trace(path, capacity=None, tile=1, check_obs=False, deferred=False, g=None, ring_slots=None):
     """Replay a reference _n_step trace through the fused rollout (injected actions); deferred:
     through mh_rollout_step_deferred (each step's windows emitted by the next step's emitter
     waves) and a final mh_rollout_flush. `g` overrides the fixture (a sliced trace)."""
@@ -39,6 +39,8 @@ def _run_trace(path, capacity=None, tile=1, check_obs=False, deferred=False, g=N
     env = HipVectorEnv(name, E, seed=1)
     h = env.handle()
     N.check(N.lib().mh_nstep_attach(h, n, 100.0, 100.0), "attach")
+    if ring_slots is not None:  # rings longer than n (the fused horizon sampler's layout)
+        N.check(N.lib().mh_nstep_reserve(h, n + ring_slots), "reserve")
     obs, _ = env.reset(reset_states=tl(g["init_reset"]))
     env.set_state(None, None, tl(g["init_steps"]))
     total = int(g["counts"].sum()) * tile
@@ -88,6 +90,17 @@ def test_windows_match_reference_sampler(path, deferred):
     for k in KEYS:
         np.testing.assert_allclose(buf.n_step_buf[k][:total].cpu().numpy(), g["w_" + k], **TOL, err_msg=k)
     assert not buf.n_step_buf["done"][:total, :-1].any()
+
+
+@pytest.mark.parametrize("extra", [1, 19])
+@pytest.mark.parametrize("deferred", [False, True], ids=["immediate", "deferred"])
+@pytest.mark.parametrize("path", TRACES, ids=os.path.basename)
+def test_windows_with_longer_rings(path, deferred, extra):
+    """Rings of n + extra slots (mh_nstep_reserve) give the same windows, in the same order."""
+    g, buf, total, _ = _run_trace(path, deferred=deferred, ring_slots=extra)
+    assert buf.size == total and int(buf.cursor[2]) == total
+    for k in KEYS:
+        np.testing.assert_allclose(buf.n_step_buf[k][:total].cpu().numpy(), g["w_" + k], **TOL, err_msg=k)
 
 
 @pytest.mark.parametrize("deferred", [False, True], ids=["immediate", "deferred"])

@@ -69,3 +69,10 @@ def test_approx_container_builds_on_cpu():
     keys = set(net.state_dict())
     assert {"log_alpha", "policy.act_high_lim", "q1.q.0.weight", "q2_target.q.4.bias", "lyapunov.lya.4.weight",
             "policy.policy.4.weight"} <= keys
+
+
+def test_hip_vector_env_exposes_the_vector_env_api():
+    """The device vector env's gym-like surface (no GPU needed to inspect it)."""
+    from msacl_amd.env.hip_vector_env import HipVectorEnv
+    for m in ("reset", "step", "get_state", "set_state", "close", "handle"):
+        assert callable(getattr(HipVectorEnv, m, None)), m
