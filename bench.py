@@ -204,6 +204,25 @@ def main():
         N.lib().mh_rollout_step_deferred(h, N.ptr(logits), None, None, None, N.ptr(sampler.obs),
                                          ctypes.byref(buffer.ws), None, None, st)
 
+    fused_h = bool(have_fused and getattr(sampler, "_fused_horizon_ok", None) and sampler._fused_horizon_ok(True))
+    H = sampler.horizon
+    noise_ptr = N.ptr(sampler._noise) if getattr(sampler, "_noise", None) is not None else None
+
+    def k_fused():  # the fused horizon kernel alone (its windows are not emitted)
+        N.lib().mh_sample_horizon(h, N.ptr(sampler._packed), sampler.envs.obs_dim, 2 * sampler.envs.act_dim,
+                                  N.ptr(sampler.obs), H, None, noise_ptr, None, None, st)
+
+    def k_fused_emit():  # the sampler's horizon: the fused kernel + k_emit_horizon into the store
+        N.lib().mh_sample_horizon(h, N.ptr(sampler._packed), sampler.envs.obs_dim, 2 * sampler.envs.act_dim,
+                                  N.ptr(sampler.obs), H, ctypes.byref(buffer.ws), noise_ptr, None, None, st)
+
+    t_fh = t_fhe = None
+    if fused_h:
+        t_fh = time_launches(k_fused, 5) * 1e-3
+        w0 = int(buffer.cursor[2].item())
+        t_fhe = time_launches(k_fused_emit, 5, warm=0) * 1e-3
+        torch.cuda.synchronize()
+        windows_fh = (int(buffer.cursor[2].item()) - w0) / 5
     t_pol = time_launches(k_policy, reps) * 1e-3 if have_fused else None
     t_step = time_launches(k_roll, reps) * 1e-3
     win1 = int(buffer.cursor[2].item())
@@ -237,9 +256,28 @@ def main():
                         "note": "separate emission launch (mh_rollout_step), not used by the sampler"},
         "method": f"HIP events around {reps} back-to-back launches after a GPU spin; emit = (rollout+emit) - rollout",
     }
+    D0, A2 = sampler.envs.obs_dim, 2 * sampler.envs.act_dim
+    flops_lockstep = 2.0 * a.envs * (D0 * 256 + 256 * 256 + 256 * A2)
+    if fused_h:
+        # the fused horizon kernel: per lockstep the policy's split-f16 MFMA work (3 f16 products
+        # per f32-equivalent product) beside the env step; HBM traffic per horizon: the ring
+        # records and the per-horizon state / observation load + store (W2 is re-read from L2)
+        bytes_fh = a.envs * (H * F * 4 + 2 * (S * 4 + XS * 8 + 16) + 2 * D_ * 4)
+        bytes_win = windows_fh * bytes_window
+        t_emit_h = max(t_fhe - t_fh, 1e-9)
+        kernels["sample_fused"] = {
+            "avg_us_per_horizon": round(t_fh * 1e6, 2), "avg_us_per_lockstep": round(t_fh / H * 1e6, 3),
+            "f16_mfma_TFLOPs": round(3 * flops_lockstep * H / t_fh / 1e12, 1),
+            "frac_f16_mfma_peak": round(3 * flops_lockstep * H / t_fh / 1e12 / PEAK_F16_MFMA_TFS, 4),
+            "hbm_bytes": bytes_fh, "GBps": round(bytes_fh / t_fh / 1e9, 1),
+            "note": "k_sample_fused<Env>: the whole horizon (policy MLP + sample + env step + ring push for "
+                    f"{H} locksteps) in one persistent launch, without its window emission"}
+        kernels["emit_horizon"] = {"avg_us": round(t_emit_h * 1e6, 2), "windows": windows_fh, "bytes": bytes_win,
+                                   "GBps": round(bytes_win / t_emit_h / 1e9, 1),
+                                   "frac": round(bytes_win / t_emit_h / 1e9 / PEAK_HBM_GBS, 4),
+                                   "note": "k_emit_horizon: the horizon's windows, ring -> replay store"}
     if t_pol is not None:
-        D0, A2 = sampler.envs.obs_dim, 2 * sampler.envs.act_dim
-        flops = 2.0 * a.envs * (D0 * 256 + 256 * 256 + 256 * A2)
+        flops = flops_lockstep
         # split-f16 arithmetic: every f32 product is 3 f16 MFMA products (hi.hi + hi.lo + lo.hi),
         # so the kernel's own ceiling is the dense f16 peak / 3 in f32-equivalent flop/s
         kernels["policy_forward"] = {"avg_us": round(t_pol * 1e6, 3), "flops": flops,
@@ -265,8 +303,8 @@ def main():
                                           "bytes": r4["env_steps"] * r4["bytes_per_unit"], "GBps": r4["GBps"],
                                           "frac": r4["frac"],
                                           "note": "k_rollout<QuadTracking> at 4,194,304 envs (beyond the Infinity Cache)"}
-    dom = "rollout_emit"
-    ach = kernels[dom]["GBps"]
+    dom = "sample_fused" if fused_h else "rollout_emit"
+    ach = kernels[dom]["f16_mfma_TFLOPs"] if fused_h else kernels[dom]["GBps"]
     # HBM bytes per launch: PMC counters cannot be read from inside this process (rocprofv3 --pmc
     # wraps the whole command), so `traffic` is the committed measurement of this same command
     # (tools/pmc.sh: separate FETCH_SIZE / WRITE_SIZE passes, tools/pmc_summary.py applies the
@@ -286,8 +324,16 @@ def main():
                 traffic_src = f"profiles/{PMC_TRAFFIC} is for other kernel sources (stale): not reported"
         except (OSError, ValueError):
             traffic = None
-    roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_source": traffic_src}
+    if fused_h:
+        roof = {"bound": "mfma", "kernel": "k_sample_fused<%s>" % a.env, "achieved": round(ach, 1),
+                "peak": PEAK_F16_MFMA_TFS, "unit": "TFLOP/s", "frac": round(ach / PEAK_F16_MFMA_TFS, 4),
+                "traffic": traffic, "traffic_source": traffic_src,
+                "flops_note": "f16 MFMA flops of the policy's split-f16 arithmetic (3 per f32-equivalent product) "
+                              "over the fused kernel's device time; its env VALU work overlaps on the same SIMDs",
+                "hbm_GBps": kernels[dom]["GBps"]}
+    else:
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": traffic, "traffic_source": traffic_src}
     if "rollout_step_4m" in kernels:
         roof["frac_4m_envs"] = kernels["rollout_step_4m"]["frac"]
 

@@ -184,6 +184,11 @@ int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, i
  * intra-workgroup waits that timed out since mh_env_create; 0 when healthy) to DEVICE int64 `out`. */
 int mh_sample_horizon_errors(mh_env_t h, int64_t* out, void* stream);
 
+/* Diagnostics of mh_sample_horizon: later horizons also write the logits every env sampled from
+ * to DEVICE [horizon][E][2*act_dim] `logits_out` and the observation it stepped from to
+ * [horizon][E][obs_dim] `obs_out` (both NULL: off). */
+int mh_sample_horizon_debug_logits(mh_env_t h, float* logits_out, float* obs_out);
+
 /* Per-env step trace of every later mh_rollout_step / mh_rollout_step_deferred of this handle,
  * in the SAME kernel instantiation the call would run anyway (the sampling one when logits are
  * given): the pre-reset observation [E][D] (SyncVectorEnv info["final_observation"], the

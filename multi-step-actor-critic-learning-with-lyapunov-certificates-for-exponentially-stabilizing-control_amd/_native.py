@@ -85,6 +85,7 @@ _PROTOS = {
     "mh_rollout_set_trace": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mh_nstep_reserve": (ctypes.c_int, [c_vp, c_i32]),
     "mh_sample_horizon_errors": (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    "mh_sample_horizon_debug_logits": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "mh_sample_horizon": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, ctypes.POINTER(WindowStore), c_vp,
                                          c_vp, c_vp, c_vp]),
     "mh_rollout_traj_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(TrajStore), c_i32,

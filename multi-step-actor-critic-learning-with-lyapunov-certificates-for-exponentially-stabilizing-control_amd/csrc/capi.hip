@@ -77,6 +77,8 @@ struct mh_env_s {
   int hcap = 0;
   int32_t* h_count = nullptr;       // [hcap][ceil(E / 64)]
   int32_t* h_list = nullptr;        // [hcap][E]
+  float* dbg_logits = nullptr;      // mh_sample_horizon_debug_logits: [H][E][2A] logits trace
+  float* dbg_obs = nullptr;         //   and [H][E][D] pre-step observations
   // deferred emission (mh_rollout_step_deferred): the last step's windows are not yet emitted
   bool pending = false;
   int parity = 0;                   // half of block_count / emit_list the next step writes
@@ -333,6 +335,8 @@ int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, i
   a.act_out = act_out;
   a.logp_out = logp_out;
   a.err = h->meta + 7;  // meta[7]: the fused kernel's error word
+  a.lgt_out = h->dbg_logits;
+  a.obs_out = h->dbg_obs;
   mh::HorizonEmitArgs ea;
   std::memset(&ea, 0, sizeof(ea));
   ea.E = h->E;
@@ -354,6 +358,14 @@ int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, i
     ea.cursor = store->cursor;
   }
   MH_HIP(mh::launch_sample_fused(h->env_id, a, ea, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_sample_horizon_debug_logits(mh_env_t h, float* logits_out, float* obs_out) {
+  if (!h) return fail(MH_EINVAL, "mh_sample_horizon_debug_logits: null handle");
+  if ((logits_out == nullptr) != (obs_out == nullptr)) return fail(MH_EINVAL, "mh_sample_horizon_debug_logits: both or neither");
+  h->dbg_logits = logits_out;
+  h->dbg_obs = obs_out;
   return MH_OK;
 }
 

@@ -640,6 +640,51 @@ MH_HD void polar3(const float* Rin, float* Rout) {
   for (int i = 0; i < 9; ++i) Rout[i] = Rin[i];
   return;
 #endif
+#ifdef MH_EXP_POLAR_MIXED_NOBRANCH  // diagnostic experiment only: two float64 steps + the mixed one, no branches
+  {
+    double X[9], G[9];
+    for (int i = 0; i < 9; ++i) X[i] = (double)Rin[i];
+    for (int it = 0; it < 2; ++it) {
+      (void)orth_err3<double>(X, G);
+      ns3_step3(X, G);
+    }
+    (void)orth_err3<double>(X, G);
+    ns_step3_mixed(X, G);
+    for (int i = 0; i < 9; ++i) Rout[i] = (float)X[i];
+    return;
+  }
+#endif
+#ifdef MH_EXP_POLAR_F64_NOBRANCH  // diagnostic experiment only: three branch-free float64 steps
+  {
+    double X[9], G[9];
+    for (int i = 0; i < 9; ++i) X[i] = (double)Rin[i];
+    for (int it = 0; it < 3; ++it) {
+      (void)orth_err3<double>(X, G);
+      ns3_step3(X, G);
+    }
+    for (int i = 0; i < 9; ++i) Rout[i] = (float)X[i];
+    return;
+  }
+#endif
+#ifdef MH_EXP_POLAR_F32  // diagnostic experiment only: three branch-free float32 Newton-Schulz steps
+  {
+    float X[9], G[9];
+    for (int i = 0; i < 9; ++i) X[i] = Rin[i];
+    for (int it = 0; it < 3; ++it) {
+      (void)orth_err3<float>(X, G);
+      float Y[9];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+          float acc = 0.0f;
+          for (int k = 0; k < 3; ++k) acc = fmaf(X[i * 3 + k], (((k * 3 + j) % 4 == 0 ? 1.0f : 0.0f) - G[k * 3 + j]) * 0.5f, acc);
+          Y[i * 3 + j] = X[i * 3 + j] + acc;
+        }
+      for (int i = 0; i < 9; ++i) X[i] = Y[i];
+    }
+    for (int i = 0; i < 9; ++i) Rout[i] = X[i];
+    return;
+  }
+#endif
   double X[9], G[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) X[i] = (double)Rin[i];

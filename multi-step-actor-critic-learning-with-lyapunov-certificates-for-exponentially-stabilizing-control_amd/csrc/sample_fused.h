@@ -29,6 +29,8 @@ struct FusedArgs {
   float* act_out;          // [H][E][A] or null
   float* logp_out;         // [H][E] or null
   int64_t* err;            // device error word: policy-wave waits that timed out (0 when healthy)
+  float* lgt_out;          // [H][E][2A] the logits each env sampled from, or null (diagnostics)
+  float* obs_out;          // [H][E][D] the observation each env stepped from, or null (diagnostics)
 };
 
 constexpr int FUSED_ENVS = 256;   // envs per workgroup (one workgroup per CU)

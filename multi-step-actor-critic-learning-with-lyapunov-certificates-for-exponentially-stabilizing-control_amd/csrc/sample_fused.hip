@@ -31,6 +31,12 @@
 #include "rollout.h"
 #include "sample_fused.h"
 
+#ifdef MH_FUSED_EXP_NO_MFMA  // experiment: the policy pass without its MFMAs (garbage logits)
+#define MH_MFMA(a, b, c) (c)
+#else
+#define MH_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0)
+#endif
+
 #ifndef MH_FUSED_STATE_IN_REGS
 #define MH_FUSED_STATE_IN_REGS 1
 #endif
@@ -94,9 +100,9 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
   auto l1_mfma = [&](const uint4* wf, const f16x8& xh, const f16x8& xl) {
     const f16x8 wh = __builtin_bit_cast(f16x8, wf[0]), wl = __builtin_bit_cast(f16x8, wf[1]);
     f32x16 h = {};
-    h = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh, h, 0, 0, 0);
-    h = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl, h, 0, 0, 0);
-    h = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh, h, 0, 0, 0);
+    h = MH_MFMA(wl, xh, h);
+    h = MH_MFMA(wh, xl, h);
+    h = MH_MFMA(wh, xh, h);
     return h;
   };
   auto l1_split = [&](const f32x16& h, float rescale, f16x8* ph, f16x8* pl) {
@@ -201,9 +207,9 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
       const f16x8 wl = __builtin_bit_cast(f16x8, cur[1]);
       {
         f32x16 acc_ob = acc[ob];
-        acc_ob = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh[s], acc_ob, 0, 0, 0);
-        acc_ob = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl[s], acc_ob, 0, 0, 0);
-        acc_ob = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh[s], acc_ob, 0, 0, 0);
+        acc_ob = MH_MFMA(wl, xh[s], acc_ob);
+        acc_ob = MH_MFMA(wh, xl[s], acc_ob);
+        acc_ob = MH_MFMA(wh, xh[s], acc_ob);
         acc[ob] = acc_ob;
       }
       if (fold && s == 1) {  // H2 block ob final: bias, ReLU, rescale, split, layer 3
@@ -225,9 +231,9 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
         for (int ks = 0; ks < 2; ++ks) {
           const f16x8 vh = __builtin_bit_cast(f16x8, w3f[2 * ks]);
           const f16x8 vl = __builtin_bit_cast(f16x8, w3f[2 * ks + 1]);
-          o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, hh[ks], o, 0, 0, 0);
-          o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, hl[ks], o, 0, 0, 0);
-          o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, hh[ks], o, 0, 0, 0);
+          o = MH_MFMA(vl, hh[ks], o);
+          o = MH_MFMA(vh, hl[ks], o);
+          o = MH_MFMA(vh, hh[ks], o);
         }
         acc[0] = o;
       }
@@ -267,6 +273,10 @@ struct EnvLane {  // one env's persistent state, held in registers across the ho
   double xs[Env::XS > 0 ? Env::XS : 1];
   int k, len, pos;
   uint32_t ctr;
+#ifdef MH_FUSED_EXP_CHECK_OBS  // experiment: the observation this lane wrote to LDS, kept
+  float keep[Env::D];
+  int have;
+#endif
 };
 
 // One lockstep of one env (lane) — k_rollout<Env, true>'s arithmetic: TanhGauss sample from the
@@ -288,9 +298,28 @@ __device__ __forceinline__ void env_lockstep(const FusedArgs& a, EnvLane<Env>& v
     float lgt[2 * A];
 #pragma unroll
     for (int i = 0; i < 2 * A; ++i) lgt[i] = lg_row[i];
+#ifdef MH_FUSED_EXP_CHECK_OBS
+    if (v.have) {
+      bool bad = false;
+#pragma unroll
+      for (int i = 0; i < D; ++i) bad = bad || (__float_as_uint(obs_row[i]) != __float_as_uint(v.keep[i]));
+      if (bad) __hip_atomic_fetch_add(a.err + 0, (int64_t)(1 << 20), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#endif
+    if (a.lgt_out) {
+#pragma unroll
+      for (int i = 0; i < 2 * A; ++i) a.lgt_out[((int64_t)t * a.E + e) * 2 * A + i] = lgt[i];
+#pragma unroll
+      for (int i = 0; i < D; ++i) a.obs_out[((int64_t)t * a.E + e) * D + i] = obs_row[i];
+    }
     // the record's pre-step observation goes to the stage now: not held across the env step
+#ifdef MH_FUSED_DIRECT_RING
+#pragma unroll
+    for (int i = 0; i < D; ++i) rec[i] = obs_row[i];
+#else
 #pragma unroll
     for (int i = 0; i < D; ++i) srec[i] = obs_row[i];
+#endif
     const float noise = a.act_noise ? a.act_noise[t] : 0.0f;
     double rowv[Env::ROWN > 0 ? Env::ROWN : 1];
     if constexpr (Env::ROWN > 0) {
@@ -368,6 +397,11 @@ __device__ __forceinline__ void env_lockstep(const FusedArgs& a, EnvLane<Env>& v
     v.ctr = v.ctr + 1u;
 #pragma unroll
     for (int i = 0; i < D; ++i) obs_row[i] = obsn[i];
+#ifdef MH_FUSED_EXP_CHECK_OBS
+#pragma unroll
+    for (int i = 0; i < D; ++i) v.keep[i] = obsn[i];
+    v.have = 1;
+#endif
 #pragma unroll
     for (int i = 0; i < A; ++i) rec[D + i] = u[i];
 #pragma unroll
@@ -386,6 +420,14 @@ __device__ __forceinline__ void env_lockstep(const FusedArgs& a, EnvLane<Env>& v
     emit_pos = v.pos - n < 0 ? v.pos - n + R : v.pos - n;
     if (done) v.len = 0;
   }
+#ifdef MH_FUSED_DIRECT_RING  // experiment: each lane stores its own record (no LDS transposition)
+  if (live) {
+    float4* dst = reinterpret_cast<float4*>(a.ring + (e * a.R + wpos) * (int64_t)F);
+#pragma unroll
+    for (int i = 0; i < F / 4; ++i) dst[i] = make_float4(rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
+  }
+  return;
+#endif
   // ring record: transposed through this wave's LDS staging so each store instruction writes
   // whole records (k_rollout's ring store); its first D floats (obs0) are already there
 #pragma unroll
@@ -428,7 +470,11 @@ void k_sample_fused(FusedArgs a) {
   __shared__ float lds_b2[PM_H];
   __shared__ float s_obs[FUSED_ENVS * D];
   __shared__ float s_lgt[FUSED_ENVS * N3C];
+#ifdef MH_FUSED_DIRECT_RING
+  __shared__ float4 s_stage[2][1];
+#else
   __shared__ float4 s_stage[2][64 * CP];
+#endif
   __shared__ int s_spos[2][64];
   __shared__ uint32_t s_bar;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -436,6 +482,13 @@ void k_sample_fused(FusedArgs a) {
   const int64_t E = a.E;
   const int64_t base = (int64_t)blockIdx.x * FUSED_ENVS;
   const int H = a.H;
+#ifdef MH_FUSED_EXP_PAD_SCRATCH  // experiment: a larger private segment per lane
+  {
+    volatile float pad[MH_FUSED_EXP_PAD_SCRATCH];
+    pad[lane % MH_FUSED_EXP_PAD_SCRATCH] = 0.0f;
+    if (a.H < 0) a.obs[0] = pad[(lane + 1) % MH_FUSED_EXP_PAD_SCRATCH];
+  }
+#endif
 
   // ---- prologue: the workgroup's observations into LDS (rows past E: zeros), the policy's
   // fold operands and layer-2 bias, chunk 0 of W2
@@ -485,8 +538,14 @@ void k_sample_fused(FusedArgs a) {
     for (int t = 0; t < H; ++t) {
       policy_pass<D>(a, L, w, w * 32, ++pass < total, target);  // A(t): H0
       __syncthreads();
+#ifdef MH_FUSED_EXP_SERIAL
+      __syncthreads();
+#endif
       if (t < H - 1) policy_pass<D>(a, L, w, FUSED_ENVS / 2 + w * 32, ++pass < total, target);  // B(t): H1
       __syncthreads();
+#ifdef MH_FUSED_EXP_SERIAL
+      __syncthreads();
+#endif
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);
   } else {
@@ -501,6 +560,9 @@ void k_sample_fused(FusedArgs a) {
     const int64_t e = base + row;
     const bool live = e < E;
     EnvLane<Env> v;
+#ifdef MH_FUSED_EXP_CHECK_OBS
+    v.have = 0;
+#endif
     if (MH_FUSED_STATE_IN_REGS && live) {
 #pragma unroll
       for (int i = 0; i < S; ++i) v.s[i] = a.state[(int64_t)i * E + e];
@@ -555,6 +617,9 @@ void k_sample_fused(FusedArgs a) {
     __syncthreads();  // the policy's first pass (H1)
     // phases A(t) (half H1 steps) and B(t) (half H0 steps), one call site for the step's body
     for (int ph = 0; ph < 2 * H; ++ph) {
+#ifdef MH_FUSED_EXP_SERIAL  // experiment: env steps never overlap a policy pass
+      __syncthreads();
+#endif
       if ((ph & 1) == (half ^ 1)) step(ph >> 1);
       __syncthreads();
     }
@@ -674,7 +739,7 @@ __global__ __launch_bounds__(256) void k_emit_horizon(HorizonEmitArgs a) {
     const int64_t sz = a.cursor[1] + total;
     a.cursor[1] = sz < M ? sz : M;
     a.cursor[2] += total;
-    a.cursor[3] = total;
+    a.cursor[3] = total - offs[(a.H - 1) * NBK];  // windows of the horizon's last lockstep (as the lockstep path)
   }
 }
 

@@ -60,10 +60,14 @@ def _assert_same(a, ba, b, bb, where):
     for k in KEYS:
         x, y = ba.n_step_buf[k][:total], bb.n_step_buf[k][:total]
         assert torch.equal(x, y), (where, k, int((x != y).sum()))
-    assert torch.equal(a.obs, b.obs), where
-    for u, v in zip(a.envs.get_state(), b.envs.get_state()):
-        if u is not None:
-            assert torch.equal(u, v), where
+    bad = []
+    for nm, u, v in zip(("obs", "state", "xstate", "steps"), (a.obs,) + tuple(a.envs.get_state()),
+                        (b.obs,) + tuple(b.envs.get_state())):
+        if u is not None and not torch.equal(u, v):
+            rows = (u != v).reshape(u.shape[0], -1).any(1).nonzero().flatten()
+            d = (u.double() - v.double()).abs().max().item()
+            bad.append((nm, int(rows.numel()), rows[:8].tolist(), d))
+    assert not bad, (where, bad)
     return total
 
 
