@@ -212,7 +212,7 @@ def main():
         N.lib().mh_sample_horizon(h, N.ptr(sampler._packed), sampler.envs.obs_dim, 2 * sampler.envs.act_dim,
                                   N.ptr(sampler.obs), H, None, noise_ptr, None, None, st)
 
-    def k_fused_emit():  # the sampler's horizon: the fused kernel + k_emit_horizon into the store
+    def k_fused_emit():  # the sampler's horizon: the fused kernel + k_emit_scan + k_emit_cells into the store
         N.lib().mh_sample_horizon(h, N.ptr(sampler._packed), sampler.envs.obs_dim, 2 * sampler.envs.act_dim,
                                   N.ptr(sampler.obs), H, ctypes.byref(buffer.ws), noise_ptr, None, None, st)
 
@@ -275,7 +275,7 @@ def main():
         kernels["emit_horizon"] = {"avg_us": round(t_emit_h * 1e6, 2), "windows": windows_fh, "bytes": bytes_win,
                                    "GBps": round(bytes_win / t_emit_h / 1e9, 1),
                                    "frac": round(bytes_win / t_emit_h / 1e9 / PEAK_HBM_GBS, 4),
-                                   "note": "k_emit_horizon: the horizon's windows, ring -> replay store"}
+                                   "note": "k_emit_scan + k_emit_cells: the horizon's windows, ring -> replay store"}
     if t_pol is not None:
         flops = flops_lockstep
         # split-f16 arithmetic: every f32 product is 3 f16 MFMA products (hi.hi + hi.lo + lo.hi),

@@ -77,6 +77,7 @@ struct mh_env_s {
   int hcap = 0;
   int32_t* h_count = nullptr;       // [hcap][ceil(E / 64)]
   int32_t* h_list = nullptr;        // [hcap][E]
+  int64_t* h_scan = nullptr;        // [hcap * ceil(E / 256) + 2]: the emission's cell scan
   float* dbg_logits = nullptr;      // mh_sample_horizon_debug_logits: [H][E][2A] logits trace
   float* dbg_obs = nullptr;         //   and [H][E][D] pre-step observations
   // deferred emission (mh_rollout_step_deferred): the last step's windows are not yet emitted
@@ -141,7 +142,7 @@ static void free_handle(mh_env_s* h) {
   for (hipEvent_t e : h->ev_pending) (void)hipEventDestroy(e);
   void* ptrs[] = {h->state, h->xstate, h->steps, h->tab, h->meta, h->ctr, h->ring, h->ring_len,
                   h->ring_pos, h->emit_rank, h->block_count, h->block_offset, h->emit_list, h->h_count,
-                  h->h_list};
+                  h->h_list, h->h_scan};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete h;
@@ -278,10 +279,13 @@ int mh_nstep_reserve(mh_env_t h, int32_t ring_slots) {
   // the fused horizon's window lists, for horizons up to ring_slots - n + 1 locksteps
   (void)hipFree(h->h_count);
   (void)hipFree(h->h_list);
+  (void)hipFree(h->h_scan);
   h->h_count = h->h_list = nullptr;
+  h->h_scan = nullptr;
   h->hcap = ring_slots - h->n + 1;
   MH_HIP(hipMalloc(&h->h_count, sizeof(int32_t) * h->hcap * ((E + 63) / 64)));
   MH_HIP(hipMalloc(&h->h_list, sizeof(int32_t) * h->hcap * E));
+  MH_HIP(hipMalloc(&h->h_scan, sizeof(int64_t) * (mh::fused_emit_cells(E, h->hcap) + 2)));
   MH_HIP(hipMemset(h->ring, 0, sizeof(float) * E * ring_slots * F));
   MH_HIP(hipMemset(h->ring_len, 0, sizeof(int32_t) * E));
   MH_HIP(hipMemset(h->ring_pos, 0, sizeof(int32_t) * E));
@@ -301,8 +305,6 @@ int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, i
   if (store && (store->capacity <= 0 || !store->cursor || !store->obs || !store->act || !store->rew ||
                 !store->cost || !store->obs2 || !store->done || !store->logp))
     return fail(MH_EINVAL, "mh_sample_horizon: incomplete window store");
-  if (store && mh::fused_emit_cells(h->E, horizon) + 1 > 12288)
-    return fail(MH_EINVAL, "mh_sample_horizon: horizon x blocks exceeds the emission scan (12288 cells)");
   if (int rc = flush_pending(h, stream)) return rc;
   mh::FusedArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -356,6 +358,7 @@ int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, i
     ea.logp = store->logp;
     ea.capacity = store->capacity;
     ea.cursor = store->cursor;
+    ea.scan = h->h_scan;
   }
   MH_HIP(mh::launch_sample_fused(h->env_id, a, ea, (hipStream_t)stream));
   return MH_OK;

@@ -35,7 +35,7 @@ struct FusedArgs {
 
 constexpr int FUSED_ENVS = 256;   // envs per workgroup (one workgroup per CU)
 constexpr int FUSED_THREADS = 512;
-// (lockstep, 256-env block) cells the horizon emission scans in LDS
+// (lockstep, 256-env block) cells of the horizon emission (one workgroup each)
 inline int64_t fused_emit_cells(int64_t E, int H) { return (int64_t)H * ((E + FUSED_ENVS - 1) / FUSED_ENVS); }
 
 struct HorizonEmitArgs {
@@ -47,6 +47,7 @@ struct HorizonEmitArgs {
   float *obs, *act, *rew, *cost, *obs2, *done, *logp;
   int64_t capacity;
   int64_t* cursor;  // {ptr, size, total, last}
+  int64_t* scan;    // [cells + 2]: exclusive window prefix per cell, total, the starting cursor
 };
 
 

@@ -22,7 +22,7 @@
 // with one workgroup barrier between phases; observations and logits pass through LDS only.
 // Windows: every full deque of lockstep t is recorded as (lane | oldest slot << 6) in a per-wave,
 // rank-ordered list; the rings hold n + H - 1 records (mh_nstep_reserve) so every window of the
-// horizon is still intact when k_emit_horizon copies them, in the reference's order (lockstep
+// horizon is still intact when k_emit_scan + k_emit_cells copy them, in the reference's order (lockstep
 // major, env index within a lockstep: base.py:178-213), into the replay store after the kernel.
 #include <type_traits>
 
@@ -644,102 +644,122 @@ void k_sample_fused(FusedArgs a) {
 
 // ------------------------------------------------------------------ horizon emission
 // Every window of the horizon, in the reference's order (lockstep major; env index within a
-// lockstep), into the store rows after the cursor (FIFO wrap; windows older than the last
-// `capacity` of this horizon are skipped as overwritten): one thread per (window, slot) record,
-// like k_emit_fused. The (lockstep, wave) counts are scanned by every workgroup in LDS.
-template <int D, int A>
-__global__ __launch_bounds__(256) void k_emit_horizon(HorizonEmitArgs a) {
-  constexpr int F = rec_floats(D, A);
-  extern __shared__ int offs[];  // [H * NBK + 1] exclusive prefix over (lockstep, 256-env block)
+// lockstep: base.py:178-213), into the store rows after the cursor (FIFO wrap; windows older than
+// the last `capacity` of this horizon are skipped as overwritten). Two launches:
+//   k_emit_scan   one workgroup: exclusive prefix of the window counts over the (lockstep,
+//                 256-env block) cells into scan[0 .. NC], the store cursor it starts from into
+//                 scan[NC + 1], then the cursor update (the emission below never reads the cursor,
+//                 so no workgroup can see it half-updated);
+//   k_emit_cells  one workgroup per cell: its windows are the contiguous store rows
+//                 scan[c] .. scan[c + 1]; thread per (window, slot) record, consecutive slots of a
+//                 window on consecutive lanes (consecutive ring records in, consecutive store
+//                 rows out).
+constexpr int SCAN_THREADS = 1024;
+
+__device__ __forceinline__ int emit_cell_count(const int32_t* cnt_t, int b, int NW) {
+  int s = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) s += 4 * b + q < NW ? cnt_t[4 * b + q] : 0;
+  return s;
+}
+
+__global__ __launch_bounds__(SCAN_THREADS) void k_emit_scan(HorizonEmitArgs a) {
   const int NW = (int)((a.E + 63) / 64);
   const int NBK = (NW + 3) / 4;
-  const int NC = a.H * NBK;
-  __shared__ int wsum[4];
+  const int64_t NC = (int64_t)a.H * NBK;
+  __shared__ int64_t wsum[SCAN_THREADS / 64];
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  auto cell_count = [&](int c) {
-    const int ts = c / NBK, b = c - ts * NBK;
-    const int32_t* cnt = a.emit_count + (int64_t)ts * NW;
-    int s = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) s += 4 * b + q < NW ? cnt[4 * b + q] : 0;
-    return s;
-  };
-  const int per = (NC + 255) / 256;
-  const int lo = min(NC, t * per), hi = min(NC, lo + per);
-  int local = 0;
-  for (int i = lo; i < hi; ++i) local += cell_count(i);
-  int incl = local;
+  const int64_t per = (NC + SCAN_THREADS - 1) / SCAN_THREADS;
+  const int64_t lo = min(NC, t * per), hi = min(NC, lo + per);
+  int64_t local = 0;
+  for (int64_t c = lo; c < hi; ++c) {
+    const int ts = (int)(c / NBK), b = (int)(c - (int64_t)ts * NBK);
+    local += emit_cell_count(a.emit_count + (int64_t)ts * NW, b, NW);
+  }
+  int64_t incl = local;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
-    const int v = __shfl_up(incl, off, 64);
+    const int64_t v = __shfl_up(incl, off, 64);
     if (lane >= off) incl += v;
   }
   if (lane == 63) wsum[wave] = incl;
   __syncthreads();
-  int wbase = 0, all = 0;
+  int64_t wbase = 0, all = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < SCAN_THREADS / 64; ++q) {
     wbase += q < wave ? wsum[q] : 0;
     all += wsum[q];
   }
-  int run = wbase + incl - local;
-  for (int i = lo; i < hi; ++i) {
-    offs[i] = run;
-    run += cell_count(i);
+  int64_t run = wbase + incl - local;
+  for (int64_t c = lo; c < hi; ++c) {
+    a.scan[c] = run;
+    const int ts = (int)(c / NBK), b = (int)(c - (int64_t)ts * NBK);
+    run += emit_cell_count(a.emit_count + (int64_t)ts * NW, b, NW);
   }
-  if (t == 0) offs[NC] = all;
-  __syncthreads();
-  const int64_t total = offs[NC];
-  const int64_t M = a.capacity;
-  const int64_t c0 = a.cursor[0];
+  __syncthreads();  // (workgroup-scope fence + barrier: thread 0 reads the scan written above)
+  if (t == 0) {
+    const int64_t M = a.capacity, c0 = a.cursor[0];
+    a.scan[NC] = all;
+    a.scan[NC + 1] = c0;
+    a.cursor[0] = (c0 + all) % M;
+    const int64_t sz = a.cursor[1] + all;
+    a.cursor[1] = sz < M ? sz : M;
+    a.cursor[2] += all;
+    // windows of the horizon's last lockstep (the lockstep path's cursor[3]): its cells are the
+    // scan's last NBK
+    a.cursor[3] = all - a.scan[NC - NBK];
+  }
+}
+
+template <int D, int A>
+__global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
+  constexpr int F = rec_floats(D, A);
+  const int NW = (int)((a.E + 63) / 64);
+  const int NBK = (NW + 3) / 4;
+  const int64_t NC = (int64_t)a.H * NBK;
+  const int64_t c = blockIdx.x;
+  const int ts = (int)(c / NBK), b = (int)(c - (int64_t)ts * NBK);
+  const int64_t total = a.scan[NC], M = a.capacity, base = a.scan[NC + 1];
+  const int64_t g0 = a.scan[c];
   const int64_t start = total > M ? total - M : 0;  // older windows are overwritten this horizon
+  const int32_t* cnt = a.emit_count + (int64_t)ts * NW;
+  int pre[5];
+  pre[0] = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) pre[q + 1] = pre[q] + (4 * b + q < NW ? cnt[4 * b + q] : 0);
+  const int nwin = pre[4];
   const int n = a.n, R = a.R;
-  for (int64_t q = (int64_t)blockIdx.x * 256 + t; q < (total - start) * n; q += (int64_t)gridDim.x * 256) {
-    const int64_t gl = q / n;
-    const int j = (int)(q - gl * n);
-    const int64_t g = start + gl;
-    int bl = 0, bh = NC - 1;  // the (lockstep, block) cell holding window g: largest offs <= g
-    while (bl < bh) {
-      const int mid = (bl + bh + 1) >> 1;
-      if ((int64_t)offs[mid] <= g) bl = mid; else bh = mid - 1;
-    }
-    const int ts = bl / NBK, b = bl - ts * NBK;
-    int r = (int)(g - offs[bl]);
-    int gw = 4 * b;  // the block's wave holding it (waves in env order)
-    const int32_t* cnt = a.emit_count + (int64_t)ts * NW;
-    while (gw + 1 < NW && gw + 1 < 4 * b + 4 && r >= cnt[gw]) r -= cnt[gw++];
-    const int packed = a.emit_list[(int64_t)ts * a.E + (int64_t)gw * 64 + r];
+  for (int i = threadIdx.x; i < nwin * n; i += 256) {
+    const int w = i / n, j = i - w * n;
+    const int64_t g = g0 + w;
+    if (g < start) continue;
+    const int q = (w >= pre[1]) + (w >= pre[2]) + (w >= pre[3]);
+    const int gw = 4 * b + q;
+    const int packed = a.emit_list[(int64_t)ts * a.E + (int64_t)gw * 64 + (w - pre[q])];
     const int64_t e = (int64_t)gw * 64 + (packed & 63);
     int slot = (packed >> 6) + j;
     slot = slot >= R ? slot - R : slot;
     float rec[F];
     const float4* src = reinterpret_cast<const float4*>(a.ring + (e * R + slot) * (int64_t)F);
 #pragma unroll
-    for (int i = 0; i < F / 4; ++i) {
-      const float4 v = src[i];
-      rec[4 * i] = v.x;
-      rec[4 * i + 1] = v.y;
-      rec[4 * i + 2] = v.z;
-      rec[4 * i + 3] = v.w;
+    for (int k = 0; k < F / 4; ++k) {
+      const float4 v = src[k];
+      rec[4 * k] = v.x;
+      rec[4 * k + 1] = v.y;
+      rec[4 * k + 2] = v.z;
+      rec[4 * k + 3] = v.w;
     }
-    const int64_t o = ((c0 + g) % M) * n + j;
+    const int64_t o = ((base + g) % M) * n + j;
 #pragma unroll
-    for (int i = 0; i < D; ++i) a.obs[o * D + i] = rec[i];
+    for (int k = 0; k < D; ++k) a.obs[o * D + k] = rec[k];
 #pragma unroll
-    for (int i = 0; i < A; ++i) a.act[o * A + i] = rec[D + i];
+    for (int k = 0; k < A; ++k) a.act[o * A + k] = rec[D + k];
 #pragma unroll
-    for (int i = 0; i < D; ++i) a.obs2[o * D + i] = rec[D + A + i];
+    for (int k = 0; k < D; ++k) a.obs2[o * D + k] = rec[D + A + k];
     a.rew[o] = rec[2 * D + A];
     a.cost[o] = rec[2 * D + A + 1];
     a.done[o] = rec[2 * D + A + 2];
     a.logp[o] = rec[2 * D + A + 3];
-  }
-  if (blockIdx.x == 0 && t == 0) {
-    a.cursor[0] = (c0 + total) % M;
-    const int64_t sz = a.cursor[1] + total;
-    a.cursor[1] = sz < M ? sz : M;
-    a.cursor[2] += total;
-    a.cursor[3] = total - offs[(a.H - 1) * NBK];  // windows of the horizon's last lockstep (as the lockstep path)
   }
 }
 
@@ -750,10 +770,10 @@ static hipError_t launch_fused_t(const FusedArgs& a, const HorizonEmitArgs& ea, 
   k_sample_fused<Env><<<grid, FUSED_THREADS, 0, st>>>(a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || ea.obs == nullptr) return e;
-  const int64_t want = (a.E * a.n + 255) / 256;
-  const int eg = (int)(want < 1 ? 1 : (want > 2048 ? 2048 : want));
-  const size_t shm = (size_t)(fused_emit_cells(a.E, a.H) + 1) * sizeof(int);
-  k_emit_horizon<Env::D, Env::A><<<eg, 256, shm, st>>>(ea);
+  k_emit_scan<<<1, SCAN_THREADS, 0, st>>>(ea);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  k_emit_cells<Env::D, Env::A><<<(unsigned)fused_emit_cells(a.E, a.H), 256, 0, st>>>(ea);
   return hipGetLastError();
 }
 

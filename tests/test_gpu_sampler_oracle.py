@@ -63,8 +63,42 @@ def _reset_box_ok(name, st):
     return np.abs(st).max(initial=0) <= 0.5
 
 
+def _quad_obs_of_state(s2, xs, k):
+    """The reference's observation map (QuadTracking.py:229-246: desired states at step k + 1,
+    cal_eR / cal_eOmega) applied to a given post-step state [x, v, R, Omega]."""
+    n = s2.shape[0]
+    Q = OE.QuadTracking
+    ex, ev, Rd, Od = Q.desired(s2[:, 0:3].copy(), s2[:, 3:6].copy(), k + 1, xs.reshape(n, 3, 3))
+    return Q.errors(s2[:, 6:15].reshape(n, 3, 3).copy(), s2[:, 15:18].copy(), ex, ev, Rd, Od)
+
+
+def _quad_allowance(xs, k, got, o2, st_got, done):
+    """QuadTracking rows whose observation is beyond 1e-5 of the float64-polar oracle's.
+
+    The observation is a function of the post-step state, and e_Omega = Omega - R^T R_d Omega_d
+    (obs components 9-11) multiplies last-bit differences of that state (the rotation R leaves
+    the polar factorisation rounded to float32) by |Omega_d|: a row measured on the MI355X was
+    3.6e-5 / 2.3e-5 off on e_Omega x / z with |Omega| ~ 2 rad/s. Such a row passes when
+    (a) the kernel's post-step state is within 1e-5 of the oracle's (asserted for every
+        continuing row by the caller), and
+    (b) the kernel's observation is within 1e-5 of the reference's observation map applied to
+        the kernel's OWN post-step state (_quad_obs_of_state),
+    i.e. both halves of the step are within 1e-5 and only their composition amplifies a
+    rounding difference. Reset rows (whose post-step state is overwritten) get no allowance.
+    Returns the rows that needed it (they must be a handful: 1 in 1.77 M env-steps measured).
+    """
+    far = ~np.isclose(got, o2, **TOL)
+    rows = np.nonzero(far.any(axis=1))[0]
+    if rows.size:
+        assert not done[rows].any(), ("reset row beyond 1e-5", rows[done[rows]])
+        mine = _quad_obs_of_state(st_got[rows], xs[rows], k[rows])
+        np.testing.assert_allclose(got[rows], mine, **TOL, err_msg=f"rows {rows}: obs of the kernel's own state")
+    return rows
+
+
 def _sampler(name, tmp_path, noise=None):
-    args = default_msacl_args(env_name=name, env_num=E, n_step=NSTEP, seed=0, env_seed=5, buffer_max_size=400_000,
+    # the store holds every window of the run (VanderPol emits 1.34 M in 40 locksteps)
+    args = default_msacl_args(env_name=name, env_num=E, n_step=NSTEP, seed=0, env_seed=5, buffer_max_size=2_000_000,
                               buffer_warm_size=0, save_folder=str(tmp_path), noise_params=noise)
     args = init_args(create_envs(**args), **args)
     sampler, buffer = create_sampler(**args), create_buffer(**args)
@@ -101,7 +135,7 @@ def test_sampled_lockstep_kernel_matches_oracle(name, noise, tmp_path):
     np.testing.assert_allclose(sampler.obs.cpu().numpy(), obs_o, **TOL)
     if quad:
         np.testing.assert_allclose(xs, xs_r, rtol=0, atol=1e-12)
-    n_reset = n_trunc = n_lp = 0
+    n_reset = n_trunc = n_lp = n_quad_allow = 0
     for t in range(STEPS.get(name, 40)):
         logits = sampler.step_traced(act, logp, trace=(real, rew, term, trunc))
         a_np, lp_np, lg = act.cpu().numpy(), logp.cpu().numpy(), logits.cpu().numpy().astype(np.float64)
@@ -126,6 +160,10 @@ def test_sampled_lockstep_kernel_matches_oracle(name, noise, tmp_path):
 
         # ---- the env step from the snapshot, with the kernel's own actions
         s_o, xs_o, o2, r2, te, tr = OE.env_step(name, st, a_np, xs, k, polar64=quad)
+        if quad:  # rows beyond 1e-5 of the float64-polar path: see _quad_allowance
+            bad = _quad_allowance(xs, k, got_real, o2, st2, got_term | got_trunc)
+            n_quad_allow += bad.size
+            o2[bad] = got_real[bad]
         np.testing.assert_allclose(got_real, o2, **TOL)
         np.testing.assert_allclose(got_rew, r2, **TOL)
         if quad:  # the reference as-is (float32 SVD) on a slice: within 1e-5 + its own SVD noise
@@ -167,6 +205,7 @@ def test_sampled_lockstep_kernel_matches_oracle(name, noise, tmp_path):
     exp = {key: np.concatenate(v) for key, v in expect.items()}
     total = exp["obs"].shape[0]
     assert total > 500 and n_reset > 0 and n_trunc > 0, (total, n_reset, n_trunc)
+    assert n_quad_allow <= 1e-5 * E * STEPS.get(name, 40), n_quad_allow  # a handful of 1.77 M env-steps
     assert noise is not None or n_lp > 1000
     assert int(buffer.cursor[2]) == total and total < buffer.max_size
     for key in KEYS:

@@ -22,7 +22,7 @@ ALIASES = {"rollout_emit": ("k_rollout<mh::QuadTracking, true>", 131072),
            "window_emit": ("k_emit_fused<12, 4>", None), "replay_gather": ("k_gather", None),
            "msacl_lyapunov": ("k_lyapunov", None), "msacl_q_target": ("k_q_target", None),
            "policy_forward": ("k_policy_forward_x3", None),
-           "sample_fused": ("k_sample_fused<mh::QuadTracking>", None), "emit_horizon": ("k_emit_horizon<12, 4>", None)}
+           "sample_fused": ("k_sample_fused<mh::QuadTracking>", None), "emit_horizon": ("k_emit_cells<12, 4>", None)}
 
 
 def load(root, counter):
