@@ -344,6 +344,34 @@ int mh_linear_backward_plan(int64_t rows, int64_t n_out, int64_t n_in, int32_t n
 int mh_linear_backward(const float* dy, const float* y, int32_t act, const float* x, const float* W, int64_t rows,
                        int64_t n_out, int64_t n_in, float* dx, float* dw, float* db, float* workspace, void* stream);
 
+/* Grouped layers: `groups` products / layer backwards of ONE shape in one launch, group q's operands
+ * at the group-0 pointers + q x the strides (floats). They replace the two critic networks q1, q2
+ * of RL/algorithm/msacl.py:227-266 (critic update) and :383-391 (the policy step's frozen
+ * critics), each evaluated by RL/apprfunc/mlp.py ActionValue.forward (mlp.py:18-30 layers) and
+ * differentiated by autograd, with one launch per layer for both networks (the engine keeps the
+ * two networks' layer parameters side by side, so their activations are the halves of one
+ * [rows][2H] buffer: leading dimension 2H, group stride H). Each group's result is bit-identical
+ * to the ungrouped entry point on that group's operands.
+ *   mh_gemm_f32_grouped: mh_gemm_f32's tall path (rows >= 2048, N % 64 == 0, K % 4 == 0, K >= 1,
+ *     16-byte aligned rows) and its one-output path (N == 1); MH_EINVAL for other shapes.
+ *   mh_linear_backward_grouped: mh_linear_backward with leading dimensions (dy and y share ld_dy;
+ *     x: ld_x; dx: ld_dx); workspace: groups x mh_linear_backward_plan's floats.
+ *   mh_head_backward_grouped: mh_head_backward with x / dx leading dimensions; workspace: groups x
+ *     mh_head_backward_workspace floats when dw is wanted. */
+int mh_gemm_f32_grouped(const float* A, const float* B, const float* bias, float* C, int64_t M, int64_t N, int64_t K,
+                        int64_t lda, int64_t ldb, int64_t ldc, int32_t trans_a, int32_t trans_b, int32_t act,
+                        int32_t groups, int64_t stride_a, int64_t stride_b, int64_t stride_bias, int64_t stride_c,
+                        void* stream);
+int mh_linear_backward_grouped(const float* dy, const float* y, int32_t act, const float* x, const float* W,
+                               int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy, int64_t ld_x, int64_t ld_dx,
+                               int32_t groups, int64_t stride_dy, int64_t stride_x, int64_t stride_w,
+                               int64_t stride_dx, int64_t stride_dw, int64_t stride_db, float* dx, float* dw,
+                               float* db, float* workspace, void* stream);
+int mh_head_backward_grouped(const float* dy, const float* x, const float* W, int64_t rows, int32_t n_out,
+                             int32_t n_in, int64_t ld_x, int64_t ld_dx, int32_t groups, int64_t stride_dy,
+                             int64_t stride_x, int64_t stride_w, int64_t stride_dx, int64_t stride_dw,
+                             int64_t stride_db, float* dx, float* dw, float* db, float* workspace, void* stream);
+
 /* StochaPolicy's head (RL/apprfunc/mlp.py:132-136) on [rows][2 act_dim] rows:
  *   out = [mean | exp(clamp(log_std, min_log_std, max_log_std))] of raw = [mean | log_std]
  * and its backward d_raw = [d_mean | d_std * std * (min <= log_std <= max)], one launch each

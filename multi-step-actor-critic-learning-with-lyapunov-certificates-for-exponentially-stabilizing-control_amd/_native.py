@@ -122,6 +122,11 @@ _PROTOS = {
                                      c_vp, c_vp]),
     "mh_gemm_workspace": (ctypes.c_int, [c_i64, c_i64, c_i64, ctypes.POINTER(c_i64)]),
     "mh_gemm_f32": (ctypes.c_int, [c_vp] * 4 + [c_i64] * 6 + [c_i32] * 3 + [c_vp, c_vp]),
+    "mh_gemm_f32_grouped": (ctypes.c_int, [c_vp] * 4 + [c_i64] * 6 + [c_i32] * 4 + [c_i64] * 4 + [c_vp]),
+    "mh_linear_backward_grouped": (ctypes.c_int, [c_vp, c_vp, c_i32, c_vp, c_vp] + [c_i64] * 6 + [c_i32] + [c_i64] * 6
+                                   + [c_vp] * 5),
+    "mh_head_backward_grouped": (ctypes.c_int, [c_vp] * 3 + [c_i64, c_i32, c_i32, c_i64, c_i64, c_i32] + [c_i64] * 6
+                                 + [c_vp] * 5),
     "mh_stocha_head": (ctypes.c_int, [c_vp, c_i64, c_i32, c_f32, c_f32, c_vp, c_vp]),
     "mh_stocha_head_backward": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_f32, c_vp, c_vp]),
     "mh_tanh_gauss_rsample": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_i32, c_vp, c_vp, c_vp]),

@@ -212,7 +212,8 @@ class _PolicyObjective(torch.autograd.Function):
         q1, q2, log_alpha = ctx.saved_tensors
         s = ctx.s
         B, n = ctx.shape
-        dq1, dq2, dlogp = torch.empty_like(q1), torch.empty_like(q2), torch.empty_like(q1)
+        dq = torch.empty((2,) + tuple(q1.shape), dtype=q1.dtype, device=q1.device)  # one buffer: TwinQ reads both
+        dq1, dq2, dlogp = dq[0], dq[1], torch.empty_like(q1)
         dlp = torch.empty(B, n, dtype=torch.float32, device=q1.device)
         _engine("msacl_policy_objective_backward", q1.device, N.ptr(q1), N.ptr(q2), N.ptr(log_alpha), N.ptr(s.ratio),
                 N.ptr(s.d_ratio), N.ptr(g_loss.contiguous()), B, n, N.ptr(dq1), N.ptr(dq2), N.ptr(dlogp), N.ptr(dlp))
@@ -245,7 +246,10 @@ class _Scratch:
 
     def __init__(self, B, n, device):
         f = lambda *s: torch.empty(*s, dtype=torch.float32, device=device)  # noqa: E731
-        self.backup, self.dq1, self.dq2 = f(B, n), f(B, n), f(B, n)
+        self.backup = f(B, n)
+        # dq1 | dq2 as the two halves of one buffer: the twin critics' grouped backward reads both
+        self.dq_both = f(2, B, n)
+        self.dq1, self.dq2 = self.dq_both[0], self.dq_both[1]
         self.abs_td, self.loss_q = f(B), f(1)
         self.is_clip, self.esl, self.lya_diff, self.loss_lya = f(B, n), f(B, n), f(B), f(1)
         # dV | dV2 as the two halves of one buffer: the two Lyapunov evaluations run as one batch
@@ -314,6 +318,10 @@ class MSACL:
         self.twin_streams = bool(kwargs.get("alg_twin_streams", True))  # q1 / q2 branches in parallel
         self._twin = None
         self._side = None
+        # the twin critics (and their targets) as one grouped network (apprfunc/_twin.py);
+        # alg_twin_grouped=False: two networks, one launch per layer each (A/B)
+        self.twin_grouped = bool(kwargs.get("alg_twin_grouped", True))
+        self._tc = None
         self.force_graph_segments = bool(kwargs.get("alg_force_graph_segments", False))
         self._static = None
         self._static_shapes = None
@@ -333,6 +341,32 @@ class MSACL:
         self._scratch = {}
         self.last_priority = None
         self._twin = self._side = None
+        self._tc = None
+
+    def _twin_critics(self, rows):
+        """(TwinCritic of q1/q2, TwinCritic of their targets) when the grouped path applies to a
+        batch of `rows` rows, else None. Built on first use (the parameters move into joint
+        buffers then); a rebuilt joint storage invalidates the captured update graphs."""
+        if not self.twin_grouped or self.device.type != "cuda" or self._head() is None:
+            return None
+        from ..apprfunc._fused import gemm_backend
+        if gemm_backend() == "blas":
+            return None
+        nets = self.networks
+        if self._tc is None:
+            from ..apprfunc._twin import TwinCritic
+            a = TwinCritic.build(nets.q1, nets.q2)
+            b = TwinCritic.build(nets.q1_target, nets.q2_target) if a is not None else None
+            self._tc = (a, b) if (a is not None and b is not None) else False
+        if not self._tc:
+            return None
+        a, b = self._tc
+        if (a.joined() | b.joined()) and self._graphs:  # parameters were re-pointed: stale graphs
+            from ._update_graph import release_graph
+            for g, _o, _p in self._graphs.values():
+                release_graph(g)
+            self._graphs, self._warm = {}, set()
+        return self._tc if a.applies(rows) else None
 
     @property
     def adjustable_parameters(self):
@@ -589,6 +623,9 @@ class MSACL:
                 _engine("policy_head", self.device, N.ptr(raw.contiguous()), N.ptr(eps.contiguous()), N.ptr(obs2), None,
                         N.ptr(hi), N.ptr(lo), B * n, A, Dd, lsl, lsh, N.ptr(xq2), N.ptr(next_logp), None)
             xa = torch.cat([obs, act], dim=-1)
+            tc = self._twin_critics(B * n)
+            if tc is not None:
+                return self._q_update_twin(tc, data, xa, xq2, next_logp, s, defer_step, stats)
             q_in = lambda q: q.q(xa).squeeze(-1)  # noqa: E731  (ActionValue.forward on the shared concat)
             qt_in = lambda q: q.q(xq2).squeeze(-1)  # noqa: E731
         else:
@@ -628,6 +665,33 @@ class MSACL:
             return s.loss_q[0], None, None
         # views of the scratch / fresh means, read by model_update right after the update
         return s.loss_q[0], q1.detach().mean(), q2.detach().mean()
+
+    def _q_update_twin(self, tc, data, xa, xq2, next_logp, s, defer_step, stats):
+        """_q_update with both critics (and both targets) as one grouped network each
+        (apprfunc/_twin.py): same math, one launch per layer instead of one per layer per critic."""
+        twin, twin_t = tc
+        rew, done = data["rew"], data["done"]
+        B, n = rew.shape
+        M = B * n
+        xa2 = xa.reshape(M, xa.shape[-1])
+        q, h1, h2 = twin.forward(xa2)
+        qt, _, _ = twin_t.forward(xq2.reshape(M, xq2.shape[-1]))
+        weight = data.get("weight") if self.per_flag else None
+        _engine(
+            "msacl_q_target", self.device,
+            N.ptr(q[0]), N.ptr(q[1]), N.ptr(qt[0]), N.ptr(qt[1]),
+            N.ptr(next_logp.contiguous()), N.ptr(rew), N.ptr(done), N.ptr(self.networks.log_alpha.detach()),
+            N.ptr(weight.contiguous() if weight is not None else None), float(self.gamma), B, n, N.ptr(s.backup),
+            N.ptr(s.dq1), N.ptr(s.dq2), N.ptr(s.loss_q), N.ptr(s.abs_td))
+        twin.backward_weights(xa2, s.dq_both.view(2, M), h1, h2)  # binds q1 / q2 .grad
+        if not defer_step:
+            D.allreduce_grads(list(self.networks.q1.parameters()) + list(self.networks.q2.parameters()))
+            adam_steps(self.networks.q1_optimizer, self.networks.q2_optimizer)
+        if self.per_flag:
+            self.last_priority = s.abs_td.clone()
+        if not stats:
+            return s.loss_q[0], None, None
+        return s.loss_q[0], q[0].mean(), q[1].mean()
 
     def _lyapunov_update(self, data, defer_step=False):
         obs, obs2, act, old_logp = data["obs"], data["obs2"], data["act"], data["logp"]
@@ -712,7 +776,13 @@ class MSACL:
                                                          old_act.reshape(B * n, A), hi, lo, lsl, lsh)
             xq = xq.reshape(B, n, Dd + A)
             new_act_logp, old_lp = new_act_logp.reshape(B, n), old_lp.reshape(B, n)
-            q1, q2 = self._twin_pair(lambda: nets.q1.q(xq).squeeze(-1), lambda: nets.q2.q(xq).squeeze(-1))
+            tc = self._twin_critics(B * n)
+            if tc is not None:
+                from ..apprfunc._twin import TwinQ
+                q1, q2 = TwinQ.apply(xq.reshape(B * n, Dd + A), tc[0])
+                q1, q2 = q1.view(B, n), q2.view(B, n)
+            else:
+                q1, q2 = self._twin_pair(lambda: nets.q1.q(xq).squeeze(-1), lambda: nets.q2.q(xq).squeeze(-1))
         else:
             dist = nets.create_action_distributions(nets.policy(obs))
             new_act, new_act_logp = dist.rsample()

@@ -892,6 +892,69 @@ int mh_linear_backward(const float* dy, const float* y, int32_t act, const float
   return MH_OK;
 }
 
+// ------------------------------------------------------------------ grouped layers (twin critics)
+int mh_gemm_f32_grouped(const float* A, const float* B, const float* bias, float* C, int64_t M, int64_t N, int64_t K,
+                        int64_t lda, int64_t ldb, int64_t ldc, int32_t trans_a, int32_t trans_b, int32_t act,
+                        int32_t groups, int64_t stride_a, int64_t stride_b, int64_t stride_bias, int64_t stride_c,
+                        void* stream) {
+  if (M < 0 || N < 0 || K <= 0 || groups < 0) return fail(MH_EINVAL, "mh_gemm_f32_grouped: bad size");
+  if (M == 0 || N == 0 || groups == 0) return MH_OK;
+  if (act < 0 || act > 2) return fail(MH_EINVAL, "mh_gemm_f32_grouped: act must be 0, 1 or 2");
+  if (!A || !B || !C) return fail(MH_EINVAL, "mh_gemm_f32_grouped: null operand");
+  if (stride_a < 0 || stride_b < 0 || stride_bias < 0 || stride_c < 0)
+    return fail(MH_EINVAL, "mh_gemm_f32_grouped: negative group stride");
+  if (ldc < N || lda < (trans_a ? M : K) || ldb < (trans_b ? K : N))
+    return fail(MH_EINVAL, "mh_gemm_f32_grouped: leading dimension smaller than the matrix");
+  const hipError_t e = mh::launch_gemm_grouped(A, B, bias, C, M, N, K, lda, ldb, ldc, trans_a != 0, trans_b != 0, act,
+                                               groups, stride_a, stride_b, stride_bias, stride_c, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue)
+    return fail(MH_EINVAL, "mh_gemm_f32_grouped: shape not supported (tall products and one-output products only)");
+  MH_HIP(e);
+  return MH_OK;
+}
+
+int mh_linear_backward_grouped(const float* dy, const float* y, int32_t act, const float* x, const float* W,
+                               int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy, int64_t ld_x, int64_t ld_dx,
+                               int32_t groups, int64_t stride_dy, int64_t stride_x, int64_t stride_w,
+                               int64_t stride_dx, int64_t stride_dw, int64_t stride_db, float* dx, float* dw,
+                               float* db, float* workspace, void* stream) {
+  if (act < 0 || act > 2) return fail(MH_EINVAL, "mh_linear_backward_grouped: act must be 0, 1 or 2");
+  int64_t ws = 0;
+  if (rows < 0 || n_out <= 0 || n_in <= 0 || groups < 0 ||
+      !mh::linear_backward_plan(rows, n_out, n_in, dx != nullptr, dw != nullptr, db != nullptr, &ws))
+    return fail(MH_EINVAL, "mh_linear_backward_grouped: shape or request not supported (see mh_linear_backward_plan)");
+  if (groups == 0) return MH_OK;
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!dy || (act != 0 && !y) || (dx && !W) || (dw && !x) || (ws > 0 && !workspace))
+    return fail(MH_EINVAL, "mh_linear_backward_grouped: null pointer");
+  if (!al16(dy) || !al16(y) || !al16(x) || !al16(W) || !al16(dx) || !al16(dw) || !al16(workspace))
+    return fail(MH_EINVAL, "mh_linear_backward_grouped: every matrix must be 16-byte aligned");
+  if (ld_dy < n_out || (dw && ld_x < n_in) || (dx && ld_dx < n_in))
+    return fail(MH_EINVAL, "mh_linear_backward_grouped: leading dimension smaller than the matrix");
+  const hipError_t e = mh::launch_linear_backward_grouped(
+      dy, act != 0 ? y : nullptr, act, x, W, rows, n_out, n_in, ld_dy, ld_x, ld_dx, groups, stride_dy, stride_x,
+      stride_w, stride_dx, stride_dw, stride_db, dx, dw, db, workspace, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue)
+    return fail(MH_EINVAL, "mh_linear_backward_grouped: strides / leading dimensions must keep 16-byte alignment");
+  MH_HIP(e);
+  return MH_OK;
+}
+
+int mh_head_backward_grouped(const float* dy, const float* x, const float* W, int64_t rows, int32_t n_out,
+                             int32_t n_in, int64_t ld_x, int64_t ld_dx, int32_t groups, int64_t stride_dy,
+                             int64_t stride_x, int64_t stride_w, int64_t stride_dx, int64_t stride_dw,
+                             int64_t stride_db, float* dx, float* dw, float* db, float* workspace, void* stream) {
+  if (rows <= 0 || n_out <= 0 || n_out > 16 || n_in <= 0 || groups < 0 || ld_x < n_in || (dx && ld_dx < n_in))
+    return fail(MH_EINVAL, "mh_head_backward_grouped: bad shape");
+  if (groups == 0) return MH_OK;
+  if (!dy || !x || (dx && !W) || ((dw || db) && !workspace) || (db && !dw))
+    return fail(MH_EINVAL, "mh_head_backward_grouped: null pointer");
+  MH_HIP(mh::launch_head_backward_grouped(dy, x, W, rows, n_out, n_in, ld_x, ld_dx, groups, stride_dy, stride_x,
+                                          stride_w, stride_dx, stride_dw, stride_db, dx, dw, db, workspace,
+                                          (hipStream_t)stream));
+  return MH_OK;
+}
+
 int mh_stocha_head(const float* raw, int64_t rows, int32_t act_dim, float min_log_std, float max_log_std, float* out,
                    void* stream) {
   if (rows < 0 || act_dim <= 0) return fail(MH_EINVAL, "mh_stocha_head: bad shape");

@@ -48,7 +48,24 @@ struct GemmArgs {
   float* db;
   float* dbp;        // [dbn][M] partial column sums (split-major, then column tile), or null
   int dbn;
+  // grouped launches (the twin critics' layers as one launch): blockIdx.y = group q, and every
+  // operand pointer of group q is its group-0 pointer + q x its stride (floats; 0 = shared)
+  int64_t gsA, gsB, gsC, gsBias, gsY, gsPart, gsDb, gsDbp;
 };
+
+// this workgroup's group (blockIdx.y) of a grouped launch: the operand pointers advanced
+__device__ __forceinline__ void gemm_group(GemmArgs& g) {
+  const int64_t q = blockIdx.y;
+  if (q == 0) return;
+  g.A += q * g.gsA;
+  g.B += q * g.gsB;
+  g.C += q * g.gsC;
+  if (g.bias) g.bias += q * g.gsBias;
+  if (g.Y) g.Y += q * g.gsY;
+  if (g.partial) g.partial += q * g.gsPart;
+  if (g.db) g.db += q * g.gsDb;
+  if (g.dbp) g.dbp += q * g.gsDbp;
+}
 
 // g = dy * act'(y) exactly as k_act_grad_colsum forms it (mlp_grad.hip)
 __device__ __forceinline__ float act_grad(float d, float t, int act) {
@@ -230,6 +247,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 
 // C = act(sum_s partial[s] + bias), splits added in order (and db = sum_s dbp[s] when set)
 __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs g) {
+  gemm_group(g);
   const int64_t MN = g.M * g.N;
   if (g.dbp) {
     // dbn = splits x column tiles partials per output (64 for a 256 x 256 layer): sixteen loads
@@ -291,6 +309,7 @@ constexpr int TLD = TK + 4;  // LDS row stride (floats): 16 rows of a b128 read 
 
 template <int RB, bool TB, int NCH, bool AG>
 __global__ __launch_bounds__(256) void k_gemm_tall(GemmArgs g, int tiles_n) {
+  gemm_group(g);
   constexpr int RM = 16 * RB;
   constexpr int NA = RM * TK / 4 / 256;  // float4 loads of A per thread per chunk
   constexpr int NB = 64 * TK / 4 / 256;  // ... of op(B)
@@ -471,6 +490,7 @@ constexpr int DLD = 80;
 
 template <int NCH, bool AG>
 __global__ __launch_bounds__(256) void k_gemm_deep(GemmArgs g, int tiles_m) {
+  gemm_group(g);
   constexpr int NF = 64 * TK / 4 / 256;  // float4 loads per operand per thread per chunk (4)
   __shared__ float lds[2][2 * TK * DLD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -665,21 +685,34 @@ static bool tall_ok(const float* A, const float* B, const float* bias, const flo
 }
 
 template <int RB>
-static hipError_t launch_tall(const GemmArgs& g, bool tb, hipStream_t st) {
+static hipError_t launch_tall(const GemmArgs& g, bool tb, hipStream_t st, int groups = 1) {
   const int tiles_n = (int)(g.N / 64);
-  const int64_t grid = ((g.M + 16 * RB - 1) / (16 * RB)) * tiles_n;
+  const dim3 grid((unsigned)(((g.M + 16 * RB - 1) / (16 * RB)) * tiles_n), (unsigned)groups);
   if (g.act_a >= 0) {  // fused layer backward: dx = (dy * act'(y)) W
     if (tb) return hipErrorInvalidValue;
-    if (g.K == 256) k_gemm_tall<RB, false, 4, true><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
-    else k_gemm_tall<RB, false, 0, true><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
+    if (g.K == 256) k_gemm_tall<RB, false, 4, true><<<grid, 256, 0, st>>>(g, tiles_n);
+    else k_gemm_tall<RB, false, 0, true><<<grid, 256, 0, st>>>(g, tiles_n);
   } else if (g.K == 256) {  // the hidden layers of every reference MLP: 4 chunks, unrolled
-    if (tb) k_gemm_tall<RB, true, 4, false><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
-    else k_gemm_tall<RB, false, 4, false><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
+    if (tb) k_gemm_tall<RB, true, 4, false><<<grid, 256, 0, st>>>(g, tiles_n);
+    else k_gemm_tall<RB, false, 4, false><<<grid, 256, 0, st>>>(g, tiles_n);
   } else {
-    if (tb) k_gemm_tall<RB, true, 0, false><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
-    else k_gemm_tall<RB, false, 0, false><<<(unsigned)grid, 256, 0, st>>>(g, tiles_n);
+    if (tb) k_gemm_tall<RB, true, 0, false><<<grid, 256, 0, st>>>(g, tiles_n);
+    else k_gemm_tall<RB, false, 0, false><<<grid, 256, 0, st>>>(g, tiles_n);
   }
   return hipGetLastError();
+}
+
+static hipError_t launch_tall_rb(const GemmArgs& g, bool tb, hipStream_t st, int groups) {
+  switch (tall_rb(g.M, g.N)) {
+    case 1: return launch_tall<1>(g, tb, st, groups);
+    case 2: return launch_tall<2>(g, tb, st, groups);
+    case 3: return launch_tall<3>(g, tb, st, groups);
+    case 4: return launch_tall<4>(g, tb, st, groups);
+    case 5: return launch_tall<5>(g, tb, st, groups);
+    case 6: return launch_tall<6>(g, tb, st, groups);
+    case 7: return launch_tall<7>(g, tb, st, groups);
+    default: return launch_tall<8>(g, tb, st, groups);
+  }
 }
 
 // ------------------------------------------------------------------ launch plan
@@ -733,6 +766,7 @@ int64_t gemm_workspace_floats(int64_t M, int64_t N, int64_t K) {
 // in order, the 64 lane sums added by a butterfly; no split-K partials or finishing launch
 // (k_gemm + k_gemm_reduce took 9 + 4 us for this shape).
 __global__ __launch_bounds__(256) void k_gemv_n1(GemmArgs g, int64_t bstride) {
+  gemm_group(g);
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= g.M) return;
@@ -929,6 +963,79 @@ hipError_t launch_linear_backward(const float* dy, const float* y, int act, cons
     if (e != hipSuccess || (S == 1 && !db)) return e;
     const int64_t want = (n_out * n_in + 255) / 256;
     k_gemm_reduce<<<(unsigned)(want < 2048 ? want : 2048), 256, 0, st>>>(g);
+    return hipGetLastError();
+  }
+  return hipSuccess;
+}
+
+// ------------------------------------------------------------------ grouped launches
+// `groups` independent products of one shape in ONE launch (blockIdx.y = group), group q's
+// operands at the group-0 pointers + q x the strides (floats): the twin critics' hidden and
+// output layers, whose two networks read the two halves of one [rows][2H] activation buffer.
+// Routes: the tall kernel (forward x W^T / g W on >= 2,048 rows) and the one-output GEMV;
+// hipErrorInvalidValue for any other shape (the caller runs the groups one by one).
+hipError_t launch_gemm_grouped(const float* A, const float* B, const float* bias, float* C, int64_t M, int64_t N,
+                               int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int ta, int tb, int act, int groups,
+                               int64_t sA, int64_t sB, int64_t sBias, int64_t sC, hipStream_t st) {
+  if (M <= 0 || N <= 0 || groups <= 0) return hipSuccess;
+  if (groups > 65535) return hipErrorInvalidValue;
+  auto al16 = [](int64_t x) { return (x & 3) == 0; };  // a float stride that keeps 16-byte alignment
+  if (tall_ok(A, B, bias, C, M, N, K, lda, ldb, ldc, ta) && (tb ? N : K) * ldb * 4 < ((int64_t)1 << 30) &&
+      al16(sA) && al16(sB) && al16(sC) && (!bias || al16(sBias))) {
+    GemmArgs g{A, B, bias, C, M, N, K, lda, ldb, ldc, act, 1, 0, nullptr, nullptr, -1, nullptr, nullptr, 0,
+               sA, sB, sC, sBias, 0, 0, 0, 0};
+    return launch_tall_rb(g, tb, st, groups);
+  }
+  if (N == 1 && !ta && M >= 256 && K > 0 && lda % 4 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)B & 15) == 0 &&
+      al16(sA) && (tb ? al16(sB) : true)) {
+    GemmArgs g{A, B, bias, C, M, N, K, lda, ldb, ldc, act, 1, 0, nullptr, nullptr, -1, nullptr, nullptr, 0,
+               sA, sB, sC, sBias, 0, 0, 0, 0};
+    k_gemv_n1<<<dim3((unsigned)((M + 3) / 4), (unsigned)groups), 256, 0, st>>>(g, tb ? 1 : ldb);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
+}
+
+// The fused layer backward (launch_linear_backward) of `groups` layers of one shape in one launch
+// per GEMM: dy / y rows of leading dimension ld_dy, x of ld_x, dx of ld_dx; group q's operands at
+// q x the strides. Workspace: groups x linear_backward_plan's per-group floats.
+hipError_t launch_linear_backward_grouped(const float* dy, const float* y, int act, const float* x, const float* W,
+                                          int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy, int64_t ld_x,
+                                          int64_t ld_dx, int groups, int64_t s_dy, int64_t s_x, int64_t s_W,
+                                          int64_t s_dx, int64_t s_dw, int64_t s_db, float* dx, float* dw, float* db,
+                                          float* workspace, hipStream_t st) {
+  if (groups <= 0) return hipSuccess;
+  if (groups > 65535 || ld_dy % 4 || ld_x % 4 || ld_dx % 4 || s_dy % 4 || s_x % 4 || s_dx % 4 || s_W % 4 ||
+      s_dw % 4)
+    return hipErrorInvalidValue;
+  if (dx) {  // dx[rows][n_in] = g[rows][n_out] . W[n_out][n_in], per group
+    if (!lb_dx_ok(rows, n_out, n_in) || rows * ld_dy * 4 >= ((int64_t)1 << 30)) return hipErrorInvalidValue;
+    GemmArgs g{dy, W, nullptr, dx, rows, n_in, n_out, ld_dy, n_in, ld_dx, 0, 1, 0, nullptr, y, act, nullptr, nullptr, 0,
+               s_dy, s_W, s_dx, 0, s_dy, 0, 0, 0};
+    const hipError_t e = launch_tall_rb(g, false, st, groups);
+    if (e != hipSuccess) return e;
+  }
+  if (dw) {  // dW[n_out][n_in] = g^T x over the rows; db[n_out] = column sums of g, per group
+    if (!lb_dw_ok(rows, n_out, n_in) || (rows + TK) * ld_dy * 4 >= ((int64_t)1 << 30) ||
+        (rows + TK) * ld_x * 4 >= ((int64_t)1 << 30))
+      return hipErrorInvalidValue;
+    const int S = deep_splits(n_out, n_in, rows);
+    const int64_t chunks = (rows + TK - 1) / TK;
+    const int64_t per = (chunks + S - 1) / S;
+    const int ntn = (int)((n_in + 63) / 64);
+    const int64_t part = S > 1 ? (int64_t)S * n_out * n_in : 0;
+    const int64_t wsg = part + (db ? (int64_t)S * ntn * n_out : 0);  // per group
+    float* dbp = db ? workspace + part : nullptr;
+    GemmArgs g{dy, x, nullptr, dw, n_out, n_in, rows, ld_dy, ld_x, n_in, 0, S, per, workspace, y, act, db, dbp,
+               S * ntn, s_dy, s_x, s_dw, 0, s_dy, wsg, s_db, wsg};
+    const int tiles_m = (int)(n_out / 64);
+    const dim3 grid((unsigned)(tiles_m * ntn * S), (unsigned)groups);
+    if (per == 5 && chunks == per * S) k_gemm_deep<5, true><<<grid, 256, 0, st>>>(g, tiles_m);
+    else k_gemm_deep<0, true><<<grid, 256, 0, st>>>(g, tiles_m);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || (S == 1 && !db)) return e;
+    const int64_t want = (n_out * n_in + 255) / 256;
+    k_gemm_reduce<<<dim3((unsigned)(want < 2048 ? want : 2048), (unsigned)groups), 256, 0, st>>>(g);
     return hipGetLastError();
   }
   return hipSuccess;

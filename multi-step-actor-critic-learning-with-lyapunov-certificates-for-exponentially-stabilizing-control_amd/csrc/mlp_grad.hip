@@ -149,16 +149,37 @@ __global__ __launch_bounds__(256) void k_colsum_finish(const float* __restrict__
 constexpr int HB_MAX_OUT = 16;
 constexpr int HB_ROWS = 64;
 
+// rows per workgroup: 16 below 16,384 rows (the update's 5,120-row heads: 320 workgroups instead of
+// 80 at 64 rows, so more than one per CU), 64 above
+__host__ __device__ inline int hb_rows(int64_t M) { return M >= 16384 ? HB_ROWS : 16; }
+
+// grouped launches (the twin critics' output layers): blockIdx.y = group q, whose dy, x, W, dx
+// and partials sit at q x the strides; x and dx rows of leading dimension ldx / lddx
+struct HeadGroup {
+  int64_t ldx, lddx, s_dy, s_x, s_W, s_dx, s_part;
+};
+
 template <int NO>
 __global__ __launch_bounds__(256) void k_head_backward(const float* __restrict__ dy, const float* __restrict__ x,
                                                        const float* __restrict__ W, int64_t M, int n_in,
                                                        float* __restrict__ dx, float* __restrict__ pdw,
-                                                       float* __restrict__ pdb) {
+                                                       float* __restrict__ pdb, HeadGroup hg) {
   __shared__ float sdy[HB_ROWS][NO];
   const int tid = threadIdx.x;
-  const int64_t r0 = (int64_t)blockIdx.x * HB_ROWS;
-  const int nr = M - r0 < HB_ROWS ? (int)(M - r0) : HB_ROWS;
-  for (int q = tid; q < HB_ROWS * NO; q += 256) {
+  if (blockIdx.y) {
+    const int64_t q = blockIdx.y;
+    dy += q * hg.s_dy;
+    x += q * hg.s_x;
+    W += q * hg.s_W;
+    if (dx) dx += q * hg.s_dx;
+    if (pdw) pdw += q * hg.s_part;
+    if (pdb) pdb += q * hg.s_part;
+  }
+  const int64_t ldx = hg.ldx, lddx = hg.lddx;
+  const int rpb = hb_rows(M);
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int nr = M - r0 < rpb ? (int)(M - r0) : rpb;
+  for (int q = tid; q < rpb * NO; q += 256) {
     const int r = q / NO, o = q - r * NO;
     sdy[r][o] = r < nr ? dy[(r0 + r) * NO + o] : 0.0f;
   }
@@ -178,7 +199,7 @@ __global__ __launch_bounds__(256) void k_head_backward(const float* __restrict__
     for (int rb = 0; rb < nr; rb += 16) {
       float xv[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) xv[u] = rb + u < nr ? x[(r0 + rb + u) * n_in + j] : 0.0f;  // 16 in flight
+      for (int u = 0; u < 16; ++u) xv[u] = rb + u < nr ? x[(r0 + rb + u) * ldx + j] : 0.0f;  // 16 in flight
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         if (rb + u >= nr) break;
@@ -189,7 +210,7 @@ __global__ __launch_bounds__(256) void k_head_backward(const float* __restrict__
           d = o == 0 ? g * w[0] : d + g * w[o];  // dy[r] . W[:, j], o ascending
           acc[o] = acc[o] + g * xv[u];
         }
-        if (dx) dx[(r0 + rb + u) * n_in + j] = d;
+        if (dx) dx[(r0 + rb + u) * lddx + j] = d;
       }
     }
     if (pdw) {
@@ -199,44 +220,66 @@ __global__ __launch_bounds__(256) void k_head_backward(const float* __restrict__
   }
 }
 
-// dW[o][j] = sum over blocks of pdw[b][o][j] (and db[o] of pdb[b][o]), blocks in order, sixteen
-// loads in flight per batch
+// dW[o][j] = sum over blocks of pdw[b][o][j] (and db[o] of pdb[b][o]): one wave per output, lane l
+// adding blocks l, l + 64, ... in order, the 64 lane sums then added by a fixed butterfly
+// (deterministic; every lane's loads in flight together: one round trip per 64 x 8 blocks, where
+// one thread per output walking all blocks in batches of 16 paid nblk / 16 round trips)
 __global__ __launch_bounds__(256) void k_head_finish(const float* __restrict__ pdw, const float* __restrict__ pdb,
                                                      int nblk, int n_out, int n_in, float* __restrict__ dw,
-                                                     float* __restrict__ db) {
+                                                     float* __restrict__ db, int64_t s_part, int64_t s_dw,
+                                                     int64_t s_db) {
+  if (blockIdx.y) {
+    const int64_t q = blockIdx.y;
+    if (pdw) pdw += q * s_part;
+    if (pdb) pdb += q * s_part;
+    if (dw) dw += q * s_dw;
+    if (db) db += q * s_db;
+  }
+  const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)n_out * n_in;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nw + (db ? n_out : 0); i += (int64_t)gridDim.x * 256) {
-    const bool isw = i < nw;
-    const float* src = isw ? pdw + i : pdb + (i - nw);
-    const int64_t stride = isw ? nw : n_out;
-    float v = 0.0f;
-    for (int b0 = 0; b0 < nblk; b0 += 16) {
-      float t[16];
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= nw + (db ? n_out : 0)) return;
+  const bool isw = i < nw;
+  const float* src = isw ? pdw + i : pdb + (i - nw);
+  const int64_t stride = isw ? nw : n_out;
+  float v = 0.0f;
+  for (int b0 = lane; b0 < nblk; b0 += 8 * 64) {
+    float t[8];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) t[u] = b0 + u < nblk ? src[(int64_t)(b0 + u) * stride] : 0.0f;
+    for (int u = 0; u < 8; ++u) t[u] = b0 + 64 * u < nblk ? src[(int64_t)(b0 + 64 * u) * stride] : 0.0f;
 #pragma unroll
-      for (int u = 0; u < 16; ++u)
-        if (b0 + u < nblk) v = (b0 + u == 0) ? t[u] : v + t[u];
-    }
+    for (int u = 0; u < 8; ++u) v = v + t[u];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = v + __shfl_xor(v, off, 64);
+  if (lane == 0) {
     if (isw) dw[i] = v;
     else db[i - nw] = v;
   }
 }
 
 int64_t head_backward_workspace(int64_t M, int n_out, int n_in) {
-  const int64_t nblk = (M + HB_ROWS - 1) / HB_ROWS;
+  const int rpb = hb_rows(M);
+  const int64_t nblk = (M + rpb - 1) / rpb;
   return nblk * n_out * (int64_t)n_in + nblk * n_out;
 }
 
-hipError_t launch_head_backward(const float* dy, const float* x, const float* W, int64_t M, int n_out, int n_in,
-                                float* dx, float* dw, float* db, float* workspace, hipStream_t st) {
-  if (M <= 0 || n_out <= 0 || n_out > HB_MAX_OUT || n_in <= 0) return hipErrorInvalidValue;
-  const int64_t nblk = (M + HB_ROWS - 1) / HB_ROWS;
+hipError_t launch_head_backward_grouped(const float* dy, const float* x, const float* W, int64_t M, int n_out,
+                                        int n_in, int64_t ldx, int64_t lddx, int groups, int64_t s_dy, int64_t s_x,
+                                        int64_t s_W, int64_t s_dx, int64_t s_dw, int64_t s_db, float* dx, float* dw,
+                                        float* db, float* workspace, hipStream_t st) {
+  if (M <= 0 || n_out <= 0 || n_out > HB_MAX_OUT || n_in <= 0 || groups <= 0 || groups > 65535 || ldx < n_in ||
+      (dx && lddx < n_in))
+    return hipErrorInvalidValue;
+  const int rpb = hb_rows(M);
+  const int64_t nblk = (M + rpb - 1) / rpb;
+  const int64_t wsg = head_backward_workspace(M, n_out, n_in);  // per group
   float* pdw = dw ? workspace : nullptr;
   float* pdb = db ? workspace + nblk * n_out * (int64_t)n_in : nullptr;
-  const unsigned grid = (unsigned)nblk;
+  const dim3 grid((unsigned)nblk, (unsigned)groups);
+  const HeadGroup hg{ldx, lddx, s_dy, s_x, s_W, s_dx, wsg};
 #define HB_CASE(K)                                                                                     \
-  case K: k_head_backward<K><<<grid, 256, 0, st>>>(dy, x, W, M, n_in, dx, pdw, pdb); break;
+  case K: k_head_backward<K><<<grid, 256, 0, st>>>(dy, x, W, M, n_in, dx, pdw, pdb, hg); break;
   switch (n_out) {
     HB_CASE(1) HB_CASE(2) HB_CASE(3) HB_CASE(4) HB_CASE(5) HB_CASE(6) HB_CASE(7) HB_CASE(8)
     HB_CASE(9) HB_CASE(10) HB_CASE(11) HB_CASE(12) HB_CASE(13) HB_CASE(14) HB_CASE(15) HB_CASE(16)
@@ -244,10 +287,17 @@ hipError_t launch_head_backward(const float* dy, const float* x, const float* W,
 #undef HB_CASE
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || (!dw && !db)) return e;
-  const int64_t outs = (int64_t)n_out * n_in + n_out;
-  const int64_t want = (outs + 255) / 256;
-  k_head_finish<<<(unsigned)(want < 1024 ? want : 1024), 256, 0, st>>>(pdw, pdb, (int)nblk, n_out, n_in, dw, db);
+  const int64_t outs = (int64_t)(dw ? n_out * (int64_t)n_in : 0) + (db ? n_out : 0);
+  // (dw is always set with db: the C ABI rejects db without dw)
+  k_head_finish<<<dim3((unsigned)((outs + 3) / 4), (unsigned)groups), 256, 0, st>>>(pdw, pdb, (int)nblk, n_out, n_in,
+                                                                                   dw, db, wsg, s_dw, s_db);
   return hipGetLastError();
+}
+
+hipError_t launch_head_backward(const float* dy, const float* x, const float* W, int64_t M, int n_out, int n_in,
+                                float* dx, float* dw, float* db, float* workspace, hipStream_t st) {
+  return launch_head_backward_grouped(dy, x, W, M, n_out, n_in, n_in, n_in, 1, 0, 0, 0, 0, 0, 0, dx, dw, db, workspace,
+                                      st);
 }
 
 // LyapunovValue's V = sum_j y_j^2 over each row (RL/apprfunc/mlp.py: torch.pow(y, 2).sum(-1)) and
@@ -336,10 +386,78 @@ __global__ __launch_bounds__(256) void k_dx_narrow(const float* __restrict__ dy,
   }
 }
 
+// The same product on the f32 MFMA for n_in <= 16 and n_out % 64 == 0 (the critics' [obs | act]
+// layer: 5,120 x 256 -> 16). k_dx_narrow above sums each output over n_out LDS products in one
+// dependent chain (17 us at 5,120 x 256 x 16: the chain's LDS latency, one workgroup per CU).
+// Here workgroup = 16 rows, wave w = a quarter of the n_out range: per lane 4 x (n_out / 64)
+// independent float4 loads of dy (and y), the 16 x 16 x 4 f32 MFMA over its k range
+// (lane l supplies A[l & 15][k] and W[k][l & 15] with k = 16 s + 4 (l >> 4) + j: a permutation
+// of k, so each lane's loads are row-contiguous float4), the four wave partials added in wave
+// order through LDS. Summation order differs from k_dx_narrow's (f32 rounding level).
+constexpr int DNM_MAX_S = 8;  // n_out / 64 <= 8 (n_out <= 512)
+__device__ __forceinline__ float act_grad_v(float d, float t, int act) {  // k_dx_narrow's g
+  if (act == 1) return t > 0.0f ? d : 0.0f;
+  if (act == 2) return d * (1.0f - t * t);
+  return d;
+}
+__global__ __launch_bounds__(256) void k_dx_narrow_mfma(const float* __restrict__ dy, const float* __restrict__ y,
+                                                        int act, const float* __restrict__ W, int64_t M, int n_out,
+                                                        int n_in, float* __restrict__ dx) {
+  __shared__ float red[3][256];
+  typedef float f32x4v __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * 16;
+  const int64_t row = r0 + (lane & 15);
+  const int S = n_out / 64;  // 16-deep k groups per wave
+  const int kb = w * 16 * S;
+  const int col = lane & 15;
+  f32x4v a[DNM_MAX_S], t[DNM_MAX_S];
+#pragma unroll
+  for (int s = 0; s < DNM_MAX_S; ++s) {
+    if (s < S) {
+      const int k = kb + 16 * s + 4 * (lane >> 4);
+      a[s] = row < M ? *reinterpret_cast<const f32x4v*>(dy + row * n_out + k) : f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+      t[s] = (act != 0 && row < M) ? *reinterpret_cast<const f32x4v*>(y + row * n_out + k) : f32x4v{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+  }
+  f32x4v acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int s = 0; s < DNM_MAX_S; ++s) {
+    if (s < S) {
+      const int k = kb + 16 * s + 4 * (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float g = act_grad_v(a[s][j], t[s][j], act);
+        const float b = col < n_in ? W[(int64_t)(k + j) * n_in + col] : 0.0f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(g, b, acc, 0, 0, 0);
+      }
+    }
+  }
+  // D map: column lane & 15, rows 4 (lane >> 4) + q
+  if (w > 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[w - 1][q * 64 + lane] = acc[q];
+  }
+  __syncthreads();
+  if (w == 0 && col < n_in) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float v = ((acc[q] + red[0][q * 64 + lane]) + red[1][q * 64 + lane]) + red[2][q * 64 + lane];
+      const int64_t r = r0 + 4 * (lane >> 4) + q;
+      if (r < M) dx[r * n_in + col] = v;
+    }
+  }
+}
+
 hipError_t launch_dx_narrow(const float* dy, const float* y, int act, const float* W, int64_t M, int n_out,
                             int n_in, float* dx, hipStream_t st) {
   if (M <= 0) return hipSuccess;
   if (n_in <= 0 || n_in > DN_MAX_IN || n_out <= 0 || n_out > 1024) return hipErrorInvalidValue;
+  if (n_in <= 16 && n_out % 64 == 0 && n_out / 64 <= DNM_MAX_S && ((uintptr_t)dy & 15) == 0 &&
+      (act == 0 || ((uintptr_t)y & 15) == 0)) {
+    k_dx_narrow_mfma<<<(unsigned)((M + 15) / 16), 256, 0, st>>>(dy, y, act, W, M, n_out, n_in, dx);
+    return hipGetLastError();
+  }
   const size_t shm = sizeof(float) * ((size_t)DN_ROWS * n_out + (size_t)n_out * n_in);
   k_dx_narrow<<<(unsigned)((M + DN_ROWS - 1) / DN_ROWS), 256, shm, st>>>(dy, y, act, W, M, n_out, n_in, dx);
   return hipGetLastError();

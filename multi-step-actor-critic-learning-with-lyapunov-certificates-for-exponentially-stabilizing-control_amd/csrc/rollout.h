@@ -147,6 +147,18 @@ hipError_t launch_dx_narrow(const float* dy, const float* y, int act, const floa
 hipError_t launch_square_sum_bwd(const float* y, const float* g, int64_t rows, int cols, float* dy, hipStream_t st);
 hipError_t launch_head_backward(const float* dy, const float* x, const float* W, int64_t M, int n_out, int n_in,
                                 float* dx, float* dw, float* db, float* workspace, hipStream_t st);
+hipError_t launch_head_backward_grouped(const float* dy, const float* x, const float* W, int64_t M, int n_out,
+                                        int n_in, int64_t ldx, int64_t lddx, int groups, int64_t s_dy, int64_t s_x,
+                                        int64_t s_W, int64_t s_dx, int64_t s_dw, int64_t s_db, float* dx, float* dw,
+                                        float* db, float* workspace, hipStream_t st);
+hipError_t launch_gemm_grouped(const float* A, const float* B, const float* bias, float* C, int64_t M, int64_t N,
+                               int64_t K, int64_t lda, int64_t ldb, int64_t ldc, int ta, int tb, int act, int groups,
+                               int64_t sA, int64_t sB, int64_t sBias, int64_t sC, hipStream_t st);
+hipError_t launch_linear_backward_grouped(const float* dy, const float* y, int act, const float* x, const float* W,
+                                          int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy, int64_t ld_x,
+                                          int64_t ld_dx, int groups, int64_t s_dy, int64_t s_x, int64_t s_W,
+                                          int64_t s_dx, int64_t s_dw, int64_t s_db, float* dx, float* dw, float* db,
+                                          float* workspace, hipStream_t st);
 constexpr int ADAM_MAX_TENSORS = 32;
 struct AdamList {  // one optimiser's tensors, passed by value in the kernel arguments
   float* p[ADAM_MAX_TENSORS];

@@ -77,6 +77,9 @@ __device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_
 // the logits in LDS. `next`: stage chunk 0 of the following pass during the last phase.
 template <int D>
 __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int row0, bool next, uint32_t& target) {
+#ifdef MH_FUSED_EXP_NO_POLICY  // cost-attribution experiment only: no policy work (the barriers stay)
+  if (a.H > 0) return;
+#endif
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
   constexpr int FPW = PM_X3_FRAGS / 4;  // W2 fragments each policy wave stages per chunk
   const int lane = threadIdx.x & 63;
@@ -523,11 +526,7 @@ void k_sample_fused(FusedArgs a) {
   }
   __syncthreads();
 
-#ifdef MH_FUSED_EXP_NO_POLICY  // cost-attribution experiment only
-  if (false) {
-#else
   if (pol) {
-#endif
     // ================= policy waves: 2H passes (H1 first, then H0 / H1 alternating)
     PolicyLds L{lds0, lds1, lds_w3, lds_b2, s_obs, s_lgt, &s_bar, a.err};
     uint32_t target = 0;
@@ -663,39 +662,62 @@ __device__ __forceinline__ int emit_cell_count(const int32_t* cnt_t, int b, int 
   return s;
 }
 
+// Rounds of SCAN_THREADS x SCAN_CPT cells: each thread loads its SCAN_CPT cells' counts with
+// independent loads (one memory latency per round instead of one per cell: a loop of dependent
+// per-cell loads took 16.7 us for the bench's 5,120 cells), then a workgroup scan of the thread
+// sums, carried across rounds.
+constexpr int SCAN_CPT = 8;
+
 __global__ __launch_bounds__(SCAN_THREADS) void k_emit_scan(HorizonEmitArgs a) {
   const int NW = (int)((a.E + 63) / 64);
   const int NBK = (NW + 3) / 4;
   const int64_t NC = (int64_t)a.H * NBK;
-  __shared__ int64_t wsum[SCAN_THREADS / 64];
+  __shared__ int64_t wsum[2][SCAN_THREADS / 64];
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  const int64_t per = (NC + SCAN_THREADS - 1) / SCAN_THREADS;
-  const int64_t lo = min(NC, t * per), hi = min(NC, lo + per);
-  int64_t local = 0;
-  for (int64_t c = lo; c < hi; ++c) {
-    const int ts = (int)(c / NBK), b = (int)(c - (int64_t)ts * NBK);
-    local += emit_cell_count(a.emit_count + (int64_t)ts * NW, b, NW);
-  }
-  int64_t incl = local;
+  int64_t carry = 0;
+  int round = 0;
+  for (int64_t c0 = 0; c0 < NC; c0 += (int64_t)SCAN_THREADS * SCAN_CPT, ++round) {
+    int cnt[SCAN_CPT];
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int64_t v = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += v;
-  }
-  if (lane == 63) wsum[wave] = incl;
-  __syncthreads();
-  int64_t wbase = 0, all = 0;
+    for (int j = 0; j < SCAN_CPT; ++j) {
+      const int64_t c = c0 + (int64_t)t * SCAN_CPT + j;
+      if (c < NC) {
+        const int ts = (int)(c / NBK), b = (int)(c - (int64_t)ts * NBK);
+        cnt[j] = emit_cell_count(a.emit_count + (int64_t)ts * NW, b, NW);
+      } else {
+        cnt[j] = 0;
+      }
+    }
+    int64_t local = 0;
 #pragma unroll
-  for (int q = 0; q < SCAN_THREADS / 64; ++q) {
-    wbase += q < wave ? wsum[q] : 0;
-    all += wsum[q];
+    for (int j = 0; j < SCAN_CPT; ++j) local += cnt[j];
+    int64_t incl = local;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int64_t v = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += v;
+    }
+    // double-buffered wave sums: round r + 1 writes the other slot, so one barrier per round
+    // suffices (every wave has read slot r & 1 before any wave passes round r + 1's barrier)
+    if (lane == 63) wsum[round & 1][wave] = incl;
+    __syncthreads();
+    int64_t wbase = 0, all = 0;
+#pragma unroll
+    for (int q = 0; q < SCAN_THREADS / 64; ++q) {
+      const int64_t s = wsum[round & 1][q];
+      wbase += q < wave ? s : 0;
+      all += s;
+    }
+    int64_t run = carry + wbase + incl - local;
+#pragma unroll
+    for (int j = 0; j < SCAN_CPT; ++j) {
+      const int64_t c = c0 + (int64_t)t * SCAN_CPT + j;
+      if (c < NC) a.scan[c] = run;
+      run += cnt[j];
+    }
+    carry += all;
   }
-  int64_t run = wbase + incl - local;
-  for (int64_t c = lo; c < hi; ++c) {
-    a.scan[c] = run;
-    const int ts = (int)(c / NBK), b = (int)(c - (int64_t)ts * NBK);
-    run += emit_cell_count(a.emit_count + (int64_t)ts * NW, b, NW);
-  }
+  const int64_t all = carry;
   __syncthreads();  // (workgroup-scope fence + barrier: thread 0 reads the scan written above)
   if (t == 0) {
     const int64_t M = a.capacity, c0 = a.cursor[0];

@@ -72,7 +72,9 @@ def _assert_same(a, ba, b, bb, where):
 
 
 CASES = [(nm, 65536, 20, False) for nm in OE.ENVS] + [("QuadTracking", 65536, 20, True), ("QuadTracking", 4000, 20, False),
-                                                     ("DuctedFan", 300, 3, False), ("TwoLink", 777, 5, False)]
+                                                     ("DuctedFan", 300, 3, False), ("TwoLink", 777, 5, False),
+                                                     # > 8,192 emission cells: k_emit_scan runs several rounds
+                                                     ("VanderPol", 200000, 20, False)]
 
 
 @pytest.mark.parametrize("name,E,n,hover", CASES, ids=[f"{c[0]}-{c[1]}-n{c[2]}{'-hover' if c[3] else ''}" for c in CASES])

@@ -144,7 +144,8 @@ def test_square_sum_matches_torch(rows, cols):
     assert torch.equal(a.grad, b.grad)
 
 
-@pytest.mark.parametrize("rows,n_in,n_out", [(5120, 16, 256), (5120, 12, 256), (1031, 32, 100), (2048, 1, 7)])
+@pytest.mark.parametrize("rows,n_in,n_out", [(5120, 16, 256), (5120, 12, 256), (1031, 32, 100), (2048, 1, 7),
+                                            (5119, 16, 512), (100, 7, 64), (33, 16, 128)])
 @pytest.mark.parametrize("act", [0, 1, 2])
 def test_dx_narrow_matches_float64(rows, n_in, n_out, act):
     """mh_dx_narrow (input gradient only of a narrow-input layer, act' on the fly) against float64."""
