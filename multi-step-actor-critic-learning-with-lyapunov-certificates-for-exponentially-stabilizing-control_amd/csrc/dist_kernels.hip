@@ -144,52 +144,75 @@ __global__ __launch_bounds__(256) void k_stocha_head_bwd(const float* __restrict
 //   rsample (eps given): act = h tanh(mu + std eps) + m and its log-prob (k_tg_rsample's math),
 //     the act written into the critic input row xq = [obs | act] (ActionValue's concat);
 //   log_prob(old_act) (old_act given): k_tg_log_prob's math;
-// in one launch instead of stocha_head + rsample + log_prob + a concat per critic. One thread per
-// row; every expression as in the separate kernels, so the values are theirs bit for bit.
+// in one launch instead of stocha_head + rsample + log_prob + a concat per critic. One LANE per
+// (row, action dim) in groups of PH_G = 8 lanes per row (A <= 8): each lane evaluates its
+// dimension's terms (the transcendental chain of one dimension instead of A of them per thread:
+// the kernel is latency-bound at B*n = 5,120 rows), and the row's sums are formed by the group's
+// first lane over the A lane values in dimension order, 0 + t0 + t1 + ..., exactly the
+// per-row loop's order: every value is the separate kernels' bit for bit.
+constexpr int PH_G = 8;
+
+__device__ __forceinline__ float ph_row_sum(float v, int A, int base) {  // sum_{i < A} v(lane base + i), in order
+  float s = 0.0f;
+  for (int i = 0; i < A; ++i) s = s + __shfl(v, base + i, 64);
+  return s;
+}
+
 __global__ __launch_bounds__(256) void k_policy_head(const float* __restrict__ raw, const float* __restrict__ eps,
                                                      const float* __restrict__ obs, const float* __restrict__ old_act,
                                                      const float* __restrict__ high, const float* __restrict__ low,
                                                      int64_t M, int A, int D, float lo, float hi,
                                                      float* __restrict__ xq, float* __restrict__ new_logp,
                                                      float* __restrict__ old_logp) {
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= M) return;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r = t / PH_G;
+  const int i = (int)(t % PH_G);
+  const int base = (threadIdx.x & 63) & ~(PH_G - 1);
+  const bool row_ok = r < M;  // (whole groups share a row: the shuffles below stay in the group)
+  const bool on = row_ok && i < A;
   const int W = D + A;
-  if (xq && obs) {
-    for (int j = 0; j < D; ++j) xq[r * W + j] = obs[r * D + j];
+  if (row_ok && xq && obs) {
+    for (int j = i; j < D; j += PH_G) xq[r * W + j] = obs[r * D + j];
   }
-  float lg = 0.0f, lt = 0.0f, lh = 0.0f, og = 0.0f, oj = 0.0f;
-  for (int i = 0; i < A; ++i) {
+  float lgv = 0.0f, ltv = 0.0f, lhv = 0.0f, ogv = 0.0f, ojv = 0.0f;
+  if (on) {
     const float mu = raw[r * 2 * A + i];
     const float sd = expf(fminf(fmaxf(raw[r * 2 * A + A + i], lo), hi));
     if (eps) {
       const float z = mu + sd * eps[r * A + i];
       const float df = z - mu;
       const float var = sd * sd;
-      lg = lg + ((-(df * df) / (2.0f * var) - logf(sd)) - kLogSqrt2Pi);
-      const float t = tanhf(z);
-      lt = lt + logf(1.000001f - t * t);
+      lgv = (-(df * df) / (2.0f * var) - logf(sd)) - kLogSqrt2Pi;
+      const float tz = tanhf(z);
+      ltv = logf(1.000001f - tz * tz);
       const float h = (high[i] - low[i]) / 2.0f, m = (high[i] + low[i]) / 2.0f;
-      lh = lh + logf(h);
-      if (xq) xq[r * W + D + i] = h * t + m;
+      lhv = logf(h);
+      if (xq) xq[r * W + D + i] = h * tz + m;
     }
     if (old_act) {
       const float hl = high[i] + low[i], dl = high[i] - low[i];
       const float z = atanhf(0.999999f * (2.0f * old_act[r * A + i] - hl) / dl);
       const float df = z - mu;
-      og = og + ((-(df * df) / (2.0f * (sd * sd)) - logf(sd)) - kLogSqrt2Pi);
-      const float t = tanhf(z);
-      oj = oj + logf(dl / 2.0f * (1.000001f - t * t));
+      ogv = (-(df * df) / (2.0f * (sd * sd)) - logf(sd)) - kLogSqrt2Pi;
+      const float tz = tanhf(z);
+      ojv = logf(dl / 2.0f * (1.000001f - tz * tz));
     }
   }
-  if (eps && new_logp) new_logp[r] = (lg - lt) - lh;
-  if (old_act && old_logp) old_logp[r] = og - oj;
+  if (eps && new_logp) {
+    const float lg = ph_row_sum(lgv, A, base), lt = ph_row_sum(ltv, A, base), lh = ph_row_sum(lhv, A, base);
+    if (row_ok && i == 0) new_logp[r] = (lg - lt) - lh;
+  }
+  if (old_act && old_logp) {
+    const float og = ph_row_sum(ogv, A, base), oj = ph_row_sum(ojv, A, base);
+    if (row_ok && i == 0) old_logp[r] = og - oj;
+  }
 }
 
 // Its backward: d_raw from the gradients of the critic input's action columns (d_xq), of the
 // sample's log-prob (d_new_logp) and of log_prob(old_act) (d_old_logp), any of them null:
 // k_tg_rsample_bwd's and k_tg_log_prob_bwd's expressions, their d_logits added as autograd
-// accumulates them (one term alone is not added to anything), then k_stocha_head_bwd's.
+// accumulates them (one term alone is not added to anything), then k_stocha_head_bwd's. One lane
+// per (row, action dim): the dimensions are independent.
 __global__ __launch_bounds__(256) void k_policy_head_bwd(const float* __restrict__ raw, const float* __restrict__ eps,
                                                          const float* __restrict__ old_act,
                                                          const float* __restrict__ high, const float* __restrict__ low,
@@ -197,59 +220,61 @@ __global__ __launch_bounds__(256) void k_policy_head_bwd(const float* __restrict
                                                          const float* __restrict__ d_new_logp,
                                                          const float* __restrict__ d_old_logp, int64_t M, int A, int D,
                                                          float lo, float hi, float* __restrict__ d_raw) {
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= M) return;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r = t / PH_G;
+  const int i = (int)(t % PH_G);
+  if (r >= M || i >= A) return;
   const int W = D + A;
   const bool samp = eps && (d_xq || d_new_logp);
   const bool score = old_act && d_old_logp;
   const float gl = d_new_logp ? d_new_logp[r] : 0.0f;
   const float go = score ? d_old_logp[r] : 0.0f;
-  for (int i = 0; i < A; ++i) {
-    const float mu = raw[r * 2 * A + i];
-    const float x = raw[r * 2 * A + A + i];
-    const float sd = expf(fminf(fmaxf(x, lo), hi));
-    float dmu = 0.0f, dsd = 0.0f;
-    if (samp) {
-      const float e = eps[r * A + i];
-      const float z = mu + sd * e;
-      const float df = z - mu;
-      const float var = sd * sd;
-      const float t = tanhf(z);
-      const float h = (high[i] - low[i]) / 2.0f;
-      const float ga = d_xq ? d_xq[r * W + D + i] : 0.0f;
-      const float u = 1.000001f - t * t;
-      const float dt = ga * h + gl * (2.0f * t / u);
-      float dz = dt * (1.0f - t * t);
-      const float q = df / var;
-      dz = dz + gl * (-q);
-      dmu = dz + gl * q;
-      const float dvar = gl * (df * df) / (2.0f * var * var);
-      dsd = dz * e + dvar * (2.0f * sd) - gl / sd;
-    }
-    if (score) {
-      const float hl = high[i] + low[i], dl = high[i] - low[i];
-      const float z = atanhf(0.999999f * (2.0f * old_act[r * A + i] - hl) / dl);
-      const float df = z - mu;
-      const float var = sd * sd;
-      const float m2 = go * (df / var);
-      const float s2 = go * ((df * df) / (2.0f * var * var)) * (2.0f * sd) - go / sd;
-      dmu = samp ? dmu + m2 : m2;
-      dsd = samp ? dsd + s2 : s2;
-    }
-    d_raw[r * 2 * A + i] = dmu;
-    const float gx = dsd * sd;
-    d_raw[r * 2 * A + A + i] = (x >= lo && x <= hi) ? gx : gx * 0.0f;
+  const float mu = raw[r * 2 * A + i];
+  const float x = raw[r * 2 * A + A + i];
+  const float sd = expf(fminf(fmaxf(x, lo), hi));
+  float dmu = 0.0f, dsd = 0.0f;
+  if (samp) {
+    const float e = eps[r * A + i];
+    const float z = mu + sd * e;
+    const float df = z - mu;
+    const float var = sd * sd;
+    const float tz = tanhf(z);
+    const float h = (high[i] - low[i]) / 2.0f;
+    const float ga = d_xq ? d_xq[r * W + D + i] : 0.0f;
+    const float u = 1.000001f - tz * tz;
+    const float dt = ga * h + gl * (2.0f * tz / u);
+    float dz = dt * (1.0f - tz * tz);
+    const float q = df / var;
+    dz = dz + gl * (-q);
+    dmu = dz + gl * q;
+    const float dvar = gl * (df * df) / (2.0f * var * var);
+    dsd = dz * e + dvar * (2.0f * sd) - gl / sd;
   }
+  if (score) {
+    const float hl = high[i] + low[i], dl = high[i] - low[i];
+    const float z = atanhf(0.999999f * (2.0f * old_act[r * A + i] - hl) / dl);
+    const float df = z - mu;
+    const float var = sd * sd;
+    const float m2 = go * (df / var);
+    const float s2 = go * ((df * df) / (2.0f * var * var)) * (2.0f * sd) - go / sd;
+    dmu = samp ? dmu + m2 : m2;
+    dsd = samp ? dsd + s2 : s2;
+  }
+  d_raw[r * 2 * A + i] = dmu;
+  const float gx = dsd * sd;
+  d_raw[r * 2 * A + A + i] = (x >= lo && x <= hi) ? gx : gx * 0.0f;
 }
 
 static inline unsigned grid_rows(int64_t M) { return (unsigned)((M + 255) / 256); }
+static inline unsigned grid_row_lanes(int64_t M) { return (unsigned)((M * PH_G + 255) / 256); }
 
 hipError_t launch_policy_head(const float* raw, const float* eps, const float* obs, const float* old_act,
                               const float* high, const float* low, int64_t M, int A, int D, float lo, float hi,
                               float* xq, float* new_logp, float* old_logp, hipStream_t st) {
   if (M <= 0) return hipSuccess;
-  k_policy_head<<<grid_rows(M), 256, 0, st>>>(raw, eps, obs, old_act, high, low, M, A, D, lo, hi, xq, new_logp,
-                                              old_logp);
+  if (A <= 0 || A > PH_G) return hipErrorInvalidValue;
+  k_policy_head<<<grid_row_lanes(M), 256, 0, st>>>(raw, eps, obs, old_act, high, low, M, A, D, lo, hi, xq, new_logp,
+                                                   old_logp);
   return hipGetLastError();
 }
 hipError_t launch_policy_head_bwd(const float* raw, const float* eps, const float* old_act, const float* high,
@@ -257,8 +282,9 @@ hipError_t launch_policy_head_bwd(const float* raw, const float* eps, const floa
                                   const float* d_old_logp, int64_t M, int A, int D, float lo, float hi, float* d_raw,
                                   hipStream_t st) {
   if (M <= 0) return hipSuccess;
-  k_policy_head_bwd<<<grid_rows(M), 256, 0, st>>>(raw, eps, old_act, high, low, d_xq, d_new_logp, d_old_logp, M, A,
-                                                  D, lo, hi, d_raw);
+  if (A <= 0 || A > PH_G) return hipErrorInvalidValue;
+  k_policy_head_bwd<<<grid_row_lanes(M), 256, 0, st>>>(raw, eps, old_act, high, low, d_xq, d_new_logp, d_old_logp, M,
+                                                       A, D, lo, hi, d_raw);
   return hipGetLastError();
 }
 

@@ -49,16 +49,53 @@ struct PolicyLds {
   uint4* c1;
   const uint4* w3;      // fold operands [ob][s][split][lane]
   const float* b2;      // layer-2 bias, [256]
+  const float* b3;      // layer-3 bias, [N3] (LDS: the pass epilogue's 16 bias reads stay off the memory path)
   const float* obs;     // [256][D] observations of the workgroup's envs
   float* lgt;           // [256][N3] logits out
   uint32_t* bar;        // policy-wave barrier counter
   int64_t* err;         // device error word (bounded waits that timed out)
 };
 
+// 16-byte LDS-DMA (global_load_lds_dwordx4: this lane's 16 bytes at gsrc -> LDS lds_dst + 16 lane) as
+// inline asm, M0 written in the same statement (cdna_hip_programming.md's recipe). Not the builtin:
+// hipcc books a global_load_lds as a FLAT access to both memory and LDS, and while one is pending
+// it widens EVERY later LDS wait to lgkmcnt(0) and every memory wait to vmcnt(0) — with W2 always
+// streaming, the ring's two-steps-ahead LDS reads were waited for one step after issue and each
+// phase's first W1 register load waited for the chunk DMA just issued. The asm DMA is invisible
+// to that bookkeeping: its completion is counted explicitly (pol_sync's vmcnt(0)).
+__device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
+  const uint32_t l = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)lds_dst);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(l)
+               : "memory");
+}
+
+#ifdef MH_FUSED_EXP_STAMPS
+// diagnostic build only: lane 0 of policy wave w of workgroup b < 4 stores s_memtime at slot `slot`
+// of pass `pass` into the debug-logits buffer (reinterpreted as uint64 [4 wg][4 wave][64 pass][32])
+#define MH_STAMP(a, pass, slot)                                                                      \
+  do {                                                                                               \
+    if (blockIdx.x < 4 && (threadIdx.x & 63) == 0 && (a).lgt_out) {                                  \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime();                                              \
+      reinterpret_cast<uint64_t*>((a).lgt_out)[((blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 + (pass)) * 32 + (slot)] = t_; \
+    }                                                                                                \
+  } while (0)
+#else
+#define MH_STAMP(a, pass, slot) \
+  do {                          \
+  } while (0)
+#endif
+
 // the four policy waves' barrier: own LDS-DMA landed (vmcnt(0)), arrive, wait for all four. The
 // wait is bounded (~1e9 cycles): a wave that gives up records it in *err (read by the tests
 // through mh_sample_horizon_errors) instead of hanging the device
 __device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_t* err) {
+#ifdef MH_FUSED_EXP_NOSYNC  // cost-attribution experiment only (races: garbage logits)
+  target += 4;
+  return;
+#endif
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   target += 4;
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -76,7 +113,10 @@ __device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_
 // all three layers; k_policy_forward_x3<1, 8>'s per-tile sequence with the observation rows and
 // the logits in LDS. `next`: stage chunk 0 of the following pass during the last phase.
 template <int D>
-__device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int row0, bool next, uint32_t& target) {
+__device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int row0, bool next, uint32_t& target,
+                            int pass_no = 0) {
+  MH_STAMP(a, pass_no, 0);
+  (void)pass_no;
 #ifdef MH_FUSED_EXP_NO_POLICY  // cost-attribution experiment only: no policy work (the barriers stay)
   if (a.H > 0) return;
 #endif
@@ -85,7 +125,6 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
   const int lane = threadIdx.x & 63;
   const int K1 = a.K1, N3 = a.N3;
   const float* P = a.P;
-  const float* b3 = P + pm_off_b3(K1);
   const uint4* W2g = reinterpret_cast<const uint4*>(P + pm_off_w2x3(K1));
   const uint4* W1g = reinterpret_cast<const uint4*>(P + pm_off_w1x3(K1));
   const PmScales scs = pm_scales(P + pm_off_scal(K1));
@@ -93,12 +132,13 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
   const float one = 1.0f;
 
   auto stage = [&](int ib, uint4* dstbuf) {
+#ifdef MH_FUSED_EXP_NODMA  // cost-attribution experiment only (stale chunks)
+    if (a.H > 0) return;
+#endif
     const uint4* src = W2g + ((int64_t)ib * PM_X3_FRAGS + pw * FPW) * 64;
     asm volatile("" : "+s"(src));
 #pragma unroll
-    for (int i = 0; i < FPW; ++i)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src + i * 64 + lane),
-                                       (void __attribute__((address_space(3)))*)(&dstbuf[(pw * FPW + i) * 64]), 16, 0, 0);
+    for (int i = 0; i < FPW; ++i) glds16(src + i * 64 + lane, &dstbuf[(pw * FPW + i) * 64]);
   };
   auto l1_mfma = [&](const uint4* wf, const f16x8& xh, const f16x8& xl) {
     const f16x8 wh = __builtin_bit_cast(f16x8, wf[0]), wl = __builtin_bit_cast(f16x8, wf[1]);
@@ -168,8 +208,9 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
     uint4* nxt_lds = B ? L.c0 : L.c1;
     const bool has_next = ib < PM_NB - 1 || next;
     const int nib = (ib + 1) & (PM_NB - 1);
+    MH_STAMP(a, pass_no, 1 + 2 * ib);
     pol_sync(L.bar, target, L.err);  // chunk ib landed in every policy wave's share
-    if (has_next) stage(nib, nxt_lds);
+    MH_STAMP(a, pass_no, 2 + 2 * ib);
     const bool pipe = !fold;
     f32x16 hn;
     f16x8 xh2[2], xl2[2];
@@ -188,8 +229,12 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
         for (int p = 0; p < 2; ++p) ring[(st + 2) % 3][p] = Lc[((st + 2) * 2 + p) * 64];
       }
       const uint4* cur = ring[st % 3];
+      if (pipe && st == 0) hn = l1_mfma(w1c, xoh, xol);
+      // the next chunk's DMA into the other buffer (every policy wave finished reading it in the
+      // previous phase: the pol_sync above), issued after this phase's first W1 use so that the
+      // use's own wait never covers it; then the W1 block two phases ahead
+      if (st == 0 && has_next) stage(nib, nxt_lds);
       if (pipe && st == 0) {
-        hn = l1_mfma(w1c, xoh, xol);
         if (ib + 2 < PM_NB) {
           w1c[0] = W1g[((ib + 2) * 2 + 0) * 64 + lane];
           w1c[1] = W1g[((ib + 2) * 2 + 1) * 64 + lane];
@@ -240,7 +285,11 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
         }
         acc[0] = o;
       }
+#ifdef MH_FUSED_EXP_FOLD_NOSB  // experiment: the compiler may interleave the fold phase's steps
+      if (!fold) __builtin_amdgcn_sched_barrier(0);
+#else
       __builtin_amdgcn_sched_barrier(0);
+#endif
     }
     if (pipe) {
       xh[0] = xh2[0];
@@ -257,15 +306,20 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
     phase(B1{}, ib + 1, false);
   }
   phase(B0{}, PM_NB - 2, false);
+#ifdef MH_FUSED_EXP_NOFOLD  // cost-attribution experiment: no layer 3 (garbage logits)
+  phase(B1{}, PM_NB - 1, false);
+#else
   phase(B1{}, PM_NB - 1, true);
+#endif
   // logits rows (registers r hold output pm_row(r, lane) of env column lane & 31), the same
   // expression as k_policy_forward_x3's store
+  MH_STAMP(a, pass_no, 17);
   const float iu = isw3 * pm_pow2(-ex[2]);
   const int row = row0 + (lane & 31);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int oo = pm_row(r, lane);
-    if (oo < N3) L.lgt[row * N3 + oo] = acc[0][r] * iu + b3[oo];
+    if (oo < N3) L.lgt[row * N3 + oo] = acc[0][r] * iu + L.b3[oo];
   }
 }
 
@@ -309,7 +363,11 @@ __device__ __forceinline__ void env_lockstep(const FusedArgs& a, EnvLane<Env>& v
       if (bad) __hip_atomic_fetch_add(a.err + 0, (int64_t)(1 << 20), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #endif
+#ifdef MH_FUSED_EXP_STAMPS
+    if (false) {
+#else
     if (a.lgt_out) {
+#endif
 #pragma unroll
       for (int i = 0; i < 2 * A; ++i) a.lgt_out[((int64_t)t * a.E + e) * 2 * A + i] = lgt[i];
 #pragma unroll
@@ -471,6 +529,7 @@ void k_sample_fused(FusedArgs a) {
   __shared__ uint4 lds1[PM_X3_FRAGS * 64];
   __shared__ uint4 lds_w3[PM_NB * 4 * 64];
   __shared__ float lds_b2[PM_H];
+  __shared__ float lds_b3[32];
   __shared__ float s_obs[FUSED_ENVS * D];
   __shared__ float s_lgt[FUSED_ENVS * N3C];
 #ifdef MH_FUSED_DIRECT_RING
@@ -507,8 +566,7 @@ void k_sample_fused(FusedArgs a) {
 #pragma unroll
     for (int i = 0; i < FOPW; ++i) {
       const int r = w * FOPW + i;
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(w3g + r * 64 + lane),
-                                       (void __attribute__((address_space(3)))*)(&lds_w3[r * 64]), 16, 0, 0);
+      glds16(w3g + r * 64 + lane, &lds_w3[r * 64]);
     }
     // compact b2 from the packed [ob][lane][16] copy: lanes 0 and 32 of each block hold all 32 rows
     const float* b2p = a.P + pm_off_b2(a.K1);
@@ -516,31 +574,32 @@ void k_sample_fused(FusedArgs a) {
       const int r = q & 15, l = ((q >> 4) & 1) * 32, ob = q >> 5;
       lds_b2[ob * 32 + pm_row(r, l)] = b2p[((int64_t)ob * 64 + l) * 16 + r];
     }
+    if (threadIdx.x < 32) lds_b3[threadIdx.x] = (int)threadIdx.x < a.N3 ? a.P[pm_off_b3(a.K1) + threadIdx.x] : 0.0f;
     const uint4* W2g = reinterpret_cast<const uint4*>(a.P + pm_off_w2x3(a.K1));
     constexpr int FPW = PM_X3_FRAGS / 4;
 #pragma unroll
-    for (int i = 0; i < FPW; ++i)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(W2g + (w * FPW + i) * 64 + lane),
-                                       (void __attribute__((address_space(3)))*)(&lds0[(w * FPW + i) * 64]), 16, 0, 0);
+    for (int i = 0; i < FPW; ++i) glds16(W2g + (w * FPW + i) * 64 + lane, &lds0[(w * FPW + i) * 64]);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's fold operands landed before the barrier
   }
   __syncthreads();
 
   if (pol) {
     // ================= policy waves: 2H passes (H1 first, then H0 / H1 alternating)
-    PolicyLds L{lds0, lds1, lds_w3, lds_b2, s_obs, s_lgt, &s_bar, a.err};
+    PolicyLds L{lds0, lds1, lds_w3, lds_b2, lds_b3, s_obs, s_lgt, &s_bar, a.err};
     uint32_t target = 0;
     const int total = 2 * H;
     int pass = 0;
-    policy_pass<D>(a, L, w, FUSED_ENVS / 2 + w * 32, ++pass < total, target);
+    policy_pass<D>(a, L, w, FUSED_ENVS / 2 + w * 32, ++pass < total, target, pass);
     __syncthreads();
     for (int t = 0; t < H; ++t) {
-      policy_pass<D>(a, L, w, w * 32, ++pass < total, target);  // A(t): H0
+      policy_pass<D>(a, L, w, w * 32, ++pass < total, target, pass);  // A(t): H0
+      MH_STAMP(a, pass, 18);
       __syncthreads();
 #ifdef MH_FUSED_EXP_SERIAL
       __syncthreads();
 #endif
-      if (t < H - 1) policy_pass<D>(a, L, w, FUSED_ENVS / 2 + w * 32, ++pass < total, target);  // B(t): H1
+      if (t < H - 1) policy_pass<D>(a, L, w, FUSED_ENVS / 2 + w * 32, ++pass < total, target, pass);  // B(t): H1
+      MH_STAMP(a, pass, 18);
       __syncthreads();
 #ifdef MH_FUSED_EXP_SERIAL
       __syncthreads();

@@ -185,7 +185,10 @@ def test_msacl_update_grouped_equals_two_networks(tmp_path):
     algs[1].networks.load_state_dict(algs[0].networks.state_dict())
     g = torch.Generator(device="cuda").manual_seed(5)
     B, n = 256, 20
-    batch = {"obs": _rand(B, n, 12, g=g), "act": torch.tanh(_rand(B, n, 4, g=g)), "rew": _rand(B, n, g=g),
+    lo = torch.as_tensor(cls.act_low, dtype=torch.float32, device="cuda")
+    hi = torch.as_tensor(cls.act_high, dtype=torch.float32, device="cuda")
+    act = lo + (hi - lo) * torch.sigmoid(_rand(B, n, 4, g=g))  # inside the action box (TanhGauss log-prob)
+    batch = {"obs": _rand(B, n, 12, g=g), "act": act.contiguous(), "rew": _rand(B, n, g=g),
              "cost": _rand(B, n, g=g).abs(), "obs2": _rand(B, n, 12, g=g),
              "done": (torch.rand(B, n, device="cuda", generator=g) < 0.05).float(), "logp": _rand(B, n, g=g)}
     for it in (0, 1):
@@ -198,7 +201,7 @@ def test_msacl_update_grouped_equals_two_networks(tmp_path):
             for k, v in outs[0].items():
                 if "time" in k:
                     continue
-                assert abs(v - outs[1][k]) <= 1e-4 * (1 + abs(v)), (it, k, v, outs[1][k])
+                assert v == v and abs(v - outs[1][k]) <= 1e-4 * (1 + abs(v)), (it, k, v, outs[1][k])
     # Adam's first steps are ~lr * sign(g): a gradient element at the summation-order noise level
     # may take the other sign (2 lr per step apart); every other element agrees to f32 noise
     for (k, p), (_, r) in zip(algs[0].networks.named_parameters(), algs[1].networks.named_parameters()):

@@ -27,7 +27,7 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
     cfg = default_msacl_args(env_name=a.env, env_num=a.envs, env_seed=1, seed=0, sample_batch_size=20, n_step=20,
-                             replay_batch_size=256, buffer_max_size=int(1e6), buffer_warm_size=5000,
+                             replay_batch_size=256, buffer_max_size=int(1e6), buffer_warm_size=0,
                              max_iteration=10 ** 9, eval_interval=10 ** 9, log_save_interval=10 ** 9,
                              apprfunc_save_interval=10 ** 9, save_folder=tempfile.mkdtemp(), num_eval_episode=1,
                              sampler_sync_timing=False, device=dev)
