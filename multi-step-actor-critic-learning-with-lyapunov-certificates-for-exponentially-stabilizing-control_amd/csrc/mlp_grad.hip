@@ -189,6 +189,23 @@ __global__ __launch_bounds__(256) void k_head_backward(const float* __restrict__
     for (int r = 0; r < nr; ++r) s = s + sdy[r][tid];
     pdb[(int64_t)blockIdx.x * NO + tid] = s;
   }
+  if (!pdw) {  // input gradient only (frozen heads): dx = dy W needs no x
+    for (int j = tid; j < n_in; j += 256) {
+      float w[NO];
+#pragma unroll
+      for (int o = 0; o < NO; ++o) w[o] = W[(int64_t)o * n_in + j];
+      for (int r = 0; r < nr; ++r) {
+        float d = 0.0f;
+#pragma unroll
+        for (int o = 0; o < NO; ++o) {
+          const float g = sdy[r][o];
+          d = o == 0 ? g * w[0] : d + g * w[o];  // dy[r] . W[:, j], o ascending (as below)
+        }
+        if (dx) dx[(r0 + r) * lddx + j] = d;
+      }
+    }
+    return;
+  }
   for (int j = tid; j < n_in; j += 256) {
     float w[NO], acc[NO];
 #pragma unroll

@@ -50,6 +50,7 @@ struct PolicyLds {
   const uint4* w3;      // fold operands [ob][s][split][lane]
   const float* b2;      // layer-2 bias, [256]
   const float* b3;      // layer-3 bias, [N3] (LDS: the pass epilogue's 16 bias reads stay off the memory path)
+  const uint4* w1;      // layer-1 fragments [blk][split][lane] (LDS: no memory loads inside a pass)
   const float* obs;     // [256][D] observations of the workgroup's envs
   float* lgt;           // [256][N3] logits out
   uint32_t* bar;        // policy-wave barrier counter
@@ -101,8 +102,7 @@ __device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   uint32_t spins = 0;
   while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
-    __builtin_amdgcn_s_sleep(1);
-    if (++spins == (1u << 24)) {
+    if (++spins == (1u << 26)) {  // (LDS polls without a sleep: the hand-off is within one CU)
       if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(err, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
@@ -126,7 +126,6 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
   const int K1 = a.K1, N3 = a.N3;
   const float* P = a.P;
   const uint4* W2g = reinterpret_cast<const uint4*>(P + pm_off_w2x3(K1));
-  const uint4* W1g = reinterpret_cast<const uint4*>(P + pm_off_w1x3(K1));
   const PmScales scs = pm_scales(P + pm_off_scal(K1));
   const float isw1 = scs.isw[0], isw2 = scs.isw[1], isw3 = scs.isw[2], R1 = scs.R1, R2 = scs.R2;
   const float one = 1.0f;
@@ -192,9 +191,9 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
   f16x8 xh[2], xl[2];
   uint4 w1c[2];
   {
-    const uint4 w10[2] = {W1g[lane], W1g[64 + lane]};
-    w1c[0] = W1g[(1 * 2 + 0) * 64 + lane];
-    w1c[1] = W1g[(1 * 2 + 1) * 64 + lane];
+    const uint4 w10[2] = {L.w1[lane], L.w1[64 + lane]};
+    w1c[0] = L.w1[(1 * 2 + 0) * 64 + lane];
+    w1c[1] = L.w1[(1 * 2 + 1) * 64 + lane];
     l1_split(l1_mfma(w10, xoh, xol), pm_pow2(ex[1] - ex[0]) * isw1, xh, xl);
   }
   const float k23 = isw2 * pm_pow2(ex[2] - ex[1]), sc3 = pm_pow2(ex[2]);
@@ -215,6 +214,57 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
     f32x16 hn;
     f16x8 xh2[2], xl2[2];
     const uint4* Lc = cur_lds + lane;
+    uint4 w3f[4];
+    f32x4 b2f[4];
+    // H2 block fb final: bias, ReLU, rescale, split, layer 3, one half (ks: registers 8 ks ..
+    // 8 ks + 7, hidden units 16 ks + ... of the block) per call. Blocks and halves are folded in
+    // the order (fb, ks) = (0, 0), (0, 1), (1, 0), ...: k_policy_forward_x3's layer-3 order
+    // (block 0: both halves split before its registers become the layer-3 accumulator acc[0])
+    auto split_half = [&](int fb, int ks, f16x8& hh, f16x8& hl) {
+      uint32_t hp[4], lp[4];
+      const f32x2 k2 = {k23, k23}, s2 = {sc3, sc3};
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const int r = 8 * ks + 2 * p;
+        const f32x2 bs = f32x2{b2f[r >> 2][r & 3], b2f[r >> 2][(r & 3) + 1]} * s2;
+        const f32x2 y = __builtin_elementwise_fma(f32x2{acc[fb][r], acc[fb][r + 1]}, k2, bs);
+        split2h_pair(relu_raw(y.x), relu_raw(y.y), one, hp[p], lp[p]);
+      }
+      hh = __builtin_bit_cast(f16x8, uint4{hp[0], hp[1], hp[2], hp[3]});
+      hl = __builtin_bit_cast(f16x8, uint4{lp[0], lp[1], lp[2], lp[3]});
+    };
+    auto fold_mfma = [&](f32x16 o, int ks, const f16x8& hh, const f16x8& hl) {
+      const f16x8 vh = __builtin_bit_cast(f16x8, w3f[2 * ks]);
+      const f16x8 vl = __builtin_bit_cast(f16x8, w3f[2 * ks + 1]);
+      o = MH_MFMA(vl, hh, o);
+      o = MH_MFMA(vh, hl, o);
+      o = MH_MFMA(vh, hh, o);
+      return o;
+    };
+    auto fold_half = [&](int fb, int ks) {
+      if (fb == 0) {
+        if (ks == 1) return;  // block 0 whole at its first fold step
+        f16x8 h0, l0, h1, l1;
+        split_half(0, 0, h0, l0);
+        split_half(0, 1, h1, l1);
+        acc[0] = fold_mfma(fold_mfma(f32x16{}, 0, h0, l0), 1, h1, l1);
+        return;
+      }
+      f16x8 hh, hl;
+      split_half(fb, ks, hh, hl);
+      acc[0] = fold_mfma(acc[0], ks, hh, hl);
+    };
+    // this step's three block MFMAs interleaved with the fold half's split VALU (one wave per SIMD:
+    // VALU between MFMAs overlaps them; the compiler otherwise issues the MFMAs first, then ~40
+    // dependent VALU with the matrix pipe idle), then the fold half's three MFMAs
+    auto fold_sched = [&]() {
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);  // VALU
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
+    };
     uint4 ring[3][2];
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
@@ -236,21 +286,11 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
       if (st == 0 && has_next) stage(nib, nxt_lds);
       if (pipe && st == 0) {
         if (ib + 2 < PM_NB) {
-          w1c[0] = W1g[((ib + 2) * 2 + 0) * 64 + lane];
-          w1c[1] = W1g[((ib + 2) * 2 + 1) * 64 + lane];
+          w1c[0] = L.w1[((ib + 2) * 2 + 0) * 64 + lane];
+          w1c[1] = L.w1[((ib + 2) * 2 + 1) * 64 + lane];
         }
       }
       if (pipe && st == 3) l1_split(hn, pm_pow2(ex[1] - ex[0]) * isw1, xh2, xl2);
-      uint4 w3f[4];
-      f32x4 b2f[4];
-      if (fold && s == 1) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          w3f[q] = L.w3[(ob * 4 + q) * 64 + lane];
-          // registers 4q .. 4q + 3 of block ob hold hidden units ob*32 + 8q + 4 (lane >> 5) + 0..3
-          b2f[q] = *reinterpret_cast<const f32x4*>(L.b2 + ob * 32 + 8 * q + 4 * (lane >> 5));
-        }
-      }
       const f16x8 wh = __builtin_bit_cast(f16x8, cur[0]);
       const f16x8 wl = __builtin_bit_cast(f16x8, cur[1]);
       {
@@ -260,36 +300,30 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
         acc_ob = MH_MFMA(wh, xh[s], acc_ob);
         acc[ob] = acc_ob;
       }
-      if (fold && s == 1) {  // H2 block ob final: bias, ReLU, rescale, split, layer 3
-        uint32_t hp[8], lp[8];
-        const f32x2 k2 = {k23, k23}, s2 = {sc3, sc3};
+      // H2 block ob - 1 (final since the previous step) folded into layer 3 during block ob's two
+      // steps, one half per step: its split waits on MFMAs issued a step earlier and overlaps
+      // this step's block-ob MFMAs
+      if (fold && ob > 0) {
+        fold_half(ob - 1, s);
+        fold_sched();
+      }
+      if (fold && s == 1) {  // block ob's layer-3 operands (block ob - 1's last use was just above)
 #pragma unroll
-        for (int p = 0; p < 8; ++p) {
-          const int r = 2 * p;
-          const f32x2 bs = f32x2{b2f[r >> 2][r & 3], b2f[r >> 2][(r & 3) + 1]} * s2;
-          const f32x2 y = __builtin_elementwise_fma(f32x2{acc[ob][r], acc[ob][r + 1]}, k2, bs);
-          split2h_pair(relu_raw(y.x), relu_raw(y.y), one, hp[p], lp[p]);
+        for (int q = 0; q < 4; ++q) {
+          w3f[q] = L.w3[(ob * 4 + q) * 64 + lane];
+          // registers 4q .. 4q + 3 of block ob hold hidden units ob*32 + 8q + 4 (lane >> 5) + 0..3
+          b2f[q] = *reinterpret_cast<const f32x4*>(L.b2 + ob * 32 + 8 * q + 4 * (lane >> 5));
         }
-        const f16x8 hh[2] = {__builtin_bit_cast(f16x8, uint4{hp[0], hp[1], hp[2], hp[3]}),
-                             __builtin_bit_cast(f16x8, uint4{hp[4], hp[5], hp[6], hp[7]})};
-        const f16x8 hl[2] = {__builtin_bit_cast(f16x8, uint4{lp[0], lp[1], lp[2], lp[3]}),
-                             __builtin_bit_cast(f16x8, uint4{lp[4], lp[5], lp[6], lp[7]})};
-        f32x16 o = ob == 0 ? f32x16{} : acc[0];
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const f16x8 vh = __builtin_bit_cast(f16x8, w3f[2 * ks]);
-          const f16x8 vl = __builtin_bit_cast(f16x8, w3f[2 * ks + 1]);
-          o = MH_MFMA(vl, hh[ks], o);
-          o = MH_MFMA(vh, hl[ks], o);
-          o = MH_MFMA(vh, hh[ks], o);
-        }
-        acc[0] = o;
       }
 #ifdef MH_FUSED_EXP_FOLD_NOSB  // experiment: the compiler may interleave the fold phase's steps
       if (!fold) __builtin_amdgcn_sched_barrier(0);
 #else
       __builtin_amdgcn_sched_barrier(0);
 #endif
+    }
+    if (fold) {
+      fold_half(PM_NB - 1, 0);
+      fold_half(PM_NB - 1, 1);
     }
     if (pipe) {
       xh[0] = xh2[0];
@@ -530,6 +564,7 @@ void k_sample_fused(FusedArgs a) {
   __shared__ uint4 lds_w3[PM_NB * 4 * 64];
   __shared__ float lds_b2[PM_H];
   __shared__ float lds_b3[32];
+  __shared__ uint4 lds_w1[PM_NB * 2 * 64];
   __shared__ float s_obs[FUSED_ENVS * D];
   __shared__ float s_lgt[FUSED_ENVS * N3C];
 #ifdef MH_FUSED_DIRECT_RING
@@ -568,6 +603,12 @@ void k_sample_fused(FusedArgs a) {
       const int r = w * FOPW + i;
       glds16(w3g + r * 64 + lane, &lds_w3[r * 64]);
     }
+    const uint4* w1g = reinterpret_cast<const uint4*>(a.P + pm_off_w1x3(a.K1));
+#pragma unroll
+    for (int i = 0; i < PM_NB * 2 / 4; ++i) {
+      const int r = w * (PM_NB * 2 / 4) + i;
+      glds16(w1g + r * 64 + lane, &lds_w1[r * 64]);
+    }
     // compact b2 from the packed [ob][lane][16] copy: lanes 0 and 32 of each block hold all 32 rows
     const float* b2p = a.P + pm_off_b2(a.K1);
     for (int q = threadIdx.x; q < PM_NB * 2 * 16; q += 256) {
@@ -585,21 +626,26 @@ void k_sample_fused(FusedArgs a) {
 
   if (pol) {
     // ================= policy waves: 2H passes (H1 first, then H0 / H1 alternating)
-    PolicyLds L{lds0, lds1, lds_w3, lds_b2, lds_b3, s_obs, s_lgt, &s_bar, a.err};
+    PolicyLds L{lds0, lds1, lds_w3, lds_b2, lds_b3, lds_w1, s_obs, s_lgt, &s_bar, a.err};
     uint32_t target = 0;
     const int total = 2 * H;
     int pass = 0;
-    policy_pass<D>(a, L, w, FUSED_ENVS / 2 + w * 32, ++pass < total, target, pass);
+    ++pass;
+    policy_pass<D>(a, L, w, FUSED_ENVS / 2 + w * 32, pass < total, target, pass - 1);
     __syncthreads();
     for (int t = 0; t < H; ++t) {
-      policy_pass<D>(a, L, w, w * 32, ++pass < total, target, pass);  // A(t): H0
-      MH_STAMP(a, pass, 18);
+      ++pass;
+      policy_pass<D>(a, L, w, w * 32, pass < total, target, pass - 1);  // A(t): H0
+      MH_STAMP(a, pass - 1, 18);
       __syncthreads();
 #ifdef MH_FUSED_EXP_SERIAL
       __syncthreads();
 #endif
-      if (t < H - 1) policy_pass<D>(a, L, w, FUSED_ENVS / 2 + w * 32, ++pass < total, target, pass);  // B(t): H1
-      MH_STAMP(a, pass, 18);
+      if (t < H - 1) {  // B(t): H1
+        ++pass;
+        policy_pass<D>(a, L, w, FUSED_ENVS / 2 + w * 32, pass < total, target, pass - 1);
+        MH_STAMP(a, pass - 1, 18);
+      }
       __syncthreads();
 #ifdef MH_FUSED_EXP_SERIAL
       __syncthreads();
@@ -733,18 +779,29 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_emit_scan(HorizonEmitArgs a) {
   const int64_t NC = (int64_t)a.H * NBK;
   __shared__ int64_t wsum[2][SCAN_THREADS / 64];
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  // the cursor, read up front (thread 0's update at the end then waits on no load)
+  int64_t cur0 = 0, cur1 = 0, cur2 = 0;
+  if (t == 0) {
+    cur0 = a.cursor[0];
+    cur1 = a.cursor[1];
+    cur2 = a.cursor[2];
+  }
   int64_t carry = 0;
   int round = 0;
   for (int64_t c0 = 0; c0 < NC; c0 += (int64_t)SCAN_THREADS * SCAN_CPT, ++round) {
     int cnt[SCAN_CPT];
+    {
+      // (lockstep, block) of this thread's first cell, then stepped: one 32-bit division per
+      // thread and round instead of a 64-bit one per cell (cells < 2^31: the launcher's bound)
+      const int c = (int)(c0 + (int64_t)t * SCAN_CPT);
+      int ts = c / NBK, b = c - ts * NBK;
 #pragma unroll
-    for (int j = 0; j < SCAN_CPT; ++j) {
-      const int64_t c = c0 + (int64_t)t * SCAN_CPT + j;
-      if (c < NC) {
-        const int ts = (int)(c / NBK), b = (int)(c - (int64_t)ts * NBK);
-        cnt[j] = emit_cell_count(a.emit_count + (int64_t)ts * NW, b, NW);
-      } else {
-        cnt[j] = 0;
+      for (int j = 0; j < SCAN_CPT; ++j) {
+        cnt[j] = (int64_t)c + j < NC ? emit_cell_count(a.emit_count + (int64_t)ts * NW, b, NW) : 0;
+        if (++b == NBK) {
+          b = 0;
+          ++ts;
+        }
       }
     }
     int64_t local = 0;
@@ -779,15 +836,15 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_emit_scan(HorizonEmitArgs a) {
   const int64_t all = carry;
   __syncthreads();  // (workgroup-scope fence + barrier: thread 0 reads the scan written above)
   if (t == 0) {
-    const int64_t M = a.capacity, c0 = a.cursor[0];
+    const int64_t M = a.capacity;
     a.scan[NC] = all;
-    a.scan[NC + 1] = c0;
-    a.cursor[0] = (c0 + all) % M;
-    const int64_t sz = a.cursor[1] + all;
+    a.scan[NC + 1] = cur0;
+    a.cursor[0] = (cur0 + all) % M;
+    const int64_t sz = cur1 + all;
     a.cursor[1] = sz < M ? sz : M;
-    a.cursor[2] += all;
+    a.cursor[2] = cur2 + all;
     // windows of the horizon's last lockstep (the lockstep path's cursor[3]): its cells are the
-    // scan's last NBK
+    // scan's last NBK, prefix all - scan[NC - NBK] (read back from this launch's own stores)
     a.cursor[3] = all - a.scan[NC - NBK];
   }
 }
