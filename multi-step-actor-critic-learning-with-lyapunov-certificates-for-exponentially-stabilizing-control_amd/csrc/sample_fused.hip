@@ -91,7 +91,9 @@ __device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
 
 // the four policy waves' barrier: own LDS-DMA landed (vmcnt(0)), arrive, wait for all four. The
 // wait is bounded (~1e9 cycles): a wave that gives up records it in *err (read by the tests
-// through mh_sample_horizon_errors) instead of hanging the device
+// through mh_sample_horizon_errors) instead of hanging the device. (A split hand-off — "landed"
+// and "read" counters, the DMA wait and arrival late in the phase, the buffer-free wait before the
+// next DMA — measured 5 % slower on the fused kernel: 641-643 vs 606-617 us per horizon.)
 __device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_t* err) {
 #ifdef MH_FUSED_EXP_NOSYNC  // cost-attribution experiment only (races: garbage logits)
   target += 4;
@@ -212,7 +214,7 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
     MH_STAMP(a, pass_no, 2 + 2 * ib);
     const bool pipe = !fold;
     f32x16 hn;
-    f16x8 xh2[2], xl2[2];
+    uint32_t l1hp[8], l1lp[8];  // the next block's layer-1 split, pair by pair
     const uint4* Lc = cur_lds + lane;
     uint4 w3f[4];
     f32x4 b2f[4];
@@ -281,8 +283,7 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
       const uint4* cur = ring[st % 3];
       if (pipe && st == 0) hn = l1_mfma(w1c, xoh, xol);
       // the next chunk's DMA into the other buffer (every policy wave finished reading it in the
-      // previous phase: the pol_sync above), issued after this phase's first W1 use so that the
-      // use's own wait never covers it; then the W1 block two phases ahead
+      // previous phase: the pol_sync above), issued after this phase's first W1 use
       if (st == 0 && has_next) stage(nib, nxt_lds);
       if (pipe && st == 0) {
         if (ib + 2 < PM_NB) {
@@ -290,7 +291,14 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
           w1c[1] = L.w1[((ib + 2) * 2 + 1) * 64 + lane];
         }
       }
-      if (pipe && st == 3) l1_split(hn, pm_pow2(ex[1] - ex[0]) * isw1, xh2, xl2);
+      // the next block's layer-1 split, one register pair per step over steps 3..10 (the
+      // split's VALU between this phase's MFMAs instead of ~60 VALU in one step: one wave per SIMD)
+      if (pipe && st >= 3 && st < 11) {
+        const int p = st - 3;
+        const float rs = pm_pow2(ex[1] - ex[0]) * isw1;
+        const f32x2 y = f32x2{hn[2 * p], hn[2 * p + 1]} * f32x2{rs, rs};
+        split2h_pair(relu_raw(y.x), relu_raw(y.y), one, l1hp[p], l1lp[p]);
+      }
       const f16x8 wh = __builtin_bit_cast(f16x8, cur[0]);
       const f16x8 wl = __builtin_bit_cast(f16x8, cur[1]);
       {
@@ -325,11 +333,11 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
       fold_half(PM_NB - 1, 0);
       fold_half(PM_NB - 1, 1);
     }
-    if (pipe) {
-      xh[0] = xh2[0];
-      xh[1] = xh2[1];
-      xl[0] = xl2[0];
-      xl[1] = xl2[1];
+    if (pipe) {  // (l1_split's packing of the pairs)
+      xh[0] = __builtin_bit_cast(f16x8, uint4{l1hp[0], l1hp[1], l1hp[2], l1hp[3]});
+      xh[1] = __builtin_bit_cast(f16x8, uint4{l1hp[4], l1hp[5], l1hp[6], l1hp[7]});
+      xl[0] = __builtin_bit_cast(f16x8, uint4{l1lp[0], l1lp[1], l1lp[2], l1lp[3]});
+      xl[1] = __builtin_bit_cast(f16x8, uint4{l1lp[4], l1lp[5], l1lp[6], l1lp[7]});
     }
   };
   using B0 = std::integral_constant<int, 0>;

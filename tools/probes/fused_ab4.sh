@@ -1,7 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 rm -f gpurun_out/fused_ab4.jsonl
-timeout -k 10 600 python -u -m pytest tests/test_gpu_fused_horizon.py tests/test_gpu_sampler_oracle.py tests/test_gpu_policy_mlp.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_f4.log 2>&1; rc=$?; tail -2 gpurun_out/t_f4.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests/test_gpu_fused_horizon.py tests/test_gpu_sampler_oracle.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_f4.log 2>&1; rc=$?; tail -2 gpurun_out/t_f4.log; [ $rc -eq 0 ] || exit $rc
 for v in build noenv; do
   if [ $v = build ]; then unset MSACL_HIP_LIB; else export MSACL_HIP_LIB=$PWD/exp_libs/fused-$v/libmsacl_hip.so; fi
   timeout -k 10 120 python tools/fused_ab.py 2> gpurun_out/fused_ab_$v.err | grep '^{' | sed "s/^{/{\"v\": \"$v\", /" >> gpurun_out/fused_ab4.jsonl || { echo "fail $v"; tail -5 gpurun_out/fused_ab_$v.err; exit 1; }
