@@ -278,6 +278,10 @@ typedef struct {
 } mh_adam_tensor_t;
 int mh_adam_multi(const mh_adam_tensor_t* tensors, int32_t n, double lr, double beta1, double beta2, double eps,
                   uint32_t* ticket, void* stream);
+/* mh_adam_multi with one learning rate per tensor (lrs[n], host array): several optimisers' steps
+ * in one launch (MSACL's policy and alpha optimisers, msacl.py:405-441). */
+int mh_adam_multi_lr(const mh_adam_tensor_t* tensors, int32_t n, const double* lrs, double beta1, double beta2,
+                     double eps, uint32_t* ticket, void* stream);
 
 /* Polyak averaging of a target network, target = target * polyak + (1 - polyak) * source
  * (both scalars rounded to float32, two roundings as p_t.mul_(polyak); p_t.add_((1 - polyak) * p)
@@ -483,6 +487,17 @@ int mh_msacl_policy_objective(const float* q1, const float* q2, const float* log
                               double n_total, float clip_eps, int32_t B, int32_t n, float* loss_q, float* entropy,
                               float* ratio, float* adv, float* loss_ppo, float* d_ratio, float* loss_policy,
                               void* stream);
+/* The policy step's objective (mh_msacl_policy_objective's outputs) AND its backward for the seed
+ * g_loss = 1 — the one MSACL.model_update uses (msacl.py:405, loss_policy.backward()) — into
+ * dq1, dq2, dlogp, dlp_new, plus the alpha gradient d/dlog_alpha of exp(log_alpha)(entropy -
+ * target_entropy) (msacl.py:429-437) into alpha_grad (nullable), in one launch: the three
+ * entry points' expressions, so their bits. */
+int mh_msacl_policy_objective_step(const float* q1, const float* q2, const float* logp, const float* log_alpha,
+                                   const float* lp_new, const float* old_logp, const float* adv_raw,
+                                   const double* stats, double n_total, float clip_eps, int32_t B, int32_t n,
+                                   float* loss_q, float* entropy, float* ratio, float* adv, float* loss_ppo,
+                                   float* d_ratio, float* loss_policy, float* dq1, float* dq2, float* dlogp,
+                                   float* dlp_new, float target_entropy, float* alpha_grad, void* stream);
 int mh_msacl_policy_objective_backward(const float* q1, const float* q2, const float* log_alpha, const float* ratio,
                                        const float* d_ratio, const float* g_loss, int32_t B, int32_t n, float* dq1,
                                        float* dq2, float* dlogp, float* dlp_new, void* stream);

@@ -113,6 +113,8 @@ _PROTOS = {
     "mh_msacl_ratio0_backward": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_vp, c_vp]),
     "mh_msacl_policy_objective": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_f64, c_f32, c_i32,
                                                  c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mh_msacl_policy_objective_step": (ctypes.c_int, [c_vp] * 8 + [c_f64, c_f32, c_i32, c_i32] + [c_vp] * 11
+                                       + [c_f32, c_vp, c_vp]),
     "mh_msacl_policy_objective_backward": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp,
                                                           c_vp, c_vp, c_vp, c_vp]),
     "mh_msacl_policy_combine": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp]),
@@ -120,6 +122,8 @@ _PROTOS = {
     "mh_polyak_multi": (ctypes.c_int, [c_vp, c_i32, ctypes.c_double, c_vp]),
     "mh_adam_multi": (ctypes.c_int, [c_vp, c_i32, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                      c_vp, c_vp]),
+    "mh_adam_multi_lr": (ctypes.c_int, [c_vp, c_i32, c_vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, c_vp,
+                                        c_vp]),
     "mh_gemm_workspace": (ctypes.c_int, [c_i64, c_i64, c_i64, ctypes.POINTER(c_i64)]),
     "mh_gemm_f32": (ctypes.c_int, [c_vp] * 4 + [c_i64] * 6 + [c_i32] * 3 + [c_vp, c_vp]),
     "mh_gemm_f32_grouped": (ctypes.c_int, [c_vp] * 4 + [c_i64] * 6 + [c_i32] * 4 + [c_i64] * 4 + [c_vp]),

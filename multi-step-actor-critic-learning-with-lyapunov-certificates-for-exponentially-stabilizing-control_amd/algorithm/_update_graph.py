@@ -17,6 +17,7 @@ it out of the create_alg registry, RL/create_pkg/create_alg.py:38-47).
 """
 from __future__ import annotations
 
+import ctypes
 import weakref
 
 import torch
@@ -83,20 +84,19 @@ class HipAdam(Adam):
 
 
 def adam_steps(*opts):
-    """opt.step() for every optimiser in `opts`, as ONE mh_adam_multi launch when they are all
-    HipAdams with a single parameter group and the same lr / betas / eps whose parameters all
-    take the kernel (the twin critics: one launch instead of two back to back on the update's
-    critical path); each parameter keeps its own step counter, so the result is the separate
-    steps'. Otherwise each optimiser steps on its own."""
+    """opt.step() for every optimiser in `opts`, as ONE Adam launch when they are all HipAdams
+    with a single parameter group and the same betas / eps whose parameters all take the kernel
+    (the twin critics; the policy and alpha optimisers): mh_adam_multi when their learning rates
+    agree, mh_adam_multi_lr (one rate per tensor) when not. Each parameter keeps its own step
+    counter, so the result is the separate steps'. Otherwise each optimiser steps on its own."""
     from .. import _native as N
     ok = len(opts) > 1 and all(isinstance(o, HipAdam) and len(o.param_groups) == 1 for o in opts)
-    entries = []
+    entries, lrs = [], []
     if ok:
         g0 = opts[0].param_groups[0]
         for o in opts:
             g = o.param_groups[0]
-            if (torch.is_tensor(g["lr"]) or g["lr"] != g0["lr"] or tuple(g["betas"]) != tuple(g0["betas"])
-                    or g["eps"] != g0["eps"]):
+            if torch.is_tensor(g["lr"]) or tuple(g["betas"]) != tuple(g0["betas"]) or g["eps"] != g0["eps"]:
                 ok = False
                 break
             e = o._hip_entries(g)
@@ -104,6 +104,7 @@ def adam_steps(*opts):
                 ok = False
                 break
             entries += e
+            lrs += [float(g["lr"])] * len(e)
         ok = ok and len(entries) > 0  # (the C ABI chunks lists longer than its per-launch table)
     if not ok:
         for o in opts:
@@ -118,8 +119,13 @@ def adam_steps(*opts):
     for i, (p, g, m, v, stp) in enumerate(entries):
         arr[i] = N.AdamTensor(p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), stp.data_ptr(), p.numel())
     with torch.no_grad():
-        N.check(N.lib().mh_adam_multi(arr, len(entries), float(g0["lr"]), float(b1), float(b2), float(g0["eps"]),
-                                      N.ptr(o0._ticket), N.stream_of(dev)), "mh_adam_multi")
+        if all(lr == lrs[0] for lr in lrs):
+            N.check(N.lib().mh_adam_multi(arr, len(entries), lrs[0], float(b1), float(b2), float(g0["eps"]),
+                                          N.ptr(o0._ticket), N.stream_of(dev)), "mh_adam_multi")
+        else:
+            lr_arr = (ctypes.c_double * len(lrs))(*lrs)
+            N.check(N.lib().mh_adam_multi_lr(arr, len(entries), lr_arr, float(b1), float(b2), float(g0["eps"]),
+                                             N.ptr(o0._ticket), N.stream_of(dev)), "mh_adam_multi_lr")
 
 
 def fused_adam(params, lr):

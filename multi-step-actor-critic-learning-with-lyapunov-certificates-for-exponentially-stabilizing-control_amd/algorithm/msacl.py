@@ -220,6 +220,25 @@ class _PolicyObjective(torch.autograd.Function):
         return dq1, dq2, dlogp, dlp, None, None, None, None, None
 
 
+def _policy_objective_step(q1, q2, logp, lp_new, old_logp, log_alpha, s, n_total, clip, target_entropy=0.0,
+                           alpha_grad=None):
+    """_PolicyObjective forward AND its backward for the unit seed of the policy step
+    (torch.autograd.backward([loss_policy], [1])), plus alpha_grad = (entropy - target_entropy)
+    exp(log_alpha) (mh_msacl_alpha_grad's expression, msacl.py:429-441) when alpha_grad is given,
+    in ONE launch (mh_msacl_policy_objective_step; the same expressions as the objective, its
+    backward with g = 1 and the alpha kernel, so the same bits). Returns the logged loss and
+    entropy and the seeds (dq1, dq2, dlogp, dlp_new) for the upstream graph."""
+    B, n = lp_new.shape
+    out = torch.empty(3, dtype=torch.float32, device=q1.device)  # loss_q, entropy, loss_policy
+    dq = s.dq_obj  # dq1 | dq2 as one buffer: TwinQ's grouped backward reads both
+    _engine("msacl_policy_objective_step", q1.device, N.ptr(q1), N.ptr(q2), N.ptr(logp), N.ptr(log_alpha),
+            N.ptr(lp_new), N.ptr(old_logp), N.ptr(s.adv_raw), N.ptr(s.stats), n_total, clip, B, n,
+            N.ptr(out[0:1]), N.ptr(out[1:2]), N.ptr(s.ratio), N.ptr(s.adv), N.ptr(s.loss_ppo), N.ptr(s.d_ratio),
+            N.ptr(out[2:3]), N.ptr(dq[0]), N.ptr(dq[1]), N.ptr(s.dlogp_obj), N.ptr(s.dlp_obj), float(target_entropy),
+            N.ptr(alpha_grad))
+    return out[2], out[1], (dq[0], dq[1], s.dlogp_obj, s.dlp_obj)
+
+
 class _Ratio0(torch.autograd.Function):
     """exp(logp_new - old_logp)[:, 0] (msacl.py:392-394) and its backward, one launch each."""
 
@@ -258,6 +277,8 @@ class _Scratch:
         self.adv_raw, self.adv, self.loss_ppo, self.d_ratio = f(B), f(B), f(1), f(B)
         self.loss_policy, self.neg_d_ratio, self.ratio = f(1), f(B), f(B)
         self.stats = torch.empty(2, dtype=torch.float64, device=device)
+        # the policy objective's gradients (dq1 | dq2, dlogp, dlp_new), written by its fused step
+        self.dq_obj, self.dlogp_obj, self.dlp_obj = f(2, B, n), f(B, n), f(B, n)
 
 
 class MSACL:
@@ -311,6 +332,7 @@ class MSACL:
         self._head_cache = _UNSET
         self._one = torch.tensor(1.0, device=self.device)
         self._alpha_grad = None
+        self._alpha_grad_ready = False  # _alpha_grad already holds this policy step's gradient
         self.use_graph = bool(kwargs.get("alg_use_graph", True))
         # the Lyapunov update shares no parameter with the critic update (both only read the
         # policy and the batch): on one GPU it runs on a second stream, concurrently
@@ -525,9 +547,10 @@ class MSACL:
         loss_policy = entropy = None
         if not do_policy:
             return loss_q, q1_mean, q2_mean, loss_lya, loss_policy, entropy
-        # data parallel: the policy and alpha gradients share one all-reduce (the alpha loss reads
-        # the policy forward's entropy, not the stepped policy), then both steps
-        merge = self._segmented() and self.auto_alpha
+        # the policy and alpha gradients share one all-reduce under data parallelism (the alpha
+        # loss reads the policy forward's entropy, not the stepped policy), and both optimiser
+        # steps are one Adam launch (disjoint parameters, each with its own learning rate)
+        merge = self.auto_alpha
         for k in range(self.policy_frequency):
             loss_policy, entropy = self._policy_update(data=data, defer_step=merge, reuse_adv=k > 0)
             if self.auto_alpha:
@@ -535,8 +558,8 @@ class MSACL:
             if merge:
                 nets = self.networks
                 D.allreduce_grads(list(nets.policy.parameters()) + [nets.log_alpha])
-                nets.policy_optimizer.step()
-                self._alpha_step()
+                adam_steps(nets.policy_optimizer, nets.alpha_optimizer)
+                self._alpha_clamp()
         # the logged scalars (msacl.py:211-222), stacked inside the update (model_update snapshots them)
         tb = torch.stack([entropy, self.networks.log_alpha.detach().exp(), q1_mean, q2_mean, loss_q, loss_lya,
                           loss_policy])
@@ -795,18 +818,27 @@ class MSACL:
             # the total) in one launch forward and one backward (mh_msacl_policy_objective)
             if side is not None:
                 main.wait_stream(side)  # the side branch wrote only the scratch's adv_raw / stats
-            loss_policy, entropy = _PolicyObjective.apply(
+            # ... and its backward for the unit seed, with the alpha gradient (the alpha loss
+            # reads this step's entropy and the unchanged log_alpha), in the same launch
+            la = self.networks.log_alpha
+            ag = None
+            if self.auto_alpha:
+                if self._alpha_grad is None:
+                    self._alpha_grad = torch.zeros_like(la)
+                ag = self._alpha_grad
+            loss_policy, entropy, seeds = _policy_objective_step(
                 q1.contiguous(), q2.contiguous(), new_act_logp.contiguous(), old_lp.contiguous(),
-                old_logp.contiguous(), self.networks.log_alpha.detach(), s, float(B * D.world_size()),
-                float(self.clip_coef))
+                old_logp.contiguous(), la.detach(), s, float(B * D.world_size()), float(self.clip_coef),
+                float(self.target_entropy) if ag is not None else 0.0, ag)
+            self._alpha_grad_ready = ag is not None
             self.networks.policy_optimizer.zero_grad()
-            torch.autograd.backward([loss_policy], [self._one])
+            torch.autograd.backward([q1, q2, new_act_logp, old_lp], list(seeds))
             if not defer_step:
                 D.allreduce_grads(list(self.networks.policy.parameters()))
                 self.networks.policy_optimizer.step()
             for p in list(self.networks.q1.parameters()) + list(self.networks.q2.parameters()):
                 p.requires_grad = True
-            return loss_policy.detach(), entropy.detach()
+            return loss_policy, entropy
         loss_policy_q, entropy = _PolicyQLoss.apply(q1.contiguous(), q2.contiguous(), new_act_logp.contiguous(),
                                                     self.networks.log_alpha.detach())
         if old_lp is None:
@@ -845,8 +877,10 @@ class MSACL:
             if self._alpha_grad is None:
                 self._alpha_grad = torch.zeros_like(la)
             la.grad = self._alpha_grad
-            _engine("msacl_alpha_grad", self.device, N.ptr(la.detach()), N.ptr(entropy.contiguous()),
-                    float(self.target_entropy), N.ptr(self._alpha_grad))
+            if not self._alpha_grad_ready:  # else written by the policy objective's launch
+                _engine("msacl_alpha_grad", self.device, N.ptr(la.detach()), N.ptr(entropy.contiguous()),
+                        float(self.target_entropy), N.ptr(self._alpha_grad))
+            self._alpha_grad_ready = False
         else:
             alpha = self._get_alpha(requires_grad=True)
             loss_alpha = alpha * (entropy - self.target_entropy)
@@ -858,6 +892,9 @@ class MSACL:
 
     def _alpha_step(self):
         self.networks.alpha_optimizer.step()
+        self._alpha_clamp()
+
+    def _alpha_clamp(self):
         if self.set_alpha_bound:
             with torch.no_grad():
                 self.networks.log_alpha.clamp_(max=math.log(self.alpha_bound))

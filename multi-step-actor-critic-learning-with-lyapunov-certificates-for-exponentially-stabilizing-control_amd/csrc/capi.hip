@@ -799,8 +799,8 @@ int mh_head_backward(const float* dy, const float* x, const float* W, int64_t ro
   return MH_OK;
 }
 
-int mh_adam_multi(const mh_adam_tensor_t* tensors, int32_t n, double lr, double beta1, double beta2, double eps,
-                  uint32_t* ticket, void* stream) {
+static int adam_multi_impl(const mh_adam_tensor_t* tensors, int32_t n, double lr, const double* lrs, double beta1,
+                           double beta2, double eps, uint32_t* ticket, void* stream) {
   if (n < 0 || (n > 0 && (!tensors || !ticket))) return fail(MH_EINVAL, "mh_adam_multi: bad argument");
   for (int32_t base = 0; base < n; base += mh::ADAM_MAX_TENSORS) {
     mh::AdamList L{};
@@ -816,10 +816,22 @@ int mh_adam_multi(const mh_adam_tensor_t* tensors, int32_t n, double lr, double 
       L.v[k] = t.exp_avg_sq;
       L.step[k] = t.step;
       L.start[k + 1] = L.start[k] + t.numel;
+      L.lr[k] = lrs ? lrs[base + k] : lr;
     }
-    MH_HIP(mh::launch_adam_multi(L, lr, beta1, beta2, eps, ticket, (hipStream_t)stream));
+    MH_HIP(mh::launch_adam_multi(L, beta1, beta2, eps, ticket, (hipStream_t)stream));
   }
   return MH_OK;
+}
+
+int mh_adam_multi(const mh_adam_tensor_t* tensors, int32_t n, double lr, double beta1, double beta2, double eps,
+                  uint32_t* ticket, void* stream) {
+  return adam_multi_impl(tensors, n, lr, nullptr, beta1, beta2, eps, ticket, stream);
+}
+
+int mh_adam_multi_lr(const mh_adam_tensor_t* tensors, int32_t n, const double* lrs, double beta1, double beta2,
+                     double eps, uint32_t* ticket, void* stream) {
+  if (n > 0 && !lrs) return fail(MH_EINVAL, "mh_adam_multi_lr: null learning-rate list");
+  return adam_multi_impl(tensors, n, 0.0, lrs, beta1, beta2, eps, ticket, stream);
 }
 
 int mh_polyak_multi(const mh_polyak_tensor_t* tensors, int32_t n, double polyak, void* stream) {

@@ -439,13 +439,22 @@ struct SingleTrackCar {
     double f[7], g5[2] = {0.0, 0.0}, g6[2] = {0.0, 0.0}, g2 = 0.0, g3 = 0.0;
     float pb = pe + beta;
     float spb, cpb;
+#ifdef MH_EXP_CAR_FASTTRIG  // cost-attribution experiment only
+    spb = __sinf(pb);
+    cpb = __cosf(pb);
+#else
     sincos32(pb, &spb, &cpb);
+#endif
     f[0] = (double)(((v * cpb) - 1.0f) + (0.0f * sye));   // SingleTrackCar.py:165
     f[1] = (double)((v * spb) - (0.0f * sxe));            // SingleTrackCar.py:166
     f[3] = -0.0;                                               // -a_ref
     f[2] = 0.0;
     const float lsum = (float)C::lsum;
+#ifdef MH_EXP_CAR_DYNONLY  // cost-attribution experiment only: every lane in the dynamic model
+    if (true) {
+#else
     if (!(fabsf(v) < 0.1f)) {
+#endif
       // dynamic model (SingleTrackCar.py:178-196, 243-256)
       float X = div32((float)C::P1, (v * (float)C::Iz) * lsum);
       float t1 = ((-X) * (float)C::K1) * psid;
@@ -471,15 +480,22 @@ struct SingleTrackCar {
       g6[1] = (double)((hb1 - hb2) - hb3);
     } else {
       // kinematic model (SingleTrackCar.py:199-204, 259-277)
+      // (a lane in this branch makes its whole wave run it: every division here is div32, sin /
+      // cos of each angle share one range reduction, and tan(delta) is their quotient, within
+      // ~2 ulp of tanf like the other f32 transcendental sites)
       const float lwb = (float)C::lwb, lr = (float)C::lr, ilwb = (float)C::ilwb;
-      float td = tan32(delta), cd = cos32(delta), cb = cos32(beta), sb = sin32(beta);
-      f[4] = (double)((((v * cb) / lwb) * td) - 0.0f);
+      float sd, cd, cb, sb;
+      sincos32(delta, &sd, &cd);
+      sincos32(beta, &sb, &cb);
+      const float td = div32(sd, cd);
+      f[4] = (double)((div32(v * cb, lwb) * td) - 0.0f);
       f[5] = 0.0;
       f[6] = 0.0;
-      float tt = (td * lr) / lwb;
-      float bdot = ((1.0f / (1.0f + powf2(tt))) * lr) / (lwb * powf2(cd));
+      float tt = div32(td * lr, lwb);
+      const float cd2 = powf2(cd);
+      float bdot = div32(div32(1.0f, 1.0f + powf2(tt)) * lr, lwb * cd2);
       g5[1] = (double)(ilwb * (cb * td));
-      float inner = ((((-v) * sb) * td) * bdot) + ((v * cb) / powf2(cd));
+      float inner = ((((-v) * sb) * td) * bdot) + div32(v * cb, cd2);
       g5[0] = (double)(ilwb * inner);
       g6[0] = (double)bdot;
     }
@@ -494,7 +510,11 @@ struct SingleTrackCar {
     out[6] = f[6] + (g6[0] * u0 + g6[1] * u1);
   }
   MH_HD static void step(float* s, double*, int, const float* u, const double*, float* obs, float* rew) {
+#ifdef MH_EXP_CAR_K  // cost-attribution experiment only: substeps per env step
+    for (int k = 0; k < MH_EXP_CAR_K; ++k) {
+#else
     for (int k = 0; k < K; ++k) {
+#endif
       double d[7];
       deriv(s, u, d);
 #pragma unroll

@@ -436,6 +436,39 @@ __global__ __launch_bounds__(256) void k_policy_objective_bwd(const float* q1, c
   dlp_new[i] = (i - b * n) == 0 ? (-(*g * d_ratio[b])) * ratio[b] : 0.0f;
 }
 
+// One policy step's objective AND its backward for the seed g = 1 (MSACL.model_update runs
+// autograd.backward(loss_policy, 1)), plus the alpha gradient (msacl.py:429-437) from the same
+// entropy: k_policy_objective, then k_policy_objective_bwd's element expressions with *g = 1 and
+// k_alpha_grad's, in one single-workgroup launch (three launches before; the expressions and
+// their order unchanged, so the same bits). alpha_grad may be null (no automatic alpha).
+__global__ __launch_bounds__(TPB) void k_policy_objective_step(
+    const float* q1, const float* q2, const float* logp, const float* log_alpha, const float* lp_new,
+    const float* old_logp, const float* adv_raw, const double* stats, double n_total, float clip_eps, int B, int n,
+    float* loss_q, float* entropy, float* ratio, float* adv, float* loss_ppo, float* d_ratio, float* loss_policy,
+    float* dq1, float* dq2, float* dlogp, float* dlp_new, float target_entropy, float* alpha_grad) {
+  __shared__ double sh[TPB];
+  policy_loss_body(q1, q2, logp, log_alpha, (int64_t)B * n, loss_q, entropy, sh);
+  for (int b = threadIdx.x; b < B; b += TPB) ratio[b] = expf(lp_new[(int64_t)b * n] - old_logp[(int64_t)b * n]);
+  __syncthreads();
+  ppo_clip_body(ratio, adv_raw, stats, n_total, clip_eps, B, adv, loss_ppo, d_ratio, sh);
+  if (threadIdx.x == 0) loss_policy[0] = (-loss_q[0]) - loss_ppo[0];
+  __syncthreads();  // d_ratio (written by the clip body) and entropy (thread 0) visible to all
+  const int64_t N = (int64_t)B * n;
+  const float alpha = expf(*log_alpha);
+  const float g1 = 1.0f;
+  const float gq = -g1;
+  const float gg = gq * (1.0f / (float)N);
+  for (int64_t i = threadIdx.x; i < N; i += TPB) {
+    const float a = q1[i], bq = q2[i];
+    dq1[i] = a == bq ? gg / 2.0f : (a > bq ? 0.0f : gg);
+    dq2[i] = a == bq ? gg / 2.0f : (a < bq ? 0.0f : gg);
+    dlogp[i] = (-gg) * alpha;
+    const int64_t b = i / n;
+    dlp_new[i] = (i - b * n) == 0 ? (-(g1 * d_ratio[b])) * ratio[b] : 0.0f;
+  }
+  if (alpha_grad && threadIdx.x == 0) alpha_grad[0] = (entropy[0] - target_entropy) * expf(log_alpha[0]);
+}
+
 thread_local std::string g_merr;
 
 }  // namespace
@@ -546,6 +579,23 @@ int mh_msacl_policy_objective(const float* q1, const float* q2, const float* log
                                                          n_total, clip_eps, B, n, loss_q, entropy, ratio, adv,
                                                          loss_ppo, d_ratio, loss_policy);
   MH_CHECK_LAUNCH("policy_objective");
+  return MH_OK;
+}
+
+int mh_msacl_policy_objective_step(const float* q1, const float* q2, const float* logp, const float* log_alpha,
+                                   const float* lp_new, const float* old_logp, const float* adv_raw,
+                                   const double* stats, double n_total, float clip_eps, int32_t B, int32_t n,
+                                   float* loss_q, float* entropy, float* ratio, float* adv, float* loss_ppo,
+                                   float* d_ratio, float* loss_policy, float* dq1, float* dq2, float* dlogp,
+                                   float* dlp_new, float target_entropy, float* alpha_grad, void* stream) {
+  if (!q1 || !q2 || !logp || !log_alpha || !lp_new || !old_logp || !adv_raw || !stats || !loss_q || !entropy ||
+      !ratio || !adv || !loss_ppo || !d_ratio || !loss_policy || !dq1 || !dq2 || !dlogp || !dlp_new || B <= 0 ||
+      n <= 0)
+    return MH_EINVAL;
+  k_policy_objective_step<<<1, TPB, 0, (hipStream_t)stream>>>(
+      q1, q2, logp, log_alpha, lp_new, old_logp, adv_raw, stats, n_total, clip_eps, B, n, loss_q, entropy, ratio, adv,
+      loss_ppo, d_ratio, loss_policy, dq1, dq2, dlogp, dlp_new, target_entropy, alpha_grad);
+  MH_CHECK_LAUNCH("policy_objective_step");
   return MH_OK;
 }
 

@@ -19,7 +19,7 @@
 
 namespace mh {
 
-__global__ __launch_bounds__(256) void k_adam_multi(AdamList L, double lr, double b1, double b2, double eps,
+__global__ __launch_bounds__(256) void k_adam_multi(AdamList L, double b1, double b2, double eps,
                                                     uint32_t* __restrict__ ticket) {
   // the scalars as PyTorch forms them from the Python floats: (1 - beta) and the bias
   // corrections in double, each rounded once to float32 where the element math uses it; one
@@ -28,7 +28,7 @@ __global__ __launch_bounds__(256) void k_adam_multi(AdamList L, double lr, doubl
   if ((int)threadIdx.x < L.n) {
     const float t = *L.step[threadIdx.x] + 1.0f;
     s_t[threadIdx.x] = t;
-    s_step_size[threadIdx.x] = (float)(lr / (1.0 - pow(b1, (double)t)));
+    s_step_size[threadIdx.x] = (float)(L.lr[threadIdx.x] / (1.0 - pow(b1, (double)t)));
     s_bc2[threadIdx.x] = (float)sqrt(1.0 - pow(b2, (double)t));
   }
   __syncthreads();
@@ -64,13 +64,12 @@ __global__ __launch_bounds__(256) void k_adam_multi(AdamList L, double lr, doubl
   }
 }
 
-hipError_t launch_adam_multi(const AdamList& L, double lr, double b1, double b2, double eps, uint32_t* ticket,
-                             hipStream_t st) {
+hipError_t launch_adam_multi(const AdamList& L, double b1, double b2, double eps, uint32_t* ticket, hipStream_t st) {
   if (L.n <= 0) return hipSuccess;
   const int64_t total = L.start[L.n];
   const int64_t want = (total + 255) / 256;
   const int grid = (int)(want < 1 ? 1 : (want < 2048 ? want : 2048));
-  k_adam_multi<<<grid, 256, 0, st>>>(L, lr, b1, b2, eps, ticket);
+  k_adam_multi<<<grid, 256, 0, st>>>(L, b1, b2, eps, ticket);
   return hipGetLastError();
 }
 

@@ -167,6 +167,7 @@ struct AdamList {  // one optimiser's tensors, passed by value in the kernel arg
   float* v[ADAM_MAX_TENSORS];
   float* step[ADAM_MAX_TENSORS];
   int64_t start[ADAM_MAX_TENSORS + 1];  // prefix sums of the element counts
+  double lr[ADAM_MAX_TENSORS];           // each tensor's learning rate (one launch may step several optimisers)
   int n;
 };
 struct PolyakList {
@@ -176,7 +177,7 @@ struct PolyakList {
   int n;
 };
 hipError_t launch_polyak_multi(const PolyakList& L, double polyak, hipStream_t st);
-hipError_t launch_adam_multi(const AdamList& L, double lr, double b1, double b2, double eps, uint32_t* ticket,
+hipError_t launch_adam_multi(const AdamList& L, double b1, double b2, double eps, uint32_t* ticket,
                              hipStream_t st);
 hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
                               const float* b3, int D, int N3, float* P, hipStream_t st);

@@ -61,6 +61,45 @@ __device__ __forceinline__ void load_row_buf(__amdgpu_buffer_rsrc_t r, int off, 
 template <int W>
 __device__ __forceinline__ void store_vec(float* dst, const float* v);
 
+// The wave's 64 rows [e0, e0 + 64) of a row-major [E][D] float tensor, each lane holding its own
+// row: written through an LDS transpose as consecutive chunks (16-byte when D % 4 == 0, else
+// 4-byte, one contiguous 256-byte run per instruction), not as D strided 4-byte stores per lane
+// (for SingleTrackCar's D = 7 each of those touched 28 lines per instruction: 264 -> 229 us per
+// 4 M-env step, DuctedFan 113 -> 101 us). Rows >= E fall
+// outside the resource and are dropped. `so` is the wave's stage (>= 16 D float4); the next
+// writer of the stage is the same wave, after these reads (LDS operations of a wave are in order).
+template <int D>
+__device__ __forceinline__ void wave_store_rows(float* dst, const float* row, int64_t e0, int64_t E, float4* so,
+                                                int lane) {
+  const int64_t nrow = e0 < E ? (E - e0 < 64 ? E - e0 : 64) : 0;
+  const __amdgpu_buffer_rsrc_t ro = soa_rsrc(dst + e0 * D, (uint32_t)(nrow * D * 4));
+  static_assert(D >= 4, "rows of <= 12 bytes are stored directly by their lanes");
+  if constexpr (D % 4 == 0) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int i = 0; i < D / 4; ++i) so[lane * (D / 4) + i] = make_float4(row[4 * i], row[4 * i + 1], row[4 * i + 2], row[4 * i + 3]);
+    __builtin_amdgcn_wave_barrier();
+    float4 v[D / 4];
+#pragma unroll
+    for (int j = 0; j < D / 4; ++j) v[j] = so[j * 64 + lane];
+#pragma unroll
+    for (int j = 0; j < D / 4; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, v[j]), ro, (j * 64 + lane) * 16, 0, 0);
+  } else {
+    float* sf = reinterpret_cast<float*>(so);
+#pragma unroll
+    for (int i = 0; i < D; ++i) sf[lane * D + i] = row[i];
+    __builtin_amdgcn_wave_barrier();
+    float v[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) v[j] = sf[j * 64 + lane];
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v[j]), ro, (j * 64 + lane) * 4, 0, 0);
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
 // Deferred emission (emitter waves w = 0..EMIT_WAVES-1 of a block in mh_rollout_step_deferred):
 // the previous step's full windows of THIS block's envs, in env-index order, into the window
 // store rows after every earlier block's and every earlier deferred step's windows (the same
@@ -159,7 +198,11 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
   bool emit = false;
   int emit_pos = 0;  // ring slot of the window's oldest record (the position after this push)
   float rec[F];      // this step's ring record (stored transposed through LDS, below)
-  float oout[D];     // next observation row (D % 4 == 0: stored transposed through LDS, below)
+  float oout[D];     // next observation row (stored transposed through LDS, below)
+  float nout[D];     // real next observation row (the same)
+  // per-wave LDS stage: the observation rows' transposes, then the ring records'
+  constexpr int RC = F / 4, RCP = RC + 1;  // ring record float4 chunks; padded LDS record stride
+  __shared__ float4 wstage[BLK / 64][64 * RCP > 16 * D ? 64 * RCP : 16 * D];
   int wpos = 0;      // the ring slot it goes to
   // store-cursor snapshot for the emission kernel, loaded up front by one thread (the grid
   // finishes with its slowest wave: three dependent round trips at the end would be exposed)
@@ -345,16 +388,21 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, xs[i]), rs_xstate, vo8, (int)(i * E * 8), 0);
     a.steps[e] = k1;
     a.ctr[e] = ctr + 1u;
-    if constexpr (D % 4 == 0) {  // stored below, transposed through LDS with the wave's rows
+    if constexpr (D >= 4) {
 #pragma unroll
-      for (int i = 0; i < D; ++i) oout[i] = obsn[i];
-    } else if (a.obs) {
+      for (int i = 0; i < D; ++i) {  // stored below, transposed through LDS with the wave's rows
+        oout[i] = obsn[i];
+        nout[i] = obs2[i];
+      }
+    } else {  // rows of <= 12 bytes: stored directly (the transpose measured slower there)
+      if (a.obs) {
 #pragma unroll
-      for (int i = 0; i < D; ++i) a.obs[e * D + i] = obsn[i];
-    }
-    if (a.real_next_obs) {
+        for (int i = 0; i < D; ++i) a.obs[e * D + i] = obsn[i];
+      }
+      if (a.real_next_obs) {
 #pragma unroll
-      for (int i = 0; i < D; ++i) a.real_next_obs[e * D + i] = obs2[i];
+        for (int i = 0; i < D; ++i) a.real_next_obs[e * D + i] = obs2[i];
+      }
     }
     if (a.reward_out) a.reward_out[e] = r;
     if (a.term_out) a.term_out[e] = term ? 1 : 0;
@@ -401,26 +449,14 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
       a.ring_pos[e] = pos;
     }
   }
-  if constexpr (D % 4 == 0) {
-    if (a.obs && env_thread) {
-      // next observations, [E][D] rows: the wave's 64 rows are one contiguous 64 * D * 4-byte
-      // range, written as consecutive 16-byte chunks per lane after an LDS transpose
-      __shared__ float4 ostage[BLK / 64][16 * D];
-      const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-      float4* so = ostage[wave];
-#pragma unroll
-      for (int i = 0; i < D / 4; ++i) so[lane * (D / 4) + i] = make_float4(oout[4 * i], oout[4 * i + 1], oout[4 * i + 2], oout[4 * i + 3]);
-      __builtin_amdgcn_wave_barrier();
+  if constexpr (D >= 4) {
+    if (env_thread && (a.obs || a.real_next_obs)) {
+      // next observations and real next observations, [E][D] rows: the wave's 64 rows are one
+      // contiguous 64 * D * 4-byte range each
+      const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
       const int64_t e0 = (int64_t)blockIdx.x * BLK + wave * 64;
-      const int64_t nrow = e0 < E ? (E - e0 < 64 ? E - e0 : 64) : 0;
-      const __amdgpu_buffer_rsrc_t ro = soa_rsrc(a.obs + e0 * D, (uint32_t)(nrow * D * 4));
-      typedef float f32x4 __attribute__((ext_vector_type(4)));
-      float4 v[D / 4];
-#pragma unroll
-      for (int j = 0; j < D / 4; ++j) v[j] = so[j * 64 + lane];
-#pragma unroll
-      for (int j = 0; j < D / 4; ++j)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, v[j]), ro, (j * 64 + lane) * 16, 0, 0);
+      if (a.real_next_obs) wave_store_rows<D>(a.real_next_obs, nout, e0, E, wstage[wave], lane);
+      if (a.obs) wave_store_rows<D>(a.obs, oout, e0, E, wstage[wave], lane);
     }
   }
   if (a.ring) {
@@ -430,11 +466,10 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
     // record's contiguous chunks, so an instruction touches 64 / (F / 4) records' lines instead
     // of 64 (one record per lane took 3.4 us of the 17.4 us QuadTracking step at E = 65,536:
     // tools/exp_variants.sh, MH_EXP_NO_RING). Staged here, stored after the block barrier.
-    constexpr int C = F / 4, CP = C + 1;  // float4 chunks per record; padded LDS record stride
-    __shared__ float4 stage[BLK / 64][64 * CP];
+    constexpr int C = RC, CP = RCP;
     __shared__ int spos[BLK / 64][64];
     if (env_thread) {
-      float4* sw = stage[wave];
+      float4* sw = wstage[wave];
 #pragma unroll
       for (int i = 0; i < C; ++i) sw[lane * CP + i] = make_float4(rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
       spos[wave][lane] = wpos;
@@ -471,7 +506,7 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
         a.meta[META_SIZE] = cur1;
         a.meta[META_GTOTAL] = cur2;
       }
-      const float4* sw = stage[wave];
+      const float4* sw = wstage[wave];
       const int64_t e0 = (int64_t)blockIdx.x * BLK + wave * 64;
       const int R = a.ring_slots;
       // the wave's slice of the ring as a buffer resource: records of envs >= E fall outside it
@@ -793,6 +828,7 @@ __global__ __launch_bounds__(256) void k_aos_to_soa(const T* src, T* dst, int W,
 }
 
 // --------------------------------------------------------------- launchers
+
 template <class Env>
 hipError_t launch_rollout_t(const StepArgs& a, hipStream_t st) {
   // logits / obs rows are read as float4 / float2 vectors (load_row_f32): the tensors must be

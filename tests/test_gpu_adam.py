@@ -73,6 +73,29 @@ def test_hip_adam_state_dict_round_trip_and_graph_capture():
     assert float(opt.state[a[0]]["step"]) == 5.0  # 1 eager + 1 warm-up + 3 replays (capture runs nothing)
 
 
+def test_adam_steps_mixed_learning_rates_equal_separate_steps():
+    """adam_steps over optimisers with different learning rates (the policy and alpha Adams:
+    mh_adam_multi_lr, one launch) equals each optimiser's own step bit for bit."""
+    from msacl_amd.algorithm._update_graph import adam_steps
+    a1, a2 = _params(3), [torch.nn.Parameter(torch.tensor(1.0, device="cuda"))]
+    b1 = [torch.nn.Parameter(p.detach().clone()) for p in a1]
+    b2 = [torch.nn.Parameter(p.detach().clone()) for p in a2]
+    oa1, oa2, ob1, ob2 = HipAdam(a1, lr=3e-4), HipAdam(a2, lr=1e-2), HipAdam(b1, lr=3e-4), HipAdam(b2, lr=1e-2)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    for _ in range(4):
+        for pa, pb in zip(a1 + a2, b1 + b2):
+            gr = torch.randn(pa.shape, device="cuda", generator=g)
+            pa.grad, pb.grad = gr.clone(), gr.clone()
+        adam_steps(oa1, oa2)
+        ob1.step()
+        ob2.step()
+    for oa, ob, pa_l, pb_l in ((oa1, ob1, a1, b1), (oa2, ob2, a2, b2)):
+        for pa, pb in zip(pa_l, pb_l):
+            assert torch.equal(pa.detach(), pb.detach())
+            for key in ("step", "exp_avg", "exp_avg_sq"):
+                assert torch.equal(oa.state[pa][key], ob.state[pb][key])
+
+
 def test_polyak_kernel_matches_foreach_bit_exact():
     """mh_polyak_multi (algorithm/_update_graph.py polyak_) vs the multi-tensor PyTorch ops it
     replaces, p_t.mul_(1 - tau); p_t.add_(tau * p): the same two float32 roundings, bit-exact."""

@@ -132,3 +132,50 @@ def test_policy_objective_equals_separate_kernels(B, n):
     assert torch.equal(s.adv, adv) and torch.equal(s.d_ratio, dr) and torch.equal(s.loss_ppo, lppo)
     for x, y in zip(a, b):
         assert torch.equal(x.grad, y.grad)
+
+
+@pytest.mark.parametrize("B,n", [(256, 20), (3, 5), (1100, 2)])
+@pytest.mark.parametrize("with_alpha", [True, False])
+def test_policy_objective_step_equals_objective_and_backward(B, n, with_alpha):
+    """mh_msacl_policy_objective_step (objective + its backward for the unit seed + the alpha
+    gradient, one launch) equals _PolicyObjective forward / backward with seed 1 and
+    mh_msacl_alpha_grad bit for bit."""
+    import msacl_amd._native as N
+    from msacl_amd.algorithm.msacl import _PolicyObjective, _Scratch, _policy_objective_step
+    g = torch.Generator(device="cuda").manual_seed(B * 11 + n)
+    q1 = torch.randn(B, n, device="cuda", generator=g)
+    q2 = torch.randn(B, n, device="cuda", generator=g)
+    q2[:, ::4] = q1[:, ::4]
+    lp = torch.randn(B, n, device="cuda", generator=g)
+    lp_new = torch.randn(B, n, device="cuda", generator=g) * 0.1
+    old = lp_new + torch.randn(B, n, device="cuda", generator=g) * 0.1
+    log_alpha = torch.tensor(-0.4, device="cuda")
+    adv_raw = torch.randn(B, device="cuda", generator=g)
+    stats = torch.stack([adv_raw.double().sum(), (adv_raw.double() ** 2).sum()])
+    target = -4.0
+
+    s1 = _Scratch(B, n, q1.device)
+    s1.adv_raw.copy_(adv_raw)
+    s1.stats.copy_(stats)
+    a = [t.clone().requires_grad_(True) for t in (q1, q2, lp, lp_new)]
+    loss, ent = _PolicyObjective.apply(a[0], a[1], a[2], a[3], old, log_alpha, s1, float(B), 0.2)
+    torch.autograd.backward([loss], [torch.tensor(1.0, device="cuda")])
+    ag_ref = torch.full((), 7.0, device="cuda")
+    N.check(N.lib().mh_msacl_alpha_grad(N.ptr(log_alpha), N.ptr(ent.contiguous()), target, N.ptr(ag_ref),
+                                        N.stream_of(q1.device)), "alpha_grad")
+
+    s2 = _Scratch(B, n, q1.device)
+    s2.adv_raw.copy_(adv_raw)
+    s2.stats.copy_(stats)
+    ag = torch.full((), 7.0, device="cuda")
+    loss2, ent2, seeds = _policy_objective_step(q1, q2, lp, lp_new, old, log_alpha, s2, float(B), 0.2, target,
+                                                ag if with_alpha else None)
+    torch.cuda.synchronize()
+    assert torch.equal(loss.detach(), loss2) and torch.equal(ent, ent2)
+    assert torch.equal(s1.adv, s2.adv) and torch.equal(s1.d_ratio, s2.d_ratio) and torch.equal(s1.ratio, s2.ratio)
+    for x, d in zip(a, seeds):
+        assert torch.equal(x.grad, d)
+    if with_alpha:
+        assert torch.equal(ag, ag_ref)
+    else:
+        assert ag.item() == 7.0
