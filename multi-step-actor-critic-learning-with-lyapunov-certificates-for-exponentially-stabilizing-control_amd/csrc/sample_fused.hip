@@ -857,9 +857,37 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_emit_scan(HorizonEmitArgs a) {
   }
 }
 
+// 64 consecutive store rows [D] (one per lane, lane order) written through an LDS transpose as
+// contiguous chunks: 16-byte stores when D % 4 == 0, else 4-byte, one contiguous run per
+// instruction instead of D strided stores per lane. `stage` is the wave's 64 * D floats; its next
+// writer is the same wave after these reads (a wave's LDS operations are in order).
+template <int D>
+__device__ __forceinline__ void emit_rows_lds(float* dst, const float* row, float* stage, int lane) {
+#pragma unroll
+  for (int k = 0; k < D; ++k) stage[lane * D + k] = row[k];
+  __builtin_amdgcn_wave_barrier();
+  if constexpr (D % 4 == 0) {
+    const float4* s4 = reinterpret_cast<const float4*>(stage);
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    float4 v[D / 4];
+#pragma unroll
+    for (int q = 0; q < D / 4; ++q) v[q] = s4[q * 64 + lane];
+#pragma unroll
+    for (int q = 0; q < D / 4; ++q) d4[q * 64 + lane] = v[q];
+  } else {
+    float v[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) v[q] = stage[q * 64 + lane];
+#pragma unroll
+    for (int q = 0; q < D; ++q) dst[q * 64 + lane] = v[q];
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <int D, int A>
 __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
   constexpr int F = rec_floats(D, A);
+  __shared__ float stage[4][64 * D];
   const int NW = (int)((a.E + 63) / 64);
   const int NBK = (NW + 3) / 4;
   const int64_t NC = (int64_t)a.H * NBK;
@@ -875,37 +903,62 @@ __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
   for (int q = 0; q < 4; ++q) pre[q + 1] = pre[q] + (4 * b + q < NW ? cnt[4 * b + q] : 0);
   const int nwin = pre[4];
   const int n = a.n, R = a.R;
-  for (int i = threadIdx.x; i < nwin * n; i += 256) {
-    const int w = i / n, j = i - w * n;
-    const int64_t g = g0 + w;
-    if (g < start) continue;
-    const int q = (w >= pre[1]) + (w >= pre[2]) + (w >= pre[3]);
-    const int gw = 4 * b + q;
-    const int packed = a.emit_list[(int64_t)ts * a.E + (int64_t)gw * 64 + (w - pre[q])];
-    const int64_t e = (int64_t)gw * 64 + (packed & 63);
-    int slot = (packed >> 6) + j;
-    slot = slot >= R ? slot - R : slot;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // wave-strided chunks of 64 records (every lane of a wave takes part in each chunk, so the
+  // chunk's rows can be stored as one block when they are 64 consecutive store rows)
+  for (int i0 = wave * 64; i0 < nwin * n; i0 += 256) {
+    const int i = i0 + lane;
+    bool valid = i < nwin * n;
     float rec[F];
-    const float4* src = reinterpret_cast<const float4*>(a.ring + (e * R + slot) * (int64_t)F);
+    int64_t o = 0;
+    if (valid) {
+      const int w = i / n, j = i - w * n;
+      const int64_t g = g0 + w;
+      valid = g >= start;
+      if (valid) {
+        const int q = (w >= pre[1]) + (w >= pre[2]) + (w >= pre[3]);
+        const int gw = 4 * b + q;
+        const int packed = a.emit_list[(int64_t)ts * a.E + (int64_t)gw * 64 + (w - pre[q])];
+        const int64_t e = (int64_t)gw * 64 + (packed & 63);
+        int slot = (packed >> 6) + j;
+        slot = slot >= R ? slot - R : slot;
+        const float4* src = reinterpret_cast<const float4*>(a.ring + (e * R + slot) * (int64_t)F);
 #pragma unroll
-    for (int k = 0; k < F / 4; ++k) {
-      const float4 v = src[k];
-      rec[4 * k] = v.x;
-      rec[4 * k + 1] = v.y;
-      rec[4 * k + 2] = v.z;
-      rec[4 * k + 3] = v.w;
+        for (int k = 0; k < F / 4; ++k) {
+          const float4 v = src[k];
+          rec[4 * k] = v.x;
+          rec[4 * k + 1] = v.y;
+          rec[4 * k + 2] = v.z;
+          rec[4 * k + 3] = v.w;
+        }
+        o = ((base + g) % M) * n + j;
+      }
     }
-    const int64_t o = ((base + g) % M) * n + j;
+    // consecutive records are consecutive store rows except across the FIFO wrap and at the
+    // chunk tail: the block store when all 64 are, the per-record stores otherwise
+    const int64_t o0 = __shfl(o, 0, 64);
+    const bool block = __ballot(valid && o == o0 + lane) == ~0ull;
+    if (block) {
+      emit_rows_lds<D>(a.obs + o0 * D, rec, stage[wave], lane);
+      emit_rows_lds<D>(a.obs2 + o0 * D, rec + D + A, stage[wave], lane);
+    } else if (valid) {
 #pragma unroll
-    for (int k = 0; k < D; ++k) a.obs[o * D + k] = rec[k];
+      for (int k = 0; k < D; ++k) a.obs[o * D + k] = rec[k];
 #pragma unroll
-    for (int k = 0; k < A; ++k) a.act[o * A + k] = rec[D + k];
+      for (int k = 0; k < D; ++k) a.obs2[o * D + k] = rec[D + A + k];
+    }
+    if (valid) {
+      if constexpr (A == 4) {  // one 16-byte row per lane: consecutive lanes, consecutive rows
+        *reinterpret_cast<float4*>(a.act + o * A) = make_float4(rec[D], rec[D + 1], rec[D + 2], rec[D + 3]);
+      } else {
 #pragma unroll
-    for (int k = 0; k < D; ++k) a.obs2[o * D + k] = rec[D + A + k];
-    a.rew[o] = rec[2 * D + A];
-    a.cost[o] = rec[2 * D + A + 1];
-    a.done[o] = rec[2 * D + A + 2];
-    a.logp[o] = rec[2 * D + A + 3];
+        for (int k = 0; k < A; ++k) a.act[o * A + k] = rec[D + k];
+      }
+      a.rew[o] = rec[2 * D + A];
+      a.cost[o] = rec[2 * D + A + 1];
+      a.done[o] = rec[2 * D + A + 2];
+      a.logp[o] = rec[2 * D + A + 3];
+    }
   }
 }
 
