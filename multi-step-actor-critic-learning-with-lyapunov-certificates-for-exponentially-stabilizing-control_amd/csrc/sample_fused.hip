@@ -768,10 +768,16 @@ void k_sample_fused(FusedArgs a) {
 //                 rows out).
 constexpr int SCAN_THREADS = 1024;
 
+// A cell's window count: its four wave counts, each loaded from a clamped index and then zeroed
+// past NW. The loads are unconditional: a load under a branch makes the compiler wait for it at
+// the join, which serialised the scan's loads into one round trip per cell (15 us per horizon).
 __device__ __forceinline__ int emit_cell_count(const int32_t* cnt_t, int b, int NW) {
+  int v[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = cnt_t[4 * b + q < NW ? 4 * b + q : NW - 1];
   int s = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) s += 4 * b + q < NW ? cnt_t[4 * b + q] : 0;
+  for (int q = 0; q < 4; ++q) s += 4 * b + q < NW ? v[q] : 0;
   return s;
 }
 
@@ -805,7 +811,9 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_emit_scan(HorizonEmitArgs a) {
       int ts = c / NBK, b = c - ts * NBK;
 #pragma unroll
       for (int j = 0; j < SCAN_CPT; ++j) {
-        cnt[j] = (int64_t)c + j < NC ? emit_cell_count(a.emit_count + (int64_t)ts * NW, b, NW) : 0;
+        const bool ok = (int64_t)c + j < NC;  // past the last cell: load cell 0, count 0
+        const int v = emit_cell_count(a.emit_count + (int64_t)(ok ? ts : 0) * NW, ok ? b : 0, NW);
+        cnt[j] = ok ? v : 0;
         if (++b == NBK) {
           b = 0;
           ++ts;
@@ -897,10 +905,12 @@ __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
   const int64_t g0 = a.scan[c];
   const int64_t start = total > M ? total - M : 0;  // older windows are overwritten this horizon
   const int32_t* cnt = a.emit_count + (int64_t)ts * NW;
-  int pre[5];
+  int pre[5], cv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) cv[q] = cnt[4 * b + q < NW ? 4 * b + q : NW - 1];  // unconditional loads
   pre[0] = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) pre[q + 1] = pre[q] + (4 * b + q < NW ? cnt[4 * b + q] : 0);
+  for (int q = 0; q < 4; ++q) pre[q + 1] = pre[q] + (4 * b + q < NW ? cv[q] : 0);
   const int nwin = pre[4];
   const int n = a.n, R = a.R;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
