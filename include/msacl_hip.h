@@ -181,8 +181,34 @@ int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, i
                       float* logp_out, void* stream);
 
 /* Diagnostics of mh_sample_horizon: copies the handle's device error word (the number of bounded
- * intra-workgroup waits that timed out since mh_env_create; 0 when healthy) to DEVICE int64 `out`. */
+ * intra-workgroup waits that timed out since mh_env_create; 0 when healthy) to int64 `out`, DEVICE
+ * or pinned HOST memory (an async copy on `stream`). A timed-out wait means that horizon's logits,
+ * and so its actions and windows, are not trustworthy: the HIP sampler reads the word every
+ * log_save_interval iterations and at close() and raises when it is non-zero. */
 int mh_sample_horizon_errors(mh_env_t h, int64_t* out, void* stream);
+
+/* Polls of one policy-wave wait of mh_sample_horizon before it gives up (and counts an error);
+ * 0 restores the default (2^26, ~1e9 cycles; a healthy hand-off takes < 1e3). Test hook: a tiny
+ * limit forces the timeout path so the caller's error reporting can be exercised. */
+int mh_sample_horizon_set_spin_limit(mh_env_t h, uint32_t limit);
+
+/* The per-env Philox counters [E] (uint32, DEVICE or pinned HOST memory) that key the in-kernel
+ * draws with the handle's seed: every lockstep step of env e draws its action normals and, if the
+ * env finishes, its reset state from (seed, e, counter) and then advances the counter by one; a
+ * drawn reset (mh_env_reset without states) also advances it by one. Part of the env batch's
+ * persistent state (checkpoints) and the key the oracle (oracle/rng.py) replays the draws from.
+ * Replaces the reference's RNG state: torch's / numpy's global generators (base.py:127-137,
+ * RL/env/<Env>.py reset()). */
+int mh_env_get_counters(mh_env_t h, uint32_t* out, void* stream);
+int mh_env_set_counters(mh_env_t h, const uint32_t* in, void* stream);
+
+/* The engine's in-kernel draws for n (env index, counter) keys under `seed` — the same inline
+ * functions the rollout and fused sampler kernels call: kind 0 writes the four standard normals of
+ * the TanhGauss action noise (out [n][4]; components 0..act_dim-1 are used), kind 1 the env's
+ * reset draw (out [n][reset_dim], the state a finishing env restarts from). env_idx [n] int64 and
+ * ctr [n] uint32 are DEVICE arrays. Used to pin the draws to oracle/rng.py. */
+int mh_rng_draw(int32_t env_id, int32_t kind, uint64_t seed, const int64_t* env_idx, const uint32_t* ctr, int64_t n,
+                float* out, void* stream);
 
 /* Diagnostics of mh_sample_horizon: later horizons also write the logits every env sampled from
  * to DEVICE [horizon][E][2*act_dim] `logits_out` and the observation it stepped from to

@@ -85,6 +85,10 @@ _PROTOS = {
     "mh_rollout_set_trace": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mh_nstep_reserve": (ctypes.c_int, [c_vp, c_i32]),
     "mh_sample_horizon_errors": (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    "mh_sample_horizon_set_spin_limit": (ctypes.c_int, [c_vp, ctypes.c_uint32]),
+    "mh_env_get_counters": (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    "mh_env_set_counters": (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    "mh_rng_draw": (ctypes.c_int, [c_i32, c_i32, c_u64, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "mh_sample_horizon_debug_logits": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "mh_sample_horizon": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, ctypes.POINTER(WindowStore), c_vp,
                                          c_vp, c_vp, c_vp]),

@@ -80,6 +80,7 @@ struct mh_env_s {
   int64_t* h_scan = nullptr;        // [hcap * ceil(E / 256) + 2]: the emission's cell scan
   float* dbg_logits = nullptr;      // mh_sample_horizon_debug_logits: [H][E][2A] logits trace
   float* dbg_obs = nullptr;         //   and [H][E][D] pre-step observations
+  uint32_t spin_limit = 0;          // mh_sample_horizon_set_spin_limit (0: the kernel's default)
   // deferred emission (mh_rollout_step_deferred): the last step's windows are not yet emitted
   bool pending = false;
   int parity = 0;                   // half of block_count / emit_list the next step writes
@@ -266,29 +267,45 @@ int mh_nstep_reserve(mh_env_t h, int32_t ring_slots) {
   // the legacy per-env emission stages a whole ring in LDS: only grids the fused emission covers
   if (ring_slots != h->n && h->grid() > mh::EMIT_FUSED_MAX_NB)
     return fail(MH_EINVAL, "mh_nstep_reserve: more ring slots than n_step need num_envs <= 1M");
-  if (ring_slots == h->R) return MH_OK;
+  // the fused horizon's window lists cover horizons up to ring_slots - n + 1 locksteps; they are
+  // sized even when the ring keeps its size (ring_slots == n: horizons of one lockstep)
+  const int hcap = ring_slots - h->n + 1;
+  const bool new_ring = ring_slots != h->R;
+  if (!new_ring && h->hcap == hcap && h->h_count) return MH_OK;
   if (int rc = flush_pending(h, nullptr)) return rc;
   MH_HIP(hipDeviceSynchronize());
   const int64_t E = h->E;
   const int F = h->info.record_floats;
+  // every buffer is allocated before anything is swapped: on failure the handle is unchanged
   float* ring = nullptr;
-  MH_HIP(hipMalloc(&ring, sizeof(float) * E * ring_slots * F));
-  (void)hipFree(h->ring);
-  h->ring = ring;
-  h->R = ring_slots;
-  // the fused horizon's window lists, for horizons up to ring_slots - n + 1 locksteps
+  int32_t *cnt = nullptr, *lst = nullptr;
+  int64_t* scan = nullptr;
+  hipError_t e = hipSuccess;
+  if (new_ring) e = hipMalloc(&ring, sizeof(float) * E * ring_slots * F);
+  if (e == hipSuccess) e = hipMalloc(&cnt, sizeof(int32_t) * hcap * ((E + 63) / 64));
+  if (e == hipSuccess) e = hipMalloc(&lst, sizeof(int32_t) * hcap * E);
+  if (e == hipSuccess) e = hipMalloc(&scan, sizeof(int64_t) * (mh::fused_emit_cells(E, hcap) + 2));
+  if (e == hipSuccess && new_ring) e = hipMemset(ring, 0, sizeof(float) * E * ring_slots * F);
+  if (e != hipSuccess) {
+    for (void* p : {(void*)ring, (void*)cnt, (void*)lst, (void*)scan})
+      if (p) (void)hipFree(p);
+    (void)hipGetLastError();
+    return fail(e == hipErrorOutOfMemory ? MH_ENOMEM : MH_EHIP, std::string("mh_nstep_reserve: ") + hipGetErrorString(e));
+  }
   (void)hipFree(h->h_count);
   (void)hipFree(h->h_list);
   (void)hipFree(h->h_scan);
-  h->h_count = h->h_list = nullptr;
-  h->h_scan = nullptr;
-  h->hcap = ring_slots - h->n + 1;
-  MH_HIP(hipMalloc(&h->h_count, sizeof(int32_t) * h->hcap * ((E + 63) / 64)));
-  MH_HIP(hipMalloc(&h->h_list, sizeof(int32_t) * h->hcap * E));
-  MH_HIP(hipMalloc(&h->h_scan, sizeof(int64_t) * (mh::fused_emit_cells(E, h->hcap) + 2)));
-  MH_HIP(hipMemset(h->ring, 0, sizeof(float) * E * ring_slots * F));
-  MH_HIP(hipMemset(h->ring_len, 0, sizeof(int32_t) * E));
-  MH_HIP(hipMemset(h->ring_pos, 0, sizeof(int32_t) * E));
+  h->h_count = cnt;
+  h->h_list = lst;
+  h->h_scan = scan;
+  h->hcap = hcap;
+  if (new_ring) {  // every deque restarts empty over the new ring
+    (void)hipFree(h->ring);
+    h->ring = ring;
+    h->R = ring_slots;
+    MH_HIP(hipMemset(h->ring_len, 0, sizeof(int32_t) * E));
+    MH_HIP(hipMemset(h->ring_pos, 0, sizeof(int32_t) * E));
+  }
   return MH_OK;
 }
 
@@ -337,6 +354,7 @@ int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, i
   a.act_out = act_out;
   a.logp_out = logp_out;
   a.err = h->meta + 7;  // meta[7]: the fused kernel's error word
+  a.spin_limit = h->spin_limit ? h->spin_limit : mh::FUSED_SPIN_LIMIT;
   a.lgt_out = h->dbg_logits;
   a.obs_out = h->dbg_obs;
   mh::HorizonEmitArgs ea;
@@ -374,7 +392,38 @@ int mh_sample_horizon_debug_logits(mh_env_t h, float* logits_out, float* obs_out
 
 int mh_sample_horizon_errors(mh_env_t h, int64_t* out, void* stream) {
   if (!h || !out) return fail(MH_EINVAL, "mh_sample_horizon_errors: null argument");
-  MH_HIP(hipMemcpyAsync(out, h->meta + 7, sizeof(int64_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  // hipMemcpyDefault: `out` may be device memory or pinned host memory (the sampler's capturable
+  // per-horizon copy of the word, read without a device sync)
+  MH_HIP(hipMemcpyAsync(out, h->meta + 7, sizeof(int64_t), hipMemcpyDefault, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_sample_horizon_set_spin_limit(mh_env_t h, uint32_t limit) {
+  if (!h) return fail(MH_EINVAL, "mh_sample_horizon_set_spin_limit: null handle");
+  h->spin_limit = limit;
+  return MH_OK;
+}
+
+int mh_env_get_counters(mh_env_t h, uint32_t* out, void* stream) {
+  if (!h || !out) return fail(MH_EINVAL, "mh_env_get_counters: null argument");
+  MH_HIP(hipMemcpyAsync(out, h->ctr, sizeof(uint32_t) * h->E, hipMemcpyDefault, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_env_set_counters(mh_env_t h, const uint32_t* in, void* stream) {
+  if (!h || !in) return fail(MH_EINVAL, "mh_env_set_counters: null argument");
+  if (int rc = flush_pending(h, stream)) return rc;
+  MH_HIP(hipMemcpyAsync(h->ctr, in, sizeof(uint32_t) * h->E, hipMemcpyDefault, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_rng_draw(int32_t env_id, int32_t kind, uint64_t seed, const int64_t* env_idx, const uint32_t* ctr, int64_t n,
+                float* out, void* stream) {
+  if (kind != 0 && kind != 1) return fail(MH_EINVAL, "mh_rng_draw: kind must be 0 (action normals) or 1 (reset draw)");
+  if (n < 0 || (n > 0 && (!env_idx || !ctr || !out))) return fail(MH_EINVAL, "mh_rng_draw: bad arguments");
+  mh_env_info_t info;
+  if (int rc = mh_env_info(env_id, &info)) return rc;
+  MH_HIP(mh::launch_rng_draw(env_id, kind, seed, env_idx, ctr, n, out, (hipStream_t)stream));
   return MH_OK;
 }
 

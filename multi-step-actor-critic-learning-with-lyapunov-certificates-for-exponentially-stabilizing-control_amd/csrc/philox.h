@@ -82,6 +82,17 @@ struct Rng {
   }
 };
 
+// The argument of TanhGaussDistribution's log-Jacobian term, 1 + EPS - tanh(z)^2
+// (act_distribution_cls.py:50-54), from t = exp(-2|z|) and rt = 1 / (1 + t). PyTorch evaluates
+// `1 + EPS - tensor` with the Python scalar rounded to float32 (1.00000095367431640625), so the
+// constant here is that value minus 1, exactly. 1 - tanh^2 = 4 t / (1 + t)^2 has no cancellation,
+// whereas float32 1.000001 - th * th keeps only a few digits once |z| > 2 (the log term's error
+// reached 1e-4 at |z| = 4): this form is within a few float32 ulp of the exact value everywhere
+// (oracle/rng.py tanh_gauss_sample, tests/test_gpu_sampler_oracle.py).
+__host__ __device__ __forceinline__ float squash_arg(float t, float rt) {
+  return 9.5367431640625e-07f + (4.0f * t) * (rt * rt);
+}
+
 __host__ __device__ __forceinline__ Rng make_rng(uint64_t seed, uint64_t env, uint64_t tick) {
   return Rng{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)env, (uint32_t)(env >> 32),
              (uint32_t)tick, (uint32_t)(tick >> 32)};

@@ -108,6 +108,8 @@ hipError_t launch_rollout(int env_id, const StepArgs& a, hipStream_t st);
 hipError_t launch_gae(const float* val, const float* val2, const float* rew, const uint8_t* done, int64_t E,
                       int H, double gamma, double lam, float* adv, float* ret, hipStream_t st);
 hipError_t launch_reset(int env_id, const StepArgs& a, hipStream_t st);
+hipError_t launch_rng_draw(int env_id, int kind, uint64_t seed, const int64_t* env_idx, const uint32_t* ctr,
+                           int64_t n, float* out, hipStream_t st);
 int64_t policy_packed_floats(int D);
 int act_grad_chunks(int64_t M);
 hipError_t launch_gemm(const float* A, const float* B, const float* bias, float* C, int64_t M, int64_t N, int64_t K,

@@ -292,7 +292,8 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
       rng.normal4f_fast(0, nz);
       // TanhGaussDistribution.sample (act_distribution_cls.py:45-57): z = mu + std * eps,
       // logp = Normal(mu, std).log_prob(z) - sum log(1 + 1e-6 - tanh(z)^2) - sum log((h-l)/2),
-      // on the hardware transcendentals (v_exp/v_log/v_rcp_f32, ~1 ulp).
+      // on the hardware transcendentals (v_exp/v_log/v_rcp_f32, ~1 ulp); the middle term through
+      // squash_arg (philox.h: no float32 cancellation near |tanh z| = 1).
       float lg = -0.0f, lt = -0.0f;
 #pragma unroll
       for (int i = 0; i < A; ++i) {
@@ -312,8 +313,9 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
         lg = lg + ((-(df * df) * __builtin_amdgcn_rcpf(2.0f * (sd * sd)) - log_sd) - 0.918938533204672742f);
         // tanh(z) = sign(z) (1 - t) / (1 + t), t = exp(-2|z|)
         const float t = __builtin_amdgcn_exp2f(-2.88539008177792682f * fabsf(z));
-        const float th = copysignf((1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t), z);
-        lt = lt + __builtin_amdgcn_logf(1.000001f - th * th) * 0.693147180559945309f;
+        const float rt = __builtin_amdgcn_rcpf(1.0f + t);
+        const float th = copysignf((1.0f - t) * rt, z);
+        lt = lt + __builtin_amdgcn_logf(squash_arg(t, rt)) * 0.693147180559945309f;
         const float lo = Env::act_lo(i), hi = Env::act_hi(i);
         const float half = (hi - lo) / 2.0f, mid = (hi + lo) / 2.0f;
         float act = half * th + mid;
@@ -567,6 +569,50 @@ template <class Env>
 __global__ __launch_bounds__(BLK) void k_reset(StepArgs a) {
   const int64_t e = (int64_t)blockIdx.x * BLK + threadIdx.x;
   if (e < a.E) reset_one<Env>(a, e);
+}
+
+// --------------------------------------------------------------- the kernels' Philox draws
+// (mh_rng_draw): for unit i the key (seed, env_idx[i], ctr[i]) the rollout / fused kernels use for
+// that env at that counter, and the SAME inline draws they make with it: kind 0 the four action
+// normals (normal4f_fast, stream 0), kind 1 the env's reset draw (ResetDraw<Env>, streams 1..4).
+template <class Env>
+__global__ __launch_bounds__(BLK) void k_rng_draw(int kind, uint64_t seed, const int64_t* env_idx,
+                                                  const uint32_t* ctr, int64_t n, float* out) {
+  const int64_t i = (int64_t)blockIdx.x * BLK + threadIdx.x;
+  if (i >= n) return;
+  const Rng r = make_rng(seed, (uint64_t)env_idx[i], ctr[i]);
+  if (kind == 0) {
+    float nz[4];
+    r.normal4f_fast(0, nz);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[i * 4 + j] = nz[j];
+  } else {
+    float rs[Env::RS];
+    ResetDraw<Env>::draw(r, rs);
+#pragma unroll
+    for (int j = 0; j < Env::RS; ++j) out[i * Env::RS + j] = rs[j];
+  }
+}
+
+template <class Env>
+static hipError_t launch_rng_draw_t(int kind, uint64_t seed, const int64_t* env_idx, const uint32_t* ctr, int64_t n,
+                                    float* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  k_rng_draw<Env><<<(unsigned)((n + BLK - 1) / BLK), BLK, 0, st>>>(kind, seed, env_idx, ctr, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_rng_draw(int env_id, int kind, uint64_t seed, const int64_t* env_idx, const uint32_t* ctr,
+                           int64_t n, float* out, hipStream_t st) {
+  switch (env_id) {
+    case ENV_VANDERPOL: return launch_rng_draw_t<VanderPol>(kind, seed, env_idx, ctr, n, out, st);
+    case ENV_PENDULUM: return launch_rng_draw_t<Pendulum>(kind, seed, env_idx, ctr, n, out, st);
+    case ENV_DUCTEDFAN: return launch_rng_draw_t<DuctedFan>(kind, seed, env_idx, ctr, n, out, st);
+    case ENV_TWOLINK: return launch_rng_draw_t<TwoLink>(kind, seed, env_idx, ctr, n, out, st);
+    case ENV_SINGLETRACKCAR: return launch_rng_draw_t<SingleTrackCar>(kind, seed, env_idx, ctr, n, out, st);
+    case ENV_QUADTRACKING: return launch_rng_draw_t<QuadTracking>(kind, seed, env_idx, ctr, n, out, st);
+  }
+  return hipErrorInvalidValue;
 }
 
 // --------------------------------------------------------------- finalize (scan + cursor)

@@ -31,7 +31,11 @@ struct FusedArgs {
   int64_t* err;            // device error word: policy-wave waits that timed out (0 when healthy)
   float* lgt_out;          // [H][E][2A] the logits each env sampled from, or null (diagnostics)
   float* obs_out;          // [H][E][D] the observation each env stepped from, or null (diagnostics)
+  uint32_t spin_limit;     // polls of a policy-wave wait before it gives up and counts an error
 };
+
+// default bound of a policy-wave wait (~1e9 cycles; a healthy hand-off takes < 1e3)
+constexpr uint32_t FUSED_SPIN_LIMIT = 1u << 26;
 
 constexpr int FUSED_ENVS = 256;   // envs per workgroup (one workgroup per CU)
 constexpr int FUSED_THREADS = 512;

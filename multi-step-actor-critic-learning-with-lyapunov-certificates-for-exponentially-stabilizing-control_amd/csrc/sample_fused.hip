@@ -94,7 +94,7 @@ __device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
 // through mh_sample_horizon_errors) instead of hanging the device. (A split hand-off — "landed"
 // and "read" counters, the DMA wait and arrival late in the phase, the buffer-free wait before the
 // next DMA — measured 5 % slower on the fused kernel: 641-643 vs 606-617 us per horizon.)
-__device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_t* err) {
+__device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_t* err, uint32_t limit) {
 #ifdef MH_FUSED_EXP_NOSYNC  // cost-attribution experiment only (races: garbage logits)
   target += 4;
   return;
@@ -104,7 +104,7 @@ __device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   uint32_t spins = 0;
   while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
-    if (++spins == (1u << 26)) {  // (LDS polls without a sleep: the hand-off is within one CU)
+    if (++spins >= limit) {  // (LDS polls without a sleep: the hand-off is within one CU)
       if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(err, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
@@ -210,7 +210,7 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
     const bool has_next = ib < PM_NB - 1 || next;
     const int nib = (ib + 1) & (PM_NB - 1);
     MH_STAMP(a, pass_no, 1 + 2 * ib);
-    pol_sync(L.bar, target, L.err);  // chunk ib landed in every policy wave's share
+    pol_sync(L.bar, target, L.err, a.spin_limit);  // chunk ib landed in every policy wave's share
     MH_STAMP(a, pass_no, 2 + 2 * ib);
     const bool pipe = !fold;
     f32x16 hn;
@@ -452,8 +452,9 @@ __device__ __forceinline__ void env_lockstep(const FusedArgs& a, EnvLane<Env>& v
         const float df = z - mu;
         lg = lg + ((-(df * df) * __builtin_amdgcn_rcpf(2.0f * (sd * sd)) - log_sd) - 0.918938533204672742f);
         const float tt = __builtin_amdgcn_exp2f(-2.88539008177792682f * fabsf(z));
-        const float th = copysignf((1.0f - tt) * __builtin_amdgcn_rcpf(1.0f + tt), z);
-        lt = lt + __builtin_amdgcn_logf(1.000001f - th * th) * 0.693147180559945309f;
+        const float rt = __builtin_amdgcn_rcpf(1.0f + tt);
+        const float th = copysignf((1.0f - tt) * rt, z);
+        lt = lt + __builtin_amdgcn_logf(squash_arg(tt, rt)) * 0.693147180559945309f;
         const float lo = Env::act_lo(i), hi = Env::act_hi(i);
         const float half = (hi - lo) / 2.0f, mid = (hi + lo) / 2.0f;
         float act = half * th + mid;

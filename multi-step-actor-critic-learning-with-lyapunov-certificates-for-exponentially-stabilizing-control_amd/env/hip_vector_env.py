@@ -7,6 +7,8 @@ Spaces are host-side and need no GPU (init_args only reads dims and limits).
 """
 from __future__ import annotations
 
+import atexit
+
 import numpy as np
 import torch
 
@@ -134,6 +136,18 @@ class HipVectorEnv:
                                          N.stream_of(dev)), "mh_env_get_state")
         return st, (xs if self.xstate_dim else None), steps
 
+    def get_counters(self):
+        """The per-env Philox counters [E] (int64 copy of the uint32 words, mh_env_get_counters):
+        with `seed` they key every in-kernel draw (oracle/rng.py replays them)."""
+        c = torch.empty(self.num_envs, dtype=torch.int32, device=self.device)
+        N.check(N.lib().mh_env_get_counters(self.handle(), N.ptr(c), N.stream_of(self.device)), "mh_env_get_counters")
+        return c.to(torch.int64) & 0xFFFFFFFF
+
+    def set_counters(self, counters):
+        c = torch.as_tensor(counters, device=self.device).to(torch.int64).to(torch.int32).contiguous()
+        N.require_device(c, "counters", torch.int32, self.num_envs, self.device)
+        N.check(N.lib().mh_env_set_counters(self.handle(), N.ptr(c), N.stream_of(self.device)), "mh_env_set_counters")
+
     def set_state(self, state, xstate=None, steps=None):
         h = self.handle()
         dev = self.device
@@ -156,12 +170,22 @@ _PENDING = []
 
 
 def _destroy_when_safe(h):
-    capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
     _PENDING.append(h)
-    if capturing:
+    drain_pending_handles()
+
+
+def drain_pending_handles():
+    """Destroy the handles whose release was deferred by a capture, unless one is in progress now
+    (called by every release, after the samplers' graph captures and at interpreter exit)."""
+    if not _PENDING:
+        return
+    if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
         return
     while _PENDING:
         N.lib().mh_env_destroy(_PENDING.pop())
+
+
+atexit.register(drain_pending_handles)
 
 
 def make_env(env_id, seed, idx, capture_video=False, run_name=""):

@@ -130,6 +130,10 @@ class NstepOffSerialTrainer:
         else:
             self.alg.model_update(replay_samples, self.iteration)
         self.networks.eval()
+        if self.iteration % self.log_save_interval == 0:
+            check = getattr(self.sampler, "check_errors", None)  # device sampler health (every rank)
+            if check is not None:
+                check()
         if self.iteration % self.log_save_interval == 0 and self.is_main:
             print("Iter = ", self.iteration, "save average sampling time!")
             add_scalars(self.sampler_tb_dict.pop(), self.writer, step=self.iteration)

@@ -25,7 +25,7 @@ import torch.nn as nn
 from ... import _native as N
 from ...utils import dist as D
 from ...create_pkg.create_alg import create_approx_contrainer
-from ...env.hip_vector_env import HipVectorEnv
+from ...env.hip_vector_env import HipVectorEnv, drain_pending_handles
 from ...utils.act_distribution_cls import TanhGaussDistribution
 from ...utils.tensorboard_setup import tb_tags
 from ..buffer.device_nstep_replay_buffer import DeviceNstepReplayBuffer, DeviceWindowBatch
@@ -72,6 +72,11 @@ class HipNstepOffSampler:
             rc = N.lib().mh_nstep_reserve(self._h, self.n_step + self.horizon - 1)
             if rc != 0:
                 self.fused_horizon = False
+        if self.fused_horizon:
+            # bound of the fused kernel's policy-wave waits; a wait that gives up is counted in the
+            # handle's cumulative error word, which check_errors() reads (no hot-path cost)
+            limit = int(kwargs.get("sampler_spin_limit", 0) or 0)  # test hook: forces the timeout path
+            N.check(N.lib().mh_sample_horizon_set_spin_limit(self._h, limit), "mh_sample_horizon_set_spin_limit")
         # GaussNoise (explore_noise.py:3-9; base.py:83-88,136-137): ONE scalar
         # np.random.normal(mean, std) per lockstep step, added to every action before the clip.
         # Drawn on the device into a 1-float tensor (capturable), read by the rollout kernel.
@@ -253,9 +258,11 @@ class HipNstepOffSampler:
             with D.cuda_graph(g):
                 self._horizon(store)
             self._graph, self._graph_key = g, key
+            drain_pending_handles()  # env handles released by a finaliser during the capture
         return self._graph
 
     def _sample(self):
+        self._handle()
         store = self._target()
         before = store.cursor[2].clone()
         with torch.no_grad():
@@ -280,20 +287,50 @@ class HipNstepOffSampler:
         tb = {tb_tags["sampler_time"]: (time.perf_counter() - t0) * 1000}
         return data, tb
 
+    def check_errors(self):
+        """Raise if a fused horizon's bounded policy-wave wait ever timed out (mh_sample_horizon_errors:
+        the logits, and so the actions and windows, of that horizon are not trustworthy). The word
+        is cumulative since the handle was created, so one read covers every horizon so far; it
+        waits for the device only when called (the trainer calls it every log_save_interval
+        iterations and at close())."""
+        if self._h is None or not self.fused_horizon:
+            return
+        out = torch.zeros(1, dtype=torch.int64, device=self.device)
+        N.check(N.lib().mh_sample_horizon_errors(self._h, N.ptr(out), N.stream_of(self.device)), "mh_sample_horizon_errors")
+        n = int(out.item())
+        if n:
+            raise RuntimeError(f"fused horizon sampler: {n} policy-wave wait(s) timed out (mh_sample_horizon_errors); "
+                               "the sampled actions and replay windows since then are corrupt")
+
     def close(self):
         """Release the sampler's device resources now: its captured horizon graph, the packed
-        policy, the staging store and the env handle (mh_env_destroy). Idempotent."""
+        policy, the staging store and the env handle (mh_env_destroy). Idempotent; every later
+        call into the sampler raises. Raises afterwards if a fused horizon reported a timed-out
+        wait (check_errors)."""
+        err = None
+        try:
+            self.check_errors()
+        except RuntimeError as ex:
+            err = ex
         g, self._graph, self._graph_key = self._graph, None, None
         if g is not None:
             g.reset()
         self._packed = self._staging = self._bound = None
         self.envs.close()
+        self._h = None
         self._noise = None
+        if err is not None:
+            raise err
+
+    def _handle(self):
+        if self._h is None:
+            raise RuntimeError("HipNstepOffSampler is closed")
+        return self._h
 
     def set_kernel_timing(self, enable: bool):
         """Per-kernel HIP-event timing (runs the horizon eagerly while enabled)."""
         self._timing = bool(enable)
-        N.check(N.lib().mh_env_set_timing(self._h, int(enable)), "mh_env_set_timing")
+        N.check(N.lib().mh_env_set_timing(self._handle(), int(enable)), "mh_env_set_timing")
 
     # ------------------------------------------------------------------ parity mode
     def step_traced(self, act_out, logp_out, trace=None):
@@ -304,6 +341,7 @@ class HipNstepOffSampler:
         (real_next_obs [E, D], reward [E], terminated u8 [E], truncated u8 [E]) device tensors is
         given, the env step's outputs (mh_rollout_set_trace). Returns the policy logits.
         Call flush() after the last step to emit its windows."""
+        self._handle()
         N.require_device(act_out, "act_out", torch.float32, self.num_envs * self.envs.act_dim, self.device)
         N.require_device(logp_out, "logp_out", torch.float32, self.num_envs, self.device)
         ptrs = [None] * 4
@@ -326,10 +364,12 @@ class HipNstepOffSampler:
 
     def flush(self):
         """Emit the windows of the last deferred lockstep step (mh_rollout_flush)."""
+        self._handle()
         self._flush()
 
     def step_injected(self, actions, logp, reset_states=None, store=None):
         """One lockstep step with injected (already clipped) actions and log-probs."""
+        self._handle()
         act = torch.as_tensor(actions, dtype=torch.float32, device=self.device).contiguous()
         lp = torch.as_tensor(logp, dtype=torch.float32, device=self.device).contiguous()
         N.require_device(act, "actions", torch.float32, self.num_envs * self.envs.act_dim, self.device)

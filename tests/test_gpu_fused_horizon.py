@@ -15,6 +15,7 @@ import torch
 
 import msacl_amd  # noqa: F401
 import msacl_amd._native as N
+from msacl_amd.utils.config import build_pipeline
 from msacl_amd.create_pkg.create_buffer import create_buffer
 from msacl_amd.create_pkg.create_envs import create_envs
 from msacl_amd.create_pkg.create_sampler import create_sampler
@@ -26,12 +27,12 @@ from oracle import envs as OE
 pytestmark = pytest.mark.gpu
 
 
-def _pair(name, E, n, tmp, noise=None, hover=False):
+def _pair(name, E, n, tmp, noise=None, hover=False, horizon=20):
     out = []
     for fused in (True, False):
         args = default_msacl_args(env_name=name, env_num=E, n_step=n, seed=0, env_seed=5, buffer_max_size=600_000,
                                   buffer_warm_size=0, save_folder=str(tmp / str(fused)), noise_params=noise,
-                                  sampler_fused_horizon=fused)
+                                  sampler_fused_horizon=fused, sample_batch_size=horizon)
         args = init_args(create_envs(**args), **args)
         s, b = create_sampler(**args), create_buffer(**args)
         s.bind_store(b)
@@ -116,3 +117,52 @@ def test_fused_horizon_needs_reserved_rings():
         assert N.lib().mh_nstep_reserve(h, 3) == -1  # fewer slots than n_step
     finally:
         N.lib().mh_env_destroy(h)
+
+
+def test_fused_horizon_of_one_lockstep(tmp_path):
+    """sample_batch_size = 1 (a horizon of one lockstep, which the reference accepts): the rings keep
+    n slots (mh_nstep_reserve(n + 0)) but the horizon's window lists are still sized, so the fused
+    path runs and equals the lockstep kernels."""
+    a, ba, b, bb = _pair("DuctedFan", 65536, 5, tmp_path, horizon=1)
+    total = 0
+    for it in range(8):
+        a.sample()
+        b.sample()
+        total = _assert_same(a, ba, b, bb, f"sample {it}")
+    assert total > 0
+
+
+def test_fused_horizon_timeouts_are_loud(tmp_path):
+    """A policy-wave wait that gives up (forced here by a spin limit of 1 poll) leaves garbage
+    logits: the sampler must not carry on silently. check_errors() raises, close() raises after
+    releasing its resources, every later call raises, and the trainer raises at its log interval."""
+    args = default_msacl_args(env_name="VanderPol", env_num=65536, n_step=4, seed=0, env_seed=5,
+                              buffer_max_size=600_000, buffer_warm_size=0, save_folder=str(tmp_path / "s"),
+                              sampler_spin_limit=1)
+    args = init_args(create_envs(**args), **args)
+    s, b = create_sampler(**args), create_buffer(**args)
+    s.bind_store(b)
+    assert s.fused_horizon
+    s.sample()
+    torch.cuda.synchronize()
+    assert _fused_errors(s) > 0
+    with pytest.raises(RuntimeError, match="timed out"):
+        s.check_errors()
+    with pytest.raises(RuntimeError, match="timed out"):
+        s.close()
+    with pytest.raises(RuntimeError, match="closed"):
+        s.sample()
+    s.close()  # idempotent once closed
+
+    args = default_msacl_args(env_name="VanderPol", env_num=4096, n_step=4, buffer_warm_size=512, buffer_max_size=50000,
+                              max_iteration=4, log_save_interval=2, eval_interval=100, save_folder=str(tmp_path / "t"),
+                              seed=0, replay_batch_size=64, sampler_spin_limit=1)
+    *_, trainer = build_pipeline(args)
+    with pytest.raises(RuntimeError, match="timed out"):
+        for _ in range(3):
+            trainer.step()
+            trainer.iteration += 1
+    try:
+        trainer.close()
+    except RuntimeError:
+        pass

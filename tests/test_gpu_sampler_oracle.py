@@ -1,28 +1,35 @@
-"""GPU parity of the BENCHMARKED sampler instantiation against the oracle.
+"""GPU parity of the BENCHMARKED sampler instantiations against the oracle.
 
-The headline runs `k_rollout<Env, true>` (csrc/rollout.hip): in-kernel TanhGauss sampling and
-clip (RL/utils/act_distribution_cls.py:45-57, RL/trainer/sampler/base.py:127-143), the env
-step, rew_plus_cost, in-kernel Philox resets (gymnasium SyncVectorEnv autoreset) and the
-deferred n-step window emission (base.py:178-217). The other parity tests drive the injected-
-action instantiation `k_rollout<Env, false>`. Here the sampler itself runs, lockstep by
-lockstep, eagerly (HipNstepOffSampler.step_traced: the same policy forward + lockstep launch as
-one iteration of the sampler's graph-captured horizon) at the configs' 65,536 envs with
-n = 20, writing its own sampled actions / log-probs and the env step's outputs
-(mh_rollout_set_trace). Before each lockstep the env state is snapshotted, and the oracle
-replays the kernel's OWN actions from that snapshot:
+The headline runs the fused horizon sampler (csrc/sample_fused.hip, tests/test_gpu_fused_horizon.py
+pins it bit for bit to the lockstep kernels) and the lockstep path runs `k_rollout<Env, true>`
+(csrc/rollout.hip): in-kernel TanhGauss sampling and clip (RL/utils/act_distribution_cls.py:45-57,
+RL/trainer/sampler/base.py:127-143), the env step, rew_plus_cost, in-kernel Philox resets
+(gymnasium SyncVectorEnv autoreset) and the deferred n-step window emission (base.py:178-217). The
+other parity tests drive the injected-action instantiation `k_rollout<Env, false>`. Here the
+sampler itself runs, lockstep by lockstep, eagerly (HipNstepOffSampler.step_traced: the same policy
+forward + lockstep launch as one iteration of the sampler's graph-captured horizon) at the configs'
+65,536 envs with n = 20, writing its own sampled actions / log-probs and the env step's outputs
+(mh_rollout_set_trace). Before each lockstep the env state and the per-env Philox counters are
+snapshotted, and the oracle recomputes from the seed alone:
 
+* the action and its log-prob: oracle/rng.py's float64 TanhGauss of (the policy kernel's logits,
+  the eps the env draws at its counter) at rtol = atol = 1e-5, every row (no atanh recovery, no
+  exclusion of saturated actions);
 * next observation (final_observation), raw reward, terminated, truncated at rtol = atol = 1e-5
   (QuadTracking against the float64-polar path, and the as-is path within 1e-5 plus the
   reference's own float32-SVD deviation: see tests/test_gpu_env.py);
-* the next state of every continuing env, its steps counter (k + 1, or 0 after a reset);
-* every reset row: the stored state is a draw of the env's reset distribution and the returned
-  observation (and QuadTracking's Rd_last) equals oracle.env_reset_from(stored state);
-* the log-prob the kernel emitted equals the float64 TanhGauss log-prob of the pre-tanh sample
-  recovered from its action and the logits the policy kernel produced;
+* the next state of every continuing env, its steps counter (k + 1, or 0 after a reset), and its
+  Philox counter (+1);
+* every reset row: the stored state is the oracle's reset draw at that env's counter (bit-exact;
+  QuadTracking's rotation block within 2e-7) and the returned observation (and QuadTracking's
+  Rd_last) equals oracle.env_reset_from(state);
 * the replay store filled by the deferred emitter waves (+ the final flush) equals the windows
-  oracle.sampler.NStepWindows assembles from the oracle's per-step records, row for row.
+  oracle.sampler.NStepWindows assembles from the oracle's per-step records — actions and log-probs
+  included — row for row.
 
 1/16 of the envs start 985-999 steps into their episode so truncation happens inside the run.
+The fused horizon's sampled actions and log-probs (mh_sample_horizon's act_out / logp_out, its
+logits trace) are checked against the oracle the same way for a whole 20-lockstep horizon.
 """
 import numpy as np
 import pytest
@@ -36,7 +43,9 @@ from msacl_amd.trainer.buffer.device_nstep_replay_buffer import KEYS
 from msacl_amd.utils.config import default_msacl_args
 from msacl_amd.utils.init_args import init_args
 from oracle import envs as OE
+from oracle import rng as OR
 from oracle import sampler as OS
+import msacl_amd._native as N
 
 pytestmark = pytest.mark.gpu
 TOL = dict(rtol=1e-5, atol=1e-5)
@@ -136,9 +145,14 @@ def test_sampled_lockstep_kernel_matches_oracle(name, noise, tmp_path):
     if quad:
         np.testing.assert_allclose(xs, xs_r, rtol=0, atol=1e-12)
     n_reset = n_trunc = n_lp = n_quad_allow = 0
+    seed, idx = env.seed, np.arange(E)
+    pol = sampler.networks.policy
+    ls_lo, ls_hi = float(getattr(pol, "min_log_std", -20.0)), float(getattr(pol, "max_log_std", 1.0))
     for t in range(STEPS.get(name, 40)):
+        ctr = env.get_counters().cpu().numpy()
         logits = sampler.step_traced(act, logp, trace=(real, rew, term, trunc))
-        a_np, lp_np, lg = act.cpu().numpy(), logp.cpu().numpy(), logits.cpu().numpy().astype(np.float64)
+        a_np, lp_np, lg32 = act.cpu().numpy(), logp.cpu().numpy(), logits.cpu().numpy()
+        noise_t = float(sampler._noise[0]) if noise is not None else 0.0
         got_real, got_rew = real.cpu().numpy(), rew.cpu().numpy()
         got_term, got_trunc = term.cpu().numpy().astype(bool), trunc.cpu().numpy().astype(bool)
         st2, xs2, k2 = env.get_state()
@@ -146,17 +160,14 @@ def test_sampled_lockstep_kernel_matches_oracle(name, noise, tmp_path):
         xs2 = xs2.cpu().numpy() if xs2 is not None else None
         obs_next = sampler.obs.cpu().numpy()
 
-        # ---- the action: in the box; its log-prob from the policy logits (no-noise runs)
+        # ---- the action and its log-prob: the oracle's TanhGauss of (logits, the env's eps)
         assert np.all((a_np >= cls.act_low) & (a_np <= cls.act_high))
-        if noise is None:
-            mu, sd = lg[:, :A], np.exp(np.clip(lg[:, A:], -20, 1))
-            th = (2 * a_np.astype(np.float64) - (hi + lo)) / (hi - lo)
-            ok = np.all(np.abs(th) < 0.95, axis=1)
-            z = np.arctanh(np.clip(th, -0.95, 0.95))
-            lp = (-((z - mu) ** 2) / (2 * sd ** 2) - np.log(sd) - 0.5 * np.log(2 * np.pi)).sum(1)
-            lp = lp - np.log(1 + 1e-6 - np.tanh(z) ** 2).sum(1) - np.log((hi - lo) / 2).sum()
-            np.testing.assert_allclose(lp_np[ok], lp[ok], rtol=1e-4, atol=5e-3)
-            n_lp += int(ok.sum())
+        eps = OR.action_normals(seed, idx, ctr)
+        a_o, lp_o = OR.tanh_gauss_sample(lg32, eps, lo, hi, ls_lo, ls_hi, noise=noise_t)
+        np.testing.assert_allclose(a_np, a_o, **TOL, err_msg="sampled action")
+        np.testing.assert_allclose(lp_np, lp_o, **TOL, err_msg="sampled log-prob")
+        n_lp += E
+        np.testing.assert_array_equal(env.get_counters().cpu().numpy(), (ctr + 1) & 0xFFFFFFFF)
 
         # ---- the env step from the snapshot, with the kernel's own actions
         s_o, xs_o, o2, r2, te, tr = OE.env_step(name, st, a_np, xs, k, polar64=quad)
@@ -188,6 +199,13 @@ def test_sampled_lockstep_kernel_matches_oracle(name, noise, tmp_path):
         obs_new = o2.copy()
         if done.any():
             assert _reset_box_ok(name, st2[done])
+            want = OR.reset_draw(name, seed, idx[done], ctr[done])
+            if quad:
+                uni = np.r_[0:6, 15:18]
+                np.testing.assert_array_equal(st2[done][:, uni], want[:, uni])
+                np.testing.assert_allclose(st2[done][:, 6:15], want[:, 6:15], rtol=0, atol=2e-7)
+            else:
+                np.testing.assert_array_equal(st2[done], want)
             _, xr, orr = OE.env_reset_from(name, st2[done])
             np.testing.assert_allclose(obs_next[done], orr, **TOL)
             if quad:
@@ -196,7 +214,8 @@ def test_sampled_lockstep_kernel_matches_oracle(name, noise, tmp_path):
 
         # ---- the oracle's n-step records (rew_plus_cost.py:18-21 with the reference's scales)
         r_s, c_s = OS.rew_plus_cost(o2, r2.astype(np.float32), 100.0, 100.0)
-        for key, w in zip(KEYS, windows.push(obs_o, a_np, r_s, c_s, o2, done, lp_np)):
+        rec = windows.push(obs_o, a_o.astype(np.float32), r_s, c_s, o2, done, lp_o.astype(np.float32))
+        for key, w in zip(KEYS, rec):
             expect[key].append(w)
         st, xs, k, obs_o = st2, xs2, k2, obs_new
 
@@ -206,8 +225,44 @@ def test_sampled_lockstep_kernel_matches_oracle(name, noise, tmp_path):
     total = exp["obs"].shape[0]
     assert total > 500 and n_reset > 0 and n_trunc > 0, (total, n_reset, n_trunc)
     assert n_quad_allow <= 1e-5 * E * STEPS.get(name, 40), n_quad_allow  # a handful of 1.77 M env-steps
-    assert noise is not None or n_lp > 1000
+    assert n_lp > 1000
     assert int(buffer.cursor[2]) == total and total < buffer.max_size
     for key in KEYS:
         np.testing.assert_allclose(buffer.n_step_buf[key][:total].cpu().numpy(), exp[key], **TOL, err_msg=key)
     assert not buffer.n_step_buf["done"][:total, :-1].any()
+
+
+@pytest.mark.parametrize("name", list(OE.ENVS))
+def test_fused_horizon_samples_match_oracle(name, tmp_path):
+    """The benchmarked kernel (mh_sample_horizon): every lockstep's sampled actions and log-probs of
+    a 20-lockstep horizon at 65,536 envs equal the oracle's TanhGauss of (the logits the kernel
+    sampled from, the eps env e draws at counter c0[e] + t) at rtol = atol = 1e-5, and every
+    counter advances by the horizon."""
+    sampler, buffer = _sampler(name, tmp_path)
+    assert sampler.fused_horizon
+    env, dev = sampler.envs, sampler.device
+    D, A, H = env.obs_dim, env.act_dim, sampler.horizon
+    cls = OE.ENVS[name]
+    lo, hi = cls.act_low.astype(np.float64), cls.act_high.astype(np.float64)
+    pol = sampler.networks.policy
+    ls_lo, ls_hi = float(getattr(pol, "min_log_std", -20.0)), float(getattr(pol, "max_log_std", 1.0))
+    sampler.sample()  # the envs move off their initial draws
+    lg = torch.empty(H, E, 2 * A, device=dev)
+    ob = torch.empty(H, E, D, device=dev)
+    act, logp = torch.empty(H, E, A, device=dev), torch.empty(H, E, device=dev)
+    N.check(N.lib().mh_sample_horizon_debug_logits(sampler._h, N.ptr(lg), N.ptr(ob)), "debug logits")
+    try:
+        c0 = env.get_counters().cpu().numpy()
+        with torch.no_grad():
+            sampler._horizon(buffer, act_out=act, logp_out=logp)
+        torch.cuda.synchronize()
+    finally:
+        N.check(N.lib().mh_sample_horizon_debug_logits(sampler._h, None, None), "debug logits off")
+    sampler.check_errors()
+    np.testing.assert_array_equal(env.get_counters().cpu().numpy(), (c0 + H) & 0xFFFFFFFF)
+    lg, act, logp = lg.cpu().numpy(), act.cpu().numpy(), logp.cpu().numpy()
+    for t in range(H):
+        eps = OR.action_normals(env.seed, np.arange(E), (c0 + t) & 0xFFFFFFFF)
+        a_o, lp_o = OR.tanh_gauss_sample(lg[t], eps, lo, hi, ls_lo, ls_hi)
+        np.testing.assert_allclose(act[t], a_o, **TOL, err_msg=f"lockstep {t} action")
+        np.testing.assert_allclose(logp[t], lp_o, **TOL, err_msg=f"lockstep {t} log-prob")
