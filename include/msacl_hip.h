@@ -402,6 +402,21 @@ int mh_head_backward_grouped(const float* dy, const float* x, const float* W, in
                              int64_t stride_x, int64_t stride_w, int64_t stride_dx, int64_t stride_dw,
                              int64_t stride_db, float* dx, float* dw, float* db, float* workspace, void* stream);
 
+/* A whole 3-layer MLP forward (RL/apprfunc/mlp.py:18-30 mlp([k1, hidden, hidden, n_out]): Linear ->
+ * act1 -> Linear -> act2 -> Linear -> act3, the policy / critic / Lyapunov networks of every
+ * reference algorithm) in ONE launch instead of one per layer: h1 = act1(x W1^T + b1),
+ * h2 = act2(h1 W2^T + b2), y = act3(h2 W3^T + b3), row-major operands (x [rows][ldx], W1 [hidden][k1],
+ * W2 [hidden][hidden], W3 [n_out][hidden]); h1 / h2 [rows][ldh] are written when non-NULL (autograd
+ * keeps them for the backward), y [rows][ldy]. Supported: k1 <= 32, hidden == 256, n_out <= 16 or a
+ * multiple of 64 up to 256; act 0 identity, 1 ReLU, 2 tanh. f32 products (MFMA), f32 accumulation.
+ * groups > 1 evaluates `groups` networks of one shape (the twin critics) in the same launch: group q
+ * reads and writes each operand at its group-0 pointer + q x group_strides[i] floats, host array
+ * {x, W1, b1, W2, b2, W3, b3, h (h1 and h2), y}. */
+int mh_mlp3_forward(const float* x, int64_t rows, int32_t k1, int64_t ldx, const float* W1, const float* b1,
+                    const float* W2, const float* b2, const float* W3, const float* b3, int32_t hidden, int32_t n_out,
+                    int32_t act1, int32_t act2, int32_t act3, float* h1, float* h2, int64_t ldh, float* y, int64_t ldy,
+                    int32_t groups, const int64_t* group_strides, void* stream);
+
 /* StochaPolicy's head (RL/apprfunc/mlp.py:132-136) on [rows][2 act_dim] rows:
  *   out = [mean | exp(clamp(log_std, min_log_std, max_log_std))] of raw = [mean | log_std]
  * and its backward d_raw = [d_mean | d_std * std * (min <= log_std <= max)], one launch each

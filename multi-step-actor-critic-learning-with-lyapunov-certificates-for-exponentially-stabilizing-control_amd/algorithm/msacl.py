@@ -698,7 +698,7 @@ class MSACL:
         M = B * n
         xa2 = xa.reshape(M, xa.shape[-1])
         q, h1, h2 = twin.forward(xa2)
-        qt, _, _ = twin_t.forward(xq2.reshape(M, xq2.shape[-1]))
+        qt, _, _ = twin_t.forward(xq2.reshape(M, xq2.shape[-1]), keep=False)
         weight = data.get("weight") if self.per_flag else None
         _engine(
             "msacl_q_target", self.device,

@@ -226,49 +226,134 @@ class LinearAct(torch.autograd.Function):
     def backward(ctx, dy):
         x, weight, y = ctx.saved_tensors
         need_x, need_w, need_b = ctx.needs_input_grad[:3]
-        act = ctx.act
-        dy = dy.contiguous()
-        if act == 0 and _HEAD_BACKWARD["on"] and _GEMM_BACKEND["name"] != "blas":
-            head = _head_backward(dy, x, weight, need_x, need_w, need_b)
-            if head is not None:
-                return head
-        if (need_x and not need_w and not need_b and _FUSED_BACKWARD["on"] and _GEMM_BACKEND["name"] != "blas"
-                and x.shape[1] <= 32 and dy.shape[0] >= 1024 and dy.shape[1] <= 1024):
-            # narrow input, input gradient only (a frozen critic's first layer): one launch
-            N = _native()
-            rows, n_out = dy.shape
-            dx = torch.empty(rows, x.shape[1], dtype=dy.dtype, device=dy.device)
-            N.check(N.lib().mh_dx_narrow(N.ptr(dy), N.ptr(y.contiguous()) if act else None, act,
-                                         N.ptr(weight.contiguous()), rows, n_out, x.shape[1], N.ptr(dx),
-                                         N.stream_of(dy.device)), "mh_dx_narrow")
-            return dx, None, None, None
-        if _FUSED_BACKWARD["on"]:
-            fused = _linear_backward_fused(dy, y, act, x, weight, need_x, need_w, need_b)
-            if fused is not None:
-                return fused
-        db = None
-        if act == 0 and not need_b:
-            g = dy
-        else:
-            N = _native()
-            M, C = dy.shape
-            chunks = ctypes.c_int32()
-            N.check(N.lib().mh_act_grad_chunks(M, ctypes.byref(chunks)), "mh_act_grad_chunks")
-            partial = torch.empty(chunks.value, C, dtype=dy.dtype, device=dy.device)
-            g = dy if act == 0 else torch.empty_like(dy)
-            db = torch.empty(C, dtype=dy.dtype, device=dy.device) if need_b else None
-            N.check(N.lib().mh_act_grad_colsum(N.ptr(dy), N.ptr(y.contiguous()) if act else None, M, C, act,
-                                               N.ptr(g) if act else None, N.ptr(db), N.ptr(partial),
-                                               N.ptr(_colsum_tickets(dy.device, C)), N.stream_of(dy.device)),
-                    "mh_act_grad_colsum")
-        M, Nout = g.shape
-        K = x.shape[1]
-        dx = dw = None
-        if need_x:
-            dx = gemm(g, weight.contiguous(), None, M, K, Nout, Nout, K, 0, 0) if _hip_dx(M, K, Nout) else g.mm(weight)
-        if need_w:
-            dw = gemm(g, x, None, Nout, K, M, Nout, K, 1, 0) if _hip_dw(Nout, K, M) else g.t().mm(x)
+        dx, dw, db = layer_backward(dy, x, weight, y, ctx.act, need_x, need_w, need_b)
         return dx, dw, db, None
+
+
+def layer_backward(dy, x, weight, y, act, need_x, need_w, need_b):
+    """The backward of y = act(x W^T + b) for the requested gradients: (dx, dW, db), each None
+    when not requested (LinearAct.backward, also the per-layer backward of MLP3)."""
+    dy = dy.contiguous()
+    if act == 0 and _HEAD_BACKWARD["on"] and _GEMM_BACKEND["name"] != "blas":
+        head = _head_backward(dy, x, weight, need_x, need_w, need_b)
+        if head is not None:
+            return head[:3]
+    if (need_x and not need_w and not need_b and _FUSED_BACKWARD["on"] and _GEMM_BACKEND["name"] != "blas"
+            and x.shape[1] <= 32 and dy.shape[0] >= 1024 and dy.shape[1] <= 1024):
+        # narrow input, input gradient only (a frozen critic's first layer): one launch
+        N = _native()
+        rows, n_out = dy.shape
+        dx = torch.empty(rows, x.shape[1], dtype=dy.dtype, device=dy.device)
+        N.check(N.lib().mh_dx_narrow(N.ptr(dy), N.ptr(y.contiguous()) if act else None, act,
+                                     N.ptr(weight.contiguous()), rows, n_out, x.shape[1], N.ptr(dx),
+                                     N.stream_of(dy.device)), "mh_dx_narrow")
+        return dx, None, None
+    if _FUSED_BACKWARD["on"]:
+        fused = _linear_backward_fused(dy, y, act, x, weight, need_x, need_w, need_b)
+        if fused is not None:
+            return fused[:3]
+    db = None
+    if act == 0 and not need_b:
+        g = dy
+    else:
+        N = _native()
+        M, C = dy.shape
+        chunks = ctypes.c_int32()
+        N.check(N.lib().mh_act_grad_chunks(M, ctypes.byref(chunks)), "mh_act_grad_chunks")
+        partial = torch.empty(chunks.value, C, dtype=dy.dtype, device=dy.device)
+        g = dy if act == 0 else torch.empty_like(dy)
+        db = torch.empty(C, dtype=dy.dtype, device=dy.device) if need_b else None
+        N.check(N.lib().mh_act_grad_colsum(N.ptr(dy), N.ptr(y.contiguous()) if act else None, M, C, act,
+                                           N.ptr(g) if act else None, N.ptr(db), N.ptr(partial),
+                                           N.ptr(_colsum_tickets(dy.device, C)), N.stream_of(dy.device)),
+                "mh_act_grad_colsum")
+    M, Nout = g.shape
+    K = x.shape[1]
+    dx = dw = None
+    if need_x:
+        dx = gemm(g, weight.contiguous(), None, M, K, Nout, Nout, K, 0, 0) if _hip_dx(M, K, Nout) else g.mm(weight)
+    if need_w:
+        dw = gemm(g, x, None, Nout, K, M, Nout, K, 1, 0) if _hip_dw(Nout, K, M) else g.t().mm(x)
+    return dx, dw, db
+
+
+# The whole 3-layer MLP forward as one launch (mh_mlp3_forward, csrc/mlp_fused.hip) where the
+# shape qualifies; MSACL_MLP3=0 restores the per-layer launches (A/B)
+_MLP3 = {"on": os.environ.get("MSACL_MLP3", "1") == "1"}
+
+
+def mlp3_forward(x, layers, acts, h_keep, groups=1, strides=None, ldh=None, y=None, ldy=None):
+    """mh_mlp3_forward: x [M][K1] -> (y, h1, h2); h1 / h2 only when h_keep. `layers` are the three
+    (weight, bias) pairs (group 0's when groups > 1)."""
+    N = _native()
+    (W1, b1), (W2, b2), (W3, b3) = layers
+    M, K1 = x.shape[0], x.shape[1]
+    H, N3 = W2.shape[-1], W3.shape[0]
+    dev = x.device
+    if ldh is None:
+        ldh = H
+    h1 = torch.empty(M, ldh, dtype=torch.float32, device=dev) if h_keep else None
+    h2 = torch.empty(M, ldh, dtype=torch.float32, device=dev) if h_keep else None
+    if y is None:
+        y = torch.empty(M, N3, dtype=torch.float32, device=dev)
+        ldy = N3
+    gs = (ctypes.c_int64 * 9)(*strides) if strides is not None else None
+    N.check(N.lib().mh_mlp3_forward(N.ptr(x), M, K1, x.stride(0), N.ptr(W1), N.ptr(b1), N.ptr(W2), N.ptr(b2),
+                                    N.ptr(W3), N.ptr(b3), H, N3, acts[0], acts[1], acts[2], N.ptr(h1), N.ptr(h2), ldh,
+                                    N.ptr(y), ldy, groups, gs, N.stream_of(dev)), "mh_mlp3_forward")
+    return y, h1, h2
+
+
+class MLP3(torch.autograd.Function):
+    """Linear -> act -> Linear -> act -> Linear -> act under autograd: forward = one
+    mh_mlp3_forward launch (h1 / h2 kept only when a gradient will be taken), backward = the
+    three layers' LinearAct backwards (layer_backward) on the kept activations."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2, W3, b3, acts):
+        keep = any(ctx.needs_input_grad[:7])
+        y, h1, h2 = mlp3_forward(x, ((W1, b1), (W2, b2), (W3, b3)), acts, keep)
+        ctx.acts = acts
+        if keep:
+            ctx.save_for_backward(x, W1, W2, W3, h1, h2, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W1, W2, W3, h1, h2, y = ctx.saved_tensors
+        nx, nW1, nb1, nW2, nb2, nW3, nb3 = ctx.needs_input_grad[:7]
+        a1, a2, a3 = ctx.acts
+        need_h2 = nx or nW1 or nb1 or nW2 or nb2
+        dh2, dW3, db3 = layer_backward(dy, h2, W3, y, a3, need_h2, nW3, nb3)
+        dx = dW1 = db1 = dW2 = db2 = None
+        if need_h2:
+            need_h1 = nx or nW1 or nb1
+            dh1, dW2, db2 = layer_backward(dh2, h1, W2, h2, a2, need_h1, nW2, nb2)
+            if need_h1:
+                dx, dW1, db1 = layer_backward(dh1, x, W1, h1, a1, nx, nW1, nb1)
+        return dx, dW1, db1, dW2, db2, dW3, db3, None
+
+
+def mlp3_layers(seq):
+    """((W1, b1), (W2, b2), (W3, b3)), (act ids) of an MLP [K1 <= 32, 256, 256, N3] that
+    mh_mlp3_forward runs, else None."""
+    mods = list(seq)
+    if len(mods) != 6:
+        return None
+    l1, a1, l2, a2, l3, a3 = mods
+    if not all(isinstance(l, nn.Linear) and l.bias is not None for l in (l1, l2, l3)):
+        return None
+    if any(type(a) not in ACT_IDS for a in (a1, a2, a3)):
+        return None
+    H, K1, N3 = l1.out_features, l1.in_features, l3.out_features
+    if H != 256 or l2.in_features != H or l2.out_features != H or l3.in_features != H or K1 > 32:
+        return None
+    if not (N3 <= 16 or (N3 % 64 == 0 and N3 <= 256)):
+        return None
+    ps = (l1.weight, l1.bias, l2.weight, l2.bias, l3.weight, l3.bias)
+    if any(not p.is_contiguous() or p.dtype != torch.float32 or p.data_ptr() % 16 for p in ps):
+        return None
+    return ((l1.weight, l1.bias), (l2.weight, l2.bias), (l3.weight, l3.bias)), tuple(ACT_IDS[type(a)] for a in (a1, a2, a3))
 
 
 class SquareSum(torch.autograd.Function):
@@ -348,6 +433,12 @@ class MLP(nn.Sequential):
         h = x.reshape(-1, x.shape[-1])
         if not h.is_contiguous():
             h = h.contiguous()
+        if _MLP3["on"] and _GEMM_BACKEND["name"] != "blas" and h.data_ptr() % 4 == 0:
+            spec = mlp3_layers(self)
+            if spec is not None:
+                (l1, l2, l3), acts = spec
+                y = MLP3.apply(h, l1[0], l1[1], l2[0], l2[1], l3[0], l3[1], acts)
+                return y.reshape(*lead, y.shape[-1])
         mods = list(self)
         for i in range(0, len(mods), 2):
             lin, act = mods[i], mods[i + 1]

@@ -132,10 +132,19 @@ class TwinCritic:
         return t
 
     # ------------------------------------------------------------------ forward / backward
-    def forward(self, x):
-        """x [rows][K] contiguous -> (q [2][rows], h1 [rows][2H], h2 [rows][2H])."""
+    def forward(self, x, keep=True):
+        """x [rows][K] contiguous -> (q [2][rows], h1 [rows][2H], h2 [rows][2H]); h1 / h2 are None
+        when not kept (no backward follows). One grouped mh_mlp3_forward launch for both critics
+        (apprfunc/_fused.py mlp3_forward), or the per-layer launches with MSACL_MLP3=0."""
         N = _native()
         M, H = x.shape[0], self.H
+        from ._fused import _MLP3, mlp3_forward
+        if _MLP3["on"] and H == 256:
+            q = torch.empty(2, M, dtype=torch.float32, device=x.device)
+            _, h1, h2 = mlp3_forward(x, ((self.W1, self.b1), (self.W2[0], self.b2[0]), (self.W3[0:1], self.b3)),
+                                     (1, 1, 0), keep, groups=2,
+                                     strides=(0, H * self.K, H, H * H, H, H, 1, H, M), ldh=2 * H, y=q, ldy=1)
+            return q, h1, h2
         h1 = torch._addmm_activation(self.b1, x, self.W1.t())  # one library GEMM + ReLU for both layer-1s
         h2 = torch.empty(M, 2 * H, dtype=torch.float32, device=x.device)
         q = torch.empty(2, M, dtype=torch.float32, device=x.device)

@@ -974,6 +974,42 @@ int mh_gemm_f32_grouped(const float* A, const float* B, const float* bias, float
   return MH_OK;
 }
 
+int mh_mlp3_forward(const float* x, int64_t rows, int32_t k1, int64_t ldx, const float* W1, const float* b1,
+                    const float* W2, const float* b2, const float* W3, const float* b3, int32_t hidden, int32_t n_out,
+                    int32_t act1, int32_t act2, int32_t act3, float* h1, float* h2, int64_t ldh, float* y, int64_t ldy,
+                    int32_t groups, const int64_t* group_strides, void* stream) {
+  if (rows < 0 || groups < 0) return fail(MH_EINVAL, "mh_mlp3_forward: bad size");
+  if (rows == 0 || groups == 0) return MH_OK;
+  if (!mh::mlp3_supported(rows, k1, hidden, n_out))
+    return fail(MH_EINVAL, "mh_mlp3_forward: shape not supported (k1 <= 32, hidden 256, n_out <= 16 or a multiple of 64 <= 256)");
+  for (int act : {act1, act2, act3})
+    if (act < 0 || act > 2) return fail(MH_EINVAL, "mh_mlp3_forward: act must be 0, 1 or 2");
+  if (!x || !W1 || !b1 || !W2 || !b2 || !W3 || !b3 || !y) return fail(MH_EINVAL, "mh_mlp3_forward: null operand");
+  if (ldx < k1 || ldy < n_out || ((h1 || h2) && ldh < hidden))
+    return fail(MH_EINVAL, "mh_mlp3_forward: leading dimension smaller than the matrix");
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!al16(W2) || !al16(W3) || !al16(h1) || !al16(h2) || (ldh & 3))
+    return fail(MH_EINVAL, "mh_mlp3_forward: W2, W3, h1, h2 must be 16-byte aligned (ldh a multiple of 4)");
+  if (groups > 1 && !group_strides) return fail(MH_EINVAL, "mh_mlp3_forward: grouped launch needs group_strides");
+  mh::Mlp3Args a;
+  std::memset(&a, 0, sizeof(a));
+  a.x = x; a.M = rows; a.ldx = ldx; a.K1 = k1; a.H = hidden; a.N3 = n_out;
+  a.act1 = act1; a.act2 = act2; a.act3 = act3;
+  a.W1 = W1; a.b1 = b1; a.W2 = W2; a.b2 = b2; a.W3 = W3; a.b3 = b3;
+  a.h1 = h1; a.h2 = h2; a.y = y; a.ldh = ldh; a.ldy = ldy;
+  if (groups > 1) {
+    const int64_t* g = group_strides;
+    for (int i = 0; i < 9; ++i)
+      if (g[i] < 0) return fail(MH_EINVAL, "mh_mlp3_forward: negative group stride");
+    if ((g[3] & 3) || (g[5] & 3) || (g[7] & 3))
+      return fail(MH_EINVAL, "mh_mlp3_forward: W2 / W3 / h group strides must keep 16-byte alignment");
+    a.gs_x = g[0]; a.gs_W1 = g[1]; a.gs_b1 = g[2]; a.gs_W2 = g[3]; a.gs_b2 = g[4]; a.gs_W3 = g[5]; a.gs_b3 = g[6];
+    a.gs_h = g[7]; a.gs_y = g[8];
+  }
+  MH_HIP(mh::launch_mlp3_forward(a, groups, (hipStream_t)stream));
+  return MH_OK;
+}
+
 int mh_linear_backward_grouped(const float* dy, const float* y, int32_t act, const float* x, const float* W,
                                int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy, int64_t ld_x, int64_t ld_dx,
                                int32_t groups, int64_t stride_dy, int64_t stride_x, int64_t stride_w,

@@ -1,0 +1,244 @@
+// mlp_fused.hip — the update's 3-layer MLPs (RL/apprfunc/mlp.py:18-30: Linear -> act -> Linear ->
+// act -> Linear -> act) forward in ONE launch (gfx950, f32-input MFMA).
+//
+//   h1 = act1(x W1^T + b1)   [M][H]      x [M][K1], K1 <= 32
+//   h2 = act2(h1 W2^T + b2)  [M][H]      H = 256
+//   y  = act3(h2 W3^T + b3)  [M][N3]     N3 <= 16, or N3 a multiple of 64 (<= 256)
+//
+// The per-layer path is three launches (the BLAS short-K GEMM, the tall kernel, a GEMV / narrow
+// GEMM: 30-35 us at 5,120 rows, most of it per-launch ramp and drain), and it writes h1 to HBM and
+// reads it back. Here a workgroup owns TM = 16 rows through all three layers:
+//   * 4 waves; in each hidden layer wave w computes output columns [64 w, 64 w + 64) as four
+//     16 x 16 accumulators (v_mfma_f32_16x16x4_f32);
+//   * the layer's input rows sit in LDS; every 16-deep K group is one ds_read_b128 per lane (the
+//     A operand of four MFMAs) and four global float4 loads of weight rows (the B operands), the
+//     loads issued three groups ahead. The K order inside a group is permuted consistently on
+//     both operands: in MFMA t of group u, lane group g = lane >> 4 contracts k = 16 u + 4 g + t,
+//     so one 16-byte load per lane and operand feeds four MFMAs;
+//   * the epilogue (bias, activation) writes the layer's output tile to LDS for the next layer,
+//     and (when the caller keeps them for the backward) as row-contiguous float4 stores to h1 / h2;
+//   * narrow output layers (N3 <= 16: the policy head, the critics' single output) split K over
+//     the four waves and add the four partial tiles in wave order through LDS.
+// Numerics: f32 MFMA products (exact) accumulated in f32 in k order within each 4-deep step; the
+// same f32 results as the per-layer kernels up to summation order.
+// Grouped launches (the twin critics, apprfunc/_twin.py): blockIdx.y = group q; every pointer is
+// advanced by q x its group stride (floats; 0 = shared).
+#include "rollout.h"
+
+namespace mh {
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int TM = 16;        // rows per workgroup
+constexpr int HID = 256;      // hidden width
+constexpr int SH = HID + 4;   // LDS row stride of a hidden tile (floats): rows 16 B apart in the banks
+constexpr int K1P = 32;       // first-layer K padded
+constexpr int SX = K1P + 4;
+constexpr int PF = 3;         // weight groups in flight
+
+__device__ __forceinline__ float act_f(float v, int act) {
+  if (act == 1) return v < 0.0f ? 0.0f : v;  // as torch.relu / gemm_act (NaN passes through)
+  if (act == 2) return tanhf(v);
+  return v;
+}
+
+// One hidden-width layer for this wave's 64 output columns: out[16][64] += in[16][K] W[n][K]^T.
+// `in` is the LDS tile (row stride SIN floats), W rows [n0, n0 + 64) of a row-major [N][K] matrix
+// behind a buffer resource (rows past N read 0). K is a multiple of 16.
+template <int SIN>
+__device__ __forceinline__ void layer_cols(const float* in, __amdgpu_buffer_rsrc_t wr, int K, int n0, int lane,
+                                           f32x4 (&acc)[4]) {
+  const int r = lane & 15, g = lane >> 4;
+  const int G = K / 16;
+  f32x4 wb[PF][4];
+  auto load = [&](int u, f32x4* dst) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int off = ((n0 + 16 * j + r) * K + 16 * u + 4 * g) * 4;
+      dst[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
+    }
+  };
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+    if (p < G) load(p, wb[p]);
+  for (int u0 = 0; u0 < G; u0 += PF) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      const int u = u0 + p;
+      if (u < G) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(in + r * SIN + 16 * u + 4 * g);
+        f32x4 b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = wb[p][j];
+        if (u + PF < G) load(u + PF, wb[p]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[j][t], acc[j], 0, 0, 0);
+      }
+    }
+  }
+}
+
+// bias + activation of this wave's 64 columns into the LDS tile `out` (row stride SH); the MFMA's
+// C map: column = lane & 15, rows 4 (lane >> 4) + q
+__device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[4], const float* bias, int act, int n0, int lane,
+                                             float* out) {
+  const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + 16 * j + c;
+    const float bv = bias[n];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[(4 * g + q) * SH + n] = act_f(acc[j][q] + bv, act);
+  }
+}
+
+// the LDS tile (16 rows x HID) to global rows m0.. (ld floats), row-contiguous float4 stores
+__device__ __forceinline__ void store_tile(const float* tile, float* dst, int64_t ld, int64_t m0, int64_t M, int cols) {
+  const int per_row = cols / 4;
+  for (int i = threadIdx.x; i < TM * per_row; i += 256) {
+    const int rr = i / per_row, c4 = i - rr * per_row;
+    if (m0 + rr < M)
+      *reinterpret_cast<f32x4*>(dst + (m0 + rr) * ld + 4 * c4) = *reinterpret_cast<const f32x4*>(tile + rr * SH + 4 * c4);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
+  __shared__ float xs[TM * SX];
+  __shared__ float hs1[TM * SH];
+  __shared__ float hs2[TM * SH];
+  __shared__ f32x4 red[4][64];
+  {
+    const int64_t q = blockIdx.y;
+    a.x += q * a.gs_x;
+    a.W1 += q * a.gs_W1;
+    a.b1 += q * a.gs_b1;
+    a.W2 += q * a.gs_W2;
+    a.b2 += q * a.gs_b2;
+    a.W3 += q * a.gs_W3;
+    a.b3 += q * a.gs_b3;
+    if (a.h1) a.h1 += q * a.gs_h;
+    if (a.h2) a.h2 += q * a.gs_h;
+    a.y += q * a.gs_y;
+  }
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t m0 = (int64_t)blockIdx.x * TM;
+  const int K1 = a.K1, K1p = (K1 + 15) & ~15;
+
+  // ---- the input rows, zero-padded to K1p columns (rows past M: zeros)
+  for (int i = tid; i < TM * K1p; i += 256) {
+    const int rr = i / K1p, k = i - rr * K1p;
+    xs[rr * SX + k] = (m0 + rr < a.M && k < K1) ? a.x[(m0 + rr) * a.ldx + k] : 0.0f;
+  }
+  __syncthreads();
+
+  const int n0 = wave * 64;
+  // ---- layer 1: K1p <= 32; weights [H][K1]: a row's float4 at k >= K1 is masked to 0 (the next row's)
+  {
+    f32x4 acc[4] = {};
+    const int r = lane & 15, g = lane >> 4;
+    for (int u = 0; u < K1p / 16; ++u) {
+      const f32x4 av = *reinterpret_cast<const f32x4*>(xs + r * SX + 16 * u + 4 * g);
+      f32x4 b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float* row = a.W1 + (int64_t)(n0 + 16 * j + r) * K1;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int k = 16 * u + 4 * g + t;
+          b[j][t] = k < K1 ? row[k] : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], b[j][t], acc[j], 0, 0, 0);
+    }
+    epilogue_lds(acc, a.b1, a.act1, n0, lane, hs1);
+  }
+  __syncthreads();
+  if (a.h1) store_tile(hs1, a.h1, a.ldh, m0, a.M, HID);
+
+  // ---- layer 2
+  {
+    const __amdgpu_buffer_rsrc_t wr =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.W2), (short)0, HID * HID * 4, 0x00020000);
+    f32x4 acc[4] = {};
+    layer_cols<SH>(hs1, wr, HID, n0, lane, acc);
+    epilogue_lds(acc, a.b2, a.act2, n0, lane, hs2);
+  }
+  __syncthreads();
+  if (a.h2) store_tile(hs2, a.h2, a.ldh, m0, a.M, HID);
+
+  // ---- layer 3
+  const int N3 = a.N3;
+  const __amdgpu_buffer_rsrc_t wr3 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.W3), (short)0, N3 * HID * 4, 0x00020000);
+  if (N3 <= 16) {
+    // one 16-column block; wave w contracts k in [64 w, 64 w + 64), the four partial tiles added
+    // in wave order
+    const int r = lane & 15, g = lane >> 4;
+    f32x4 acc = {};
+#pragma unroll
+    for (int uu = 0; uu < 4; ++uu) {
+      const int u = wave * 4 + uu;
+      const f32x4 av = *reinterpret_cast<const f32x4*>(hs2 + r * SH + 16 * u + 4 * g);
+      const f32x4 bv = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr3, (r * HID + 16 * u + 4 * g) * 4, 0, 0));
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bv[t], acc, 0, 0, 0);
+    }
+    red[wave][lane] = acc;
+    __syncthreads();
+    if (wave == 0) {
+      f32x4 s = red[0][lane];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) s = s + red[w][lane];
+      const int n = lane & 15;
+      if (n < N3) {
+        const float bv = a.b3[n];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t row = m0 + 4 * g + q;
+          if (row < a.M) a.y[row * a.ldy + n] = act_f(s[q] + bv, a.act3);
+        }
+      }
+    }
+  } else {
+    // N3 = 64 c: wave w takes output columns [N3 / 4 * w, ...) in 16-column blocks of 64-wide passes
+    for (int nb = wave * 64; nb < N3; nb += 256) {
+      f32x4 acc[4] = {};
+      layer_cols<SH>(hs2, wr3, HID, nb, lane, acc);
+      const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nb + 16 * j + c;
+        const float bv = a.b3[n];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int64_t row = m0 + 4 * g + q;
+          if (row < a.M) a.y[row * a.ldy + n] = act_f(acc[j][q] + bv, a.act3);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+bool mlp3_supported(int64_t M, int K1, int H, int N3) {
+  return M > 0 && K1 >= 1 && K1 <= K1P && H == HID && N3 >= 1 && (N3 <= 16 || (N3 % 64 == 0 && N3 <= 256));
+}
+
+hipError_t launch_mlp3_forward(const Mlp3Args& a, int groups, hipStream_t st) {
+  if (!mlp3_supported(a.M, a.K1, a.H, a.N3) || groups < 1) return hipErrorInvalidValue;
+  const int64_t tiles = (a.M + TM - 1) / TM;
+  k_mlp3_fwd<<<dim3((unsigned)tiles, (unsigned)groups), 256, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace mh

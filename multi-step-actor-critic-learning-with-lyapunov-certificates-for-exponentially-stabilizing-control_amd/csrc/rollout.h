@@ -178,6 +178,19 @@ struct PolyakList {
   int64_t start[ADAM_MAX_TENSORS + 1];
   int n;
 };
+// the fused 3-layer MLP forward (mlp_fused.hip)
+struct Mlp3Args {
+  const float* x;
+  int64_t M, ldx;
+  int K1, H, N3;
+  int act1, act2, act3;  // 0 identity, 1 ReLU, 2 tanh
+  const float *W1, *b1, *W2, *b2, *W3, *b3;
+  float *h1, *h2, *y;    // h1 / h2 may be null (not kept)
+  int64_t ldh, ldy;
+  int64_t gs_x, gs_W1, gs_b1, gs_W2, gs_b2, gs_W3, gs_b3, gs_h, gs_y;
+};
+bool mlp3_supported(int64_t M, int K1, int H, int N3);
+hipError_t launch_mlp3_forward(const Mlp3Args& a, int groups, hipStream_t st);
 hipError_t launch_polyak_multi(const PolyakList& L, double polyak, hipStream_t st);
 hipError_t launch_adam_multi(const AdamList& L, double b1, double b2, double eps, uint32_t* ticket,
                              hipStream_t st);

@@ -801,11 +801,34 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_emit_scan(HorizonEmitArgs a) {
     cur1 = a.cursor[1];
     cur2 = a.cursor[2];
   }
+  // When every lockstep's wave counts form whole cells (NW % 4 == 0: E a multiple of 256), cell c's
+  // four counts are the 16 bytes at emit_count + 4 c, so the round's counts are loaded as
+  // consecutive int4 per lane (a wave-instruction reads 1 KB of consecutive lines) and regrouped
+  // through LDS; the general path below loads each thread's own 8 consecutive cells, whose lanes
+  // sit 128 B apart (a line per lane per load: 32 instructions x 64 lines per wave, ~15 us).
+  __shared__ int s_cnt[SCAN_THREADS * SCAN_CPT];
+  const bool whole = (NW & 3) == 0;
   int64_t carry = 0;
   int round = 0;
   for (int64_t c0 = 0; c0 < NC; c0 += (int64_t)SCAN_THREADS * SCAN_CPT, ++round) {
     int cnt[SCAN_CPT];
-    {
+    if (whole) {
+      const int4* cells = reinterpret_cast<const int4*>(a.emit_count);
+      int4 v[SCAN_CPT];
+#pragma unroll
+      for (int j = 0; j < SCAN_CPT; ++j) {
+        const int64_t c = c0 + t + (int64_t)j * SCAN_THREADS;
+        v[j] = cells[c < NC ? c : NC - 1];  // unconditional (clamped) loads, all in flight
+      }
+#pragma unroll
+      for (int j = 0; j < SCAN_CPT; ++j) {
+        const int64_t c = c0 + t + (int64_t)j * SCAN_THREADS;
+        s_cnt[t + j * SCAN_THREADS] = c < NC ? v[j].x + v[j].y + v[j].z + v[j].w : 0;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < SCAN_CPT; ++j) cnt[j] = s_cnt[t * SCAN_CPT + j];
+    } else {
       // (lockstep, block) of this thread's first cell, then stepped: one 32-bit division per
       // thread and round instead of a 64-bit one per cell (cells < 2^31: the launcher's bound)
       const int c = (int)(c0 + (int64_t)t * SCAN_CPT);

@@ -1,0 +1,135 @@
+"""GPU: the fused 3-layer MLP forward (mh_mlp3_forward, csrc/mlp_fused.hip) against a float64
+evaluation of each layer (RL/apprfunc/mlp.py:18-30: Linear -> act -> Linear -> act -> Linear -> act).
+
+Each layer is checked on the kernel's own input to it (h1 and h2 as the kernel wrote them), so the
+bound does not compound: |err| <= 2e-6 sqrt(K) sum_k |a_k w_k| + 1e-6 (tests/test_gpu_gemm.py's
+f32-accumulation bound), plus tanhf's ulp where the activation is tanh. Shapes: the policy
+(K1 = D, ReLU, N3 = 2A), the critics (K1 = D + A, N3 = 1), the Lyapunov network (tanh, N3 = 256),
+ragged row counts and every supported K1; the grouped (twin-critic) launch; and the MLP module's
+forward / backward through the fused launch against the per-layer launches."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+import msacl_amd  # noqa: F401
+import msacl_amd._native as N
+from msacl_amd.apprfunc import _fused as F
+
+pytestmark = pytest.mark.gpu
+ACT = {0: lambda v: v, 1: lambda v: np.maximum(v, 0.0), 2: np.tanh}
+
+
+def _params(K1, N3, seed, H=256, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    f = lambda *s: (torch.rand(*s, generator=g) * 2 - 1)  # noqa: E731
+    W1, b1 = f(H, K1) / K1 ** 0.5 * scale, f(H) * 0.1
+    W2, b2 = f(H, H) / H ** 0.5 * scale, f(H) * 0.1
+    W3, b3 = f(N3, H) / H ** 0.5 * scale, f(N3) * 0.1
+    return [t.cuda().contiguous() for t in (W1, b1, W2, b2, W3, b3)]
+
+
+def _check_layer(out, inp, W, b, act, what):
+    a, w = inp.double().cpu().numpy(), W.double().cpu().numpy()
+    lin = a @ w.T + b.double().cpu().numpy()
+    mag = np.abs(a) @ np.abs(w).T + np.abs(b.double().cpu().numpy())
+    ref = ACT[act](lin)
+    tol = 2e-6 * (a.shape[1] ** 0.5) * mag + 1e-6 + (2e-7 * np.abs(ref) if act == 2 else 0.0)
+    err = np.abs(out.double().cpu().numpy() - ref)
+    assert np.all(err <= tol), f"{what}: max err {err.max():.3e}, worst ratio {(err / tol).max():.3f}"
+
+
+def _run(x, ps, acts, keep=True, N3=None):
+    W1, b1, W2, b2, W3, b3 = ps
+    M, K1 = x.shape
+    N3 = W3.shape[0]
+    h1 = torch.full((M, 256), float("nan"), device="cuda") if keep else None
+    h2 = torch.full((M, 256), float("nan"), device="cuda") if keep else None
+    y = torch.full((M, N3), float("nan"), device="cuda")
+    N.check(N.lib().mh_mlp3_forward(N.ptr(x), M, K1, K1, *[N.ptr(t) for t in ps], 256, N3, *acts, N.ptr(h1), N.ptr(h2),
+                                    256, N.ptr(y), N3, 1, None, N.stream_of()), "mh_mlp3_forward")
+    torch.cuda.synchronize()
+    return y, h1, h2
+
+
+CASES = [("policy", 5120, 12, 8, (1, 1, 0)), ("critic", 5120, 16, 1, (1, 1, 0)), ("lyapunov", 10240, 12, 256, (2, 2, 0)),
+         ("ragged", 1000, 12, 8, (1, 1, 0)), ("tiny", 17, 6, 2, (1, 1, 0)), ("k1", 300, 1, 4, (1, 2, 0)),
+         ("k20", 777, 20, 16, (2, 1, 0)), ("k32", 2048, 32, 64, (1, 1, 2)), ("n128", 512, 14, 128, (2, 2, 1))]
+
+
+@pytest.mark.parametrize("name,M,K1,N3,acts", CASES, ids=[c[0] for c in CASES])
+def test_mlp3_forward_matches_float64_layers(name, M, K1, N3, acts):
+    ps = _params(K1, N3, seed=M + K1)
+    x = (torch.rand(M, K1, generator=torch.Generator().manual_seed(1)) * 4 - 2).cuda()
+    y, h1, h2 = _run(x, ps, acts)
+    W1, b1, W2, b2, W3, b3 = ps
+    _check_layer(h1, x, W1, b1, acts[0], "layer 1")
+    _check_layer(h2, h1, W2, b2, acts[1], "layer 2")
+    _check_layer(y, h2, W3, b3, acts[2], "layer 3")
+    # without the kept activations: the same output, bit for bit
+    y2, _, _ = _run(x, ps, acts, keep=False)
+    assert torch.equal(y, y2)
+
+
+def test_mlp3_forward_grouped_equals_ungrouped():
+    """Two networks of one shape in one launch (the twin critics' joint buffers: W1 [2H][K],
+    W2 [2][H][H], W3 [2][H], h [M][2H]); each group equals its ungrouped launch bit for bit."""
+    M, K, H = 5120, 16, 256
+    a, b = _params(K, 1, seed=3), _params(K, 1, seed=4)
+    W1 = torch.cat([a[0], b[0]]).contiguous()
+    b1 = torch.cat([a[1], b[1]]).contiguous()
+    W2 = torch.stack([a[2], b[2]]).contiguous()
+    b2 = torch.stack([a[3], b[3]]).contiguous()
+    W3 = torch.cat([a[4], b[4]]).contiguous()
+    b3 = torch.cat([a[5], b[5]]).contiguous()
+    x = torch.randn(M, K, device="cuda")
+    h1 = torch.empty(M, 2 * H, device="cuda")
+    h2 = torch.empty(M, 2 * H, device="cuda")
+    q = torch.empty(2, M, device="cuda")
+    gs = (ctypes.c_int64 * 9)(0, H * K, H, H * H, H, H, 1, H, M)
+    N.check(N.lib().mh_mlp3_forward(N.ptr(x), M, K, K, N.ptr(W1), N.ptr(b1), N.ptr(W2), N.ptr(b2), N.ptr(W3), N.ptr(b3),
+                                    H, 1, 1, 1, 0, N.ptr(h1), N.ptr(h2), 2 * H, N.ptr(q), 1, 2, gs, N.stream_of()),
+            "grouped")
+    for g, ps in enumerate((a, b)):
+        y, k1, k2 = _run(x, ps, (1, 1, 0))
+        assert torch.equal(q[g], y[:, 0]), g
+        assert torch.equal(h1[:, g * H:(g + 1) * H], k1), g
+        assert torch.equal(h2[:, g * H:(g + 1) * H], k2), g
+
+
+def test_mlp3_rejects_unsupported_shapes():
+    ps = _params(12, 8, seed=0)
+    x = torch.zeros(64, 40, device="cuda")
+    y = torch.empty(64, 8, device="cuda")
+    assert N.lib().mh_mlp3_forward(N.ptr(x), 64, 40, 40, *[N.ptr(t) for t in ps], 256, 8, 1, 1, 0, None, None, 256,
+                                   N.ptr(y), 8, 1, None, N.stream_of()) == -1  # K1 > 32
+    assert N.lib().mh_mlp3_forward(N.ptr(x), 64, 12, 40, *[N.ptr(t) for t in ps], 256, 20, 1, 1, 0, None, None, 256,
+                                   N.ptr(y), 20, 1, None, N.stream_of()) == -1  # N3 = 20
+
+
+@pytest.mark.parametrize("acts", [(nn.ReLU, nn.ReLU, nn.Identity), (nn.Tanh, nn.Tanh, nn.Identity)])
+def test_mlp_module_fused_forward_backward_matches_per_layer(acts):
+    """The MLP module (apprfunc/_fused.py) through MLP3 vs through the per-layer LinearAct launches:
+    outputs within the f32 summation-order bound, every gradient rtol 1e-4 / atol 1e-5 of its scale."""
+    torch.manual_seed(0)
+    mods = [nn.Linear(12, 256), acts[0](), nn.Linear(256, 256), acts[1](), nn.Linear(256, 8), acts[2]()]
+    net = F.MLP(*mods).cuda()
+    x = torch.randn(256, 20, 12, device="cuda", requires_grad=True)
+    g = torch.randn(256, 20, 8, device="cuda")
+    outs = []
+    for on in (True, False):
+        F._MLP3["on"] = on
+        try:
+            net.zero_grad()
+            xx = x.detach().clone().requires_grad_(True)
+            y = net(xx)
+            y.backward(g)
+            outs.append((y.detach(), xx.grad.clone(), [p.grad.clone() for p in net.parameters()]))
+        finally:
+            F._MLP3["on"] = True
+    (ya, gxa, gpa), (yb, gxb, gpb) = outs
+    torch.testing.assert_close(ya, yb, rtol=1e-5, atol=1e-5 * float(yb.abs().max()))
+    for u, v in [(gxa, gxb)] + list(zip(gpa, gpb)):
+        torch.testing.assert_close(u, v, rtol=1e-4, atol=1e-5 * float(v.abs().max()))

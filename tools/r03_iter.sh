@@ -16,4 +16,5 @@ if [ -n "$PROF" ]; then
     python3 bench.py --steps ${BENCH_STEPS:-20} --warmup ${BENCH_WARMUP:-5} --no-cpu-baseline ${BENCH_ARGS} \
     > gpurun_out/prof_bench.log 2>&1; rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
   python3 tools/trace_split.py "$(find gpurun_out/prof -name '*kernel_trace.csv' | head -1)" gpurun_out/trace_split.csv
+  python3 tools/step_timeline.py "$(find gpurun_out/prof -name "*kernel_trace.csv" | head -1)" gpurun_out/step_timeline.txt && head -25 gpurun_out/step_timeline.txt
 fi
