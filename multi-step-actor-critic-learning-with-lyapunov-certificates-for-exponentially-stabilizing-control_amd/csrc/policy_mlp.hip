@@ -974,10 +974,15 @@ static hipError_t launch_fwd_t(const float* P, const float* obs, int64_t E, int 
   const int grid = (int)(want < cus ? want : cus);
   const int mode = policy_mode();
   if (D <= 15 && mode == 2) {  // K = 16 holds the observation and the bias input
-    static int w8 = -1;  // MH_POLICY_WAVES=4: one wave per SIMD with 2 tiles (A/B); default 8
+    // default (round 4): one wave per SIMD with 2 tiles (k_policy_forward_x3<2, 4>, 512 registers,
+    // nothing spilled); MH_POLICY_WAVES=8: two waves per SIMD with 1 tile each, whose 256-register
+    // budget spilled 32 VGPRs to scratch in every phase — the 9x WRITE_SIZE of the logits' bytes
+    // (profiles/r03_pmc_traffic_v4.json) was those spill stores, not the 16-byte logits rows. The
+    // two measured equal at the kernel in round 2 (27.9-28.1 vs 27.9 us, profiles/r02_policy_waves4_ab.jsonl).
+    static int w8 = -1;
     if (w8 < 0) {
       const char* v = getenv("MH_POLICY_WAVES");
-      w8 = (v && atoi(v) == 4) ? 0 : 1;
+      w8 = (v && atoi(v) == 8) ? 1 : 0;
     }
     const int64_t want3 = (tiles + 7) / 8;  // 8 tiles per workgroup either way
     const int grid3 = (int)(want3 < cus ? want3 : cus);

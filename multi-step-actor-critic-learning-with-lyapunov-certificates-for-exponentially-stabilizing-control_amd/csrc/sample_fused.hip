@@ -53,9 +53,38 @@ struct PolicyLds {
   const uint4* w1;      // layer-1 fragments [blk][split][lane] (LDS: no memory loads inside a pass)
   const float* obs;     // [256][D] observations of the workgroup's envs
   float* lgt;           // [256][N3] logits out
-  uint32_t* bar;        // policy-wave barrier counter
+  uint32_t* bar;        // policy-wave barrier counter (MH_FUSED_POLICY_DMA)
   int64_t* err;         // device error word (bounded waits that timed out)
+  uint32_t* landed;     // loader path: chunk c of the horizon is in LDS once landed >= 2 (c + 1)
+  uint32_t* released;   // loader path: chunk c's buffer is free again once released >= 4 (c + 1)
 };
+
+#ifndef MH_FUSED_POLICY_DMA
+// W2 chunks are staged by LOADER waves: in each pass the env waves of the half that is not stepping
+// (they would otherwise wait at the pass's closing barrier) issue the pass's chunk DMAs, wait for
+// them to land and publish each chunk through an LDS counter; the policy waves only wait for that
+// counter and release each buffer after their last read of it. The policy waves' instruction
+// stream then carries no LDS-DMA issue (8 pieces per wave per phase, ~100 cycles each inside an
+// MFMA phase: MI355X_MICROARCH.md, constants) and no drain of their own DMA, and no policy wave
+// waits for the others (each waits only for the data it reads).
+#define MH_FUSED_LOADERS 1
+#endif
+#ifdef MH_FUSED_LOADERS
+constexpr bool kLoaders = true;
+#else
+constexpr bool kLoaders = false;
+#endif
+
+// bounded LDS-counter wait (the same bound and error word as pol_sync)
+__device__ __forceinline__ void wait_count(uint32_t* ctr, uint32_t target, int64_t* err, uint32_t limit) {
+  uint32_t spins = 0;
+  while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+    if (++spins >= limit) {
+      if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(err, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+}
 
 // 16-byte LDS-DMA (global_load_lds_dwordx4: this lane's 16 bytes at gsrc -> LDS lds_dst + 16 lane) as
 // inline asm, M0 written in the same statement (cdna_hip_programming.md's recipe). Not the builtin:
@@ -65,7 +94,9 @@ struct PolicyLds {
 // phase's first W1 register load waited for the chunk DMA just issued. The asm DMA is invisible
 // to that bookkeeping: its completion is counted explicitly (pol_sync's vmcnt(0)).
 __device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
-  const uint32_t l = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)lds_dst);
+  // the destination is wave-uniform at every call site: pinned to an SGPR (M0's source)
+  const uint32_t l = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) void*)lds_dst));
   uint32_t keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
@@ -114,9 +145,12 @@ __device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_
 // One pass: the 32-env tile `row0 .. row0 + 31` (workgroup-local rows) of policy wave pw through
 // all three layers; k_policy_forward_x3<1, 8>'s per-tile sequence with the observation rows and
 // the logits in LDS. `next`: stage chunk 0 of the following pass during the last phase.
-template <int D>
+// LOAD: the W2 chunks are staged by loader waves (wait for `landed`, release each buffer); else
+// the four policy waves stage them themselves (pol_sync). D = 0: the observation width is Drt.
+template <int D, bool LOAD = kLoaders>
 __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int row0, bool next, uint32_t& target,
-                            int pass_no = 0) {
+                            int pass_no = 0, int Drt = 0) {
+  const int DD = D > 0 ? D : Drt;
   MH_STAMP(a, pass_no, 0);
   (void)pass_no;
 #ifdef MH_FUSED_EXP_NO_POLICY  // cost-attribution experiment only: no policy work (the barriers stay)
@@ -173,7 +207,7 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int k = 8 * (lane >> 5) + j;
-      x[j] = k < D ? L.obs[row * D + k] : (k == D ? 1.0f : 0.0f);
+      x[j] = k < DD ? L.obs[row * DD + k] : (k == DD ? 1.0f : 0.0f);
       m = fmaxf(m, fabsf(x[j]));
     }
     m = fmaxf(m, __shfl_xor(m, 32));
@@ -210,7 +244,12 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
     const bool has_next = ib < PM_NB - 1 || next;
     const int nib = (ib + 1) & (PM_NB - 1);
     MH_STAMP(a, pass_no, 1 + 2 * ib);
-    pol_sync(L.bar, target, L.err, a.spin_limit);  // chunk ib landed in every policy wave's share
+    if constexpr (LOAD) {
+      // chunk c = 8 pass + ib of the horizon: staged and published by the pass's loader waves
+      wait_count(L.landed, 2u * (uint32_t)(PM_NB * pass_no + ib + 1), L.err, a.spin_limit);
+    } else {
+      pol_sync(L.bar, target, L.err, a.spin_limit);  // chunk ib landed in every policy wave's share
+    }
     MH_STAMP(a, pass_no, 2 + 2 * ib);
     const bool pipe = !fold;
     f32x16 hn;
@@ -284,7 +323,9 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
       if (pipe && st == 0) hn = l1_mfma(w1c, xoh, xol);
       // the next chunk's DMA into the other buffer (every policy wave finished reading it in the
       // previous phase: the pol_sync above), issued after this phase's first W1 use
-      if (st == 0 && has_next) stage(nib, nxt_lds);
+      if constexpr (!LOAD) {
+        if (st == 0 && has_next) stage(nib, nxt_lds);
+      }
       if (pipe && st == 0) {
         if (ib + 2 < PM_NB) {
           w1c[0] = L.w1[((ib + 2) * 2 + 0) * 64 + lane];
@@ -328,6 +369,11 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
 #else
       __builtin_amdgcn_sched_barrier(0);
 #endif
+    }
+    if constexpr (LOAD) {
+      // every fragment of this chunk is in registers (step 15's MFMAs consumed the last reads): the
+      // buffer may be overwritten by the loaders
+      if (lane == 0) __hip_atomic_fetch_add(L.released, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (fold) {
       fold_half(PM_NB - 1, 0);
@@ -561,6 +607,32 @@ __device__ __forceinline__ void env_lockstep(const FusedArgs& a, EnvLane<Env>& v
   // barrier; within this wave the reads above complete before its next writes (in order)
 }
 
+// ------------------------------------------------------------------ loader waves
+#ifdef MH_FUSED_LOADERS
+// Loader wave l (0, 1) of pass p: stages chunks 8 p + 1 .. 8 p + 7 of the horizon and chunk 0 of
+// the next pass (chunk 8 p + 8), each into buffer c & 1 once the policy waves released the chunk
+// two before it, its half of the 32 pieces, then publishes it. Returns after the last chunk
+// landed, so nothing is in flight across the pass's closing barrier.
+__device__ void load_pass(const FusedArgs& a, const PolicyLds& L, int p, int npass, int l) {
+  constexpr int HALF = PM_X3_FRAGS / 2;  // pieces (1 KB each) per loader wave per chunk
+  const int lane = threadIdx.x & 63;
+  const uint4* W2g = reinterpret_cast<const uint4*>(a.P + pm_off_w2x3(a.K1));
+  const int last = p + 1 < npass ? PM_NB : PM_NB - 1;
+  for (int i = 1; i <= last; ++i) {
+    const uint32_t c = (uint32_t)(PM_NB * p + i);
+    wait_count(L.released, c >= 2 ? 4u * (c - 1) : 0u, L.err, a.spin_limit);  // chunk c - 2's buffer free
+    const int ib = i & (PM_NB - 1);
+    uint4* dst = (c & 1) ? L.c1 : L.c0;
+    const uint4* src = W2g + ((int64_t)ib * PM_X3_FRAGS + l * HALF) * 64;
+    asm volatile("" : "+s"(src));
+#pragma unroll
+    for (int f = 0; f < HALF; ++f) glds16(src + f * 64 + lane, &dst[(l * HALF + f) * 64]);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's pieces are in LDS
+    if (lane == 0) __hip_atomic_fetch_add(L.landed, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+#endif
+
 // ------------------------------------------------------------------ the kernel
 template <class Env>
 __global__ __launch_bounds__(FUSED_THREADS) __attribute__((amdgpu_waves_per_eu(2, 2)))
@@ -583,6 +655,7 @@ void k_sample_fused(FusedArgs a) {
 #endif
   __shared__ int s_spos[2][64];
   __shared__ uint32_t s_bar;
+  __shared__ uint32_t s_landed, s_released;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int64_t E = a.E;
@@ -602,7 +675,11 @@ void k_sample_fused(FusedArgs a) {
     const int64_t g = base * D + i;
     s_obs[i] = g < E * D ? a.obs[g] : 0.0f;
   }
-  if (threadIdx.x == 0) s_bar = 0u;
+  if (threadIdx.x == 0) {
+    s_bar = 0u;
+    s_landed = 2u;  // chunk 0 of the first pass: staged by the prologue below (both "loader" halves)
+    s_released = 0u;
+  }
   const bool pol = w < 4;
   if (pol) {
     const uint4* w3g = reinterpret_cast<const uint4*>(a.P + pm_off_w3x3(a.K1));
@@ -635,7 +712,7 @@ void k_sample_fused(FusedArgs a) {
 
   if (pol) {
     // ================= policy waves: 2H passes (H1 first, then H0 / H1 alternating)
-    PolicyLds L{lds0, lds1, lds_w3, lds_b2, lds_b3, lds_w1, s_obs, s_lgt, &s_bar, a.err};
+    PolicyLds L{lds0, lds1, lds_w3, lds_b2, lds_b3, lds_w1, s_obs, s_lgt, &s_bar, a.err, &s_landed, &s_released};
     uint32_t target = 0;
     const int total = 2 * H;
     int pass = 0;
@@ -663,6 +740,9 @@ void k_sample_fused(FusedArgs a) {
     __builtin_amdgcn_s_waitcnt(0x0F70);
   } else {
 #ifdef MH_FUSED_EXP_NO_ENV  // cost-attribution experiment only
+#ifdef MH_FUSED_LOADERS
+#error "MH_FUSED_EXP_NO_ENV removes the loader waves: build it with MH_FUSED_POLICY_DMA"
+#endif
     if (false)
 #endif
     {
@@ -688,6 +768,10 @@ void k_sample_fused(FusedArgs a) {
     }
     const int NW = (int)((E + 63) / 64);
     const int gw = (int)(e / 64);
+#ifdef MH_FUSED_LOADERS
+    const PolicyLds LL{lds0, lds1, lds_w3, lds_b2, lds_b3, lds_w1, s_obs, s_lgt, &s_bar, a.err, &s_landed, &s_released};
+    const int npass = 2 * H;
+#endif
     float4* stage = s_stage[ew & 1];
     int* spos = s_spos[ew & 1];
     auto step = [&](int t) {
@@ -727,13 +811,23 @@ void k_sample_fused(FusedArgs a) {
             lane | (emit_pos << 6);
       }
     };
+#ifdef MH_FUSED_LOADERS
+    if (half == 0) load_pass(a, LL, 0, npass, ew & 1);  // the policy's first pass (H1): H0's waves load
+#endif
     __syncthreads();  // the policy's first pass (H1)
-    // phases A(t) (half H1 steps) and B(t) (half H0 steps), one call site for the step's body
+    // phases A(t) (half H1 steps) and B(t) (half H0 steps), one call site for the step's body; the
+    // other half's waves stage the pass's W2 chunks (phase ph runs policy pass ph + 1)
     for (int ph = 0; ph < 2 * H; ++ph) {
 #ifdef MH_FUSED_EXP_SERIAL  // experiment: env steps never overlap a policy pass
       __syncthreads();
 #endif
-      if ((ph & 1) == (half ^ 1)) step(ph >> 1);
+      if ((ph & 1) == (half ^ 1)) {
+        step(ph >> 1);
+      } else {
+#ifdef MH_FUSED_LOADERS
+        if (ph + 1 < npass) load_pass(a, LL, ph + 1, npass, ew & 1);
+#endif
+      }
       __syncthreads();
     }
     if (MH_FUSED_STATE_IN_REGS && live) {

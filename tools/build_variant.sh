@@ -6,7 +6,7 @@ ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 SRC="$ROOT/multi-step-actor-critic-learning-with-lyapunov-certificates-for-exponentially-stabilizing-control_amd/csrc"
 OUT="$ROOT/exp_libs/$1"
 mkdir -p "$OUT/obj"
-for f in rollout sample_fused capi msacl_kernels per gae policy_mlp mlp_grad optim dist_kernels gemm; do
+for f in rollout sample_fused capi msacl_kernels per gae policy_mlp mlp_grad optim dist_kernels gemm mlp_fused; do
   extra=""; [ "$f" = sample_fused ] && extra="-fno-slp-vectorize"  # as the Makefile
   /opt/rocm/bin/hipcc $extra -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -Wno-unused-function \
     -I"$ROOT/include" -I"$SRC" $2 -c "$SRC/$f.hip" -o "$OUT/obj/$f.o" &
