@@ -417,6 +417,20 @@ int mh_mlp3_forward(const float* x, int64_t rows, int32_t k1, int64_t ldx, const
                     int32_t act1, int32_t act2, int32_t act3, float* h1, float* h2, int64_t ldh, float* y, int64_t ldy,
                     int32_t groups, const int64_t* group_strides, void* stream);
 
+/* The input-gradient chain of mh_mlp3_forward's network (its autograd backward, identity output
+ * activation) in ONE launch: with dy [rows][ldy] the gradient of y,
+ *   g2 = (dy W3) * act2'(h2),  g1 = (g2 W2) * act1'(h1),  dx = g1 W1
+ * (act' read from the kept activations h1 / h2 [rows][ldh], as autograd's threshold / tanh
+ * backward). g2 / g1 [rows][ldg] (the weight gradients' left operands: dW2 = g2^T h1, db2 = column
+ * sums of g2, ...) and dx [rows][ldx] are written when non-NULL. groups > 1: `groups` networks of
+ * one shape (the twin critics), group q's operands at + q x group_strides[i] floats, host array
+ * {dy, h (h1 and h2), W1, W2, W3, g (g1 and g2)}; dx is the SUM of the groups' input gradients (what
+ * autograd accumulates for an input both critics read). Shapes as mh_mlp3_forward. */
+int mh_mlp3_backward(const float* dy, int64_t ldy, const float* h1, const float* h2, int64_t ldh, const float* W1,
+                     const float* W2, const float* W3, int64_t rows, int32_t k1, int32_t hidden, int32_t n_out,
+                     int32_t act1, int32_t act2, float* g2, float* g1, int64_t ldg, float* dx, int64_t ldx,
+                     int32_t groups, const int64_t* group_strides, void* stream);
+
 /* StochaPolicy's head (RL/apprfunc/mlp.py:132-136) on [rows][2 act_dim] rows:
  *   out = [mean | exp(clamp(log_std, min_log_std, max_log_std))] of raw = [mean | log_std]
  * and its backward d_raw = [d_mean | d_std * std * (min <= log_std <= max)], one launch each

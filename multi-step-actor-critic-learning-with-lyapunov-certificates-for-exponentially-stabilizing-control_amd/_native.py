@@ -137,6 +137,8 @@ _PROTOS = {
                                  + [c_vp] * 5),
     "mh_mlp3_forward": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i64] + [c_vp] * 6 + [c_i32] * 5
                         + [c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "mh_mlp3_backward": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64] + [c_i32] * 5
+                         + [c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mh_stocha_head": (ctypes.c_int, [c_vp, c_i64, c_i32, c_f32, c_f32, c_vp, c_vp]),
     "mh_stocha_head_backward": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_f32, c_vp, c_vp]),
     "mh_tanh_gauss_rsample": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_i32, c_vp, c_vp, c_vp]),

@@ -324,6 +324,17 @@ class MLP3(torch.autograd.Function):
         nx, nW1, nb1, nW2, nb2, nW3, nb3 = ctx.needs_input_grad[:7]
         a1, a2, a3 = ctx.acts
         need_h2 = nx or nW1 or nb1 or nW2 or nb2
+        if nx and not (nW1 or nb1 or nW2 or nb2 or nW3 or nb3) and a3 == 0:
+            # input gradient only (a frozen network): the whole chain in one mh_mlp3_backward launch
+            N = _native()
+            M, K1 = x.shape
+            dx = torch.empty(M, K1, dtype=torch.float32, device=x.device)
+            dyc = dy.contiguous()
+            N.check(N.lib().mh_mlp3_backward(N.ptr(dyc), dyc.shape[1], N.ptr(h1), N.ptr(h2), h1.shape[1], N.ptr(W1),
+                                             N.ptr(W2), N.ptr(W3), M, K1, W2.shape[0], W3.shape[0], a1, a2, None,
+                                             None, W2.shape[0], N.ptr(dx), K1, 1, None, N.stream_of(x.device)),
+                    "mh_mlp3_backward")
+            return dx, None, None, None, None, None, None, None
         dh2, dW3, db3 = layer_backward(dy, h2, W3, y, a3, need_h2, nW3, nb3)
         dx = dW1 = db1 = dW2 = db2 = None
         if need_h2:

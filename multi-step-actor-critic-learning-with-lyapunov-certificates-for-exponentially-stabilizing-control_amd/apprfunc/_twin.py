@@ -201,9 +201,20 @@ class TwinCritic:
         self._grads()
 
     def input_grad(self, dq, h1, h2):
-        """d/dx of sum_q <dq[q], q-critic(x)> (frozen critics): [rows][K]."""
+        """d/dx of sum_q <dq[q], q-critic(x)> (frozen critics): [rows][K]. One mh_mlp3_backward
+        launch for both critics' whole input-gradient chain (the sum of the two input gradients
+        formed in registers), or the per-layer launches with MSACL_MLP3=0."""
         N = _native()
         M = h1.shape[0]
+        from ._fused import _MLP3
+        if _MLP3["on"] and self.H == 256:
+            H, K = self.H, self.K
+            dx = torch.empty(M, K, dtype=torch.float32, device=h1.device)
+            gs = (ctypes.c_int64 * 6)(M, H, H * K, H * H, H, 0)
+            N.check(N.lib().mh_mlp3_backward(N.ptr(dq), 1, N.ptr(h1), N.ptr(h2), 2 * H, N.ptr(self.W1), N.ptr(self.W2),
+                                             N.ptr(self.W3), M, K, H, 1, 1, 1, None, None, H, N.ptr(dx), K, 2, gs,
+                                             N.stream_of(h1.device)), "mh_mlp3_backward (twin input gradient)")
+            return dx
         dh1 = self._back_l23(dq, h1, h2, False)
         dx = torch.empty(M, self.K, dtype=torch.float32, device=h1.device)
         N.check(N.lib().mh_dx_narrow(N.ptr(dh1), N.ptr(h1), 1, N.ptr(self.W1), M, 2 * self.H, self.K, N.ptr(dx),

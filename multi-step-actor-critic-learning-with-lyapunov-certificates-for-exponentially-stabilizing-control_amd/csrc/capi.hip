@@ -1010,6 +1010,39 @@ int mh_mlp3_forward(const float* x, int64_t rows, int32_t k1, int64_t ldx, const
   return MH_OK;
 }
 
+int mh_mlp3_backward(const float* dy, int64_t ldy, const float* h1, const float* h2, int64_t ldh, const float* W1,
+                     const float* W2, const float* W3, int64_t rows, int32_t k1, int32_t hidden, int32_t n_out,
+                     int32_t act1, int32_t act2, float* g2, float* g1, int64_t ldg, float* dx, int64_t ldx,
+                     int32_t groups, const int64_t* group_strides, void* stream) {
+  if (rows < 0 || groups < 0) return fail(MH_EINVAL, "mh_mlp3_backward: bad size");
+  if (rows == 0 || groups == 0) return MH_OK;
+  if (!mh::mlp3_supported(rows, k1, hidden, n_out))
+    return fail(MH_EINVAL, "mh_mlp3_backward: shape not supported (k1 <= 32, hidden 256, n_out <= 16 or a multiple of 64 <= 256)");
+  if (act1 < 0 || act1 > 2 || act2 < 0 || act2 > 2) return fail(MH_EINVAL, "mh_mlp3_backward: act must be 0, 1 or 2");
+  if (!dy || !h1 || !h2 || !W1 || !W2 || !W3) return fail(MH_EINVAL, "mh_mlp3_backward: null operand");
+  if (ldy < n_out || ldh < hidden || ((g1 || g2) && ldg < hidden) || (dx && ldx < k1))
+    return fail(MH_EINVAL, "mh_mlp3_backward: leading dimension smaller than the matrix");
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!al16(g1) || !al16(g2) || ((g1 || g2) && (ldg & 3)))
+    return fail(MH_EINVAL, "mh_mlp3_backward: g1 / g2 must be 16-byte aligned (ldg a multiple of 4)");
+  if (groups > 1 && !group_strides) return fail(MH_EINVAL, "mh_mlp3_backward: grouped launch needs group_strides");
+  mh::Mlp3BwdArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.dy = dy; a.ldy = ldy; a.h1 = h1; a.h2 = h2; a.ldh = ldh;
+  a.W1 = W1; a.W2 = W2; a.W3 = W3; a.M = rows; a.K1 = k1; a.H = hidden; a.N3 = n_out;
+  a.act1 = act1; a.act2 = act2; a.groups = groups;
+  a.g2 = g2; a.g1 = g1; a.ldg = ldg; a.dx = dx; a.ldx = ldx;
+  if (groups > 1) {
+    const int64_t* g = group_strides;
+    for (int i = 0; i < 6; ++i)
+      if (g[i] < 0) return fail(MH_EINVAL, "mh_mlp3_backward: negative group stride");
+    if (g[5] & 3) return fail(MH_EINVAL, "mh_mlp3_backward: the g group stride must keep 16-byte alignment");
+    a.gs_dy = g[0]; a.gs_h = g[1]; a.gs_W1 = g[2]; a.gs_W2 = g[3]; a.gs_W3 = g[4]; a.gs_g = g[5];
+  }
+  MH_HIP(mh::launch_mlp3_backward(a, (hipStream_t)stream));
+  return MH_OK;
+}
+
 int mh_linear_backward_grouped(const float* dy, const float* y, int32_t act, const float* x, const float* W,
                                int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy, int64_t ld_x, int64_t ld_dx,
                                int32_t groups, int64_t stride_dy, int64_t stride_x, int64_t stride_w,

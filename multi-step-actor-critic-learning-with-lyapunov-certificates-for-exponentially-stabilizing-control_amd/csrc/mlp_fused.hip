@@ -228,10 +228,178 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
   }
 }
 
+// ------------------------------------------------------------------ backward: the input-gradient chain
+// The contraction of a backward product runs over the weight's OUTPUT index (dh = g W, W [N][K]):
+// in MFMA t of group u, lane group g contracts weight row 16 u + 4 g + t, so each lane's four B
+// values lie in four rows (scalar loads, 64 consecutive bytes per 16 lanes). Rows past `nrows` read 0.
+// (the weight rows are HID floats long; rows at or past `nrows` lie beyond the buffer resource)
+__device__ __forceinline__ void layer_cols_t(const float* in, int sin, __amdgpu_buffer_rsrc_t wr, int nrows, int n0,
+                                             int lane, f32x4 (&acc)[4]) {
+  const int c = lane & 15, g = lane >> 4;
+  const int G = (nrows + 15) / 16;
+  const int voff = ((4 * g) * HID + n0 + c) * 4;  // + (t HID + 16 j) 4: immediate offsets
+  float wb[PF][4][4];
+  auto load = [&](int u, float (*dst)[4]) {
+    const int soff = __builtin_amdgcn_readfirstlane(u * 16 * HID * 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        dst[j][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, voff + (t * HID + 16 * j) * 4,
+                                                                                 soff, 0));
+  };
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+    if (p < G) load(p, wb[p]);
+#pragma unroll 1
+  for (int u0 = 0; u0 < G; u0 += PF) {
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      const int u = u0 + p;
+      if (u < G) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(in + c * sin + 16 * u + 4 * g);
+        float b[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) b[j][t] = wb[p][j][t];
+        if (u + PF < G) load(u + PF, wb[p]);
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[j][t], acc[j], 0, 0, 0);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ float act_grad_f(float d, float t, int act) {  // gemm.hip act_grad
+  if (act == 1) return t > 0.0f ? d : 0.0f;
+  if (act == 2) return d * (1.0f - t * t);
+  return d;
+}
+
+// dh = acc (this wave's 64 columns) -> g = dh * act'(h) (h [rows][ldh] global) into the LDS tile
+// `out` and, when gdst is set, to global rows (ldg)
+__device__ __forceinline__ void grad_epilogue(const f32x4 (&acc)[4], const float* h, int64_t ldh, int act, int n0,
+                                              int lane, int64_t m0, int64_t M, float* out) {
+  const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + 16 * j + c;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t row = m0 + 4 * g + q;
+      const float t = row < M ? h[row * ldh + n] : 0.0f;
+      out[(4 * g + q) * SH + n] = row < M ? act_grad_f(acc[j][q], t, act) : 0.0f;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mlp3_bwd(Mlp3BwdArgs a) {
+  __shared__ float gs3[TM * SH];  // the output gradient tile (N3 <= 256 columns)
+  __shared__ float gs2[TM * SH];
+  __shared__ float gs1[TM * SH];
+  __shared__ f32x4 red[4][2][64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t m0 = (int64_t)blockIdx.x * TM;
+  const int N3 = a.N3, K1 = a.K1, n0 = wave * 64;
+  const int N3p = (N3 + 15) & ~15;
+  f32x4 dxa[2] = {};
+  for (int q = 0; q < a.groups; ++q) {
+    const float* dy = a.dy + q * a.gs_dy;
+    const float* h1 = a.h1 + q * a.gs_h;
+    const float* h2 = a.h2 + q * a.gs_h;
+    const float* W1 = a.W1 + q * a.gs_W1;
+    const float* W2 = a.W2 + q * a.gs_W2;
+    const float* W3 = a.W3 + q * a.gs_W3;
+    if (q > 0) __syncthreads();  // the previous group's tiles are read
+    for (int i = tid; i < TM * N3p; i += 256) {
+      const int rr = i / N3p, k = i - rr * N3p;
+      gs3[rr * SH + k] = (m0 + rr < a.M && k < N3) ? dy[(m0 + rr) * a.ldy + k] : 0.0f;
+    }
+    __syncthreads();
+    // dh2 = g3 W3 (contraction over W3's N3 rows), g2 = dh2 * act2'(h2)
+    {
+      const __amdgpu_buffer_rsrc_t wr =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(W3), (short)0, N3 * HID * 4, 0x00020000);
+      f32x4 acc[4] = {};
+      layer_cols_t(gs3, SH, wr, N3, n0, lane, acc);
+      grad_epilogue(acc, h2, a.ldh, a.act2, n0, lane, m0, a.M, gs2);
+    }
+    __syncthreads();
+    if (a.g2) store_tile(gs2, a.g2 + q * a.gs_g, a.ldg, m0, a.M, HID);
+    // dh1 = g2 W2, g1 = dh1 * act1'(h1)
+    {
+      const __amdgpu_buffer_rsrc_t wr =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(W2), (short)0, HID * HID * 4, 0x00020000);
+      f32x4 acc[4] = {};
+      layer_cols_t(gs2, SH, wr, HID, n0, lane, acc);
+      grad_epilogue(acc, h1, a.ldh, a.act1, n0, lane, m0, a.M, gs1);
+    }
+    __syncthreads();
+    if (a.g1) store_tile(gs1, a.g1 + q * a.gs_g, a.ldg, m0, a.M, HID);
+    // dx += g1 W1 (W1 [H][K1]: contraction over its H rows, wave w rows [64 w, 64 w + 64); two
+    // 16-column blocks of K1 <= 32)
+    if (a.dx) {
+      const int c = lane & 15, g = lane >> 4;
+      const __amdgpu_buffer_rsrc_t wr =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(W1), (short)0, HID * K1 * 4, 0x00020000);
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu) {
+        const int u = wave * 4 + uu;
+        const f32x4 av = *reinterpret_cast<const f32x4*>(gs1 + c * SH + 16 * u + 4 * g);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          float bv[4];
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int k = 16 * u + 4 * g + t, col = 16 * cb + c;
+            bv[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                  wr, col < K1 ? (k * K1 + col) * 4 : 0x7ffffff0, 0, 0));
+          }
+#pragma unroll
+          for (int t = 0; t < 4; ++t) dxa[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bv[t], dxa[cb], 0, 0, 0);
+        }
+      }
+    }
+  }
+  if (a.dx) {  // the four waves' partials (rows of W1 they contracted) added in wave order
+    red[wave][0][lane] = dxa[0];
+    red[wave][1][lane] = dxa[1];
+    __syncthreads();
+    if (wave == 0) {
+      const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        f32x4 s = red[0][cb][lane];
+#pragma unroll
+        for (int w = 1; w < 4; ++w) s = s + red[w][cb][lane];
+        const int col = 16 * cb + c;
+        if (col < K1) {
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const int64_t row = m0 + 4 * g + qq;
+            if (row < a.M) a.dx[row * a.ldx + col] = s[qq];
+          }
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
 
 bool mlp3_supported(int64_t M, int K1, int H, int N3) {
   return M > 0 && K1 >= 1 && K1 <= K1P && H == HID && N3 >= 1 && (N3 <= 16 || (N3 % 64 == 0 && N3 <= 256));
+}
+
+hipError_t launch_mlp3_backward(const Mlp3BwdArgs& a, hipStream_t st) {
+  if (!mlp3_supported(a.M, a.K1, a.H, a.N3) || a.groups < 1) return hipErrorInvalidValue;
+  const int64_t tiles = (a.M + TM - 1) / TM;
+  k_mlp3_bwd<<<(unsigned)tiles, 256, 0, st>>>(a);
+  return hipGetLastError();
 }
 
 hipError_t launch_mlp3_forward(const Mlp3Args& a, int groups, hipStream_t st) {

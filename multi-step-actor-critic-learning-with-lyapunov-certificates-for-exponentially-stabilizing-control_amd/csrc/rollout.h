@@ -189,6 +189,24 @@ struct Mlp3Args {
   int64_t ldh, ldy;
   int64_t gs_x, gs_W1, gs_b1, gs_W2, gs_b2, gs_W3, gs_b3, gs_h, gs_y;
 };
+// the fused 3-layer MLP input-gradient chain (mlp_fused.hip): g2 = (dy W3) * act2'(h2),
+// g1 = (g2 W2) * act1'(h1), dx = sum over groups of g1 W1 (dy is the gradient of the identity-
+// activated output)
+struct Mlp3BwdArgs {
+  const float* dy;
+  int64_t ldy, gs_dy;
+  const float *h1, *h2;
+  int64_t ldh, gs_h;
+  const float *W1, *W2, *W3;
+  int64_t gs_W1, gs_W2, gs_W3;
+  int64_t M;
+  int K1, H, N3, act1, act2, groups;
+  float *g2, *g1;  // optional
+  int64_t ldg, gs_g;
+  float* dx;       // optional [M][ldx]
+  int64_t ldx;
+};
+hipError_t launch_mlp3_backward(const Mlp3BwdArgs& a, hipStream_t st);
 bool mlp3_supported(int64_t M, int K1, int H, int N3);
 hipError_t launch_mlp3_forward(const Mlp3Args& a, int groups, hipStream_t st);
 hipError_t launch_polyak_multi(const PolyakList& L, double polyak, hipStream_t st);

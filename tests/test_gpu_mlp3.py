@@ -133,3 +133,60 @@ def test_mlp_module_fused_forward_backward_matches_per_layer(acts):
     torch.testing.assert_close(ya, yb, rtol=1e-5, atol=1e-5 * float(yb.abs().max()))
     for u, v in [(gxa, gxb)] + list(zip(gpa, gpb)):
         torch.testing.assert_close(u, v, rtol=1e-4, atol=1e-5 * float(v.abs().max()))
+
+
+@pytest.mark.parametrize("K1,N3,acts", [(12, 8, (1, 1)), (16, 1, (1, 1)), (12, 256, (2, 2)), (20, 16, (2, 1)),
+                                        (5, 64, (1, 2))])
+def test_mlp3_backward_chain_matches_float64(K1, N3, acts):
+    """mh_mlp3_backward: g2 = (dy W3) act2'(h2), g1 = (g2 W2) act1'(h1), dx = g1 W1, each checked on
+    the kernel's own previous gradient against float64 (the forward's bound)."""
+    M = 3000
+    ps = _params(K1, N3, seed=K1 * N3)
+    W1, b1, W2, b2, W3, b3 = ps
+    x = torch.randn(M, K1, device="cuda")
+    y, h1, h2 = _run(x, ps, acts + (0,))
+    dy = torch.randn(M, N3, device="cuda")
+    g2 = torch.empty(M, 256, device="cuda")
+    g1 = torch.empty(M, 256, device="cuda")
+    dx = torch.empty(M, K1, device="cuda")
+    N.check(N.lib().mh_mlp3_backward(N.ptr(dy), N3, N.ptr(h1), N.ptr(h2), 256, N.ptr(W1), N.ptr(W2), N.ptr(W3), M,
+                                     K1, 256, N3, acts[0], acts[1], N.ptr(g2), N.ptr(g1), 256, N.ptr(dx), K1, 1, None,
+                                     N.stream_of()), "mh_mlp3_backward")
+    torch.cuda.synchronize()
+    D = lambda t: t.double().cpu().numpy()  # noqa: E731
+    dact = {1: lambda h: (h > 0).astype(np.float64), 2: lambda h: 1.0 - h * h}
+
+    def check(out, g, W, h, act, what):
+        lin = D(g) @ D(W)
+        mag = np.abs(D(g)) @ np.abs(D(W))
+        ref = lin * (dact[act](D(h)) if act else 1.0)
+        tol = (2e-6 * (g.shape[1] ** 0.5) * mag + 1e-6) * (np.abs(dact[act](D(h))) if act else 1.0) + 1e-7
+        err = np.abs(D(out) - ref)
+        assert np.all(err <= tol), f"{what}: max err {err.max():.3e}, worst ratio {(err / tol).max():.3f}"
+
+    check(g2, dy, W3, h2, acts[1], "g2")
+    check(g1, g2, W2, h1, acts[0], "g1")
+    check(dx, g1, W1, None, 0, "dx")
+
+
+def test_twin_input_grad_chain_equals_per_layer():
+    """TwinCritic.input_grad through mh_mlp3_backward (both critics, the input gradients summed in
+    one launch) vs the per-layer launches: equal to the f32 summation-order bound."""
+    from msacl_amd.apprfunc._twin import TwinCritic
+    from msacl_amd.apprfunc.mlp import ActionValue
+    torch.manual_seed(1)
+    kw = dict(obs_dim=12, act_dim=4, hidden_sizes=[256, 256], hidden_activation="relu", output_activation="linear")
+    q1, q2 = ActionValue(**kw).cuda(), ActionValue(**kw).cuda()
+    tc = TwinCritic.build(q1, q2)
+    M = 5120
+    x = torch.randn(M, 16, device="cuda")
+    q, h1, h2 = tc.forward(x)
+    dq = torch.randn(2, M, device="cuda")
+    outs = []
+    for on in (True, False):
+        F._MLP3["on"] = on
+        try:
+            outs.append(tc.input_grad(dq, h1, h2))
+        finally:
+            F._MLP3["on"] = True
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-5 * float(outs[1].abs().max()))

@@ -65,7 +65,8 @@ def _worker(env_name, n_envs, seconds, threads, seed, start_evt, q):
 
 
 def host_topology():
-    info = {"nproc": os.cpu_count()}
+    info = {"nproc": os.cpu_count(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "max_jobs": os.environ.get("MAX_JOBS")}
     try:
         info["affinity"] = len(os.sched_getaffinity(0))
     except AttributeError:
