@@ -431,6 +431,27 @@ int mh_mlp3_backward(const float* dy, int64_t ldy, const float* h1, const float*
                      int32_t act1, int32_t act2, float* g2, float* g1, int64_t ldg, float* dx, int64_t ldx,
                      int32_t groups, const int64_t* group_strides, void* stream);
 
+/* Several weight gradients of one backward (the three layers of an MLP, both twin critics') in two
+ * launches: for each product, dw [n_out][n_in] = g^T x over `rows` and, when db is non-NULL,
+ * db [n_out] = the column sums of g, with g [rows][ld_g] the layer's pre-activation gradient (as
+ * mh_mlp3_backward writes it) and x [rows][ld_x] the layer's input. Every product is split over the
+ * rows into partials that one reduce launch adds in split order (deterministic). Supported: rows >=
+ * 1024, 16-byte aligned g / x with ld_g, ld_x multiples of 4, and either n_out % 64 == 0 and
+ * n_in % 4 == 0, or a narrow layer n_out < 64, n_out % 4 == 0, n_in % 64 == 0, ld_g == n_out; at most
+ * 6 products. Replaces the per-layer weight-gradient GEMMs + bias reductions of autograd
+ * (RL/apprfunc/mlp.py:18-30 layers). workspace: mh_weight_grads_workspace floats. */
+typedef struct {
+  const float* g;
+  int64_t ld_g;
+  const float* x;
+  int64_t ld_x;
+  int64_t n_out, n_in;
+  float* dw;
+  float* db;
+} mh_wgrad_t;
+int mh_weight_grads_workspace(const mh_wgrad_t* products, int32_t n, int64_t rows, int64_t* floats_out);
+int mh_weight_grads(const mh_wgrad_t* products, int32_t n, int64_t rows, float* workspace, void* stream);
+
 /* StochaPolicy's head (RL/apprfunc/mlp.py:132-136) on [rows][2 act_dim] rows:
  *   out = [mean | exp(clamp(log_std, min_log_std, max_log_std))] of raw = [mean | log_std]
  * and its backward d_raw = [d_mean | d_std * std * (min <= log_std <= max)], one launch each

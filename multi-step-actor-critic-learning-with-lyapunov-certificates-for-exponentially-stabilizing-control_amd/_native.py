@@ -49,6 +49,12 @@ class PolyakTensor(ctypes.Structure):
     _fields_ = [("target", ctypes.c_void_p), ("source", ctypes.c_void_p), ("numel", ctypes.c_int64)]
 
 
+class Wgrad(ctypes.Structure):
+    """mh_wgrad_t (include/msacl_hip.h)."""
+    _fields_ = [("g", ctypes.c_void_p), ("ld_g", ctypes.c_int64), ("x", ctypes.c_void_p), ("ld_x", ctypes.c_int64),
+                ("n_out", ctypes.c_int64), ("n_in", ctypes.c_int64), ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p)]
+
+
 class TrajStore(ctypes.Structure):
     _fields_ = [
         ("obs", c_vp), ("act", c_vp), ("rew", c_vp), ("cost", c_vp), ("obs2", c_vp), ("done", c_vp),
@@ -139,6 +145,8 @@ _PROTOS = {
                         + [c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mh_mlp3_backward": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64] + [c_i32] * 5
                          + [c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "mh_weight_grads_workspace": (ctypes.c_int, [c_vp, c_i32, c_i64, ctypes.POINTER(c_i64)]),
+    "mh_weight_grads": (ctypes.c_int, [c_vp, c_i32, c_i64, c_vp, c_vp]),
     "mh_stocha_head": (ctypes.c_int, [c_vp, c_i64, c_i32, c_f32, c_f32, c_vp, c_vp]),
     "mh_stocha_head_backward": (ctypes.c_int, [c_vp, c_vp, c_vp, c_i64, c_i32, c_f32, c_f32, c_vp, c_vp]),
     "mh_tanh_gauss_rsample": (ctypes.c_int, [c_vp] * 4 + [c_i64, c_i32, c_vp, c_vp, c_vp]),

@@ -304,6 +304,35 @@ def mlp3_forward(x, layers, acts, h_keep, groups=1, strides=None, ldh=None, y=No
     return y, h1, h2
 
 
+_WG_WS = {}
+
+
+def wgrad_ok(g, ld_g, x, ld_x, n_out, n_in, rows):
+    """mh_weight_grads takes this product (include/msacl_hip.h)."""
+    if rows < 1024 or ld_g % 4 or ld_x % 4 or g.data_ptr() % 16 or x.data_ptr() % 16:
+        return False
+    if n_out % 64 == 0 and n_in % 4 == 0:
+        return True
+    return n_out < 64 and n_out % 4 == 0 and n_in % 64 == 0 and ld_g == n_out
+
+
+def weight_grads(products, rows, dev):
+    """mh_weight_grads over `products` = [(g, ld_g, x, ld_x, n_out, n_in, dw, db)] (dw / db tensors,
+    db may be None): every dw = g^T x and db = column sums of g in two launches."""
+    N = _native()
+    arr = (N.Wgrad * len(products))()
+    for i, (g, ld_g, x, ld_x, n_out, n_in, dw, db) in enumerate(products):
+        arr[i] = N.Wgrad(g.data_ptr(), ld_g, x.data_ptr(), ld_x, n_out, n_in, dw.data_ptr(),
+                         db.data_ptr() if db is not None else None)
+    key = (dev, rows, tuple((p[4], p[5], p[1], p[3], p[7] is not None) for p in products))
+    ws = _WG_WS.get(key)
+    if ws is None:
+        f = ctypes.c_int64()
+        N.check(N.lib().mh_weight_grads_workspace(arr, len(products), rows, ctypes.byref(f)), "mh_weight_grads_workspace")
+        ws = _WG_WS[key] = torch.empty(max(f.value, 1), dtype=torch.float32, device=dev)
+    N.check(N.lib().mh_weight_grads(arr, len(products), rows, N.ptr(ws), N.stream_of(dev)), "mh_weight_grads")
+
+
 class MLP3(torch.autograd.Function):
     """Linear -> act -> Linear -> act -> Linear -> act under autograd: forward = one
     mh_mlp3_forward launch (h1 / h2 kept only when a gradient will be taken), backward = the
@@ -335,6 +364,42 @@ class MLP3(torch.autograd.Function):
                                              None, W2.shape[0], N.ptr(dx), K1, 1, None, N.stream_of(x.device)),
                     "mh_mlp3_backward")
             return dx, None, None, None, None, None, None, None
+        if a3 == 0 and _MLP3["on"]:
+            # the input-gradient chain in one launch (g2 / g1 kept for the weight gradients), then
+            # every layer's weight / bias gradient in two more (mh_weight_grads); a product that
+            # launch does not take goes through the per-layer path
+            N = _native()
+            M, K1 = x.shape
+            H, N3, dev = W2.shape[0], W3.shape[0], x.device
+            want2, want1 = nW2 or nb2, nW1 or nb1
+            e = lambda *sh: torch.empty(*sh, dtype=torch.float32, device=dev)  # noqa: E731
+            g2 = e(M, H) if want2 else None
+            g1 = e(M, H) if want1 else None
+            dx = e(M, K1) if nx else None
+            dyc = dy.contiguous()
+            if want2 or want1 or nx:
+                N.check(N.lib().mh_mlp3_backward(N.ptr(dyc), N3, N.ptr(h1), N.ptr(h2), H, N.ptr(W1), N.ptr(W2),
+                                                 N.ptr(W3), M, K1, H, N3, a1, a2, N.ptr(g2), N.ptr(g1), H, N.ptr(dx), K1,
+                                                 1, None, N.stream_of(dev)), "mh_mlp3_backward")
+            out = {}
+            prods = []
+            for name, want, nw, nb, g, ld_g, xin, ld_x, n_out, n_in, W in (
+                    ("3", nW3 or nb3, nW3, nb3, dyc, N3, h2, H, N3, H, W3),
+                    ("2", want2, nW2, nb2, g2, H, h1, H, H, H, W2),
+                    ("1", want1, nW1, nb1, g1, H, x, K1, H, K1, W1)):
+                if not want:
+                    out[name] = (None, None)
+                    continue
+                dw, db = e(n_out, n_in), (e(n_out) if nb else None)
+                if wgrad_ok(g, ld_g, xin, ld_x, n_out, n_in, M):
+                    prods.append((g, ld_g, xin, ld_x, n_out, n_in, dw, db))
+                    out[name] = (dw if nw else None, db)
+                else:  # the per-layer path on the chain's gradient (identity: it is already g)
+                    _, dw2, db2_ = layer_backward(g, xin, W, g, 0, False, nw, nb)
+                    out[name] = (dw2, db2_)
+            if prods:
+                weight_grads(prods, M, dev)
+            return (dx, out["1"][0], out["1"][1], out["2"][0], out["2"][1], out["3"][0], out["3"][1], None)
         dh2, dW3, db3 = layer_backward(dy, h2, W3, y, a3, need_h2, nW3, nb3)
         dx = dW1 = db1 = dW2 = db2 = None
         if need_h2:

@@ -185,9 +185,35 @@ class TwinCritic:
 
     def backward_weights(self, x, dq, h1, h2):
         """Gradients of sum_q <dq[q], q-critic(x)> w.r.t. both critics' parameters, written into the
-        joint gradient buffers and bound as the parameters' .grad."""
+        joint gradient buffers and bound as the parameters' .grad. With the fused path: both critics'
+        g2 / g1 from one mh_mlp3_backward launch, the output layers' gradients from the grouped head
+        backward, and the hidden layers' (both critics' layer 2 and the joint layer 1) from one
+        mh_weight_grads pair of launches."""
         N = _native()
         M = x.shape[0]
+        from ._fused import _MLP3, weight_grads, wgrad_ok
+        H, K = self.H, self.K
+        if (_MLP3["on"] and H == 256 and wgrad_ok(x, K, x, K, 2 * H, K, M)
+                and wgrad_ok(h1, 2 * H, h1, 2 * H, H, H, M)):
+            dev = x.device
+            st = N.stream_of(dev)
+            g2 = torch.empty(M, 2 * H, dtype=torch.float32, device=dev)
+            g1 = torch.empty(M, 2 * H, dtype=torch.float32, device=dev)
+            gs = (ctypes.c_int64 * 6)(M, H, H * K, H * H, H, H)
+            N.check(N.lib().mh_mlp3_backward(N.ptr(dq), 1, N.ptr(h1), N.ptr(h2), 2 * H, N.ptr(self.W1), N.ptr(self.W2),
+                                             N.ptr(self.W3), M, K, H, 1, 1, 1, N.ptr(g2), N.ptr(g1), 2 * H, None, K, 2,
+                                             gs, st), "mh_mlp3_backward (twin weights)")
+            n = ctypes.c_int64()
+            N.check(N.lib().mh_head_backward_workspace(M, 1, H, ctypes.byref(n)), "mh_head_backward_workspace")
+            wsh = self._workspace(("head", M), 2 * n.value)
+            N.check(N.lib().mh_head_backward_grouped(
+                N.ptr(dq), N.ptr(h2), N.ptr(self.W3), M, 1, H, 2 * H, 2 * H, 2, M, H, H, H, H, 1, None,
+                N.ptr(self.gW3), N.ptr(self.gb3), N.ptr(wsh), st), "mh_head_backward_grouped (dW3)")
+            prods = [(g2[:, q * H:], 2 * H, h1[:, q * H:], 2 * H, H, H, self.gW2[q], self.gb2[q]) for q in range(2)]
+            prods.append((g1, 2 * H, x, K, 2 * H, K, self.gW1, self.gb1))
+            weight_grads(prods, M, dev)
+            self._grads()
+            return
         dh1 = self._back_l23(dq, h1, h2, True)
         ok, n = ctypes.c_int32(), ctypes.c_int64()
         N.check(N.lib().mh_linear_backward_plan(M, 2 * self.H, self.K, 0, 1, 1, ctypes.byref(ok), ctypes.byref(n)),

@@ -1043,6 +1043,35 @@ int mh_mlp3_backward(const float* dy, int64_t ldy, const float* h1, const float*
   return MH_OK;
 }
 
+static bool wgrad_specs(const mh_wgrad_t* products, int32_t n, std::vector<mh::WgradSpec>& v) {
+  if (!products || n < 1 || n > 6) return false;
+  v.resize(n);
+  for (int i = 0; i < n; ++i) {
+    const mh_wgrad_t& p = products[i];
+    if (!p.g || !p.x || !p.dw || p.n_out <= 0 || p.n_in <= 0 || p.ld_g < p.n_out || p.ld_x < p.n_in) return false;
+    v[i] = mh::WgradSpec{p.g, p.ld_g, p.x, p.ld_x, p.n_out, p.n_in, p.dw, p.db};
+  }
+  return true;
+}
+
+int mh_weight_grads_workspace(const mh_wgrad_t* products, int32_t n, int64_t rows, int64_t* floats_out) {
+  if (!floats_out) return fail(MH_EINVAL, "mh_weight_grads_workspace: null out");
+  std::vector<mh::WgradSpec> v;
+  if (!wgrad_specs(products, n, v) || !mh::weight_grads_plan(v.data(), n, rows, floats_out))
+    return fail(MH_EINVAL, "mh_weight_grads_workspace: products not supported (see msacl_hip.h)");
+  return MH_OK;
+}
+
+int mh_weight_grads(const mh_wgrad_t* products, int32_t n, int64_t rows, float* workspace, void* stream) {
+  std::vector<mh::WgradSpec> v;
+  int64_t need = 0;
+  if (!wgrad_specs(products, n, v) || !mh::weight_grads_plan(v.data(), n, rows, &need))
+    return fail(MH_EINVAL, "mh_weight_grads: products not supported (see msacl_hip.h)");
+  if (need > 0 && !workspace) return fail(MH_EINVAL, "mh_weight_grads: workspace required");
+  MH_HIP(mh::launch_weight_grads(v.data(), n, rows, workspace, (hipStream_t)stream));
+  return MH_OK;
+}
+
 int mh_linear_backward_grouped(const float* dy, const float* y, int32_t act, const float* x, const float* W,
                                int64_t rows, int64_t n_out, int64_t n_in, int64_t ld_dy, int64_t ld_x, int64_t ld_dx,
                                int32_t groups, int64_t stride_dy, int64_t stride_x, int64_t stride_w,

@@ -24,6 +24,8 @@
 // Numerics: each output is an f32 fma chain over k (MFMA f32 is exact per product, one rounding
 // per accumulate), split partials added in order; agrees with the BLAS result to f32
 // summation-order rounding.
+#include <cstring>
+
 #include "rollout.h"
 
 namespace mh {
@@ -245,15 +247,15 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
   }
 }
 
-// C = act(sum_s partial[s] + bias), splits added in order (and db = sum_s dbp[s] when set)
-__global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs g) {
-  gemm_group(g);
+// C = act(sum_s partial[s] + bias), splits added in order (and db = sum_s dbp[s] when set);
+// block b of nb strides over the elements. transC: C is written transposed (C[col][row], ldc).
+__device__ __forceinline__ void gemm_reduce_body(const GemmArgs& g, int64_t b, int64_t nb, bool transC = false) {
   const int64_t MN = g.M * g.N;
   if (g.dbp) {
     // dbn = splits x column tiles partials per output (64 for a 256 x 256 layer): sixteen loads
     // in flight per batch, added in partial order (a load-add loop paid one round trip per
     // partial: 18.8 us for this reduce)
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < g.M; i += (int64_t)gridDim.x * 256) {
+    for (int64_t i = b * 256 + threadIdx.x; i < g.M; i += nb * 256) {
       float v = 0.0f;
       for (int s0 = 0; s0 < g.dbn; s0 += 16) {
         float x[16];
@@ -267,7 +269,7 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs g) {
     }
   }
   if (g.S <= 1) return;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < MN; i += (int64_t)gridDim.x * 256) {
+  for (int64_t i = b * 256 + threadIdx.x; i < MN; i += nb * 256) {
     // eight partials in flight per batch (a load-add loop waits one round trip per split)
     float v = 0.0f;
     for (int s0 = 0; s0 < g.S; s0 += 8) {
@@ -279,8 +281,13 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs g) {
         if (s0 + u < g.S) v = (s0 + u == 0) ? x[u] : v + x[u];
     }
     const int64_t row = i / g.N, col = i - row * g.N;
-    g.C[row * g.ldc + col] = gemm_act(g.bias ? v + g.bias[col] : v, g.act);
+    g.C[transC ? col * g.ldc + row : row * g.ldc + col] = gemm_act(g.bias ? v + g.bias[col] : v, g.act);
   }
+}
+
+__global__ __launch_bounds__(256) void k_gemm_reduce(GemmArgs g) {
+  gemm_group(g);
+  gemm_reduce_body(g, blockIdx.x, gridDim.x);
 }
 
 // ------------------------------------------------------------------ tall products
@@ -489,14 +496,11 @@ __global__ __launch_bounds__(256) void k_gemm_tall(GemmArgs g, int tiles_n) {
 constexpr int DLD = 80;
 
 template <int NCH, bool AG>
-__global__ __launch_bounds__(256) void k_gemm_deep(GemmArgs g, int tiles_m) {
-  gemm_group(g);
+__device__ __forceinline__ void gemm_deep_body(const GemmArgs& g, int tiles_m, int bid, float (*lds)[2 * TK * DLD]) {
   constexpr int NF = 64 * TK / 4 / 256;  // float4 loads per operand per thread per chunk (4)
-  __shared__ float lds[2][2 * TK * DLD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ntn = (int)((g.N + 63) / 64);  // column tiles (one, partly used, when N < 64)
   const int tiles = tiles_m * ntn;
-  const int bid = (int)blockIdx.x;
   const int tile = bid % tiles, split = bid / tiles;
   const int m0 = (tile % tiles_m) * 64, n0 = (tile / tiles_m) * 64;
   const int K = (int)g.K, lda = (int)g.lda, ldb = (int)g.ldb;
@@ -629,6 +633,63 @@ __global__ __launch_bounds__(256) void k_gemm_deep(GemmArgs g, int tiles_m) {
     if (n0 + 4 * (f % 16) < (int)g.N)
       *reinterpret_cast<f32x4*>(out + (int64_t)(m0 + f / 16) * ld + n0 + 4 * (f % 16)) =
           *reinterpret_cast<const f32x4*>(Cs + (f / 16) * DLD + 4 * (f % 16));
+  }
+}
+
+template <int NCH, bool AG>
+__global__ __launch_bounds__(256) void k_gemm_deep(GemmArgs g, int tiles_m) {
+  gemm_group(g);
+  __shared__ float lds[2][2 * TK * DLD];
+  gemm_deep_body<NCH, AG>(g, tiles_m, (int)blockIdx.x, lds);
+}
+
+// ------------------------------------------------------------------ several weight gradients at once
+// Up to MULTI_MAX deep products (dW = g^T x with the bias gradient) in ONE launch and their split
+// reduces in one more: the three layers of an MLP backward (and both twin critics') are independent
+// once the input-gradient chain has formed their left operands (mh_mlp3_backward). Product p owns
+// workgroups [start[p], start[p + 1]); every product is split over its rows (S >= 2) so its result
+// always goes through the reduce, which may write it transposed (dW3 computed as h2^T g3 = dW3^T
+// when the layer has fewer than 64 outputs) and may also sum the columns of a narrow matrix
+// (db3 = column sums of g3, `cs_src` [rows][cs_n]) in fixed order.
+constexpr int MULTI_MAX = 6;
+struct DeepMulti {
+  GemmArgs g[MULTI_MAX];
+  int tiles_m[MULTI_MAX];
+  int start[MULTI_MAX + 1];
+  int rstart[MULTI_MAX + 1];  // reduce blocks
+  int trans[MULTI_MAX];
+  const float* cs_src[MULTI_MAX];  // column sums of [rows][cs_n] into cs_dst (or null)
+  int64_t cs_rows[MULTI_MAX];
+  int cs_n[MULTI_MAX];
+  float* cs_dst[MULTI_MAX];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void k_gemm_deep_multi(DeepMulti d) {
+  __shared__ float lds[2][2 * TK * DLD];
+  const int b = blockIdx.x;
+  int p = 0;
+  while (p + 1 < d.n && b >= d.start[p + 1]) ++p;
+  gemm_deep_body<0, true>(d.g[p], d.tiles_m[p], b - d.start[p], lds);
+}
+
+__global__ __launch_bounds__(256) void k_gemm_reduce_multi(DeepMulti d) {
+  const int b = blockIdx.x;
+  int p = 0;
+  while (p + 1 < d.n && b >= d.rstart[p + 1]) ++p;
+  const int rb = b - d.rstart[p], nrb = d.rstart[p + 1] - d.rstart[p];
+  gemm_reduce_body(d.g[p], rb, nrb, d.trans[p] != 0);
+  if (d.cs_src[p] && rb == 0) {
+    // column sums of a narrow [rows][cs_n] matrix: wave w sums columns w, w + 4, ... over the rows
+    // in fixed order (lane-strided partials, then a fixed butterfly)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int c = w; c < d.cs_n[p]; c += 4) {
+      float v = 0.0f;
+      for (int64_t r = lane; r < d.cs_rows[p]; r += 64) v += d.cs_src[p][r * d.cs_n[p] + c];
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+      if (lane == 0) d.cs_dst[p][c] = v;
+    }
   }
 }
 
@@ -966,6 +1027,91 @@ hipError_t launch_linear_backward(const float* dy, const float* y, int act, cons
     return hipGetLastError();
   }
   return hipSuccess;
+}
+
+// ------------------------------------------------------------------ several weight gradients
+// product p: dw[n_out][n_in] = g^T x over `rows`, db = column sums of g. Returns false when a
+// product does not fit (the caller takes the per-layer path); ws_floats: workspace needed.
+static bool wgrad_plan(const WgradSpec* ps, int n, int64_t rows, DeepMulti* d, int64_t* ws_floats, float* ws) {
+  if (n < 1 || n > MULTI_MAX || rows < 1024) return false;
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  int64_t off = 0;
+  int start = 0, rstart = 0;
+  if (d) std::memset(d, 0, sizeof(*d));
+  for (int i = 0; i < n; ++i) {
+    const WgradSpec& q = ps[i];
+    if (q.ld_g % 4 || q.ld_x % 4 || !al16(q.g) || !al16(q.x) || !q.dw) return false;
+    const bool normal = q.n_out % 64 == 0 && q.n_in % 4 == 0;
+    const bool swapped = !normal && q.n_out < 64 && q.n_out % 4 == 0 && q.n_in % 64 == 0;
+    if (!normal && !swapped) return false;
+    const int64_t M = swapped ? q.n_in : q.n_out, N = swapped ? q.n_out : q.n_in;
+    if ((rows + TK) * (swapped ? q.ld_x : q.ld_g) * 4 >= ((int64_t)1 << 30) ||
+        (rows + TK) * (swapped ? q.ld_g : q.ld_x) * 4 >= ((int64_t)1 << 30))
+      return false;
+    int S = deep_splits(M, N, rows);
+    const int64_t chunks = (rows + TK - 1) / TK;
+    if (S < 2) S = chunks >= 2 ? 2 : 1;
+    if (S < 2) return false;
+    const int64_t per = (chunks + S - 1) / S;
+    S = (int)((chunks + per - 1) / per);
+    if (S < 2) return false;
+    const int ntn = (int)((N + 63) / 64), tiles_m = (int)(M / 64);
+    const bool dbp = q.db && normal;
+    const int64_t need = (int64_t)S * M * N + (dbp ? (int64_t)S * ntn * M : 0);
+    if (d) {
+      GemmArgs g{};
+      g.A = swapped ? q.x : q.g;
+      g.B = swapped ? q.g : q.x;
+      g.C = q.dw;
+      g.M = M; g.N = N; g.K = rows;
+      g.lda = swapped ? q.ld_x : q.ld_g;
+      g.ldb = swapped ? q.ld_g : q.ld_x;
+      g.ldc = swapped ? M : N;  // transposed write: dw[n_out][n_in] = C^T, row length n_in = M
+      g.act = 0; g.S = S; g.kc_per = per; g.partial = ws + off;
+      g.act_a = 0;
+      g.db = dbp ? q.db : nullptr;
+      g.dbp = dbp ? ws + off + (int64_t)S * M * N : nullptr;
+      g.dbn = S * ntn;
+      d->g[i] = g;
+      d->tiles_m[i] = tiles_m;
+      d->start[i] = start;
+      d->rstart[i] = rstart;
+      d->trans[i] = swapped ? 1 : 0;
+      if (swapped && q.db) {
+        d->cs_src[i] = q.g;
+        d->cs_rows[i] = rows;
+        d->cs_n[i] = (int)q.n_out;
+        d->cs_dst[i] = q.db;
+        if (q.ld_g != q.n_out) return false;  // the column-sum job reads [rows][n_out] packed
+      }
+    }
+    off += need;
+    start += tiles_m * ntn * S;
+    const int64_t rb = (M * N + 255) / 256;
+    rstart += (int)(rb < 512 ? rb : 512);
+  }
+  if (d) {
+    d->start[n] = start;
+    d->rstart[n] = rstart;
+    d->n = n;
+  }
+  *ws_floats = off;
+  return true;
+}
+
+bool weight_grads_plan(const WgradSpec* ps, int n, int64_t rows, int64_t* ws_floats) {
+  return wgrad_plan(ps, n, rows, nullptr, ws_floats, nullptr);
+}
+
+hipError_t launch_weight_grads(const WgradSpec* ps, int n, int64_t rows, float* ws, hipStream_t st) {
+  DeepMulti d;
+  int64_t need = 0;
+  if (!wgrad_plan(ps, n, rows, &d, &need, ws)) return hipErrorInvalidValue;
+  k_gemm_deep_multi<<<(unsigned)d.start[n], 256, 0, st>>>(d);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  k_gemm_reduce_multi<<<(unsigned)d.rstart[n], 256, 0, st>>>(d);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ grouped launches

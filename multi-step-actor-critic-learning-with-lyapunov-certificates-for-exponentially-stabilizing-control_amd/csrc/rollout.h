@@ -207,6 +207,18 @@ struct Mlp3BwdArgs {
   int64_t ldx;
 };
 hipError_t launch_mlp3_backward(const Mlp3BwdArgs& a, hipStream_t st);
+// several weight gradients dw = g^T x, db = column sums of g in two launches (gemm.hip)
+struct WgradSpec {
+  const float* g;
+  int64_t ld_g;
+  const float* x;
+  int64_t ld_x;
+  int64_t n_out, n_in;
+  float* dw;
+  float* db;
+};
+bool weight_grads_plan(const WgradSpec* ps, int n, int64_t rows, int64_t* ws_floats);
+hipError_t launch_weight_grads(const WgradSpec* ps, int n, int64_t rows, float* ws, hipStream_t st);
 bool mlp3_supported(int64_t M, int K1, int H, int N3);
 hipError_t launch_mlp3_forward(const Mlp3Args& a, int groups, hipStream_t st);
 hipError_t launch_polyak_multi(const PolyakList& L, double polyak, hipStream_t st);

@@ -75,10 +75,14 @@ constexpr bool kLoaders = true;
 constexpr bool kLoaders = false;
 #endif
 
-// bounded LDS-counter wait (the same bound and error word as pol_sync)
+// bounded LDS-counter wait (the same bound and error word as pol_sync). SLEEP: the loader waves
+// poll with s_sleep between reads (they share each SIMD and the LDS with a policy wave, and wait
+// for a phase's worth of MFMAs); the policy waves poll back to back (their data is normally there)
+template <bool SLEEP = false>
 __device__ __forceinline__ void wait_count(uint32_t* ctr, uint32_t target, int64_t* err, uint32_t limit) {
   uint32_t spins = 0;
   while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+    if (SLEEP) __builtin_amdgcn_s_sleep(2);
     if (++spins >= limit) {
       if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(err, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
@@ -620,7 +624,7 @@ __device__ void load_pass(const FusedArgs& a, const PolicyLds& L, int p, int npa
   const int last = p + 1 < npass ? PM_NB : PM_NB - 1;
   for (int i = 1; i <= last; ++i) {
     const uint32_t c = (uint32_t)(PM_NB * p + i);
-    wait_count(L.released, c >= 2 ? 4u * (c - 1) : 0u, L.err, a.spin_limit);  // chunk c - 2's buffer free
+    wait_count<true>(L.released, c >= 2 ? 4u * (c - 1) : 0u, L.err, a.spin_limit);  // chunk c - 2's buffer free
     const int ib = i & (PM_NB - 1);
     uint4* dst = (c & 1) ? L.c1 : L.c0;
     const uint4* src = W2g + ((int64_t)ib * PM_X3_FRAGS + l * HALF) * 64;

@@ -190,3 +190,55 @@ def test_twin_input_grad_chain_equals_per_layer():
         finally:
             F._MLP3["on"] = True
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-5 * float(outs[1].abs().max()))
+
+
+@pytest.mark.parametrize("rows", [5120, 3001])
+def test_weight_grads_multi_matches_float64(rows):
+    """mh_weight_grads: the three layers' dW = g^T x and db = column sums of g of a policy-shaped MLP
+    (a narrow output layer computed transposed, a 256 x 256 layer, a K1 = 12 input layer) in two
+    launches, each element against float64 within 2e-6 sqrt(rows) sum|g x| + 1e-6."""
+    from msacl_amd.apprfunc._fused import weight_grads
+    torch.manual_seed(rows)
+    dev = "cuda"
+    g3, h2 = torch.randn(rows, 8, device=dev), torch.rand(rows, 256, device=dev)
+    g2, h1 = torch.randn(rows, 256, device=dev), torch.rand(rows, 256, device=dev)
+    g1, x = torch.randn(rows, 256, device=dev), torch.randn(rows, 12, device=dev)
+    outs = [(torch.empty(8, 256, device=dev), torch.empty(8, device=dev)),
+            (torch.empty(256, 256, device=dev), torch.empty(256, device=dev)),
+            (torch.empty(256, 12, device=dev), None)]
+    weight_grads([(g3, 8, h2, 256, 8, 256) + outs[0], (g2, 256, h1, 256, 256, 256) + outs[1],
+                  (g1, 256, x, 12, 256, 12) + outs[2]], rows, torch.device(dev))
+    torch.cuda.synchronize()
+    D = lambda t: t.double().cpu().numpy()  # noqa: E731
+    for (g, xin), (dw, db) in zip(((g3, h2), (g2, h1), (g1, x)), outs):
+        ref = D(g).T @ D(xin)
+        tol = 2e-6 * rows ** 0.5 * (np.abs(D(g)).T @ np.abs(D(xin))) + 1e-6
+        assert np.all(np.abs(D(dw) - ref) <= tol), np.abs(D(dw) - ref).max()
+        if db is not None:
+            rb = D(g).sum(0)
+            assert np.all(np.abs(D(db) - rb) <= 2e-6 * rows ** 0.5 * np.abs(D(g)).sum(0) + 1e-6)
+
+
+def test_twin_weight_grads_fused_equals_per_layer():
+    """TwinCritic.backward_weights through the chain + mh_weight_grads vs the per-layer launches:
+    every gradient within rtol 1e-4 / atol 1e-5 of its scale."""
+    from msacl_amd.apprfunc._twin import TwinCritic
+    from msacl_amd.apprfunc.mlp import ActionValue
+    torch.manual_seed(2)
+    kw = dict(obs_dim=12, act_dim=4, hidden_sizes=[256, 256], hidden_activation="relu", output_activation="linear")
+    q1, q2 = ActionValue(**kw).cuda(), ActionValue(**kw).cuda()
+    tc = TwinCritic.build(q1, q2)
+    M = 5120
+    x = torch.randn(M, 16, device="cuda")
+    dq = torch.randn(2, M, device="cuda")
+    res = []
+    for on in (True, False):
+        F._MLP3["on"] = on
+        try:
+            q, h1, h2 = tc.forward(x)
+            tc.backward_weights(x, dq, h1, h2)
+            res.append([t.clone() for t in (tc.gW1, tc.gb1, tc.gW2, tc.gb2, tc.gW3, tc.gb3)])
+        finally:
+            F._MLP3["on"] = True
+    for u, v in zip(*res):
+        torch.testing.assert_close(u, v, rtol=1e-4, atol=1e-5 * float(v.abs().max()))
