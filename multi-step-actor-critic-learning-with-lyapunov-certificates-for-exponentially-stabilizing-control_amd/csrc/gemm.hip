@@ -53,6 +53,9 @@ struct GemmArgs {
   // grouped launches (the twin critics' layers as one launch): blockIdx.y = group q, and every
   // operand pointer of group q is its group-0 pointer + q x its stride (floats; 0 = shared)
   int64_t gsA, gsB, gsC, gsBias, gsY, gsPart, gsDb, gsDbp;
+  // deep kernel, dbB set: dbp [S][N] holds the column sums of B over each split's K slice (the
+  // bias gradient of a layer whose dW is computed transposed, x^T g: g is the B operand)
+  int dbB;
 };
 
 // this workgroup's group (blockIdx.y) of a grouped launch: the operand pointers advanced
@@ -252,15 +255,16 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs g) {
 __device__ __forceinline__ void gemm_reduce_body(const GemmArgs& g, int64_t b, int64_t nb, bool transC = false) {
   const int64_t MN = g.M * g.N;
   if (g.dbp) {
+    const int64_t dlen = g.dbB ? g.N : g.M;
     // dbn = splits x column tiles partials per output (64 for a 256 x 256 layer): sixteen loads
     // in flight per batch, added in partial order (a load-add loop paid one round trip per
     // partial: 18.8 us for this reduce)
-    for (int64_t i = b * 256 + threadIdx.x; i < g.M; i += nb * 256) {
+    for (int64_t i = b * 256 + threadIdx.x; i < dlen; i += nb * 256) {
       float v = 0.0f;
       for (int s0 = 0; s0 < g.dbn; s0 += 16) {
         float x[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) x[u] = s0 + u < g.dbn ? g.dbp[(int64_t)(s0 + u) * g.M + i] : 0.0f;
+        for (int u = 0; u < 16; ++u) x[u] = s0 + u < g.dbn ? g.dbp[(int64_t)(s0 + u) * dlen + i] : 0.0f;
 #pragma unroll
         for (int u = 0; u < 16; ++u)
           if (s0 + u < g.dbn) v = (s0 + u == 0) ? x[u] : v + x[u];
@@ -569,13 +573,19 @@ __device__ __forceinline__ void gemm_deep_body(const GemmArgs& g, int tiles_m, i
   // tn, tn + ntn, ... (thread: column tid & 63, every fourth of those rows from tid >> 6), in
   // order, in a register
   const int tn = tile / tiles_m;
-  const bool colsum = AG && g.dbp;
+  const bool colsum = AG && g.dbp && !g.dbB;
+  // dbB: the column sums of B instead, formed by the first row tile of each column tile (the
+  // others hold the same B chunk); thread: column tid & 63, every fourth k row from tid >> 6
+  const bool colsumB = AG && g.dbp && g.dbB && tile % tiles_m == 0;
   float cs = 0.0f;
   auto mma = [&](int c) {
     const float* As = lds[c & 1];
     const float* Bs = lds[c & 1] + TK * DLD;
     if (colsum) {
       for (int kr = tn + ntn * (tid >> 6); kr < TK; kr += 4 * ntn) cs = cs + As[kr * DLD + (tid & 63)];
+    }
+    if (colsumB) {
+      for (int kr = tid >> 6; kr < TK; kr += 4) cs = cs + Bs[kr * DLD + (tid & 63)];
     }
 #pragma unroll
     for (int t = 0; t < TK / 4; ++t) {
@@ -621,11 +631,14 @@ __device__ __forceinline__ void gemm_deep_body(const GemmArgs& g, int tiles_m, i
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int q = 0; q < 4; ++q) Cs[(32 * wm + 16 * i + 4 * kk + q) * DLD + 32 * wn + 16 * j + r] = acc[i][j][q];
-  if (colsum) lds[1][tid] = cs;
+  if (colsum || colsumB) lds[1][tid] = cs;
   __syncthreads();
-  if (colsum && tid < 64) {  // the four row groups of this workgroup's share, in order
+  if ((colsum || colsumB) && tid < 64) {  // the four row groups of this workgroup's share, in order
     const float v = ((lds[1][tid] + lds[1][64 + tid]) + lds[1][128 + tid]) + lds[1][192 + tid];
-    g.dbp[((int64_t)split * ntn + tn) * g.M + m0 + tid] = v;
+    if (colsum)
+      g.dbp[((int64_t)split * ntn + tn) * g.M + m0 + tid] = v;
+    else if (n0 + tid < (int)g.N)
+      g.dbp[(int64_t)split * g.N + n0 + tid] = v;
   }
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -649,8 +662,8 @@ __global__ __launch_bounds__(256) void k_gemm_deep(GemmArgs g, int tiles_m) {
 // once the input-gradient chain has formed their left operands (mh_mlp3_backward). Product p owns
 // workgroups [start[p], start[p + 1]); every product is split over its rows (S >= 2) so its result
 // always goes through the reduce, which may write it transposed (dW3 computed as h2^T g3 = dW3^T
-// when the layer has fewer than 64 outputs) and may also sum the columns of a narrow matrix
-// (db3 = column sums of g3, `cs_src` [rows][cs_n]) in fixed order.
+// when the layer has fewer than 64 outputs; its bias gradient is then the column sums of the B
+// operand g3, formed per split in the deep kernel: GemmArgs::dbB).
 constexpr int MULTI_MAX = 6;
 struct DeepMulti {
   GemmArgs g[MULTI_MAX];
@@ -658,10 +671,6 @@ struct DeepMulti {
   int start[MULTI_MAX + 1];
   int rstart[MULTI_MAX + 1];  // reduce blocks
   int trans[MULTI_MAX];
-  const float* cs_src[MULTI_MAX];  // column sums of [rows][cs_n] into cs_dst (or null)
-  int64_t cs_rows[MULTI_MAX];
-  int cs_n[MULTI_MAX];
-  float* cs_dst[MULTI_MAX];
   int n;
 };
 
@@ -679,18 +688,6 @@ __global__ __launch_bounds__(256) void k_gemm_reduce_multi(DeepMulti d) {
   while (p + 1 < d.n && b >= d.rstart[p + 1]) ++p;
   const int rb = b - d.rstart[p], nrb = d.rstart[p + 1] - d.rstart[p];
   gemm_reduce_body(d.g[p], rb, nrb, d.trans[p] != 0);
-  if (d.cs_src[p] && rb == 0) {
-    // column sums of a narrow [rows][cs_n] matrix: wave w sums columns w, w + 4, ... over the rows
-    // in fixed order (lane-strided partials, then a fixed butterfly)
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int c = w; c < d.cs_n[p]; c += 4) {
-      float v = 0.0f;
-      for (int64_t r = lane; r < d.cs_rows[p]; r += 64) v += d.cs_src[p][r * d.cs_n[p] + c];
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-      if (lane == 0) d.cs_dst[p][c] = v;
-    }
-  }
 }
 
 static bool deep_ok(const float* A, const float* B, const float* bias, int64_t M, int64_t N, int64_t K, int64_t lda,
@@ -1056,8 +1053,8 @@ static bool wgrad_plan(const WgradSpec* ps, int n, int64_t rows, DeepMulti* d, i
     S = (int)((chunks + per - 1) / per);
     if (S < 2) return false;
     const int ntn = (int)((N + 63) / 64), tiles_m = (int)(M / 64);
-    const bool dbp = q.db && normal;
-    const int64_t need = (int64_t)S * M * N + (dbp ? (int64_t)S * ntn * M : 0);
+    const bool dbp = q.db != nullptr;  // normal: column sums of A = g; swapped: of B = g
+    const int64_t need = (int64_t)S * M * N + (dbp ? (normal ? (int64_t)S * ntn * M : (int64_t)S * N) : 0);
     if (d) {
       GemmArgs g{};
       g.A = swapped ? q.x : q.g;
@@ -1071,19 +1068,13 @@ static bool wgrad_plan(const WgradSpec* ps, int n, int64_t rows, DeepMulti* d, i
       g.act_a = 0;
       g.db = dbp ? q.db : nullptr;
       g.dbp = dbp ? ws + off + (int64_t)S * M * N : nullptr;
-      g.dbn = S * ntn;
+      g.dbn = normal ? S * ntn : S;
+      g.dbB = swapped ? 1 : 0;
       d->g[i] = g;
       d->tiles_m[i] = tiles_m;
       d->start[i] = start;
       d->rstart[i] = rstart;
       d->trans[i] = swapped ? 1 : 0;
-      if (swapped && q.db) {
-        d->cs_src[i] = q.g;
-        d->cs_rows[i] = rows;
-        d->cs_n[i] = (int)q.n_out;
-        d->cs_dst[i] = q.db;
-        if (q.ld_g != q.n_out) return false;  // the column-sum job reads [rows][n_out] packed
-      }
     }
     off += need;
     start += tiles_m * ntn * S;

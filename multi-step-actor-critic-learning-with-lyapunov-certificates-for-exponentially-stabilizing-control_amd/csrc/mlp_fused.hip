@@ -36,64 +36,86 @@ constexpr int HID = 256;      // hidden width
 constexpr int SH = HID + 4;   // LDS row stride of a hidden tile (floats): rows 16 B apart in the banks
 constexpr int K1P = 32;       // first-layer K padded
 constexpr int SX = K1P + 4;
-constexpr int PF = 3;         // weight groups in flight
+constexpr int PF = 4;         // weight groups in the load ring: three in flight behind the MFMAs
 
-__device__ __forceinline__ float act_f(float v, int act) {
-  if (act == 1) return v < 0.0f ? 0.0f : v;  // as torch.relu / gemm_act (NaN passes through)
-  if (act == 2) return tanhf(v);
+// The load ring is enforced with scheduling barriers: left to itself the scheduler regroups the
+// fully unrolled loop and waits on each group's loads right after issuing them (one L2 latency per
+// 16-deep group — the r04 first cut measured 41 us at 5,120 rows, latency-bound).
+#define MH_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+template <int ACT>
+__device__ __forceinline__ float act_t(float v) {
+  if constexpr (ACT == 1) return v < 0.0f ? 0.0f : v;  // as torch.relu / gemm_act (NaN passes through)
+  if constexpr (ACT == 2) return tanhf(v);
   return v;
 }
 
-// One hidden-width layer for this wave's 64 output columns: out[16][64] += in[16][K] W[n][K]^T.
-// `in` is the LDS tile (row stride SIN floats), W rows [n0, n0 + 64) of a row-major [N][K] matrix
-// behind a buffer resource (rows past N read 0). K is a multiple of 16.
-template <int SIN>
-__device__ __forceinline__ void layer_cols(const float* in, __amdgpu_buffer_rsrc_t wr, int K, int n0, int lane,
+__device__ __forceinline__ float act_f(float v, int act) {
+  if (act == 1) return act_t<1>(v);
+  if (act == 2) return act_t<2>(v);
+  return v;
+}
+
+// One hidden-width layer for this wave's 64 output columns: out[16][64] += in[16][K] W[n][K]^T,
+// K = 16 G. `in` is the LDS tile (row stride SIN floats), W rows [n0, n0 + 64) of a row-major [N][K]
+// matrix behind a buffer resource (rows past N read 0). Group u's four weight float4s are issued
+// PF - 1 groups before its MFMAs; its A operand (one ds_read_b128) one group before.
+template <int SIN, int G>
+__device__ __forceinline__ void layer_cols(const float* in, __amdgpu_buffer_rsrc_t wr, int n0, int lane,
                                            f32x4 (&acc)[4]) {
+  constexpr int K = 16 * G;
   const int r = lane & 15, g = lane >> 4;
-  const int G = K / 16;
+  const int voff = ((n0 + r) * K + 4 * g) * 4;
   f32x4 wb[PF][4];
-  auto load = [&](int u, f32x4* dst) {
+  auto load = [&](int u, f32x4 (&dst)[4]) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int off = ((n0 + 16 * j + r) * K + 16 * u + 4 * g) * 4;
-      dst[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
-    }
+    for (int j = 0; j < 4; ++j)
+      dst[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, voff + (16 * j * K + 16 * u) * 4, 0, 0));
   };
+  const float* arow = in + r * SIN + 4 * g;
 #pragma unroll
-  for (int p = 0; p < PF; ++p)
+  for (int p = 0; p < PF - 1; ++p)
     if (p < G) load(p, wb[p]);
-  for (int u0 = 0; u0 < G; u0 += PF) {
+  f32x4 a_cur = *reinterpret_cast<const f32x4*>(arow);
 #pragma unroll
-    for (int p = 0; p < PF; ++p) {
-      const int u = u0 + p;
-      if (u < G) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(in + r * SIN + 16 * u + 4 * g);
-        f32x4 b[4];
+  for (int u = 0; u < G; ++u) {
+    if (u + PF - 1 < G) load(u + PF - 1, wb[(u + PF - 1) % PF]);
+    f32x4 a_nxt = a_cur;
+    if (u + 1 < G) a_nxt = *reinterpret_cast<const f32x4*>(arow + 16 * (u + 1));
+    MH_SCHED_FENCE();
 #pragma unroll
-        for (int j = 0; j < 4; ++j) b[j] = wb[p][j];
-        if (u + PF < G) load(u + PF, wb[p]);
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[j][t], acc[j], 0, 0, 0);
-      }
-    }
+      for (int j = 0; j < 4; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t], wb[u % PF][j][t], acc[j], 0, 0, 0);
+    MH_SCHED_FENCE();
+    a_cur = a_nxt;
   }
 }
 
 // bias + activation of this wave's 64 columns into the LDS tile `out` (row stride SH); the MFMA's
 // C map: column = lane & 15, rows 4 (lane >> 4) + q
-__device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[4], const float* bias, int act, int n0, int lane,
-                                             float* out) {
+template <int ACT>
+__device__ __forceinline__ void epilogue_lds_t(const f32x4 (&acc)[4], const float (&bias)[4], int n0, int lane,
+                                               float* out) {
   const int c = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int n = n0 + 16 * j + c;
-    const float bv = bias[n];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) out[(4 * g + q) * SH + n] = act_f(acc[j][q] + bv, act);
+    for (int q = 0; q < 4; ++q) out[(4 * g + q) * SH + n] = act_t<ACT>(acc[j][q] + bias[j]);
   }
+}
+
+// bias[j] = the bias of column n0 + 16 j + (lane & 15), loaded up front
+__device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[4], const float (&bias)[4], int act, int n0, int lane,
+                                             float* out) {
+  if (act == 1)
+    epilogue_lds_t<1>(acc, bias, n0, lane, out);
+  else if (act == 2)
+    epilogue_lds_t<2>(acc, bias, n0, lane, out);
+  else
+    epilogue_lds_t<0>(acc, bias, n0, lane, out);
 }
 
 // the LDS tile (16 rows x HID) to global rows m0.. (ld floats), row-contiguous float4 stores
@@ -128,6 +150,34 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t m0 = (int64_t)blockIdx.x * TM;
   const int K1 = a.K1, K1p = (K1 + 15) & ~15;
+  const int n0 = wave * 64;
+  const int r = lane & 15, g = lane >> 4;
+
+  // ---- the hidden layers' biases and layer 1's weights first (their latency overlaps the input
+  // staging): W1 [H][K1], lane group
+  // g of column n reads k = 16 u + 4 g + t; k >= K1 lands past the buffer's end and reads 0
+  float w1[2][4][4], bias1[4], bias2[4];
+  {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      bias1[j] = a.b1[n0 + 16 * j + r];
+      bias2[j] = a.b2[n0 + 16 * j + r];
+    }
+    const __amdgpu_buffer_rsrc_t wr1 =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.W1), (short)0, HID * K1 * 4, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int k = 16 * u + 4 * g + t, n = n0 + 16 * j + r;
+          w1[u][j][t] = (u * 16 < K1p)
+                            ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                            wr1, k < K1 ? (n * K1 + k) * 4 : 0x7ffffff0, 0, 0))
+                            : 0.0f;
+        }
+  }
 
   // ---- the input rows, zero-padded to K1p columns (rows past M: zeros)
   for (int i = tid; i < TM * K1p; i += 256) {
@@ -136,61 +186,57 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
   }
   __syncthreads();
 
-  const int n0 = wave * 64;
-  // ---- layer 1: K1p <= 32; weights [H][K1]: a row's float4 at k >= K1 is masked to 0 (the next row's)
+  const __amdgpu_buffer_rsrc_t wr2 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.W2), (short)0, HID * HID * 4, 0x00020000);
+  // ---- layer 1: K1p <= 32
   {
     f32x4 acc[4] = {};
-    const int r = lane & 15, g = lane >> 4;
-    for (int u = 0; u < K1p / 16; ++u) {
-      const f32x4 av = *reinterpret_cast<const f32x4*>(xs + r * SX + 16 * u + 4 * g);
-      f32x4 b[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float* row = a.W1 + (int64_t)(n0 + 16 * j + r) * K1;
+    for (int u = 0; u < 2; ++u) {
+      if (u * 16 < K1p) {
+        const f32x4 av = *reinterpret_cast<const f32x4*>(xs + r * SX + 16 * u + 4 * g);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int k = 16 * u + 4 * g + t;
-          b[j][t] = k < K1 ? row[k] : 0.0f;
-        }
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], w1[u][j][t], acc[j], 0, 0, 0);
       }
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], b[j][t], acc[j], 0, 0, 0);
     }
-    epilogue_lds(acc, a.b1, a.act1, n0, lane, hs1);
+    epilogue_lds(acc, bias1, a.act1, n0, lane, hs1);
   }
   __syncthreads();
   if (a.h1) store_tile(hs1, a.h1, a.ldh, m0, a.M, HID);
 
   // ---- layer 2
+  const int N3 = a.N3;
+  const __amdgpu_buffer_rsrc_t wr3 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.W3), (short)0, N3 * HID * 4, 0x00020000);
+  f32x4 w3[4];  // the narrow output layer's weights (N3 <= 16), issued before layer 2's epilogue
   {
-    const __amdgpu_buffer_rsrc_t wr =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.W2), (short)0, HID * HID * 4, 0x00020000);
     f32x4 acc[4] = {};
-    layer_cols<SH>(hs1, wr, HID, n0, lane, acc);
-    epilogue_lds(acc, a.b2, a.act2, n0, lane, hs2);
+    layer_cols<SH, HID / 16>(hs1, wr2, n0, lane, acc);
+    if (N3 <= 16) {
+#pragma unroll
+      for (int uu = 0; uu < 4; ++uu)
+        w3[uu] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr3, (r * HID + 16 * (wave * 4 + uu) + 4 * g) * 4, 0, 0));
+    }
+    MH_SCHED_FENCE();
+    epilogue_lds(acc, bias2, a.act2, n0, lane, hs2);
   }
   __syncthreads();
   if (a.h2) store_tile(hs2, a.h2, a.ldh, m0, a.M, HID);
 
   // ---- layer 3
-  const int N3 = a.N3;
-  const __amdgpu_buffer_rsrc_t wr3 =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.W3), (short)0, N3 * HID * 4, 0x00020000);
   if (N3 <= 16) {
     // one 16-column block; wave w contracts k in [64 w, 64 w + 64), the four partial tiles added
     // in wave order
-    const int r = lane & 15, g = lane >> 4;
     f32x4 acc = {};
 #pragma unroll
     for (int uu = 0; uu < 4; ++uu) {
       const int u = wave * 4 + uu;
       const f32x4 av = *reinterpret_cast<const f32x4*>(hs2 + r * SH + 16 * u + 4 * g);
-      const f32x4 bv = __builtin_bit_cast(
-          f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr3, (r * HID + 16 * u + 4 * g) * 4, 0, 0));
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bv[t], acc, 0, 0, 0);
+      for (int t = 0; t < 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], w3[uu][t], acc, 0, 0, 0);
     }
     red[wave][lane] = acc;
     __syncthreads();
@@ -212,8 +258,8 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
     // N3 = 64 c: wave w takes output columns [N3 / 4 * w, ...) in 16-column blocks of 64-wide passes
     for (int nb = wave * 64; nb < N3; nb += 256) {
       f32x4 acc[4] = {};
-      layer_cols<SH>(hs2, wr3, HID, nb, lane, acc);
-      const int c = lane & 15, g = lane >> 4;
+      layer_cols<SH, HID / 16>(hs2, wr3, nb, lane, acc);
+      const int c = lane & 15;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = nb + 16 * j + c;
@@ -233,14 +279,16 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
 // in MFMA t of group u, lane group g contracts weight row 16 u + 4 g + t, so each lane's four B
 // values lie in four rows (scalar loads, 64 consecutive bytes per 16 lanes). Rows past `nrows` read 0.
 // (the weight rows are HID floats long; rows at or past `nrows` lie beyond the buffer resource)
-__device__ __forceinline__ void layer_cols_t(const float* in, int sin, __amdgpu_buffer_rsrc_t wr, int nrows, int n0,
-                                             int lane, f32x4 (&acc)[4]) {
+// Same load ring as layer_cols (depth PFT: sixteen scalars a group), group u issued PFT - 1 groups ahead.
+constexpr int PFT = 3;
+template <int G>
+__device__ __forceinline__ void layer_cols_t(const float* in, int sin, __amdgpu_buffer_rsrc_t wr, int n0, int lane,
+                                             f32x4 (&acc)[4]) {
   const int c = lane & 15, g = lane >> 4;
-  const int G = (nrows + 15) / 16;
   const int voff = ((4 * g) * HID + n0 + c) * 4;  // + (t HID + 16 j) 4: immediate offsets
-  float wb[PF][4][4];
-  auto load = [&](int u, float (*dst)[4]) {
-    const int soff = __builtin_amdgcn_readfirstlane(u * 16 * HID * 4);
+  float wb[PFT][4][4];
+  auto load = [&](int u, float (&dst)[4][4]) {
+    const int soff = u * 16 * HID * 4;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -248,41 +296,73 @@ __device__ __forceinline__ void layer_cols_t(const float* in, int sin, __amdgpu_
         dst[j][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, voff + (t * HID + 16 * j) * 4,
                                                                                  soff, 0));
   };
+  const float* arow = in + c * sin + 4 * g;
 #pragma unroll
-  for (int p = 0; p < PF; ++p)
+  for (int p = 0; p < PFT - 1; ++p)
     if (p < G) load(p, wb[p]);
-#pragma unroll 1
-  for (int u0 = 0; u0 < G; u0 += PF) {
+  f32x4 a_cur = *reinterpret_cast<const f32x4*>(arow);
 #pragma unroll
-    for (int p = 0; p < PF; ++p) {
-      const int u = u0 + p;
-      if (u < G) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(in + c * sin + 16 * u + 4 * g);
-        float b[4][4];
+  for (int u = 0; u < G; ++u) {
+    if (u + PFT - 1 < G) load(u + PFT - 1, wb[(u + PFT - 1) % PFT]);
+    f32x4 a_nxt = a_cur;
+    if (u + 1 < G) a_nxt = *reinterpret_cast<const f32x4*>(arow + 16 * (u + 1));
+    MH_SCHED_FENCE();
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
-          for (int t = 0; t < 4; ++t) b[j][t] = wb[p][j][t];
-        if (u + PF < G) load(u + PF, wb[p]);
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[t], b[j][t], acc[j], 0, 0, 0);
-      }
-    }
+      for (int j = 0; j < 4; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t], wb[u % PFT][j][t], acc[j], 0, 0, 0);
+    MH_SCHED_FENCE();
+    a_cur = a_nxt;
   }
 }
 
-__device__ __forceinline__ float act_grad_f(float d, float t, int act) {  // gemm.hip act_grad
-  if (act == 1) return t > 0.0f ? d : 0.0f;
-  if (act == 2) return d * (1.0f - t * t);
+// the output-gradient contraction over W3's N3 rows: N3 <= 16 or a multiple of 64
+__device__ __forceinline__ void layer_cols_t_n3(const float* in, __amdgpu_buffer_rsrc_t wr, int N3, int n0, int lane,
+                                                f32x4 (&acc)[4]) {
+  if (N3 <= 16)
+    layer_cols_t<1>(in, SH, wr, n0, lane, acc);
+  else if (N3 == 64)
+    layer_cols_t<4>(in, SH, wr, n0, lane, acc);
+  else if (N3 == 128)
+    layer_cols_t<8>(in, SH, wr, n0, lane, acc);
+  else if (N3 == 192)
+    layer_cols_t<12>(in, SH, wr, n0, lane, acc);
+  else
+    layer_cols_t<16>(in, SH, wr, n0, lane, acc);
+}
+
+// this wave's 64 columns of the forward activations h (rows m0.., row stride ldh), for the
+// gradient epilogue; issued before the layer's MFMAs so that their latency hides behind them
+// (rows past M read 0 through the buffer's bound)
+__device__ __forceinline__ void load_h_tile(const float* h, int64_t ldh, int64_t m0, int64_t M, int n0, int lane,
+                                            float (&hv)[4][4]) {
+  const int c = lane & 15, g = lane >> 4;
+  const int64_t rows = M - m0 < TM ? M - m0 : TM;
+  const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(h + m0 * ldh), (short)0, (int)(((rows - 1) * ldh + HID) * 4), 0x00020000);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rr = 4 * g + q;
+      hv[j][q] = rr < rows ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                           hr, (int)((rr * ldh + n0 + 16 * j + c) * 4), 0, 0))
+                           : 0.0f;
+    }
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_grad_t(float d, float t) {  // gemm.hip act_grad
+  if constexpr (ACT == 1) return t > 0.0f ? d : 0.0f;
+  if constexpr (ACT == 2) return d * (1.0f - t * t);
   return d;
 }
 
-// dh = acc (this wave's 64 columns) -> g = dh * act'(h) (h [rows][ldh] global) into the LDS tile
-// `out` and, when gdst is set, to global rows (ldg)
-__device__ __forceinline__ void grad_epilogue(const f32x4 (&acc)[4], const float* h, int64_t ldh, int act, int n0,
-                                              int lane, int64_t m0, int64_t M, float* out) {
+// dh = acc (this wave's 64 columns) -> g = dh * act'(h) into the LDS tile `out`; rows past M: 0
+template <int ACT>
+__device__ __forceinline__ void grad_epilogue_t(const f32x4 (&acc)[4], const float (&hv)[4][4], int n0, int lane,
+                                                int64_t m0, int64_t M, float* out) {
   const int c = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -290,13 +370,22 @@ __device__ __forceinline__ void grad_epilogue(const f32x4 (&acc)[4], const float
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int64_t row = m0 + 4 * g + q;
-      const float t = row < M ? h[row * ldh + n] : 0.0f;
-      out[(4 * g + q) * SH + n] = row < M ? act_grad_f(acc[j][q], t, act) : 0.0f;
+      out[(4 * g + q) * SH + n] = row < M ? act_grad_t<ACT>(acc[j][q], hv[j][q]) : 0.0f;
     }
   }
 }
 
-__global__ __launch_bounds__(256) void k_mlp3_bwd(Mlp3BwdArgs a) {
+__device__ __forceinline__ void grad_epilogue(const f32x4 (&acc)[4], const float (&hv)[4][4], int act, int n0,
+                                              int lane, int64_t m0, int64_t M, float* out) {
+  if (act == 1)
+    grad_epilogue_t<1>(acc, hv, n0, lane, m0, M, out);
+  else if (act == 2)
+    grad_epilogue_t<2>(acc, hv, n0, lane, m0, M, out);
+  else
+    grad_epilogue_t<0>(acc, hv, n0, lane, m0, M, out);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_mlp3_bwd(Mlp3BwdArgs a) {
   __shared__ float gs3[TM * SH];  // the output gradient tile (N3 <= 256 columns)
   __shared__ float gs2[TM * SH];
   __shared__ float gs1[TM * SH];
@@ -324,9 +413,11 @@ __global__ __launch_bounds__(256) void k_mlp3_bwd(Mlp3BwdArgs a) {
     {
       const __amdgpu_buffer_rsrc_t wr =
           __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(W3), (short)0, N3 * HID * 4, 0x00020000);
+      float hv[4][4];
+      load_h_tile(h2, a.ldh, m0, a.M, n0, lane, hv);
       f32x4 acc[4] = {};
-      layer_cols_t(gs3, SH, wr, N3, n0, lane, acc);
-      grad_epilogue(acc, h2, a.ldh, a.act2, n0, lane, m0, a.M, gs2);
+      layer_cols_t_n3(gs3, wr, N3, n0, lane, acc);
+      grad_epilogue(acc, hv, a.act2, n0, lane, m0, a.M, gs2);
     }
     __syncthreads();
     if (a.g2) store_tile(gs2, a.g2 + q * a.gs_g, a.ldg, m0, a.M, HID);
@@ -334,9 +425,11 @@ __global__ __launch_bounds__(256) void k_mlp3_bwd(Mlp3BwdArgs a) {
     {
       const __amdgpu_buffer_rsrc_t wr =
           __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(W2), (short)0, HID * HID * 4, 0x00020000);
+      float hv[4][4];
+      load_h_tile(h1, a.ldh, m0, a.M, n0, lane, hv);
       f32x4 acc[4] = {};
-      layer_cols_t(gs2, SH, wr, HID, n0, lane, acc);
-      grad_epilogue(acc, h1, a.ldh, a.act1, n0, lane, m0, a.M, gs1);
+      layer_cols_t<HID / 16>(gs2, SH, wr, n0, lane, acc);
+      grad_epilogue(acc, hv, a.act1, n0, lane, m0, a.M, gs1);
     }
     __syncthreads();
     if (a.g1) store_tile(gs1, a.g1 + q * a.gs_g, a.ldg, m0, a.M, HID);

@@ -53,22 +53,22 @@ struct PolicyLds {
   const uint4* w1;      // layer-1 fragments [blk][split][lane] (LDS: no memory loads inside a pass)
   const float* obs;     // [256][D] observations of the workgroup's envs
   float* lgt;           // [256][N3] logits out
-  uint32_t* bar;        // policy-wave barrier counter (MH_FUSED_POLICY_DMA)
+  uint32_t* bar;        // policy-wave barrier counter (default chunk staging)
   int64_t* err;         // device error word (bounded waits that timed out)
   uint32_t* landed;     // loader path: chunk c of the horizon is in LDS once landed >= 2 (c + 1)
   uint32_t* released;   // loader path: chunk c's buffer is free again once released >= 4 (c + 1)
 };
 
-#ifndef MH_FUSED_POLICY_DMA
-// W2 chunks are staged by LOADER waves: in each pass the env waves of the half that is not stepping
-// (they would otherwise wait at the pass's closing barrier) issue the pass's chunk DMAs, wait for
-// them to land and publish each chunk through an LDS counter; the policy waves only wait for that
-// counter and release each buffer after their last read of it. The policy waves' instruction
-// stream then carries no LDS-DMA issue (8 pieces per wave per phase, ~100 cycles each inside an
-// MFMA phase: MI355X_MICROARCH.md, constants) and no drain of their own DMA, and no policy wave
-// waits for the others (each waits only for the data it reads).
-#define MH_FUSED_LOADERS 1
-#endif
+// W2 chunk staging. Default: each policy wave issues its share of the pass's chunk DMAs itself
+// (LDS-DMA, two buffers, a policy-wave barrier per chunk).
+// MH_FUSED_LOADERS: the chunks are staged by LOADER waves instead: in each pass the env waves of
+// the half that is not stepping (they would otherwise wait at the pass's closing barrier) issue the
+// pass's chunk DMAs, wait for them to land and publish each chunk through an LDS counter; the
+// policy waves only wait for that counter and release each buffer after their last read of it, so
+// their instruction stream carries no LDS-DMA issue and no policy wave waits for the others. It
+// measured SLOWER on MI355X (QuadTracking, 65,536 envs, 20 lock-steps: 637-641 us per horizon vs
+// 585-595 us for the default; profiles/r04_fused_loader_ab.jsonl): the loader half's polling and
+// the extra LDS-counter round trips cost more than the policy waves' DMA issue slots.
 #ifdef MH_FUSED_LOADERS
 constexpr bool kLoaders = true;
 #else
@@ -745,7 +745,7 @@ void k_sample_fused(FusedArgs a) {
   } else {
 #ifdef MH_FUSED_EXP_NO_ENV  // cost-attribution experiment only
 #ifdef MH_FUSED_LOADERS
-#error "MH_FUSED_EXP_NO_ENV removes the loader waves: build it with MH_FUSED_POLICY_DMA"
+#error "MH_FUSED_EXP_NO_ENV removes the loader waves: build it without MH_FUSED_LOADERS"
 #endif
     if (false)
 #endif
