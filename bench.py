@@ -170,9 +170,40 @@ def main():
         torch.cuda.synchronize()
         ph_s += tb_ - ta
         ph_u += time.perf_counter() - tb_
+    # host enqueue rate: the host time of trainer steps without a sync (it only blocks when the
+    # device queue is full or a call waits) against the same steps' wall time: equal = host-bound
+    k_host = 6
+    host_parts = {}
+
+    def timed(obj, name):  # wrap a bound method with a host timer (restored below)
+        fn = getattr(obj, name)
+
+        def w(*args, **kw):
+            t = time.perf_counter()
+            try:
+                return fn(*args, **kw)
+            finally:
+                host_parts[name] = host_parts.get(name, 0.0) + time.perf_counter() - t
+        setattr(obj, name, w)
+        return name
+
+    wrapped = [(trainer, timed(trainer, "_sample")), (trainer, timed(trainer, "_replay_batch")),
+               (alg, timed(alg, "model_update")), (buffer, timed(buffer, "add_batch"))]
+    torch.cuda.synchronize()
+    th0 = time.perf_counter()
+    for _ in range(k_host):
+        one_step()
+    th1 = time.perf_counter()
+    torch.cuda.synchronize()
+    th2 = time.perf_counter()
+    for obj, name in wrapped:
+        delattr(obj, name)
     phases = {"sample_ms": round(ph_s / 2 * 1e3, 3), "replay_and_update_ms": round(ph_u / 2 * 1e3, 3),
               "sampler_only_env_steps_per_s": round(a.envs * horizon / (ph_s / 2), 1),
-              "update_to_data_ratio": round(1.0 / (a.envs * horizon), 9)}
+              "update_to_data_ratio": round(1.0 / (a.envs * horizon), 9),
+              "host_enqueue_ms_per_step": round((th1 - th0) / k_host * 1e3, 3),
+              "wall_ms_per_step_same_steps": round((th2 - th0) / k_host * 1e3, 3),
+              "host_ms_per_step_by_call": {k: round(v / k_host * 1e3, 3) for k, v in host_parts.items()}}
 
     # ---- per-kernel durations, right after the timed region: HIP events on the launch stream
     # around R back-to-back launches of the engine's lockstep kernels on the live pipeline state

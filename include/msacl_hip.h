@@ -495,6 +495,16 @@ int mh_replay_gather(const mh_window_store_t* store, int32_t n_step, int32_t obs
                      float* out_act, float* out_rew, float* out_cost, float* out_obs2,
                      float* out_done, float* out_logp, void* stream);
 
+/* mh_replay_gather plus the two joint layouts the MSACL update reads, so that it concatenates
+ * nothing per update (RL/algorithm/msacl.py:236-238 q(obs, act) and :395-396 V(obs_0), V(obs2)):
+ * out_obs_act [batch][n][obs_dim + act_dim] = [obs | act] rows; out_v_in [batch + batch n][obs_dim]
+ * = obs[b][0] for every b, then obs2[b][t] rows in (b, t) order. Either may be NULL. */
+int mh_replay_gather_joint(const mh_window_store_t* store, int32_t n_step, int32_t obs_dim,
+                           int32_t act_dim, const int64_t* idx, int64_t batch, float* out_obs,
+                           float* out_act, float* out_rew, float* out_cost, float* out_obs2,
+                           float* out_done, float* out_logp, float* out_obs_act, float* out_v_in,
+                           void* stream);
+
 /* Device uniform indices in [0, size) from the store cursor (np.random.randint at
  * nstep_replay_buffer.py:138), keyed by (seed, draw counter). */
 int mh_replay_sample_indices(const mh_window_store_t* store, uint64_t seed, uint64_t counter,

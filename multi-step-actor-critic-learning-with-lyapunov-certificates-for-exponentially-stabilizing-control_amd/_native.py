@@ -158,6 +158,8 @@ _PROTOS = {
     "mh_env_read_timing": (ctypes.c_int, [c_vp, ctypes.POINTER(c_f64), ctypes.POINTER(c_i64), c_i32]),
     "mh_replay_gather": (ctypes.c_int, [ctypes.POINTER(WindowStore), c_i32, c_i32, c_i32, c_vp, c_i64,
                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "mh_replay_gather_joint": (ctypes.c_int, [ctypes.POINTER(WindowStore), c_i32, c_i32, c_i32, c_vp, c_i64]
+                               + [c_vp] * 10),
     "mh_replay_sample_indices": (ctypes.c_int, [ctypes.POINTER(WindowStore), c_u64, c_u64, c_i64, c_vp, c_vp]),
     "mh_msacl_q_target": (ctypes.c_int, [c_vp] * 9 + [c_f32, c_i32, c_i32] + [c_vp] * 5 + [c_vp]),
     "mh_msacl_lyapunov": (ctypes.c_int, [c_vp] * 9 + [c_f32] * 4 + [c_i32] * 3 + [c_vp] * 6 + [c_vp]),

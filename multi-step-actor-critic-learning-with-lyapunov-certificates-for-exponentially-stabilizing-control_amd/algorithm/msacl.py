@@ -19,6 +19,7 @@ formulas as host loops) — chosen by configuration, never as a fallback of the 
 __all__ = ["ApproxContainer", "MSACL"]
 
 import math
+import os
 import time
 from copy import deepcopy
 from collections.abc import Mapping
@@ -334,6 +335,9 @@ class MSACL:
         self._alpha_grad = None
         self._alpha_grad_ready = False  # _alpha_grad already holds this policy step's gradient
         self.use_graph = bool(kwargs.get("alg_use_graph", True))
+        # the trainer asks a device replay buffer for the batch's [obs | act] and [obs_0; obs2]
+        # layouts too (gathered, not concatenated per update); MSACL_JOINT_BATCH=0: torch.cat (A/B)
+        self.wants_joint_batch = (self.device.type == "cuda" and os.environ.get("MSACL_JOINT_BATCH", "1") == "1")
         # the Lyapunov update shares no parameter with the critic update (both only read the
         # policy and the batch): on one GPU it runs on a second stream, concurrently
         self.concurrent = bool(kwargs.get("alg_concurrent_streams", True))
@@ -645,7 +649,9 @@ class MSACL:
                 next_logp = torch.empty(B, n, dtype=torch.float32, device=self.device)
                 _engine("policy_head", self.device, N.ptr(raw.contiguous()), N.ptr(eps.contiguous()), N.ptr(obs2), None,
                         N.ptr(hi), N.ptr(lo), B * n, A, Dd, lsl, lsh, N.ptr(xq2), N.ptr(next_logp), None)
-            xa = torch.cat([obs, act], dim=-1)
+            xa = data.get("obs_act")  # [obs | act], written by the replay gather (mh_replay_gather_joint)
+            if xa is None:
+                xa = torch.cat([obs, act], dim=-1)
             tc = self._twin_critics(B * n)
             if tc is not None:
                 return self._q_update_twin(tc, data, xa, xq2, next_logp, s, defer_step, stats)
@@ -758,7 +764,10 @@ class MSACL:
         with torch.no_grad():
             # V(obs_0) and V(obs2) as one batch (msacl.py:395-396)
             D_ = obs.shape[-1]
-            V_all = self.networks.lyapunov(torch.cat([obs[:, 0], obs2.reshape(-1, D_)], 0))
+            v_in = data.get("v_in")  # [obs[:, 0]; obs2 rows], written by the replay gather
+            if v_in is None:
+                v_in = torch.cat([obs[:, 0], obs2.reshape(-1, D_)], 0)
+            V_all = self.networks.lyapunov(v_in)
             V0 = V_all[:B].contiguous()
             V2 = V_all[B:].reshape(B, n).contiguous()
         _engine("msacl_stability_adv", self.device, N.ptr(V0), N.ptr(V2), N.ptr(self.lya_diff_coef),

@@ -279,7 +279,23 @@ def layer_backward(dy, x, weight, y, act, need_x, need_w, need_b):
 
 # The whole 3-layer MLP forward as one launch (mh_mlp3_forward, csrc/mlp_fused.hip) where the
 # shape qualifies; MSACL_MLP3=0 restores the per-layer launches (A/B)
-_MLP3 = {"on": os.environ.get("MSACL_MLP3", "1") == "1"}
+_MLP3 = {"on": os.environ.get("MSACL_MLP3", "1") == "1",
+         # wide outputs (N3 a multiple of 64: the policy trunk): forward through the per-layer
+         # kernels (every CU on a column block) instead of the one-launch kernel, which re-reads the
+         # 256 x 256 weights per 16-row tile twice there; MSACL_MLP3_WIDE=1 takes the fused forward
+         "wide_fwd": os.environ.get("MSACL_MLP3_WIDE", "0") == "1"}
+
+
+def _linear_act(x, W, b, act):
+    """LinearAct's forward kernels without autograd: act(x W^T + b)."""
+    M, K = x.shape
+    Nout = W.shape[0]
+    if _hip_forward(M, Nout, act, K):
+        return gemm(x, W.contiguous(), b.contiguous(), M, Nout, K, x.stride(0), K, 0, 1, act)
+    if act == 1:
+        return torch._addmm_activation(b, x, W.t())
+    y = torch.addmm(b, x, W.t())
+    return torch.tanh_(y) if act == 2 else y
 
 
 def mlp3_forward(x, layers, acts, h_keep, groups=1, strides=None, ldh=None, y=None, ldy=None):
@@ -341,7 +357,12 @@ class MLP3(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W1, b1, W2, b2, W3, b3, acts):
         keep = any(ctx.needs_input_grad[:7])
-        y, h1, h2 = mlp3_forward(x, ((W1, b1), (W2, b2), (W3, b3)), acts, keep)
+        if W3.shape[0] > 16 and not _MLP3["wide_fwd"]:
+            h1 = _linear_act(x, W1, b1, acts[0])
+            h2 = _linear_act(h1, W2, b2, acts[1])
+            y = _linear_act(h2, W3, b3, acts[2])
+        else:
+            y, h1, h2 = mlp3_forward(x, ((W1, b1), (W2, b2), (W3, b3)), acts, keep)
         ctx.acts = acts
         if keep:
             ctx.save_for_backward(x, W1, W2, W3, h1, h2, y)

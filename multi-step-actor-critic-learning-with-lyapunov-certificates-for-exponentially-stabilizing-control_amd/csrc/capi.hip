@@ -1223,6 +1223,27 @@ int mh_replay_gather(const mh_window_store_t* store, int32_t n_step, int32_t obs
   g.s_obs2 = store->obs2; g.s_done = store->done; g.s_logp = store->logp;
   g.o_obs = out_obs; g.o_act = out_act; g.o_rew = out_rew; g.o_cost = out_cost;
   g.o_obs2 = out_obs2; g.o_done = out_done; g.o_logp = out_logp;
+  g.o_obs_act = nullptr; g.o_v_in = nullptr;
+  MH_HIP(mh::launch_gather(g, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_replay_gather_joint(const mh_window_store_t* store, int32_t n_step, int32_t obs_dim, int32_t act_dim,
+                           const int64_t* idx, int64_t batch, float* out_obs, float* out_act, float* out_rew,
+                           float* out_cost, float* out_obs2, float* out_done, float* out_logp, float* out_obs_act,
+                           float* out_v_in, void* stream) {
+  if (!store || !idx) return fail(MH_EINVAL, "mh_replay_gather_joint: null store/idx");
+  mh::GatherArgs g;
+  g.idx = idx;
+  g.batch = batch;
+  g.n = n_step;
+  g.D = obs_dim;
+  g.A = act_dim;
+  g.s_obs = store->obs; g.s_act = store->act; g.s_rew = store->rew; g.s_cost = store->cost;
+  g.s_obs2 = store->obs2; g.s_done = store->done; g.s_logp = store->logp;
+  g.o_obs = out_obs; g.o_act = out_act; g.o_rew = out_rew; g.o_cost = out_cost;
+  g.o_obs2 = out_obs2; g.o_done = out_done; g.o_logp = out_logp;
+  g.o_obs_act = out_obs_act; g.o_v_in = out_v_in;
   MH_HIP(mh::launch_gather(g, (hipStream_t)stream));
   return MH_OK;
 }

@@ -36,7 +36,13 @@ constexpr int HID = 256;      // hidden width
 constexpr int SH = HID + 4;   // LDS row stride of a hidden tile (floats): rows 16 B apart in the banks
 constexpr int K1P = 32;       // first-layer K padded
 constexpr int SX = K1P + 4;
-constexpr int PF = 4;         // weight groups in the load ring: three in flight behind the MFMAs
+#ifndef MH_MLP_PF
+#define MH_MLP_PF 4
+#endif
+#ifndef MH_MLP_PFT
+#define MH_MLP_PFT 3
+#endif
+constexpr int PF = MH_MLP_PF;  // weight groups in the load ring: PF - 1 in flight behind the MFMAs
 
 // The load ring is enforced with scheduling barriers: left to itself the scheduler regroups the
 // fully unrolled loop and waits on each group's loads right after issuing them (one L2 latency per
@@ -60,37 +66,68 @@ __device__ __forceinline__ float act_f(float v, int act) {
 // K = 16 G. `in` is the LDS tile (row stride SIN floats), W rows [n0, n0 + 64) of a row-major [N][K]
 // matrix behind a buffer resource (rows past N read 0). Group u's four weight float4s are issued
 // PF - 1 groups before its MFMAs; its A operand (one ds_read_b128) one group before.
-template <int SIN, int G>
-__device__ __forceinline__ void layer_cols(const float* in, __amdgpu_buffer_rsrc_t wr, int n0, int lane,
-                                           f32x4 (&acc)[4]) {
+// layer_cols_pre issues the ring's first PF - 1 groups (the caller may do so long before the layer:
+// the forward issues layer 2's at kernel start, beside layer 1's weights), layer_cols_run the rest.
+template <int G>
+__device__ __forceinline__ void wring_load(__amdgpu_buffer_rsrc_t wr, int n0, int lane, int u, f32x4 (&dst)[4]) {
   constexpr int K = 16 * G;
   const int r = lane & 15, g = lane >> 4;
   const int voff = ((n0 + r) * K + 4 * g) * 4;
-  f32x4 wb[PF][4];
-  auto load = [&](int u, f32x4 (&dst)[4]) {
+#ifdef MH_MLP_EXP_PACKED  // cost-attribution experiment only: fragment-ordered addresses (wrong results)
+  for (int j = 0; j < 4; ++j)
+    dst[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           wr, (((n0 / 16 + j) * G + u) * 64 + lane) * 16, 0, 0));
+  return;
+#endif
+#ifdef MH_MLP_EXP_NOLOAD  // cost-attribution experiment only: no weight loads (wrong results)
+  for (int j = 0; j < 4; ++j) dst[j] = f32x4{(float)voff, 0.f, 1.f, (float)u};
+  return;
+#endif
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      dst[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, voff + (16 * j * K + 16 * u) * 4, 0, 0));
-  };
-  const float* arow = in + r * SIN + 4 * g;
+  for (int j = 0; j < 4; ++j)
+    dst[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, voff + (16 * j * K + 16 * u) * 4, 0, 0));
+}
+
+template <int G>
+__device__ __forceinline__ void layer_cols_pre(__amdgpu_buffer_rsrc_t wr, int n0, int lane, f32x4 (&wb)[PF][4]) {
 #pragma unroll
   for (int p = 0; p < PF - 1; ++p)
-    if (p < G) load(p, wb[p]);
+    if (p < G) wring_load<G>(wr, n0, lane, p, wb[p]);
+}
+
+template <int SIN, int G>
+__device__ __forceinline__ void layer_cols_run(const float* in, __amdgpu_buffer_rsrc_t wr, int n0, int lane,
+                                               f32x4 (&acc)[4], f32x4 (&wb)[PF][4]) {
+  const int r = lane & 15, g = lane >> 4;
+  const float* arow = in + r * SIN + 4 * g;
   f32x4 a_cur = *reinterpret_cast<const f32x4*>(arow);
 #pragma unroll
   for (int u = 0; u < G; ++u) {
-    if (u + PF - 1 < G) load(u + PF - 1, wb[(u + PF - 1) % PF]);
+    if (u + PF - 1 < G) wring_load<G>(wr, n0, lane, u + PF - 1, wb[(u + PF - 1) % PF]);
     f32x4 a_nxt = a_cur;
     if (u + 1 < G) a_nxt = *reinterpret_cast<const f32x4*>(arow + 16 * (u + 1));
     MH_SCHED_FENCE();
+#ifdef MH_MLP_EXP_NOMFMA  // cost-attribution experiment only: operands consumed, no MFMA (wrong results)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] += a_cur * wb[u % PF][j];
+#else
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t], wb[u % PF][j][t], acc[j], 0, 0, 0);
+#endif
     MH_SCHED_FENCE();
     a_cur = a_nxt;
   }
+}
+
+template <int SIN, int G>
+__device__ __forceinline__ void layer_cols(const float* in, __amdgpu_buffer_rsrc_t wr, int n0, int lane,
+                                           f32x4 (&acc)[4]) {
+  f32x4 wb[PF][4];
+  layer_cols_pre<G>(wr, n0, lane, wb);
+  layer_cols_run<SIN, G>(in, wr, n0, lane, acc, wb);
 }
 
 // bias + activation of this wave's 64 columns into the LDS tile `out` (row stride SH); the MFMA's
@@ -156,6 +193,12 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
   // ---- the hidden layers' biases and layer 1's weights first (their latency overlaps the input
   // staging): W1 [H][K1], lane group
   // g of column n reads k = 16 u + 4 g + t; k >= K1 lands past the buffer's end and reads 0
+  // layer 2's first weight groups go out first: they depend on nothing, and layer 2 then starts
+  // without a round trip
+  const __amdgpu_buffer_rsrc_t wr2 =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.W2), (short)0, HID * HID * 4, 0x00020000);
+  f32x4 wb2[PF][4];
+  layer_cols_pre<HID / 16>(wr2, n0, lane, wb2);
   float w1[2][4][4], bias1[4], bias2[4];
   {
 #pragma unroll
@@ -180,14 +223,21 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
   }
 
   // ---- the input rows, zero-padded to K1p columns (rows past M: zeros)
-  for (int i = tid; i < TM * K1p; i += 256) {
-    const int rr = i / K1p, k = i - rr * K1p;
-    xs[rr * SX + k] = (m0 + rr < a.M && k < K1) ? a.x[(m0 + rr) * a.ldx + k] : 0.0f;
+  {  // TM x K1p <= 512 elements: both of a thread's loads issued before either store
+    float xv[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = tid + 256 * s, rr = i / K1p, k = i - rr * K1p;
+      xv[s] = (i < TM * K1p && m0 + rr < a.M && k < K1) ? a.x[(m0 + rr) * a.ldx + k] : 0.0f;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int i = tid + 256 * s, rr = i / K1p, k = i - rr * K1p;
+      if (i < TM * K1p) xs[rr * SX + k] = xv[s];
+    }
   }
   __syncthreads();
 
-  const __amdgpu_buffer_rsrc_t wr2 =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.W2), (short)0, HID * HID * 4, 0x00020000);
   // ---- layer 1: K1p <= 32
   {
     f32x4 acc[4] = {};
@@ -213,7 +263,7 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
   f32x4 w3[4];  // the narrow output layer's weights (N3 <= 16), issued before layer 2's epilogue
   {
     f32x4 acc[4] = {};
-    layer_cols<SH, HID / 16>(hs1, wr2, n0, lane, acc);
+    layer_cols_run<SH, HID / 16>(hs1, wr2, n0, lane, acc, wb2);
     if (N3 <= 16) {
 #pragma unroll
       for (int uu = 0; uu < 4; ++uu)
@@ -280,30 +330,44 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
 // values lie in four rows (scalar loads, 64 consecutive bytes per 16 lanes). Rows past `nrows` read 0.
 // (the weight rows are HID floats long; rows at or past `nrows` lie beyond the buffer resource)
 // Same load ring as layer_cols (depth PFT: sixteen scalars a group), group u issued PFT - 1 groups ahead.
-constexpr int PFT = 3;
+constexpr int PFT = MH_MLP_PFT;
 template <int G>
-__device__ __forceinline__ void layer_cols_t(const float* in, int sin, __amdgpu_buffer_rsrc_t wr, int n0, int lane,
-                                             f32x4 (&acc)[4]) {
+__device__ __forceinline__ void wring_t_load(__amdgpu_buffer_rsrc_t wr, int n0, int lane, int u, float (&dst)[4][4]) {
   const int c = lane & 15, g = lane >> 4;
   const int voff = ((4 * g) * HID + n0 + c) * 4;  // + (t HID + 16 j) 4: immediate offsets
-  float wb[PFT][4][4];
-  auto load = [&](int u, float (&dst)[4][4]) {
-    const int soff = u * 16 * HID * 4;
+  const int soff = u * 16 * HID * 4;
+#ifdef MH_MLP_EXP_PACKED  // cost-attribution experiment only: fragment-ordered addresses (wrong results)
+  for (int j = 0; j < 4; ++j) {
+    const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  wr, (((n0 / 16 + j) * G + u) * 64 + lane) * 16, 0, 0));
+    for (int t = 0; t < 4; ++t) dst[j][t] = v[t];
+  }
+  return;
+#endif
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int t = 0; t < 4; ++t)
-        dst[j][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, voff + (t * HID + 16 * j) * 4,
-                                                                                 soff, 0));
-  };
+    for (int t = 0; t < 4; ++t)
+      dst[j][t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, voff + (t * HID + 16 * j) * 4,
+                                                                               soff, 0));
+}
+
+template <int G, int D = PFT>
+__device__ __forceinline__ void layer_cols_t_pre(__amdgpu_buffer_rsrc_t wr, int n0, int lane, float (&wb)[D][4][4]) {
+#pragma unroll
+  for (int p = 0; p < D - 1; ++p)
+    if (p < G) wring_t_load<G>(wr, n0, lane, p, wb[p]);
+}
+
+template <int G, int D = PFT>
+__device__ __forceinline__ void layer_cols_t_run(const float* in, int sin, __amdgpu_buffer_rsrc_t wr, int n0, int lane,
+                                                 f32x4 (&acc)[4], float (&wb)[D][4][4]) {
+  const int c = lane & 15, g = lane >> 4;
   const float* arow = in + c * sin + 4 * g;
-#pragma unroll
-  for (int p = 0; p < PFT - 1; ++p)
-    if (p < G) load(p, wb[p]);
   f32x4 a_cur = *reinterpret_cast<const f32x4*>(arow);
 #pragma unroll
   for (int u = 0; u < G; ++u) {
-    if (u + PFT - 1 < G) load(u + PFT - 1, wb[(u + PFT - 1) % PFT]);
+    if (u + D - 1 < G) wring_t_load<G>(wr, n0, lane, u + D - 1, wb[(u + D - 1) % D]);
     f32x4 a_nxt = a_cur;
     if (u + 1 < G) a_nxt = *reinterpret_cast<const f32x4*>(arow + 16 * (u + 1));
     MH_SCHED_FENCE();
@@ -311,25 +375,31 @@ __device__ __forceinline__ void layer_cols_t(const float* in, int sin, __amdgpu_
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t], wb[u % PFT][j][t], acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t], wb[u % D][j][t], acc[j], 0, 0, 0);
     MH_SCHED_FENCE();
     a_cur = a_nxt;
   }
 }
 
-// the output-gradient contraction over W3's N3 rows: N3 <= 16 or a multiple of 64
+template <int G, int D = PFT>
+__device__ __forceinline__ void layer_cols_t(const float* in, int sin, __amdgpu_buffer_rsrc_t wr, int n0, int lane,
+                                             f32x4 (&acc)[4]) {
+  float wb[D][4][4];
+  layer_cols_t_pre<G, D>(wr, n0, lane, wb);
+  layer_cols_t_run<G, D>(in, sin, wr, n0, lane, acc, wb);
+}
+
+// the output-gradient contraction over W3's N3 rows, N3 a multiple of 64
 __device__ __forceinline__ void layer_cols_t_n3(const float* in, __amdgpu_buffer_rsrc_t wr, int N3, int n0, int lane,
                                                 f32x4 (&acc)[4]) {
-  if (N3 <= 16)
-    layer_cols_t<1>(in, SH, wr, n0, lane, acc);
-  else if (N3 == 64)
-    layer_cols_t<4>(in, SH, wr, n0, lane, acc);
+  if (N3 == 64)
+    layer_cols_t<4, 3>(in, SH, wr, n0, lane, acc);
   else if (N3 == 128)
-    layer_cols_t<8>(in, SH, wr, n0, lane, acc);
+    layer_cols_t<8, 3>(in, SH, wr, n0, lane, acc);
   else if (N3 == 192)
-    layer_cols_t<12>(in, SH, wr, n0, lane, acc);
+    layer_cols_t<12, 3>(in, SH, wr, n0, lane, acc);
   else
-    layer_cols_t<16>(in, SH, wr, n0, lane, acc);
+    layer_cols_t<16, 3>(in, SH, wr, n0, lane, acc);
 }
 
 // this wave's 64 columns of the forward activations h (rows m0.., row stride ldh), for the
@@ -385,6 +455,9 @@ __device__ __forceinline__ void grad_epilogue(const f32x4 (&acc)[4], const float
     grad_epilogue_t<0>(acc, hv, n0, lane, m0, M, out);
 }
 
+// NARROW (N3 <= 16): the W2 product's weight ring is issued before the W3 product; the wide form
+// (N3 a multiple of 64) has no registers for that beside the W3 product's own ring.
+template <bool NARROW>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_mlp3_bwd(Mlp3BwdArgs a) {
   __shared__ float gs3[TM * SH];  // the output gradient tile (N3 <= 256 columns)
   __shared__ float gs2[TM * SH];
@@ -404,6 +477,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     const float* W2 = a.W2 + q * a.gs_W2;
     const float* W3 = a.W3 + q * a.gs_W3;
     if (q > 0) __syncthreads();  // the previous group's tiles are read
+    // the W2 product's first weight groups and the h2 tile go out before the output-gradient
+    // staging: they depend on nothing, and their round trip overlaps it and the W3 product
+    const __amdgpu_buffer_rsrc_t wr2 =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(W2), (short)0, HID * HID * 4, 0x00020000);
+    float wb2[PFT][4][4];
+    if constexpr (NARROW) layer_cols_t_pre<HID / 16>(wr2, n0, lane, wb2);
+    float hv2[4][4];
+    load_h_tile(h2, a.ldh, m0, a.M, n0, lane, hv2);
     for (int i = tid; i < TM * N3p; i += 256) {
       const int rr = i / N3p, k = i - rr * N3p;
       gs3[rr * SH + k] = (m0 + rr < a.M && k < N3) ? dy[(m0 + rr) * a.ldy + k] : 0.0f;
@@ -413,22 +494,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     {
       const __amdgpu_buffer_rsrc_t wr =
           __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(W3), (short)0, N3 * HID * 4, 0x00020000);
-      float hv[4][4];
-      load_h_tile(h2, a.ldh, m0, a.M, n0, lane, hv);
       f32x4 acc[4] = {};
-      layer_cols_t_n3(gs3, wr, N3, n0, lane, acc);
-      grad_epilogue(acc, hv, a.act2, n0, lane, m0, a.M, gs2);
+      if constexpr (NARROW)
+        layer_cols_t<1>(gs3, SH, wr, n0, lane, acc);
+      else
+        layer_cols_t_n3(gs3, wr, N3, n0, lane, acc);
+      grad_epilogue(acc, hv2, a.act2, n0, lane, m0, a.M, gs2);
     }
     __syncthreads();
     if (a.g2) store_tile(gs2, a.g2 + q * a.gs_g, a.ldg, m0, a.M, HID);
     // dh1 = g2 W2, g1 = dh1 * act1'(h1)
     {
-      const __amdgpu_buffer_rsrc_t wr =
-          __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(W2), (short)0, HID * HID * 4, 0x00020000);
       float hv[4][4];
       load_h_tile(h1, a.ldh, m0, a.M, n0, lane, hv);
       f32x4 acc[4] = {};
-      layer_cols_t<HID / 16>(gs2, SH, wr, n0, lane, acc);
+      if constexpr (NARROW)
+        layer_cols_t_run<HID / 16>(gs2, SH, wr2, n0, lane, acc, wb2);
+      else
+        layer_cols_t<HID / 16, 3>(gs2, SH, wr2, n0, lane, acc);  // (registers: the wide form keeps depth 3)
       grad_epilogue(acc, hv, a.act1, n0, lane, m0, a.M, gs1);
     }
     __syncthreads();
@@ -491,7 +574,10 @@ bool mlp3_supported(int64_t M, int K1, int H, int N3) {
 hipError_t launch_mlp3_backward(const Mlp3BwdArgs& a, hipStream_t st) {
   if (!mlp3_supported(a.M, a.K1, a.H, a.N3) || a.groups < 1) return hipErrorInvalidValue;
   const int64_t tiles = (a.M + TM - 1) / TM;
-  k_mlp3_bwd<<<(unsigned)tiles, 256, 0, st>>>(a);
+  if (a.N3 <= 16)
+    k_mlp3_bwd<true><<<(unsigned)tiles, 256, 0, st>>>(a);
+  else
+    k_mlp3_bwd<false><<<(unsigned)tiles, 256, 0, st>>>(a);
   return hipGetLastError();
 }
 

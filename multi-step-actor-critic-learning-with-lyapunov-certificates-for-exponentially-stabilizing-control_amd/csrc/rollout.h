@@ -102,6 +102,10 @@ struct GatherArgs {
   int n, D, A;
   const float *s_obs, *s_act, *s_rew, *s_cost, *s_obs2, *s_done, *s_logp;
   float *o_obs, *o_act, *o_rew, *o_cost, *o_obs2, *o_done, *o_logp;
+  // joint layouts the update consumes (null: not written): o_obs_act [batch][n][D + A] = [obs | act]
+  // rows (the critics' input), o_v_in [batch + batch n][D] = obs(b, 0) rows then the obs2 rows (the
+  // Lyapunov network's batch of the stability advantage)
+  float *o_obs_act, *o_v_in;
 };
 
 hipError_t launch_rollout(int env_id, const StepArgs& a, hipStream_t st);

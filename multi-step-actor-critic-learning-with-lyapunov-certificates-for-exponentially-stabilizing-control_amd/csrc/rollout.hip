@@ -821,7 +821,34 @@ __device__ __forceinline__ void gather_rows(const float* src, float* dst, const 
   }
 }
 
+// the joint layouts: element-wise (D + A and D are small), rows of the windows at idx
+__device__ __forceinline__ void gather_joint(const GatherArgs& a) {
+  const int64_t n = a.n, D = a.D, A = a.A;
+  if (blockIdx.y == 7) {
+    const int64_t W = D + A, total = a.batch * n * W;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
+      const int64_t row = q / W, c = q - row * W, b = row / n, t = row - b * n, w = a.idx[b];
+      a.o_obs_act[q] = c < D ? a.s_obs[(w * n + t) * D + c] : a.s_act[(w * n + t) * A + (c - D)];
+    }
+  } else {
+    const int64_t total = (a.batch + a.batch * n) * D;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
+      const int64_t row = q / D, c = q - row * D;
+      if (row < a.batch) {
+        a.o_v_in[q] = a.s_obs[(a.idx[row] * n) * D + c];
+      } else {
+        const int64_t r = row - a.batch, b = r / n, t = r - b * n;
+        a.o_v_in[q] = a.s_obs2[(a.idx[b] * n + t) * D + c];
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_gather(GatherArgs a) {
+  if (blockIdx.y >= 7) {
+    if ((blockIdx.y == 7 && a.o_obs_act) || (blockIdx.y == 8 && a.o_v_in)) gather_joint(a);
+    return;
+  }
   const float* src;
   float* dst;
   int w;
@@ -957,7 +984,7 @@ hipError_t launch_gather(const GatherArgs& a, hipStream_t st) {
   if (a.batch <= 0) return hipSuccess;
   const int64_t vec = (a.batch * (int64_t)a.n * (a.D > a.A ? a.D : a.A) + 1023) / 1024;  // float4s of the widest array
   const int gx = (int)(vec < 1 ? 1 : (vec > 2048 ? 2048 : vec));
-  k_gather<<<dim3(gx, 7), 256, 0, st>>>(a);
+  k_gather<<<dim3(gx, (a.o_obs_act || a.o_v_in) ? 9 : 7), 256, 0, st>>>(a);
   return hipGetLastError();
 }
 hipError_t launch_sample_idx(const int64_t* cursor, uint64_t seed, uint64_t counter, int64_t batch,

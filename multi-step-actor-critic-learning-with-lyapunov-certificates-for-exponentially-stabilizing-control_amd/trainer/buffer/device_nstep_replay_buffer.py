@@ -146,24 +146,40 @@ class DeviceNstepReplayBuffer:
                 return False
         return True
 
-    def gather(self, idx, out=None):
+    def _joint_shapes(self, B):
+        n, D, A = self.n_step, self.obsv_dim, self.act_dim
+        return {"obs_act": (B, n, D + A), "v_in": (B + B * n, D)}
+
+    def gather(self, idx, out=None, joint=False):
         """The windows at `idx` as [B, n, ...] tensors; into `out` (a dict of such tensors, e.g.
         the update graph's static inputs, so the replayed update needs no copy) when it fits,
-        otherwise into fresh tensors."""
+        otherwise into fresh tensors. joint (or `out` holding them): also the update's joint
+        layouts "obs_act" = [obs | act] and "v_in" = [obs[:, 0]; obs2 rows] (mh_replay_gather_joint)."""
         B = int(idx.numel())
         n, D, A = self.n_step, self.obsv_dim, self.act_dim
+        e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
+        js = self._joint_shapes(B)
         if self._fits(out, B):
-            out = {k: out[k] for k in KEYS}
+            dst = {k: out[k] for k in KEYS}
+            for k, shp in js.items():
+                t = out.get(k)
+                if (t is not None and tuple(t.shape) == shp and t.dtype == torch.float32 and t.device == self.device
+                        and t.is_contiguous()):
+                    dst[k] = t
         else:
-            e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
-            out = {"obs": e(B, n, D), "act": e(B, n, A), "rew": e(B, n), "cost": e(B, n), "obs2": e(B, n, D),
+            dst = {"obs": e(B, n, D), "act": e(B, n, A), "rew": e(B, n), "cost": e(B, n), "obs2": e(B, n, D),
                    "done": e(B, n), "logp": e(B, n)}
+            if joint:
+                dst.update({k: e(*shp) for k, shp in js.items()})
         idx = idx.to(self.device, torch.int64).contiguous()
-        N.check(N.lib().mh_replay_gather(ctypes.byref(self.ws), n, D, A, N.ptr(idx), B,
-                                         *[N.ptr(out[k]) for k in KEYS], N.stream_of(self.device)), "mh_replay_gather")
-        return out
+        N.check(N.lib().mh_replay_gather_joint(ctypes.byref(self.ws), n, D, A, N.ptr(idx), B,
+                                               *[N.ptr(dst[k]) for k in KEYS], N.ptr(dst.get("obs_act")),
+                                               N.ptr(dst.get("v_in")), N.stream_of(self.device)),
+                "mh_replay_gather_joint")
+        return dst
 
-    def sample_batch(self, batch_size: int, out=None) -> dict:
-        """nstep_replay_buffer.py:136-148. `out` (optional): destination tensors (gather)."""
+    def sample_batch(self, batch_size: int, out=None, joint=False) -> dict:
+        """nstep_replay_buffer.py:136-148. `out` (optional): destination tensors (gather); joint:
+        add the update's joint layouts (gather)."""
         idx = self.sample_indices(batch_size)
-        return self.gather(idx, out) if out is not None else self.gather(idx)
+        return self.gather(idx, out, joint)

@@ -91,6 +91,8 @@ class NstepOffSerialTrainer:
         out = self.alg.replay_inputs(self.replay_batch_size) if hasattr(self.alg, "replay_inputs") else None
         if out is not None:
             return self.buffer.sample_batch(self.replay_batch_size, out=out)
+        if getattr(self.alg, "wants_joint_batch", False) and hasattr(self.buffer, "_joint_shapes"):
+            return self.buffer.sample_batch(self.replay_batch_size, joint=True)
         return self.buffer.sample_batch(self.replay_batch_size)
 
     def _overlap_next(self):

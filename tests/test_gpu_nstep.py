@@ -135,6 +135,26 @@ def test_replay_gather_and_indices():
     assert counts.min() > 0.5 * 100000 / total  # roughly uniform
     batch = buf.sample_batch(256)
     assert batch["obs"].shape == (256, int(g["n_step"]), 6) and batch["rew"].shape == (256, int(g["n_step"]))
+    assert "obs_act" not in batch and "v_in" not in batch  # the reference's seven keys unless asked
+
+
+def test_replay_gather_joint_layouts():
+    """mh_replay_gather_joint: the update's [obs | act] rows and [obs[:, 0]; obs2 rows] batch equal
+    the torch.cat of the gathered arrays the update would otherwise form (msacl.py:236-238, 395-396),
+    bit for bit, fresh and into static destinations (also with repeated / boundary indices)."""
+    path = os.path.join(G, "nstep_DuctedFan.npz")
+    g, buf, total, _ = _run_trace(path)
+    idx = torch.tensor([0, 5, total - 1, 3, 3, total - 2], device="cuda")
+    out = buf.gather(idx, joint=True)
+    n, D = out["obs"].shape[1], out["obs"].shape[2]
+    torch.testing.assert_close(out["obs_act"], torch.cat([out["obs"], out["act"]], -1), rtol=0, atol=0)
+    torch.testing.assert_close(out["v_in"], torch.cat([out["obs"][:, 0], out["obs2"].reshape(-1, D)], 0),
+                               rtol=0, atol=0)
+    static = {k: torch.full_like(v, float("nan")) for k, v in out.items()}
+    buf.gather(idx, out=static)
+    for k in out:
+        torch.testing.assert_close(static[k], out[k], rtol=0, atol=0)
+    assert out["v_in"].shape == (6 + 6 * n, D)
 
 
 def n_of(g):

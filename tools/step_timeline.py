@@ -33,7 +33,10 @@ def main():
         avg = sum(s[0] for s in timed) / len(timed) / 1e3
         print(f"  mean span {avg:.1f} us", file=out)
     shown = set()
+    med = sorted(s[0] for s in timed)[len(timed) // 2] if timed else 0
     for span, samp, upd, nk, busy, seg in reversed(timed):
+        if span > 3 * med:  # the last timed step runs into the post-timed diagnostics
+            continue
         kind = "long" if nk > sum(s[3] for s in timed) / len(timed) else "short"
         if kind in shown:
             continue
