@@ -352,6 +352,16 @@ int mh_policy_head_backward(const float* raw, const float* eps, const float* old
                             const float* low, const float* d_xq, const float* d_new_logp, const float* d_old_logp,
                             int64_t rows, int32_t A, int32_t D, float log_std_lo, float log_std_hi, float* d_raw,
                             void* stream);
+/* mh_policy_head with the rsample noise drawn in-kernel (TanhGaussDistribution.rsample's
+ * torch.normal draw, act_distribution_cls.py:45-49, whose values are distribution-matched only):
+ * eps_out[r][i] = standard normal from Philox4x32-10 keyed by (seed, row r, counter[0]), Box-Muller,
+ * written for the backward (mh_policy_head_backward's eps). counter: device uint64[2], zeroed once;
+ * every launch advances counter[0] by one on the device (counter[1] is its workgroup arrival
+ * count), so a captured graph draws new noise on each replay. */
+int mh_policy_head_sample(const float* raw, const float* obs, const float* old_act, const float* high, const float* low,
+                          int64_t rows, int32_t A, int32_t D, float log_std_lo, float log_std_hi, uint64_t seed,
+                          uint64_t* counter, float* eps_out, float* xq, float* new_logp, float* old_logp,
+                          void* stream);
 /* Input gradient of y = act(x W^T + b) for a narrow input (n_in <= 32, n_out <= 1024) when no
  * weight / bias gradient is wanted (a frozen critic's first layer): dx = (dy * act'(y)) W with the
  * activation derivative formed on the fly. Row-major contiguous dy, y [rows][n_out], W [n_out][n_in]. */

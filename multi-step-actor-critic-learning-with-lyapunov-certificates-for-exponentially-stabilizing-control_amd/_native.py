@@ -109,6 +109,7 @@ _PROTOS = {
                                       c_vp, c_vp, c_vp]),
     "mh_policy_head_backward": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32,
                                                c_f32, c_f32, c_vp, c_vp]),
+    "mh_policy_head_sample": (ctypes.c_int, [c_vp] * 5 + [c_i64, c_i32, c_i32, c_f32, c_f32, c_u64] + [c_vp] * 6),
     "mh_dx_narrow": (ctypes.c_int, [c_vp, c_vp, c_i32, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp]),
     "mh_square_sum": (ctypes.c_int, [c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mh_square_sum_backward": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),

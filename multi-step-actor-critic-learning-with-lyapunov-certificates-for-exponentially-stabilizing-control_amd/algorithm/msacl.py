@@ -88,6 +88,9 @@ class ApproxContainer(nn.Module):
 
 
 _UNSET = object()
+# torch's normal draw as imported: a test that monkeypatches it (recorded-noise injection) keeps
+# the torch draw path; otherwise the update's rsample noise is drawn inside the head kernel
+_TORCH_STANDARD_NORMAL = tdn._standard_normal
 
 
 def _stacked(a, b):
@@ -164,13 +167,20 @@ class _PolicyHead(torch.autograd.Function):
     rsample + two concats + log_prob forward and their four backward kernels + gradient adds."""
 
     @staticmethod
-    def forward(ctx, raw, eps, obs, old_act, high, low, lo, hi):
+    def forward(ctx, raw, eps, obs, old_act, high, low, lo, hi, rng=None):
         R, A, D = raw.shape[0], raw.shape[1] // 2, obs.shape[1]
         xq = torch.empty(R, D + A, dtype=raw.dtype, device=raw.device)
         new_logp = torch.empty(R, dtype=raw.dtype, device=raw.device)
         old_logp = torch.empty(R, dtype=raw.dtype, device=raw.device)
-        _engine("policy_head", raw.device, N.ptr(raw), N.ptr(eps), N.ptr(obs), N.ptr(old_act), N.ptr(high), N.ptr(low),
-                R, A, D, lo, hi, N.ptr(xq), N.ptr(new_logp), N.ptr(old_logp))
+        if eps is None:  # rng = (seed, counter): the noise drawn in-kernel, kept for the backward
+            eps = torch.empty(R, A, dtype=raw.dtype, device=raw.device)
+            N.check(N.lib().mh_policy_head_sample(N.ptr(raw), N.ptr(obs), N.ptr(old_act), N.ptr(high), N.ptr(low), R,
+                                                  A, D, lo, hi, rng[0], N.ptr(rng[1]), N.ptr(eps), N.ptr(xq),
+                                                  N.ptr(new_logp), N.ptr(old_logp), N.stream_of(raw.device)),
+                    "mh_policy_head_sample")
+        else:
+            _engine("policy_head", raw.device, N.ptr(raw), N.ptr(eps), N.ptr(obs), N.ptr(old_act), N.ptr(high),
+                    N.ptr(low), R, A, D, lo, hi, N.ptr(xq), N.ptr(new_logp), N.ptr(old_logp))
         ctx.save_for_backward(raw, eps, old_act, high, low)
         ctx.dims = (R, A, D, lo, hi)
         return xq, new_logp, old_logp
@@ -183,7 +193,7 @@ class _PolicyHead(torch.autograd.Function):
         c = lambda t: None if t is None else t.contiguous()  # noqa: E731
         _engine("policy_head_backward", raw.device, N.ptr(raw), N.ptr(eps), N.ptr(old_act), N.ptr(high), N.ptr(low),
                 N.ptr(c(d_xq)), N.ptr(c(d_new_logp)), N.ptr(c(d_old_logp)), R, A, D, lo, hi, N.ptr(d_raw))
-        return d_raw, None, None, None, None, None, None, None
+        return d_raw, None, None, None, None, None, None, None, None
 
 
 class _PolicyObjective(torch.autograd.Function):
@@ -338,6 +348,12 @@ class MSACL:
         # the trainer asks a device replay buffer for the batch's [obs | act] and [obs_0; obs2]
         # layouts too (gathered, not concatenated per update); MSACL_JOINT_BATCH=0: torch.cat (A/B)
         self.wants_joint_batch = (self.device.type == "cuda" and os.environ.get("MSACL_JOINT_BATCH", "1") == "1")
+        # the update's rsample noise drawn inside the policy-head kernel (Philox, a device counter);
+        # MSACL_KERNEL_NOISE=0: torch's normal draw (A/B)
+        self._kernel_noise = os.environ.get("MSACL_KERNEL_NOISE", "1") == "1"
+        self._noise_seed = ((int(kwargs.get("seed", 0) or 0) * 0x9E3779B97F4A7C15 + 0x6A09E667F3BCC909
+                             + (D.rank() << 40)) & ((1 << 64) - 1))
+        self._noise_ctr = None
         # the Lyapunov update shares no parameter with the critic update (both only read the
         # policy and the batch): on one GPU it runs on a second stream, concurrently
         self.concurrent = bool(kwargs.get("alg_concurrent_streams", True))
@@ -420,9 +436,20 @@ class MSACL:
 
     def _noise(self, raw):
         """The rsample noise, drawn where TanhGaussDistribution.rsample draws it (same generator
-        call, same shape: the tests' recorded-noise injection sees the same sequence)."""
+        call, same shape: the tests' recorded-noise injection sees the same sequence). None on a
+        HIP device when nothing patched the draw: the head kernel then draws it (mh_policy_head_sample,
+        _noise_rng), saving the normal_ launch per head."""
+        if (self._kernel_noise and raw.is_cuda and tdn._standard_normal is _TORCH_STANDARD_NORMAL):
+            return None
         shape = raw.shape[:-1] + (raw.shape[-1] // 2,)
         return tdn._standard_normal(shape, dtype=raw.dtype, device=raw.device)
+
+    def _noise_rng(self):
+        """(seed, device counter) of the in-kernel rsample noise: the counter advances on the
+        device once per head launch, so graph replays draw new noise; the seed differs per rank."""
+        if self._noise_ctr is None:
+            self._noise_ctr = torch.zeros(2, dtype=torch.int64, device=self.device)
+        return self._noise_seed, self._noise_ctr
 
     def _buf(self, B, n):
         key = (B, n)
@@ -647,8 +674,16 @@ class MSACL:
                 eps = self._noise(raw)
                 xq2 = torch.empty(B, n, Dd + A, dtype=torch.float32, device=self.device)
                 next_logp = torch.empty(B, n, dtype=torch.float32, device=self.device)
-                _engine("policy_head", self.device, N.ptr(raw.contiguous()), N.ptr(eps.contiguous()), N.ptr(obs2), None,
-                        N.ptr(hi), N.ptr(lo), B * n, A, Dd, lsl, lsh, N.ptr(xq2), N.ptr(next_logp), None)
+                if eps is None:
+                    seed, ctr = self._noise_rng()
+                    eps_out = torch.empty(B * n, A, dtype=torch.float32, device=self.device)
+                    N.check(N.lib().mh_policy_head_sample(N.ptr(raw.contiguous()), N.ptr(obs2), None, N.ptr(hi),
+                                                          N.ptr(lo), B * n, A, Dd, lsl, lsh, seed, N.ptr(ctr),
+                                                          N.ptr(eps_out), N.ptr(xq2), N.ptr(next_logp), None,
+                                                          N.stream_of(self.device)), "mh_policy_head_sample")
+                else:
+                    _engine("policy_head", self.device, N.ptr(raw.contiguous()), N.ptr(eps.contiguous()), N.ptr(obs2),
+                            None, N.ptr(hi), N.ptr(lo), B * n, A, Dd, lsl, lsh, N.ptr(xq2), N.ptr(next_logp), None)
             xa = data.get("obs_act")  # [obs | act], written by the replay gather (mh_replay_gather_joint)
             if xa is None:
                 xa = torch.cat([obs, act], dim=-1)
@@ -804,8 +839,9 @@ class MSACL:
             raw = nets.policy.policy(obs)
             eps = self._noise(raw)
             xq, new_act_logp, old_lp = _PolicyHead.apply(raw.reshape(B * n, 2 * A).contiguous(),
-                                                         eps.reshape(B * n, A).contiguous(), obs.reshape(B * n, Dd),
-                                                         old_act.reshape(B * n, A), hi, lo, lsl, lsh)
+                                                         None if eps is None else eps.reshape(B * n, A).contiguous(),
+                                                         obs.reshape(B * n, Dd), old_act.reshape(B * n, A), hi, lo,
+                                                         lsl, lsh, self._noise_rng() if eps is None else None)
             xq = xq.reshape(B, n, Dd + A)
             new_act_logp, old_lp = new_act_logp.reshape(B, n), old_lp.reshape(B, n)
             tc = self._twin_critics(B * n)

@@ -797,6 +797,19 @@ int mh_policy_head(const float* raw, const float* eps, const float* obs, const f
   return MH_OK;
 }
 
+int mh_policy_head_sample(const float* raw, const float* obs, const float* old_act, const float* high, const float* low,
+                          int64_t rows, int32_t A, int32_t D, float log_std_lo, float log_std_hi, uint64_t seed,
+                          uint64_t* counter, float* eps_out, float* xq, float* new_logp, float* old_logp,
+                          void* stream) {
+  if (rows < 0 || A <= 0 || A > 8 || D < 0) return fail(MH_EINVAL, "mh_policy_head_sample: bad shape");
+  if (!raw || !high || !low || !counter || !eps_out || (!xq && !new_logp) || (xq && !obs && D > 0))
+    return fail(MH_EINVAL, "mh_policy_head_sample: null pointer");
+  MH_HIP(mh::launch_policy_head(raw, nullptr, obs, old_act, high, low, rows, A, D, log_std_lo, log_std_hi, xq,
+                                new_logp, old_logp, (hipStream_t)stream, seed,
+                                reinterpret_cast<unsigned long long*>(counter), eps_out));
+  return MH_OK;
+}
+
 int mh_policy_head_backward(const float* raw, const float* eps, const float* old_act, const float* high,
                             const float* low, const float* d_xq, const float* d_new_logp, const float* d_old_logp,
                             int64_t rows, int32_t A, int32_t D, float log_std_lo, float log_std_hi, float* d_raw,

@@ -158,18 +158,46 @@ __device__ __forceinline__ float ph_row_sum(float v, int A, int base) {  // sum_
   return s;
 }
 
+// In-kernel rsample noise (eps null, eps_out set): lane (r, i) draws its standard normal from
+// Philox4x32-10 keyed by (seed, row r, launch counter ctr[0]) — Box-Muller normal4f, stream i / 4,
+// component i % 4 — and writes it to eps_out for the backward. ctr[0] advances by one per launch:
+// the last workgroup to arrive (ctr[1], an arrival count every workgroup bumps after it has read
+// ctr[0]) increments it and re-arms ctr[1], so a captured graph draws fresh noise on every replay
+// without a host-side generator (the torch normal_ launch it replaces).
 __global__ __launch_bounds__(256) void k_policy_head(const float* __restrict__ raw, const float* __restrict__ eps,
                                                      const float* __restrict__ obs, const float* __restrict__ old_act,
                                                      const float* __restrict__ high, const float* __restrict__ low,
                                                      int64_t M, int A, int D, float lo, float hi,
                                                      float* __restrict__ xq, float* __restrict__ new_logp,
-                                                     float* __restrict__ old_logp) {
+                                                     float* __restrict__ old_logp, uint64_t seed,
+                                                     unsigned long long* ctr, float* __restrict__ eps_out) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t r = t / PH_G;
   const int i = (int)(t % PH_G);
   const int base = (threadIdx.x & 63) & ~(PH_G - 1);
   const bool row_ok = r < M;  // (whole groups share a row: the shuffles below stay in the group)
   const bool on = row_ok && i < A;
+  const bool draw = !eps && eps_out && ctr;
+  float e_draw = 0.0f;
+  if (draw) {
+    const unsigned long long c = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (on) {
+      float nv[4];
+      make_rng(seed, (uint64_t)r, (uint64_t)c).normal4f((uint32_t)(i >> 2), nv);
+      e_draw = nv[i & 3];
+      eps_out[r * A + i] = e_draw;
+    }
+    __syncthreads();  // every lane of the workgroup has read ctr[0]
+    if (threadIdx.x == 0) {
+      __threadfence();
+      const unsigned int arrived =
+          __hip_atomic_fetch_add(reinterpret_cast<unsigned int*>(ctr + 1), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (arrived == gridDim.x - 1) {  // the last workgroup: every other has read the counter
+        __hip_atomic_store(reinterpret_cast<unsigned int*>(ctr + 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
   const int W = D + A;
   if (row_ok && xq && obs) {
     for (int j = i; j < D; j += PH_G) xq[r * W + j] = obs[r * D + j];
@@ -178,8 +206,8 @@ __global__ __launch_bounds__(256) void k_policy_head(const float* __restrict__ r
   if (on) {
     const float mu = raw[r * 2 * A + i];
     const float sd = expf(fminf(fmaxf(raw[r * 2 * A + A + i], lo), hi));
-    if (eps) {
-      const float z = mu + sd * eps[r * A + i];
+    if (eps || draw) {
+      const float z = mu + sd * (draw ? e_draw : eps[r * A + i]);
       const float df = z - mu;
       const float var = sd * sd;
       lgv = (-(df * df) / (2.0f * var) - logf(sd)) - kLogSqrt2Pi;
@@ -198,7 +226,7 @@ __global__ __launch_bounds__(256) void k_policy_head(const float* __restrict__ r
       ojv = logf(dl / 2.0f * (1.000001f - tz * tz));
     }
   }
-  if (eps && new_logp) {
+  if ((eps || draw) && new_logp) {
     const float lg = ph_row_sum(lgv, A, base), lt = ph_row_sum(ltv, A, base), lh = ph_row_sum(lhv, A, base);
     if (row_ok && i == 0) new_logp[r] = (lg - lt) - lh;
   }
@@ -270,11 +298,12 @@ static inline unsigned grid_row_lanes(int64_t M) { return (unsigned)((M * PH_G +
 
 hipError_t launch_policy_head(const float* raw, const float* eps, const float* obs, const float* old_act,
                               const float* high, const float* low, int64_t M, int A, int D, float lo, float hi,
-                              float* xq, float* new_logp, float* old_logp, hipStream_t st) {
+                              float* xq, float* new_logp, float* old_logp, hipStream_t st, uint64_t seed,
+                              unsigned long long* ctr, float* eps_out) {
   if (M <= 0) return hipSuccess;
   if (A <= 0 || A > PH_G) return hipErrorInvalidValue;
   k_policy_head<<<grid_row_lanes(M), 256, 0, st>>>(raw, eps, obs, old_act, high, low, M, A, D, lo, hi, xq, new_logp,
-                                                   old_logp);
+                                                   old_logp, seed, ctr, eps_out);
   return hipGetLastError();
 }
 hipError_t launch_policy_head_bwd(const float* raw, const float* eps, const float* old_act, const float* high,

@@ -141,7 +141,8 @@ hipError_t launch_act_grad_colsum(const float* dy, const float* y, int64_t M, in
 int act_grad_tickets(int N);
 hipError_t launch_policy_head(const float* raw, const float* eps, const float* obs, const float* old_act,
                               const float* high, const float* low, int64_t M, int A, int D, float lo, float hi,
-                              float* xq, float* new_logp, float* old_logp, hipStream_t st);
+                              float* xq, float* new_logp, float* old_logp, hipStream_t st, uint64_t seed = 0,
+                              unsigned long long* ctr = nullptr, float* eps_out = nullptr);
 hipError_t launch_policy_head_bwd(const float* raw, const float* eps, const float* old_act, const float* high,
                                   const float* low, const float* d_xq, const float* d_new_logp,
                                   const float* d_old_logp, int64_t M, int A, int D, float lo, float hi, float* d_raw,

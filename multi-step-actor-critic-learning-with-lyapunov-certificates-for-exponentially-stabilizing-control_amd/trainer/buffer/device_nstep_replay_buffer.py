@@ -182,4 +182,6 @@ class DeviceNstepReplayBuffer:
         """nstep_replay_buffer.py:136-148. `out` (optional): destination tensors (gather); joint:
         add the update's joint layouts (gather)."""
         idx = self.sample_indices(batch_size)
+        if out is None and not joint:
+            return self.gather(idx)  # (the 1-step ReplayBuffer's gather takes idx only)
         return self.gather(idx, out, joint)

@@ -34,9 +34,9 @@ class PrioritizedReplayBuffer(DeviceNstepReplayBuffer):
                                        self.max_size, N.ptr(self.max_prio), N.stream_of(self.device)), "mh_per_set_new")
         self._seen.copy_(self.cursor)
 
-    def sample_batch(self, batch_size: int, out=None) -> dict:
+    def sample_batch(self, batch_size: int, out=None, joint=False) -> dict:
         """Proportional draw + IS weights, then the window gather (into `out` when it fits,
-        DeviceNstepReplayBuffer.gather; its "idx" / "weight" too)."""
+        DeviceNstepReplayBuffer.gather; its "idx" / "weight" too; joint: the update's joint layouts)."""
         fits = self._fits(out, batch_size)
         idx = out.get("idx") if fits else None
         w = out.get("weight") if fits else None
@@ -48,7 +48,7 @@ class PrioritizedReplayBuffer(DeviceNstepReplayBuffer):
                                       batch_size, self.beta, N.ptr(idx), N.ptr(w), N.stream_of(self.device)),
                 "mh_per_sample")
         self._per_draws += 1
-        out = self.gather(idx, out)
+        out = self.gather(idx, out, joint)
         out["idx"] = idx
         out["weight"] = w
         return out

@@ -168,8 +168,8 @@ def test_gather_into_update_inputs_equals_copy(tmp_path, monkeypatch, buffer_nam
         seen = []
         orig = buffer.sample_batch
 
-        def spy(bs, out=None):
-            r = orig(bs, out=out) if out is not None else orig(bs)
+        def spy(bs, out=None, **kw):
+            r = orig(bs, out=out, **kw) if out is not None else orig(bs, **kw)
             seen.append(all(r[k].data_ptr() == alg._static[k].data_ptr() for k in ("obs", "rew"))
                         if alg._static is not None else False)
             return r
