@@ -77,7 +77,7 @@ struct mh_env_s {
   int hcap = 0;
   int32_t* h_count = nullptr;       // [hcap][ceil(E / 64)]
   int32_t* h_list = nullptr;        // [hcap][E]
-  int64_t* h_scan = nullptr;        // [hcap * ceil(E / 256) + 2]: the emission's cell scan
+  int32_t* h_scan = nullptr;        // [hcap + 2]: the emission's per-lockstep window totals + arrival count
   float* dbg_logits = nullptr;      // mh_sample_horizon_debug_logits: [H][E][2A] logits trace
   float* dbg_obs = nullptr;         //   and [H][E][D] pre-step observations
   uint32_t spin_limit = 0;          // mh_sample_horizon_set_spin_limit (0: the kernel's default)
@@ -278,13 +278,14 @@ int mh_nstep_reserve(mh_env_t h, int32_t ring_slots) {
   const int F = h->info.record_floats;
   // every buffer is allocated before anything is swapped: on failure the handle is unchanged
   float* ring = nullptr;
-  int32_t *cnt = nullptr, *lst = nullptr;
-  int64_t* scan = nullptr;
+  int32_t *cnt = nullptr, *lst = nullptr, *scan = nullptr;
   hipError_t e = hipSuccess;
   if (new_ring) e = hipMalloc(&ring, sizeof(float) * E * ring_slots * F);
   if (e == hipSuccess) e = hipMalloc(&cnt, sizeof(int32_t) * hcap * ((E + 63) / 64));
   if (e == hipSuccess) e = hipMalloc(&lst, sizeof(int32_t) * hcap * E);
-  if (e == hipSuccess) e = hipMalloc(&scan, sizeof(int64_t) * (mh::fused_emit_cells(E, hcap) + 2));
+  // the emission's per-lockstep window totals [hcap] and its arrival count, zero between horizons
+  if (e == hipSuccess) e = hipMalloc(&scan, sizeof(int32_t) * (hcap + 2));
+  if (e == hipSuccess) e = hipMemset(scan, 0, sizeof(int32_t) * (hcap + 2));
   if (e == hipSuccess && new_ring) e = hipMemset(ring, 0, sizeof(float) * E * ring_slots * F);
   if (e != hipSuccess) {
     for (void* p : {(void*)ring, (void*)cnt, (void*)lst, (void*)scan})
@@ -351,6 +352,7 @@ int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, i
   a.act_noise = act_noise;
   a.emit_count = h->h_count;
   a.emit_list = h->h_list;
+  a.ts_total = h->h_scan;
   a.act_out = act_out;
   a.logp_out = logp_out;
   a.err = h->meta + 7;  // meta[7]: the fused kernel's error word
@@ -376,7 +378,8 @@ int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, i
     ea.logp = store->logp;
     ea.capacity = store->capacity;
     ea.cursor = store->cursor;
-    ea.scan = h->h_scan;
+    ea.ts_total = h->h_scan;
+    ea.arrive = reinterpret_cast<uint32_t*>(h->h_scan + h->hcap);
   }
   MH_HIP(mh::launch_sample_fused(h->env_id, a, ea, (hipStream_t)stream));
   return MH_OK;

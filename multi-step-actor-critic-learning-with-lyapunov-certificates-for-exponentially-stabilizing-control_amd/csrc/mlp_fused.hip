@@ -95,81 +95,98 @@ __device__ __forceinline__ void layer_cols_pre(__amdgpu_buffer_rsrc_t wr, int n0
     if (p < G) wring_load<G>(wr, n0, lane, p, wb[p]);
 }
 
-template <int SIN, int G>
+// RT row tiles of 16 (the workgroup's TM = 16 RT rows): each weight fragment feeds RT MFMAs, so a
+// workgroup streams the layer's weights once per 16 RT rows.
+template <int SIN, int G, int RT = 1>
 __device__ __forceinline__ void layer_cols_run(const float* in, __amdgpu_buffer_rsrc_t wr, int n0, int lane,
-                                               f32x4 (&acc)[4], f32x4 (&wb)[PF][4]) {
+                                               f32x4 (&acc)[RT][4], f32x4 (&wb)[PF][4]) {
   const int r = lane & 15, g = lane >> 4;
   const float* arow = in + r * SIN + 4 * g;
-  f32x4 a_cur = *reinterpret_cast<const f32x4*>(arow);
+  f32x4 a_cur[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) a_cur[rt] = *reinterpret_cast<const f32x4*>(arow + 16 * rt * SIN);
 #pragma unroll
   for (int u = 0; u < G; ++u) {
     if (u + PF - 1 < G) wring_load<G>(wr, n0, lane, u + PF - 1, wb[(u + PF - 1) % PF]);
-    f32x4 a_nxt = a_cur;
-    if (u + 1 < G) a_nxt = *reinterpret_cast<const f32x4*>(arow + 16 * (u + 1));
+    f32x4 a_nxt[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+      a_nxt[rt] = u + 1 < G ? *reinterpret_cast<const f32x4*>(arow + 16 * rt * SIN + 16 * (u + 1)) : a_cur[rt];
     MH_SCHED_FENCE();
 #ifdef MH_MLP_EXP_NOMFMA  // cost-attribution experiment only: operands consumed, no MFMA (wrong results)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] += a_cur * wb[u % PF][j];
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[rt][j] += a_cur[rt] * wb[u % PF][j];
 #else
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t], wb[u % PF][j][t], acc[j], 0, 0, 0);
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[rt][t], wb[u % PF][j][t], acc[rt][j], 0, 0, 0);
 #endif
     MH_SCHED_FENCE();
-    a_cur = a_nxt;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) a_cur[rt] = a_nxt[rt];
   }
 }
 
-template <int SIN, int G>
+template <int SIN, int G, int RT = 1>
 __device__ __forceinline__ void layer_cols(const float* in, __amdgpu_buffer_rsrc_t wr, int n0, int lane,
-                                           f32x4 (&acc)[4]) {
+                                           f32x4 (&acc)[RT][4]) {
   f32x4 wb[PF][4];
   layer_cols_pre<G>(wr, n0, lane, wb);
-  layer_cols_run<SIN, G>(in, wr, n0, lane, acc, wb);
+  layer_cols_run<SIN, G, RT>(in, wr, n0, lane, acc, wb);
 }
 
-// bias + activation of this wave's 64 columns into the LDS tile `out` (row stride SH); the MFMA's
-// C map: column = lane & 15, rows 4 (lane >> 4) + q
-template <int ACT>
-__device__ __forceinline__ void epilogue_lds_t(const f32x4 (&acc)[4], const float (&bias)[4], int n0, int lane,
+// bias + activation of this wave's 64 columns into the LDS tile `out` (row stride SH), row tiles
+// 0 .. RT - 1; the MFMA's C map: column = lane & 15, rows 16 rt + 4 (lane >> 4) + q
+template <int ACT, int RT>
+__device__ __forceinline__ void epilogue_lds_t(const f32x4 (&acc)[RT][4], const float (&bias)[4], int n0, int lane,
                                                float* out) {
   const int c = lane & 15, g = lane >> 4;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + 16 * j + c;
+  for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) out[(4 * g + q) * SH + n] = act_t<ACT>(acc[j][q] + bias[j]);
-  }
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + 16 * j + c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) out[(16 * rt + 4 * g + q) * SH + n] = act_t<ACT>(acc[rt][j][q] + bias[j]);
+    }
 }
 
 // bias[j] = the bias of column n0 + 16 j + (lane & 15), loaded up front
-__device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[4], const float (&bias)[4], int act, int n0, int lane,
-                                             float* out) {
+template <int RT>
+__device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[RT][4], const float (&bias)[4], int act, int n0,
+                                             int lane, float* out) {
   if (act == 1)
-    epilogue_lds_t<1>(acc, bias, n0, lane, out);
+    epilogue_lds_t<1, RT>(acc, bias, n0, lane, out);
   else if (act == 2)
-    epilogue_lds_t<2>(acc, bias, n0, lane, out);
+    epilogue_lds_t<2, RT>(acc, bias, n0, lane, out);
   else
-    epilogue_lds_t<0>(acc, bias, n0, lane, out);
+    epilogue_lds_t<0, RT>(acc, bias, n0, lane, out);
 }
 
-// the LDS tile (16 rows x HID) to global rows m0.. (ld floats), row-contiguous float4 stores
-__device__ __forceinline__ void store_tile(const float* tile, float* dst, int64_t ld, int64_t m0, int64_t M, int cols) {
+// the LDS tile (rows x HID) to global rows m0.. (ld floats), row-contiguous float4 stores
+__device__ __forceinline__ void store_tile(const float* tile, float* dst, int64_t ld, int64_t m0, int64_t M, int cols,
+                                           int rows = TM) {
   const int per_row = cols / 4;
-  for (int i = threadIdx.x; i < TM * per_row; i += 256) {
+  for (int i = threadIdx.x; i < rows * per_row; i += 256) {
     const int rr = i / per_row, c4 = i - rr * per_row;
     if (m0 + rr < M)
       *reinterpret_cast<f32x4*>(dst + (m0 + rr) * ld + 4 * c4) = *reinterpret_cast<const f32x4*>(tile + rr * SH + 4 * c4);
   }
 }
 
+template <int RT>
 __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
-  __shared__ float xs[TM * SX];
-  __shared__ float hs1[TM * SH];
-  __shared__ float hs2[TM * SH];
-  __shared__ f32x4 red[4][64];
+  constexpr int TR = 16 * RT;  // rows per workgroup
+  __shared__ float xs[TR * SX];
+  __shared__ float hs1[TR * SH];
+  __shared__ float hs2[TR * SH];
+  __shared__ f32x4 red[4][RT][64];
   {
     const int64_t q = blockIdx.y;
     a.x += q * a.gs_x;
@@ -185,20 +202,20 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
   }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t m0 = (int64_t)blockIdx.x * TM;
+  const int64_t m0 = (int64_t)blockIdx.x * TR;
   const int K1 = a.K1, K1p = (K1 + 15) & ~15;
   const int n0 = wave * 64;
   const int r = lane & 15, g = lane >> 4;
 
-  // ---- the hidden layers' biases and layer 1's weights first (their latency overlaps the input
-  // staging): W1 [H][K1], lane group
-  // g of column n reads k = 16 u + 4 g + t; k >= K1 lands past the buffer's end and reads 0
   // layer 2's first weight groups go out first: they depend on nothing, and layer 2 then starts
   // without a round trip
   const __amdgpu_buffer_rsrc_t wr2 =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.W2), (short)0, HID * HID * 4, 0x00020000);
   f32x4 wb2[PF][4];
   layer_cols_pre<HID / 16>(wr2, n0, lane, wb2);
+  // ---- the hidden layers' biases and layer 1's weights (their latency overlaps the input
+  // staging): W1 [H][K1], lane group g of column n reads k = 16 u + 4 g + t; k >= K1 lands past
+  // the buffer's end and reads 0
   float w1[2][4][4], bias1[4], bias2[4];
   {
 #pragma unroll
@@ -222,39 +239,44 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
         }
   }
 
-  // ---- the input rows, zero-padded to K1p columns (rows past M: zeros)
-  {  // TM x K1p <= 512 elements: both of a thread's loads issued before either store
-    float xv[2];
+  // ---- the input rows, zero-padded to K1p columns (rows past M: zeros); TR x K1p <= 512 RT
+  // elements: a thread's loads all issued before its stores
+  {
+    float xv[2 * RT];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < 2 * RT; ++s) {
       const int i = tid + 256 * s, rr = i / K1p, k = i - rr * K1p;
-      xv[s] = (i < TM * K1p && m0 + rr < a.M && k < K1) ? a.x[(m0 + rr) * a.ldx + k] : 0.0f;
+      xv[s] = (i < TR * K1p && m0 + rr < a.M && k < K1) ? a.x[(m0 + rr) * a.ldx + k] : 0.0f;
     }
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < 2 * RT; ++s) {
       const int i = tid + 256 * s, rr = i / K1p, k = i - rr * K1p;
-      if (i < TM * K1p) xs[rr * SX + k] = xv[s];
+      if (i < TR * K1p) xs[rr * SX + k] = xv[s];
     }
   }
   __syncthreads();
 
   // ---- layer 1: K1p <= 32
   {
-    f32x4 acc[4] = {};
+    f32x4 acc[RT][4] = {};
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       if (u * 16 < K1p) {
-        const f32x4 av = *reinterpret_cast<const f32x4*>(xs + r * SX + 16 * u + 4 * g);
 #pragma unroll
-        for (int t = 0; t < 4; ++t)
+        for (int rt = 0; rt < RT; ++rt) {
+          const f32x4 av = *reinterpret_cast<const f32x4*>(xs + (16 * rt + r) * SX + 16 * u + 4 * g);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], w1[u][j][t], acc[j], 0, 0, 0);
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], w1[u][j][t], acc[rt][j], 0, 0, 0);
+        }
       }
     }
-    epilogue_lds(acc, bias1, a.act1, n0, lane, hs1);
+    epilogue_lds<RT>(acc, bias1, a.act1, n0, lane, hs1);
   }
   __syncthreads();
-  if (a.h1) store_tile(hs1, a.h1, a.ldh, m0, a.M, HID);
+  if (a.h1) store_tile(hs1, a.h1, a.ldh, m0, a.M, HID, TR);
 
   // ---- layer 2
   const int N3 = a.N3;
@@ -262,8 +284,8 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.W3), (short)0, N3 * HID * 4, 0x00020000);
   f32x4 w3[4];  // the narrow output layer's weights (N3 <= 16), issued before layer 2's epilogue
   {
-    f32x4 acc[4] = {};
-    layer_cols_run<SH, HID / 16>(hs1, wr2, n0, lane, acc, wb2);
+    f32x4 acc[RT][4] = {};
+    layer_cols_run<SH, HID / 16, RT>(hs1, wr2, n0, lane, acc, wb2);
     if (N3 <= 16) {
 #pragma unroll
       for (int uu = 0; uu < 4; ++uu)
@@ -271,55 +293,62 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
             f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr3, (r * HID + 16 * (wave * 4 + uu) + 4 * g) * 4, 0, 0));
     }
     MH_SCHED_FENCE();
-    epilogue_lds(acc, bias2, a.act2, n0, lane, hs2);
+    epilogue_lds<RT>(acc, bias2, a.act2, n0, lane, hs2);
   }
   __syncthreads();
-  if (a.h2) store_tile(hs2, a.h2, a.ldh, m0, a.M, HID);
+  if (a.h2) store_tile(hs2, a.h2, a.ldh, m0, a.M, HID, TR);
 
   // ---- layer 3
   if (N3 <= 16) {
     // one 16-column block; wave w contracts k in [64 w, 64 w + 64), the four partial tiles added
     // in wave order
-    f32x4 acc = {};
+    f32x4 acc[RT] = {};
 #pragma unroll
     for (int uu = 0; uu < 4; ++uu) {
       const int u = wave * 4 + uu;
-      const f32x4 av = *reinterpret_cast<const f32x4*>(hs2 + r * SH + 16 * u + 4 * g);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], w3[uu][t], acc, 0, 0, 0);
+      for (int rt = 0; rt < RT; ++rt) {
+        const f32x4 av = *reinterpret_cast<const f32x4*>(hs2 + (16 * rt + r) * SH + 16 * u + 4 * g);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], w3[uu][t], acc[rt], 0, 0, 0);
+      }
     }
-    red[wave][lane] = acc;
-    __syncthreads();
-    if (wave == 0) {
-      f32x4 s = red[0][lane];
 #pragma unroll
-      for (int w = 1; w < 4; ++w) s = s + red[w][lane];
+    for (int rt = 0; rt < RT; ++rt) red[wave][rt][lane] = acc[rt];
+    __syncthreads();
+    if (wave < RT) {  // wave rt sums row tile rt's four partials
+      const int rt = wave;
+      f32x4 sum = red[0][rt][lane];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) sum = sum + red[w][rt][lane];
       const int n = lane & 15;
       if (n < N3) {
         const float bv = a.b3[n];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int64_t row = m0 + 4 * g + q;
-          if (row < a.M) a.y[row * a.ldy + n] = act_f(s[q] + bv, a.act3);
+          const int64_t row = m0 + 16 * rt + 4 * g + q;
+          if (row < a.M) a.y[row * a.ldy + n] = act_f(sum[q] + bv, a.act3);
         }
       }
     }
   } else {
     // N3 = 64 c: wave w takes output columns [N3 / 4 * w, ...) in 16-column blocks of 64-wide passes
     for (int nb = wave * 64; nb < N3; nb += 256) {
-      f32x4 acc[4] = {};
-      layer_cols<SH, HID / 16>(hs2, wr3, nb, lane, acc);
+      f32x4 acc[RT][4] = {};
+      layer_cols<SH, HID / 16, RT>(hs2, wr3, nb, lane, acc);
       const int c = lane & 15;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = nb + 16 * j + c;
-        const float bv = a.b3[n];
+      for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int64_t row = m0 + 4 * g + q;
-          if (row < a.M) a.y[row * a.ldy + n] = act_f(acc[j][q] + bv, a.act3);
+        for (int j = 0; j < 4; ++j) {
+          const int n = nb + 16 * j + c;
+          const float bv = a.b3[n];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int64_t row = m0 + 16 * rt + 4 * g + q;
+            if (row < a.M) a.y[row * a.ldy + n] = act_f(acc[rt][j][q] + bv, a.act3);
+          }
         }
-      }
     }
   }
 }
@@ -359,67 +388,78 @@ __device__ __forceinline__ void layer_cols_t_pre(__amdgpu_buffer_rsrc_t wr, int 
     if (p < G) wring_t_load<G>(wr, n0, lane, p, wb[p]);
 }
 
-template <int G, int D = PFT>
+template <int G, int D = PFT, int RT = 1>
 __device__ __forceinline__ void layer_cols_t_run(const float* in, int sin, __amdgpu_buffer_rsrc_t wr, int n0, int lane,
-                                                 f32x4 (&acc)[4], float (&wb)[D][4][4]) {
+                                                 f32x4 (&acc)[RT][4], float (&wb)[D][4][4]) {
   const int c = lane & 15, g = lane >> 4;
   const float* arow = in + c * sin + 4 * g;
-  f32x4 a_cur = *reinterpret_cast<const f32x4*>(arow);
+  f32x4 a_cur[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) a_cur[rt] = *reinterpret_cast<const f32x4*>(arow + 16 * rt * sin);
 #pragma unroll
   for (int u = 0; u < G; ++u) {
     if (u + D - 1 < G) wring_t_load<G>(wr, n0, lane, u + D - 1, wb[(u + D - 1) % D]);
-    f32x4 a_nxt = a_cur;
-    if (u + 1 < G) a_nxt = *reinterpret_cast<const f32x4*>(arow + 16 * (u + 1));
+    f32x4 a_nxt[RT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+      a_nxt[rt] = u + 1 < G ? *reinterpret_cast<const f32x4*>(arow + 16 * rt * sin + 16 * (u + 1)) : a_cur[rt];
     MH_SCHED_FENCE();
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[t], wb[u % D][j][t], acc[j], 0, 0, 0);
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a_cur[rt][t], wb[u % D][j][t], acc[rt][j], 0, 0, 0);
     MH_SCHED_FENCE();
-    a_cur = a_nxt;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) a_cur[rt] = a_nxt[rt];
   }
 }
 
-template <int G, int D = PFT>
+template <int G, int D = PFT, int RT = 1>
 __device__ __forceinline__ void layer_cols_t(const float* in, int sin, __amdgpu_buffer_rsrc_t wr, int n0, int lane,
-                                             f32x4 (&acc)[4]) {
+                                             f32x4 (&acc)[RT][4]) {
   float wb[D][4][4];
   layer_cols_t_pre<G, D>(wr, n0, lane, wb);
-  layer_cols_t_run<G, D>(in, sin, wr, n0, lane, acc, wb);
+  layer_cols_t_run<G, D, RT>(in, sin, wr, n0, lane, acc, wb);
 }
 
 // the output-gradient contraction over W3's N3 rows, N3 a multiple of 64
+template <int RT>
 __device__ __forceinline__ void layer_cols_t_n3(const float* in, __amdgpu_buffer_rsrc_t wr, int N3, int n0, int lane,
-                                                f32x4 (&acc)[4]) {
+                                                f32x4 (&acc)[RT][4]) {
   if (N3 == 64)
-    layer_cols_t<4, 3>(in, SH, wr, n0, lane, acc);
+    layer_cols_t<4, 3, RT>(in, SH, wr, n0, lane, acc);
   else if (N3 == 128)
-    layer_cols_t<8, 3>(in, SH, wr, n0, lane, acc);
+    layer_cols_t<8, 3, RT>(in, SH, wr, n0, lane, acc);
   else if (N3 == 192)
-    layer_cols_t<12, 3>(in, SH, wr, n0, lane, acc);
+    layer_cols_t<12, 3, RT>(in, SH, wr, n0, lane, acc);
   else
-    layer_cols_t<16, 3>(in, SH, wr, n0, lane, acc);
+    layer_cols_t<16, 3, RT>(in, SH, wr, n0, lane, acc);
 }
 
-// this wave's 64 columns of the forward activations h (rows m0.., row stride ldh), for the
-// gradient epilogue; issued before the layer's MFMAs so that their latency hides behind them
-// (rows past M read 0 through the buffer's bound)
+// this wave's 64 columns of the forward activations h (rows m0.., row stride ldh) in row tiles
+// 0 .. RT - 1, for the gradient epilogue; issued before the layer's MFMAs so that their latency
+// hides behind them (rows past M read 0)
+template <int RT>
 __device__ __forceinline__ void load_h_tile(const float* h, int64_t ldh, int64_t m0, int64_t M, int n0, int lane,
-                                            float (&hv)[4][4]) {
+                                            float (&hv)[RT][4][4]) {
   const int c = lane & 15, g = lane >> 4;
-  const int64_t rows = M - m0 < TM ? M - m0 : TM;
+  const int64_t rows = M - m0 < 16 * RT ? M - m0 : 16 * RT;
   const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(h + m0 * ldh), (short)0, (int)(((rows - 1) * ldh + HID) * 4), 0x00020000);
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int rr = 4 * g + q;
-      hv[j][q] = rr < rows ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                           hr, (int)((rr * ldh + n0 + 16 * j + c) * 4), 0, 0))
-                           : 0.0f;
-    }
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rr = 16 * rt + 4 * g + q;
+        hv[rt][j][q] = rr < rows ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                 hr, (int)((rr * ldh + n0 + 16 * j + c) * 4), 0, 0))
+                                 : 0.0f;
+      }
 }
 
 template <int ACT>
@@ -430,45 +470,51 @@ __device__ __forceinline__ float act_grad_t(float d, float t) {  // gemm.hip act
 }
 
 // dh = acc (this wave's 64 columns) -> g = dh * act'(h) into the LDS tile `out`; rows past M: 0
-template <int ACT>
-__device__ __forceinline__ void grad_epilogue_t(const f32x4 (&acc)[4], const float (&hv)[4][4], int n0, int lane,
-                                                int64_t m0, int64_t M, float* out) {
+template <int ACT, int RT>
+__device__ __forceinline__ void grad_epilogue_t(const f32x4 (&acc)[RT][4], const float (&hv)[RT][4][4], int n0,
+                                                int lane, int64_t m0, int64_t M, float* out) {
   const int c = lane & 15, g = lane >> 4;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = n0 + 16 * j + c;
+  for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t row = m0 + 4 * g + q;
-      out[(4 * g + q) * SH + n] = row < M ? act_grad_t<ACT>(acc[j][q], hv[j][q]) : 0.0f;
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + 16 * j + c;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int rr = 16 * rt + 4 * g + q;
+        out[rr * SH + n] = m0 + rr < M ? act_grad_t<ACT>(acc[rt][j][q], hv[rt][j][q]) : 0.0f;
+      }
     }
-  }
 }
 
-__device__ __forceinline__ void grad_epilogue(const f32x4 (&acc)[4], const float (&hv)[4][4], int act, int n0,
+template <int RT>
+__device__ __forceinline__ void grad_epilogue(const f32x4 (&acc)[RT][4], const float (&hv)[RT][4][4], int act, int n0,
                                               int lane, int64_t m0, int64_t M, float* out) {
   if (act == 1)
-    grad_epilogue_t<1>(acc, hv, n0, lane, m0, M, out);
+    grad_epilogue_t<1, RT>(acc, hv, n0, lane, m0, M, out);
   else if (act == 2)
-    grad_epilogue_t<2>(acc, hv, n0, lane, m0, M, out);
+    grad_epilogue_t<2, RT>(acc, hv, n0, lane, m0, M, out);
   else
-    grad_epilogue_t<0>(acc, hv, n0, lane, m0, M, out);
+    grad_epilogue_t<0, RT>(acc, hv, n0, lane, m0, M, out);
 }
 
 // NARROW (N3 <= 16): the W2 product's weight ring is issued before the W3 product; the wide form
-// (N3 a multiple of 64) has no registers for that beside the W3 product's own ring.
-template <bool NARROW>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_mlp3_bwd(Mlp3BwdArgs a) {
-  __shared__ float gs3[TM * SH];  // the output gradient tile (N3 <= 256 columns)
-  __shared__ float gs2[TM * SH];
-  __shared__ float gs1[TM * SH];
-  __shared__ f32x4 red[4][2][64];
+// (N3 a multiple of 64) has no registers for that beside the W3 product's own ring. RT row tiles
+// of 16 per wave (the workgroup's 16 RT rows): each weight fragment feeds RT MFMAs.
+template <bool NARROW, int RT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT == 1 ? 2 : 1))) void k_mlp3_bwd(
+    Mlp3BwdArgs a) {
+  constexpr int TR = 16 * RT;
+  __shared__ float gs3[TR * SH];  // the output gradient tile (N3 <= 256 columns)
+  __shared__ float gs2[TR * SH];
+  __shared__ float gs1[TR * SH];
+  __shared__ f32x4 red[4][RT][2][64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t m0 = (int64_t)blockIdx.x * TM;
+  const int64_t m0 = (int64_t)blockIdx.x * TR;
   const int N3 = a.N3, K1 = a.K1, n0 = wave * 64;
   const int N3p = (N3 + 15) & ~15;
-  f32x4 dxa[2] = {};
+  f32x4 dxa[RT][2] = {};
   for (int q = 0; q < a.groups; ++q) {
     const float* dy = a.dy + q * a.gs_dy;
     const float* h1 = a.h1 + q * a.gs_h;
@@ -483,9 +529,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(W2), (short)0, HID * HID * 4, 0x00020000);
     float wb2[PFT][4][4];
     if constexpr (NARROW) layer_cols_t_pre<HID / 16>(wr2, n0, lane, wb2);
-    float hv2[4][4];
-    load_h_tile(h2, a.ldh, m0, a.M, n0, lane, hv2);
-    for (int i = tid; i < TM * N3p; i += 256) {
+    float hv2[RT][4][4];
+    load_h_tile<RT>(h2, a.ldh, m0, a.M, n0, lane, hv2);
+    for (int i = tid; i < TR * N3p; i += 256) {
       const int rr = i / N3p, k = i - rr * N3p;
       gs3[rr * SH + k] = (m0 + rr < a.M && k < N3) ? dy[(m0 + rr) * a.ldy + k] : 0.0f;
     }
@@ -494,28 +540,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     {
       const __amdgpu_buffer_rsrc_t wr =
           __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(W3), (short)0, N3 * HID * 4, 0x00020000);
-      f32x4 acc[4] = {};
+      f32x4 acc[RT][4] = {};
       if constexpr (NARROW)
-        layer_cols_t<1>(gs3, SH, wr, n0, lane, acc);
+        layer_cols_t<1, PFT, RT>(gs3, SH, wr, n0, lane, acc);
       else
-        layer_cols_t_n3(gs3, wr, N3, n0, lane, acc);
-      grad_epilogue(acc, hv2, a.act2, n0, lane, m0, a.M, gs2);
+        layer_cols_t_n3<RT>(gs3, wr, N3, n0, lane, acc);
+      grad_epilogue<RT>(acc, hv2, a.act2, n0, lane, m0, a.M, gs2);
     }
     __syncthreads();
-    if (a.g2) store_tile(gs2, a.g2 + q * a.gs_g, a.ldg, m0, a.M, HID);
+    if (a.g2) store_tile(gs2, a.g2 + q * a.gs_g, a.ldg, m0, a.M, HID, TR);
     // dh1 = g2 W2, g1 = dh1 * act1'(h1)
     {
-      float hv[4][4];
-      load_h_tile(h1, a.ldh, m0, a.M, n0, lane, hv);
-      f32x4 acc[4] = {};
+      float hv[RT][4][4];
+      load_h_tile<RT>(h1, a.ldh, m0, a.M, n0, lane, hv);
+      f32x4 acc[RT][4] = {};
       if constexpr (NARROW)
-        layer_cols_t_run<HID / 16>(gs2, SH, wr2, n0, lane, acc, wb2);
+        layer_cols_t_run<HID / 16, PFT, RT>(gs2, SH, wr2, n0, lane, acc, wb2);
       else
-        layer_cols_t<HID / 16, 3>(gs2, SH, wr2, n0, lane, acc);  // (registers: the wide form keeps depth 3)
-      grad_epilogue(acc, hv, a.act1, n0, lane, m0, a.M, gs1);
+        layer_cols_t<HID / 16, 3, RT>(gs2, SH, wr2, n0, lane, acc);  // (registers: the wide form keeps depth 3)
+      grad_epilogue<RT>(acc, hv, a.act1, n0, lane, m0, a.M, gs1);
     }
     __syncthreads();
-    if (a.g1) store_tile(gs1, a.g1 + q * a.gs_g, a.ldg, m0, a.M, HID);
+    if (a.g1) store_tile(gs1, a.g1 + q * a.gs_g, a.ldg, m0, a.M, HID, TR);
     // dx += g1 W1 (W1 [H][K1]: contraction over its H rows, wave w rows [64 w, 64 w + 64); two
     // 16-column blocks of K1 <= 32)
     if (a.dx) {
@@ -525,7 +571,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
       for (int uu = 0; uu < 4; ++uu) {
         const int u = wave * 4 + uu;
-        const f32x4 av = *reinterpret_cast<const f32x4*>(gs1 + c * SH + 16 * u + 4 * g);
+        f32x4 av[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+          av[rt] = *reinterpret_cast<const f32x4*>(gs1 + (16 * rt + c) * SH + 16 * u + 4 * g);
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
           float bv[4];
@@ -536,28 +585,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
                                                   wr, col < K1 ? (k * K1 + col) * 4 : 0x7ffffff0, 0, 0));
           }
 #pragma unroll
-          for (int t = 0; t < 4; ++t) dxa[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[t], bv[t], dxa[cb], 0, 0, 0);
+          for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+              dxa[rt][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[rt][t], bv[t], dxa[rt][cb], 0, 0, 0);
         }
       }
     }
   }
   if (a.dx) {  // the four waves' partials (rows of W1 they contracted) added in wave order
-    red[wave][0][lane] = dxa[0];
-    red[wave][1][lane] = dxa[1];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      red[wave][rt][0][lane] = dxa[rt][0];
+      red[wave][rt][1][lane] = dxa[rt][1];
+    }
     __syncthreads();
-    if (wave == 0) {
+    if (wave < RT) {  // wave rt: row tile rt
+      const int rt = wave;
       const int c = lane & 15, g = lane >> 4;
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
-        f32x4 s = red[0][cb][lane];
+        f32x4 sum = red[0][rt][cb][lane];
 #pragma unroll
-        for (int w = 1; w < 4; ++w) s = s + red[w][cb][lane];
+        for (int w = 1; w < 4; ++w) sum = sum + red[w][rt][cb][lane];
         const int col = 16 * cb + c;
         if (col < K1) {
 #pragma unroll
           for (int qq = 0; qq < 4; ++qq) {
-            const int64_t row = m0 + 4 * g + qq;
-            if (row < a.M) a.dx[row * a.ldx + col] = s[qq];
+            const int64_t row = m0 + 16 * rt + 4 * g + qq;
+            if (row < a.M) a.dx[row * a.ldx + col] = sum[qq];
           }
         }
       }
@@ -573,18 +629,44 @@ bool mlp3_supported(int64_t M, int K1, int H, int N3) {
 
 hipError_t launch_mlp3_backward(const Mlp3BwdArgs& a, hipStream_t st) {
   if (!mlp3_supported(a.M, a.K1, a.H, a.N3) || a.groups < 1) return hipErrorInvalidValue;
-  const int64_t tiles = (a.M + TM - 1) / TM;
-  if (a.N3 <= 16)
-    k_mlp3_bwd<true><<<(unsigned)tiles, 256, 0, st>>>(a);
-  else
-    k_mlp3_bwd<false><<<(unsigned)tiles, 256, 0, st>>>(a);
+  static const int force_rt = [] {  // MH_MLP_BWD_RT = 1: one row tile per wave (A/B)
+    const char* e = getenv("MH_MLP_BWD_RT");
+    return e ? atoi(e) : 0;
+  }();
+  if (force_rt == 1) {
+    const int64_t tiles = (a.M + TM - 1) / TM;
+    if (a.N3 <= 16)
+      k_mlp3_bwd<true, 1><<<(unsigned)tiles, 256, 0, st>>>(a);
+    else
+      k_mlp3_bwd<false, 1><<<(unsigned)tiles, 256, 0, st>>>(a);
+  } else {
+    const int64_t tiles = (a.M + 31) / 32;
+    if (a.N3 <= 16)
+      k_mlp3_bwd<true, 2><<<(unsigned)tiles, 256, 0, st>>>(a);
+    else
+      k_mlp3_bwd<false, 2><<<(unsigned)tiles, 256, 0, st>>>(a);
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_mlp3_forward(const Mlp3Args& a, int groups, hipStream_t st) {
   if (!mlp3_supported(a.M, a.K1, a.H, a.N3) || groups < 1) return hipErrorInvalidValue;
-  const int64_t tiles = (a.M + TM - 1) / TM;
-  k_mlp3_fwd<<<dim3((unsigned)tiles, (unsigned)groups), 256, 0, st>>>(a);
+  // two row tiles per wave: half the weight traffic per row (M = 5,120: 17.4 vs 22.4 us, though
+  // only 160 workgroups; 10,240: 29.9 vs 33.2; the policy trunk's N3 = 256: 30.0 vs 38.9;
+  // tools/mlp3_bench.py); MH_MLP_RT = 1 or 4 for the A/B
+  static const int force_rt = [] {
+    const char* e = getenv("MH_MLP_RT");
+    return e ? atoi(e) : 0;
+  }();
+  const int64_t tiles2 = (a.M + 31) / 32;
+  if (force_rt == 4) {
+    k_mlp3_fwd<4><<<dim3((unsigned)((a.M + 63) / 64), (unsigned)groups), 256, 0, st>>>(a);
+  } else if (force_rt != 1) {
+    k_mlp3_fwd<2><<<dim3((unsigned)tiles2, (unsigned)groups), 256, 0, st>>>(a);
+  } else {
+    const int64_t tiles = (a.M + TM - 1) / TM;
+    k_mlp3_fwd<1><<<dim3((unsigned)tiles, (unsigned)groups), 256, 0, st>>>(a);
+  }
   return hipGetLastError();
 }
 

@@ -810,7 +810,11 @@ void k_sample_fused(FusedArgs a) {
 #endif
       const unsigned long long m = __ballot(emit);
       if (base + ew * 64 < E) {
-        if (lane == 0) a.emit_count[(int64_t)t * NW + gw] = __popcll(m);
+        if (lane == 0) {
+          const int nw = __popcll(m);
+          a.emit_count[(int64_t)t * NW + gw] = nw;
+          if (nw) __hip_atomic_fetch_add(a.ts_total + t, nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (emit) a.emit_list[(int64_t)t * E + (int64_t)gw * 64 + __popcll(m & ((1ull << lane) - 1ull))] =
             lane | (emit_pos << 6);
       }
@@ -856,136 +860,15 @@ void k_sample_fused(FusedArgs a) {
 // ------------------------------------------------------------------ horizon emission
 // Every window of the horizon, in the reference's order (lockstep major; env index within a
 // lockstep: base.py:178-213), into the store rows after the cursor (FIFO wrap; windows older than
-// the last `capacity` of this horizon are skipped as overwritten). Two launches:
-//   k_emit_scan   one workgroup: exclusive prefix of the window counts over the (lockstep,
-//                 256-env block) cells into scan[0 .. NC], the store cursor it starts from into
-//                 scan[NC + 1], then the cursor update (the emission below never reads the cursor,
-//                 so no workgroup can see it half-updated);
-//   k_emit_cells  one workgroup per cell: its windows are the contiguous store rows
-//                 scan[c] .. scan[c + 1]; thread per (window, slot) record, consecutive slots of a
-//                 window on consecutive lanes (consecutive ring records in, consecutive store
-//                 rows out).
-constexpr int SCAN_THREADS = 1024;
-
-// A cell's window count: its four wave counts, each loaded from a clamped index and then zeroed
-// past NW. The loads are unconditional: a load under a branch makes the compiler wait for it at
-// the join, which serialised the scan's loads into one round trip per cell (15 us per horizon).
-__device__ __forceinline__ int emit_cell_count(const int32_t* cnt_t, int b, int NW) {
-  int v[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) v[q] = cnt_t[4 * b + q < NW ? 4 * b + q : NW - 1];
-  int s = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) s += 4 * b + q < NW ? v[q] : 0;
-  return s;
-}
-
-// Rounds of SCAN_THREADS x SCAN_CPT cells: each thread loads its SCAN_CPT cells' counts with
-// independent loads (one memory latency per round instead of one per cell: a loop of dependent
-// per-cell loads took 16.7 us for the bench's 5,120 cells), then a workgroup scan of the thread
-// sums, carried across rounds.
-constexpr int SCAN_CPT = 8;
-
-__global__ __launch_bounds__(SCAN_THREADS) void k_emit_scan(HorizonEmitArgs a) {
-  const int NW = (int)((a.E + 63) / 64);
-  const int NBK = (NW + 3) / 4;
-  const int64_t NC = (int64_t)a.H * NBK;
-  __shared__ int64_t wsum[2][SCAN_THREADS / 64];
-  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
-  // the cursor, read up front (thread 0's update at the end then waits on no load)
-  int64_t cur0 = 0, cur1 = 0, cur2 = 0;
-  if (t == 0) {
-    cur0 = a.cursor[0];
-    cur1 = a.cursor[1];
-    cur2 = a.cursor[2];
-  }
-  // When every lockstep's wave counts form whole cells (NW % 4 == 0: E a multiple of 256), cell c's
-  // four counts are the 16 bytes at emit_count + 4 c, so the round's counts are loaded as
-  // consecutive int4 per lane (a wave-instruction reads 1 KB of consecutive lines) and regrouped
-  // through LDS; the general path below loads each thread's own 8 consecutive cells, whose lanes
-  // sit 128 B apart (a line per lane per load: 32 instructions x 64 lines per wave, ~15 us).
-  __shared__ int s_cnt[SCAN_THREADS * SCAN_CPT];
-  const bool whole = (NW & 3) == 0;
-  int64_t carry = 0;
-  int round = 0;
-  for (int64_t c0 = 0; c0 < NC; c0 += (int64_t)SCAN_THREADS * SCAN_CPT, ++round) {
-    int cnt[SCAN_CPT];
-    if (whole) {
-      const int4* cells = reinterpret_cast<const int4*>(a.emit_count);
-      int4 v[SCAN_CPT];
-#pragma unroll
-      for (int j = 0; j < SCAN_CPT; ++j) {
-        const int64_t c = c0 + t + (int64_t)j * SCAN_THREADS;
-        v[j] = cells[c < NC ? c : NC - 1];  // unconditional (clamped) loads, all in flight
-      }
-#pragma unroll
-      for (int j = 0; j < SCAN_CPT; ++j) {
-        const int64_t c = c0 + t + (int64_t)j * SCAN_THREADS;
-        s_cnt[t + j * SCAN_THREADS] = c < NC ? v[j].x + v[j].y + v[j].z + v[j].w : 0;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < SCAN_CPT; ++j) cnt[j] = s_cnt[t * SCAN_CPT + j];
-    } else {
-      // (lockstep, block) of this thread's first cell, then stepped: one 32-bit division per
-      // thread and round instead of a 64-bit one per cell (cells < 2^31: the launcher's bound)
-      const int c = (int)(c0 + (int64_t)t * SCAN_CPT);
-      int ts = c / NBK, b = c - ts * NBK;
-#pragma unroll
-      for (int j = 0; j < SCAN_CPT; ++j) {
-        const bool ok = (int64_t)c + j < NC;  // past the last cell: load cell 0, count 0
-        const int v = emit_cell_count(a.emit_count + (int64_t)(ok ? ts : 0) * NW, ok ? b : 0, NW);
-        cnt[j] = ok ? v : 0;
-        if (++b == NBK) {
-          b = 0;
-          ++ts;
-        }
-      }
-    }
-    int64_t local = 0;
-#pragma unroll
-    for (int j = 0; j < SCAN_CPT; ++j) local += cnt[j];
-    int64_t incl = local;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int64_t v = __shfl_up(incl, off, 64);
-      if (lane >= off) incl += v;
-    }
-    // double-buffered wave sums: round r + 1 writes the other slot, so one barrier per round
-    // suffices (every wave has read slot r & 1 before any wave passes round r + 1's barrier)
-    if (lane == 63) wsum[round & 1][wave] = incl;
-    __syncthreads();
-    int64_t wbase = 0, all = 0;
-#pragma unroll
-    for (int q = 0; q < SCAN_THREADS / 64; ++q) {
-      const int64_t s = wsum[round & 1][q];
-      wbase += q < wave ? s : 0;
-      all += s;
-    }
-    int64_t run = carry + wbase + incl - local;
-#pragma unroll
-    for (int j = 0; j < SCAN_CPT; ++j) {
-      const int64_t c = c0 + (int64_t)t * SCAN_CPT + j;
-      if (c < NC) a.scan[c] = run;
-      run += cnt[j];
-    }
-    carry += all;
-  }
-  const int64_t all = carry;
-  __syncthreads();  // (workgroup-scope fence + barrier: thread 0 reads the scan written above)
-  if (t == 0) {
-    const int64_t M = a.capacity;
-    a.scan[NC] = all;
-    a.scan[NC + 1] = cur0;
-    a.cursor[0] = (cur0 + all) % M;
-    const int64_t sz = cur1 + all;
-    a.cursor[1] = sz < M ? sz : M;
-    a.cursor[2] = cur2 + all;
-    // windows of the horizon's last lockstep (the lockstep path's cursor[3]): its cells are the
-    // scan's last NBK, prefix all - scan[NC - NBK] (read back from this launch's own stores)
-    a.cursor[3] = all - a.scan[NC - NBK];
-  }
-}
+// the last `capacity` of this horizon are skipped as overwritten), in ONE launch: k_emit_cells, a
+// workgroup per (lockstep, 256-env block) cell. A cell's first store row is its exclusive window
+// prefix: the lockstep totals before it (ts_total, summed by the fused kernel's waves with atomic
+// adds: integer, so order-free) plus the wave counts of the cells before it in its lockstep (at
+// most E / 64 counts, reduced by the workgroup). The last workgroup to arrive (every other one has
+// read the cursor by then) advances the cursor and re-zeroes ts_total for the next horizon. (A
+// separate single-workgroup scan launch over the 5,120 cells took 8.6 us per horizon.)
+// Within a cell: thread per (window, slot) record, consecutive slots of a window on consecutive
+// lanes (consecutive ring records in, consecutive store rows out).
 
 // 64 consecutive store rows [D] (one per lane, lane order) written through an LDS transpose as
 // contiguous chunks: 16-byte stores when D % 4 == 0, else 4-byte, one contiguous run per
@@ -1018,15 +901,34 @@ template <int D, int A>
 __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
   constexpr int F = rec_floats(D, A);
   __shared__ float stage[4][64 * D];
+  __shared__ int s_pre[4];
   const int NW = (int)((a.E + 63) / 64);
   const int NBK = (NW + 3) / 4;
-  const int64_t NC = (int64_t)a.H * NBK;
   const int64_t c = blockIdx.x;
   const int ts = (int)(c / NBK), b = (int)(c - (int64_t)ts * NBK);
-  const int64_t total = a.scan[NC], M = a.capacity, base = a.scan[NC + 1];
-  const int64_t g0 = a.scan[c];
-  const int64_t start = total > M ? total - M : 0;  // older windows are overwritten this horizon
   const int32_t* cnt = a.emit_count + (int64_t)ts * NW;
+  // the cursor the horizon starts from (every workgroup reads it before it arrives below)
+  const int64_t base = a.cursor[0], size0 = a.cursor[1], total0 = a.cursor[2], M = a.capacity;
+  // this cell's exclusive prefix: the lockstep totals before ts, then the wave counts of the
+  // lockstep's cells before b
+  int64_t total = 0, pre_ts = 0;
+  int last_ts = 0;
+  for (int t2 = 0; t2 < a.H; ++t2) {
+    const int v = a.ts_total[t2];
+    total += v;
+    pre_ts += t2 < ts ? v : 0;
+    last_ts = v;
+  }
+  {
+    int part = 0;
+    for (int i = threadIdx.x; i < 4 * b; i += 256) part += cnt[i];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off, 64);
+    if ((threadIdx.x & 63) == 0) s_pre[threadIdx.x >> 6] = part;
+  }
+  __syncthreads();
+  const int64_t g0 = pre_ts + (int64_t)(s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3]);
+  const int64_t start = total > M ? total - M : 0;  // older windows are overwritten this horizon
   int pre[5], cv[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) cv[q] = cnt[4 * b + q < NW ? 4 * b + q : NW - 1];  // unconditional loads
@@ -1092,6 +994,20 @@ __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
       a.logp[o] = rec[2 * D + A + 3];
     }
   }
+  // arrival: the last workgroup advances the cursor and re-arms ts_total / arrive
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const uint32_t arrived = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (arrived == gridDim.x - 1) {
+      a.cursor[0] = (base + total) % M;
+      a.cursor[1] = size0 + total < M ? size0 + total : M;
+      a.cursor[2] = total0 + total;
+      a.cursor[3] = last_ts;  // windows of the horizon's last lockstep (the lockstep path's cursor[3])
+      for (int t2 = 0; t2 < a.H; ++t2) __hip_atomic_store(a.ts_total + t2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // ------------------------------------------------------------------ launchers
@@ -1100,10 +1016,9 @@ static hipError_t launch_fused_t(const FusedArgs& a, const HorizonEmitArgs& ea, 
   const int grid = (int)((a.E + FUSED_ENVS - 1) / FUSED_ENVS);
   k_sample_fused<Env><<<grid, FUSED_THREADS, 0, st>>>(a);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || ea.obs == nullptr) return e;
-  k_emit_scan<<<1, SCAN_THREADS, 0, st>>>(ea);
-  e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (ea.obs == nullptr)  // no emission: re-arm the lockstep totals here
+    return hipMemsetAsync(a.ts_total, 0, sizeof(int32_t) * a.H, st);
   k_emit_cells<Env::D, Env::A><<<(unsigned)fused_emit_cells(a.E, a.H), 256, 0, st>>>(ea);
   return hipGetLastError();
 }
