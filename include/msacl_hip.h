@@ -427,6 +427,16 @@ int mh_mlp3_forward(const float* x, int64_t rows, int32_t k1, int64_t ldx, const
                     int32_t act1, int32_t act2, int32_t act3, float* h1, float* h2, int64_t ldh, float* y, int64_t ldy,
                     int32_t groups, const int64_t* group_strides, void* stream);
 
+/* Two network sets of one shape in ONE mh_mlp3_forward launch (the twin critics on [obs | act] and
+ * the twin target critics on [obs2 | next act], RL/algorithm/msacl.py:240-247): set A = {x, params
+ * = {W1, b1, W2, b2, W3, b3}, h1, h2, y} as in mh_mlp3_forward, set B = {x_b, params_b, y_b} run as
+ * groups [groups, 2 groups) with the same group strides, its activations never kept. Each set's
+ * results equal its own mh_mlp3_forward call bit for bit. */
+int mh_mlp3_forward_pair(const float* x, const float* x_b, int64_t rows, int32_t k1, int64_t ldx,
+                         const float* const* params, const float* const* params_b, int32_t hidden, int32_t n_out,
+                         int32_t act1, int32_t act2, int32_t act3, float* h1, float* h2, int64_t ldh, float* y,
+                         float* y_b, int64_t ldy, int32_t groups, const int64_t* group_strides, void* stream);
+
 /* The input-gradient chain of mh_mlp3_forward's network (its autograd backward, identity output
  * activation) in ONE launch: with dy [rows][ldy] the gradient of y,
  *   g2 = (dy W3) * act2'(h2),  g1 = (g2 W2) * act1'(h1),  dx = g1 W1

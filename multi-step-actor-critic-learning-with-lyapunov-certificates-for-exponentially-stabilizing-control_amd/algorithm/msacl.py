@@ -738,8 +738,13 @@ class MSACL:
         B, n = rew.shape
         M = B * n
         xa2 = xa.reshape(M, xa.shape[-1])
-        q, h1, h2 = twin.forward(xa2)
-        qt, _, _ = twin_t.forward(xq2.reshape(M, xq2.shape[-1]), keep=False)
+        xq2f = xq2.reshape(M, xq2.shape[-1])
+        both = twin.forward_pair(xa2, twin_t, xq2f)  # critics + target critics in one launch
+        if both is not None:
+            q, h1, h2, qt = both
+        else:
+            q, h1, h2 = twin.forward(xa2)
+            qt, _, _ = twin_t.forward(xq2f, keep=False)
         weight = data.get("weight") if self.per_flag else None
         _engine(
             "msacl_q_target", self.device,

@@ -155,6 +155,27 @@ class TwinCritic:
                                             1, 0, 1, 0, 2, H, H, 1, M, st), "mh_gemm_f32_grouped (layer 3)")
         return q, h1, h2
 
+    def forward_pair(self, x, other, x_other):
+        """(q, h1, h2) = self.forward(x) and q_other = other.forward(x_other, keep=False)[0] in ONE
+        launch (mh_mlp3_forward_pair: `other` — the target critics — as the launch's second network
+        set); None when the fused path does not apply (the caller runs the two forwards)."""
+        from ._fused import _MLP3
+        M, H, K = x.shape[0], self.H, self.K
+        if not (_MLP3["on"] and H == 256 and other.H == H and other.K == K and x_other.shape == x.shape
+                and x.is_contiguous() and x_other.is_contiguous()):
+            return None
+        N = _native()
+        q = torch.empty(2, M, dtype=torch.float32, device=x.device)
+        qo = torch.empty(2, M, dtype=torch.float32, device=x.device)
+        h1 = torch.empty(M, 2 * H, dtype=torch.float32, device=x.device)
+        h2 = torch.empty(M, 2 * H, dtype=torch.float32, device=x.device)
+        arr = lambda t: (ctypes.c_void_p * 6)(*[p.data_ptr() for p in (t.W1, t.b1, t.W2, t.b2, t.W3, t.b3)])  # noqa: E731
+        gs = (ctypes.c_int64 * 9)(0, H * K, H, H * H, H, H, 1, H, M)
+        N.check(N.lib().mh_mlp3_forward_pair(N.ptr(x), N.ptr(x_other), M, K, K, arr(self), arr(other), H, 1, 1, 1, 0,
+                                             N.ptr(h1), N.ptr(h2), 2 * H, N.ptr(q), N.ptr(qo), 1, 2, gs,
+                                             N.stream_of(x.device)), "mh_mlp3_forward_pair")
+        return q, h1, h2, qo
+
     def _back_l23(self, dq, h1, h2, want_w):
         N = _native()
         M, H = h1.shape[0], self.H

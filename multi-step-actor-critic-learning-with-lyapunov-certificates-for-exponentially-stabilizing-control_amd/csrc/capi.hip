@@ -77,7 +77,8 @@ struct mh_env_s {
   int hcap = 0;
   int32_t* h_count = nullptr;       // [hcap][ceil(E / 64)]
   int32_t* h_list = nullptr;        // [hcap][E]
-  int32_t* h_scan = nullptr;        // [hcap + 2]: the emission's per-lockstep window totals + arrival count
+  int64_t* h_scan = nullptr;        // the emission's bookkeeping (mh_nstep_reserve): aux [hcap + 2], then
+                                    // int32 lockstep totals [hcap] + arrival count
   float* dbg_logits = nullptr;      // mh_sample_horizon_debug_logits: [H][E][2A] logits trace
   float* dbg_obs = nullptr;         //   and [H][E][D] pre-step observations
   uint32_t spin_limit = 0;          // mh_sample_horizon_set_spin_limit (0: the kernel's default)
@@ -278,14 +279,17 @@ int mh_nstep_reserve(mh_env_t h, int32_t ring_slots) {
   const int F = h->info.record_floats;
   // every buffer is allocated before anything is swapped: on failure the handle is unchanged
   float* ring = nullptr;
-  int32_t *cnt = nullptr, *lst = nullptr, *scan = nullptr;
+  int32_t *cnt = nullptr, *lst = nullptr;
+  int64_t* scan = nullptr;
   hipError_t e = hipSuccess;
   if (new_ring) e = hipMalloc(&ring, sizeof(float) * E * ring_slots * F);
   if (e == hipSuccess) e = hipMalloc(&cnt, sizeof(int32_t) * hcap * ((E + 63) / 64));
   if (e == hipSuccess) e = hipMalloc(&lst, sizeof(int32_t) * hcap * E);
-  // the emission's per-lockstep window totals [hcap] and its arrival count, zero between horizons
-  if (e == hipSuccess) e = hipMalloc(&scan, sizeof(int32_t) * (hcap + 2));
-  if (e == hipSuccess) e = hipMemset(scan, 0, sizeof(int32_t) * (hcap + 2));
+  // the horizon's emission bookkeeping: int64 aux [hcap + 2] ({total, start cursor, lockstep
+  // prefixes}), then int32 per-lockstep window totals [hcap] and the arrival count, zero between
+  // horizons
+  if (e == hipSuccess) e = hipMalloc(&scan, sizeof(int64_t) * (hcap + 2) + sizeof(int32_t) * (hcap + 2));
+  if (e == hipSuccess) e = hipMemset(scan, 0, sizeof(int64_t) * (hcap + 2) + sizeof(int32_t) * (hcap + 2));
   if (e == hipSuccess && new_ring) e = hipMemset(ring, 0, sizeof(float) * E * ring_slots * F);
   if (e != hipSuccess) {
     for (void* p : {(void*)ring, (void*)cnt, (void*)lst, (void*)scan})
@@ -352,7 +356,11 @@ int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, i
   a.act_noise = act_noise;
   a.emit_count = h->h_count;
   a.emit_list = h->h_list;
-  a.ts_total = h->h_scan;
+  a.aux = h->h_scan;
+  a.ts_total = reinterpret_cast<int32_t*>(h->h_scan + h->hcap + 2);
+  a.arrive = reinterpret_cast<uint32_t*>(a.ts_total + h->hcap);
+  a.cursor = store ? store->cursor : nullptr;
+  a.capacity = store ? store->capacity : 0;
   a.act_out = act_out;
   a.logp_out = logp_out;
   a.err = h->meta + 7;  // meta[7]: the fused kernel's error word
@@ -377,9 +385,7 @@ int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, i
     ea.done = store->done;
     ea.logp = store->logp;
     ea.capacity = store->capacity;
-    ea.cursor = store->cursor;
-    ea.ts_total = h->h_scan;
-    ea.arrive = reinterpret_cast<uint32_t*>(h->h_scan + h->hcap);
+    ea.aux = h->h_scan;
   }
   MH_HIP(mh::launch_sample_fused(h->env_id, a, ea, (hipStream_t)stream));
   return MH_OK;
@@ -990,10 +996,13 @@ int mh_gemm_f32_grouped(const float* A, const float* B, const float* bias, float
   return MH_OK;
 }
 
-int mh_mlp3_forward(const float* x, int64_t rows, int32_t k1, int64_t ldx, const float* W1, const float* b1,
-                    const float* W2, const float* b2, const float* W3, const float* b3, int32_t hidden, int32_t n_out,
-                    int32_t act1, int32_t act2, int32_t act3, float* h1, float* h2, int64_t ldh, float* y, int64_t ldy,
-                    int32_t groups, const int64_t* group_strides, void* stream) {
+// mh_mlp3_forward's body; `second`: {x, W1, b1, W2, b2, W3, b3, y} of a second network set run
+// as groups [groups, 2 groups) of the same launch (mh_mlp3_forward_pair), or null
+static int mlp3_forward_impl(const float* x, int64_t rows, int32_t k1, int64_t ldx, const float* W1, const float* b1,
+                             const float* W2, const float* b2, const float* W3, const float* b3, int32_t hidden,
+                             int32_t n_out, int32_t act1, int32_t act2, int32_t act3, float* h1, float* h2,
+                             int64_t ldh, float* y, int64_t ldy, int32_t groups, const int64_t* group_strides,
+                             const void* const* second, void* stream) {
   if (rows < 0 || groups < 0) return fail(MH_EINVAL, "mh_mlp3_forward: bad size");
   if (rows == 0 || groups == 0) return MH_OK;
   if (!mh::mlp3_supported(rows, k1, hidden, n_out))
@@ -1022,8 +1031,42 @@ int mh_mlp3_forward(const float* x, int64_t rows, int32_t k1, int64_t ldx, const
     a.gs_x = g[0]; a.gs_W1 = g[1]; a.gs_b1 = g[2]; a.gs_W2 = g[3]; a.gs_b2 = g[4]; a.gs_W3 = g[5]; a.gs_b3 = g[6];
     a.gs_h = g[7]; a.gs_y = g[8];
   }
+  if (second) {
+    a.x_b = static_cast<const float*>(second[0]);
+    a.W1_b = static_cast<const float*>(second[1]);
+    a.b1_b = static_cast<const float*>(second[2]);
+    a.W2_b = static_cast<const float*>(second[3]);
+    a.b2_b = static_cast<const float*>(second[4]);
+    a.W3_b = static_cast<const float*>(second[5]);
+    a.b3_b = static_cast<const float*>(second[6]);
+    a.y_b = static_cast<float*>(const_cast<void*>(second[7]));
+    a.groups_b = groups;
+  }
   MH_HIP(mh::launch_mlp3_forward(a, groups, (hipStream_t)stream));
   return MH_OK;
+}
+
+int mh_mlp3_forward(const float* x, int64_t rows, int32_t k1, int64_t ldx, const float* W1, const float* b1,
+                    const float* W2, const float* b2, const float* W3, const float* b3, int32_t hidden, int32_t n_out,
+                    int32_t act1, int32_t act2, int32_t act3, float* h1, float* h2, int64_t ldh, float* y, int64_t ldy,
+                    int32_t groups, const int64_t* group_strides, void* stream) {
+  return mlp3_forward_impl(x, rows, k1, ldx, W1, b1, W2, b2, W3, b3, hidden, n_out, act1, act2, act3, h1, h2, ldh,
+                           y, ldy, groups, group_strides, nullptr, stream);
+}
+
+int mh_mlp3_forward_pair(const float* x, const float* x_b, int64_t rows, int32_t k1, int64_t ldx,
+                         const float* const* params, const float* const* params_b, int32_t hidden, int32_t n_out,
+                         int32_t act1, int32_t act2, int32_t act3, float* h1, float* h2, int64_t ldh, float* y,
+                         float* y_b, int64_t ldy, int32_t groups, const int64_t* group_strides, void* stream) {
+  if (!params || !params_b || !x_b || !y_b) return fail(MH_EINVAL, "mh_mlp3_forward_pair: null operand");
+  for (int i = 0; i < 6; ++i)
+    if (!params[i] || !params_b[i]) return fail(MH_EINVAL, "mh_mlp3_forward_pair: null operand");
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!al16(params_b[2]) || !al16(params_b[4]))
+    return fail(MH_EINVAL, "mh_mlp3_forward_pair: W2, W3 must be 16-byte aligned");
+  const void* second[8] = {x_b, params_b[0], params_b[1], params_b[2], params_b[3], params_b[4], params_b[5], y_b};
+  return mlp3_forward_impl(x, rows, k1, ldx, params[0], params[1], params[2], params[3], params[4], params[5], hidden,
+                           n_out, act1, act2, act3, h1, h2, ldh, y, ldy, groups, group_strides, second, stream);
 }
 
 int mh_mlp3_backward(const float* dy, int64_t ldy, const float* h1, const float* h2, int64_t ldh, const float* W1,

@@ -188,7 +188,20 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
   __shared__ float hs2[TR * SH];
   __shared__ f32x4 red[4][RT][64];
   {
-    const int64_t q = blockIdx.y;
+    int64_t q = blockIdx.y;
+    if (q >= a.groups_a) {  // the second network set (its activations are not kept)
+      q -= a.groups_a;
+      a.x = a.x_b;
+      a.W1 = a.W1_b;
+      a.b1 = a.b1_b;
+      a.W2 = a.W2_b;
+      a.b2 = a.b2_b;
+      a.W3 = a.W3_b;
+      a.b3 = a.b3_b;
+      a.y = a.y_b;
+      a.h1 = nullptr;
+      a.h2 = nullptr;
+    }
     a.x += q * a.gs_x;
     a.W1 += q * a.gs_W1;
     a.b1 += q * a.gs_b1;
@@ -629,11 +642,13 @@ bool mlp3_supported(int64_t M, int K1, int H, int N3) {
 
 hipError_t launch_mlp3_backward(const Mlp3BwdArgs& a, hipStream_t st) {
   if (!mlp3_supported(a.M, a.K1, a.H, a.N3) || a.groups < 1) return hipErrorInvalidValue;
-  static const int force_rt = [] {  // MH_MLP_BWD_RT = 1: one row tile per wave (A/B)
+  // one row tile per wave: two (MH_MLP_BWD_RT=2, one workgroup per CU for its 116 KB of LDS)
+  // measured slower (10,240 rows: 38.7 vs 27.4 us; N3 = 256: 34.7 vs 30.0; tools/mlp3_bench.py)
+  static const int force_rt = [] {
     const char* e = getenv("MH_MLP_BWD_RT");
     return e ? atoi(e) : 0;
   }();
-  if (force_rt == 1) {
+  if (force_rt != 2) {
     const int64_t tiles = (a.M + TM - 1) / TM;
     if (a.N3 <= 16)
       k_mlp3_bwd<true, 1><<<(unsigned)tiles, 256, 0, st>>>(a);
@@ -649,8 +664,11 @@ hipError_t launch_mlp3_backward(const Mlp3BwdArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_mlp3_forward(const Mlp3Args& a, int groups, hipStream_t st) {
-  if (!mlp3_supported(a.M, a.K1, a.H, a.N3) || groups < 1) return hipErrorInvalidValue;
+hipError_t launch_mlp3_forward(const Mlp3Args& a_in, int groups, hipStream_t st) {
+  if (!mlp3_supported(a_in.M, a_in.K1, a_in.H, a_in.N3) || groups < 1 || a_in.groups_b < 0) return hipErrorInvalidValue;
+  Mlp3Args a = a_in;
+  a.groups_a = groups;
+  groups += a.groups_b;
   // two row tiles per wave: half the weight traffic per row (M = 5,120: 17.4 vs 22.4 us, though
   // only 160 workgroups; 10,240: 29.9 vs 33.2; the policy trunk's N3 = 256: 30.0 vs 38.9;
   // tools/mlp3_bench.py); MH_MLP_RT = 1 or 4 for the A/B

@@ -193,6 +193,12 @@ struct Mlp3Args {
   float *h1, *h2, *y;    // h1 / h2 may be null (not kept)
   int64_t ldh, ldy;
   int64_t gs_x, gs_W1, gs_b1, gs_W2, gs_b2, gs_W3, gs_b3, gs_h, gs_y;
+  // a second network set of the same shapes and group strides in the same launch (groups
+  // [groups_a, groups_a + groups_b) of the grid: the twin target critics beside the twin critics),
+  // its activations never kept; groups_b = 0: none
+  const float *x_b, *W1_b, *b1_b, *W2_b, *b2_b, *W3_b, *b3_b;
+  float* y_b;
+  int groups_a, groups_b;
 };
 // the fused 3-layer MLP input-gradient chain (mlp_fused.hip): g2 = (dy W3) * act2'(h2),
 // g1 = (g2 W2) * act1'(h1), dx = sum over groups of g1 W1 (dy is the gradient of the identity-

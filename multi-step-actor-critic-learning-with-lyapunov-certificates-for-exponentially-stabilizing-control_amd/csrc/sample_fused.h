@@ -26,8 +26,13 @@ struct FusedArgs {
   const float* act_noise;  // [H] GaussNoise scalars (one per lockstep) or null
   int32_t* emit_count;     // [H][NW] windows completed per (lockstep, 64-env wave)
   int32_t* emit_list;      // [H][E] per wave, rank-ordered (lane | oldest slot << 6)
-  int32_t* ts_total;       // [H] windows completed per lockstep (atomic adds; zero on entry, re-zeroed
-                           // by the emission's last workgroup)
+  int32_t* ts_total;       // [H] windows completed per lockstep (atomic adds; zero on entry: the last
+                           // workgroup to finish turns them into aux's prefixes and re-zeroes them)
+  uint32_t* arrive;        // workgroup arrival count (0 between horizons)
+  int64_t* aux;            // out: {total windows, store cursor before the horizon, prefix[0 .. H)}
+  int64_t* cursor;         // the window store's {ptr, size, total, last} (advanced by the last
+                           // workgroup), or null: no store
+  int64_t capacity;
   float* act_out;          // [H][E][A] or null
   float* logp_out;         // [H][E] or null
   int64_t* err;            // device error word: policy-wave waits that timed out (0 when healthy)
@@ -52,9 +57,7 @@ struct HorizonEmitArgs {
   const int32_t* emit_list;   // [H][E]
   float *obs, *act, *rew, *cost, *obs2, *done, *logp;
   int64_t capacity;
-  int64_t* cursor;    // {ptr, size, total, last}
-  int32_t* ts_total;  // [H] windows per lockstep (FusedArgs::ts_total)
-  uint32_t* arrive;   // the emission's workgroup arrival count (0 between horizons)
+  const int64_t* aux;  // FusedArgs::aux
 };
 
 

@@ -855,6 +855,34 @@ void k_sample_fused(FusedArgs a) {
     const int64_t g = base * D + i;
     if (g < E * D) a.obs[g] = s_obs[i];
   }
+  // ---- the emission's bookkeeping, by the last workgroup to finish (every lockstep count is in):
+  // the per-lockstep window prefixes and the total into aux, with the store cursor they start
+  // from; the cursor advanced past the horizon's windows; the counts re-zeroed for the next horizon
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const uint32_t arrived = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (arrived == gridDim.x - 1) {
+      int64_t run = 0;
+      int last = 0;
+      for (int t = 0; t < H; ++t) {
+        last = __hip_atomic_load(a.ts_total + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.aux[2 + t] = run;
+        run += last;
+        __hip_atomic_store(a.ts_total + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      a.aux[0] = run;
+      if (a.cursor) {
+        const int64_t M = a.capacity, c0 = a.cursor[0], c1 = a.cursor[1];
+        a.aux[1] = c0;
+        a.cursor[0] = (c0 + run) % M;
+        a.cursor[1] = c1 + run < M ? c1 + run : M;
+        a.cursor[2] += run;
+        a.cursor[3] = last;  // windows of the horizon's last lockstep (the lockstep path's cursor[3])
+      }
+      __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // ------------------------------------------------------------------ horizon emission
@@ -862,11 +890,11 @@ void k_sample_fused(FusedArgs a) {
 // lockstep: base.py:178-213), into the store rows after the cursor (FIFO wrap; windows older than
 // the last `capacity` of this horizon are skipped as overwritten), in ONE launch: k_emit_cells, a
 // workgroup per (lockstep, 256-env block) cell. A cell's first store row is its exclusive window
-// prefix: the lockstep totals before it (ts_total, summed by the fused kernel's waves with atomic
-// adds: integer, so order-free) plus the wave counts of the cells before it in its lockstep (at
-// most E / 64 counts, reduced by the workgroup). The last workgroup to arrive (every other one has
-// read the cursor by then) advances the cursor and re-zeroes ts_total for the next horizon. (A
-// separate single-workgroup scan launch over the 5,120 cells took 8.6 us per horizon.)
+// prefix: the lockstep's prefix (aux, formed at the end of the fused kernel from per-lockstep
+// totals its waves summed with integer atomic adds: order-free) plus the wave counts of the cells
+// before it in its lockstep (at most E / 64 counts, reduced by the workgroup). The fused kernel's
+// last workgroup also advanced the store cursor. (A separate single-workgroup scan launch over the
+// 5,120 cells took 8.6 us per horizon.)
 // Within a cell: thread per (window, slot) record, consecutive slots of a window on consecutive
 // lanes (consecutive ring records in, consecutive store rows out).
 
@@ -907,19 +935,13 @@ __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
   const int64_t c = blockIdx.x;
   const int ts = (int)(c / NBK), b = (int)(c - (int64_t)ts * NBK);
   const int32_t* cnt = a.emit_count + (int64_t)ts * NW;
-  // the cursor the horizon starts from (every workgroup reads it before it arrives below)
-  const int64_t base = a.cursor[0], size0 = a.cursor[1], total0 = a.cursor[2], M = a.capacity;
-  // this cell's exclusive prefix: the lockstep totals before ts, then the wave counts of the
-  // lockstep's cells before b
-  int64_t total = 0, pre_ts = 0;
-  int last_ts = 0;
-  for (int t2 = 0; t2 < a.H; ++t2) {
-    const int v = a.ts_total[t2];
-    total += v;
-    pre_ts += t2 < ts ? v : 0;
-    last_ts = v;
+  __shared__ int64_t s_hdr[3];
+  if (threadIdx.x == 0) {  // one lane reads the shared header (every workgroup reads the same line)
+    s_hdr[0] = a.aux[0];
+    s_hdr[1] = a.aux[1];
+    s_hdr[2] = a.aux[2 + ts];
   }
-  {
+  {  // the wave counts of the lockstep's cells before b
     int part = 0;
     for (int i = threadIdx.x; i < 4 * b; i += 256) part += cnt[i];
 #pragma unroll
@@ -927,7 +949,8 @@ __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
     if ((threadIdx.x & 63) == 0) s_pre[threadIdx.x >> 6] = part;
   }
   __syncthreads();
-  const int64_t g0 = pre_ts + (int64_t)(s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3]);
+  const int64_t total = s_hdr[0], base = s_hdr[1], M = a.capacity;
+  const int64_t g0 = s_hdr[2] + (int64_t)(s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3]);
   const int64_t start = total > M ? total - M : 0;  // older windows are overwritten this horizon
   int pre[5], cv[4];
 #pragma unroll
@@ -994,20 +1017,6 @@ __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
       a.logp[o] = rec[2 * D + A + 3];
     }
   }
-  // arrival: the last workgroup advances the cursor and re-arms ts_total / arrive
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const uint32_t arrived = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (arrived == gridDim.x - 1) {
-      a.cursor[0] = (base + total) % M;
-      a.cursor[1] = size0 + total < M ? size0 + total : M;
-      a.cursor[2] = total0 + total;
-      a.cursor[3] = last_ts;  // windows of the horizon's last lockstep (the lockstep path's cursor[3])
-      for (int t2 = 0; t2 < a.H; ++t2) __hip_atomic_store(a.ts_total + t2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 // ------------------------------------------------------------------ launchers
@@ -1016,9 +1025,7 @@ static hipError_t launch_fused_t(const FusedArgs& a, const HorizonEmitArgs& ea, 
   const int grid = (int)((a.E + FUSED_ENVS - 1) / FUSED_ENVS);
   k_sample_fused<Env><<<grid, FUSED_THREADS, 0, st>>>(a);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  if (ea.obs == nullptr)  // no emission: re-arm the lockstep totals here
-    return hipMemsetAsync(a.ts_total, 0, sizeof(int32_t) * a.H, st);
+  if (e != hipSuccess || ea.obs == nullptr) return e;
   k_emit_cells<Env::D, Env::A><<<(unsigned)fused_emit_cells(a.E, a.H), 256, 0, st>>>(ea);
   return hipGetLastError();
 }

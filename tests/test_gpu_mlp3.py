@@ -192,6 +192,24 @@ def test_twin_input_grad_chain_equals_per_layer():
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-5 * float(outs[1].abs().max()))
 
 
+@pytest.mark.parametrize("M", [5120, 3001])
+def test_twin_forward_pair_equals_two_forwards(M):
+    """TwinCritic.forward_pair (mh_mlp3_forward_pair: the critics and the target critics as the two
+    network sets of one launch) equals the two separate forwards bit for bit."""
+    from msacl_amd.apprfunc._twin import TwinCritic
+    from msacl_amd.apprfunc.mlp import ActionValue
+    torch.manual_seed(2)
+    kw = dict(obs_dim=12, act_dim=4, hidden_sizes=[256, 256], hidden_activation="relu", output_activation="linear")
+    nets = [ActionValue(**kw).cuda() for _ in range(4)]
+    tc, tt = TwinCritic.build(nets[0], nets[1]), TwinCritic.build(nets[2], nets[3])
+    x, xo = torch.randn(M, 16, device="cuda"), torch.randn(M, 16, device="cuda")
+    q, h1, h2, qo = tc.forward_pair(x, tt, xo)
+    q_ref, h1_ref, h2_ref = tc.forward(x)
+    qo_ref, _, _ = tt.forward(xo, keep=False)
+    for a, b in ((q, q_ref), (h1, h1_ref), (h2, h2_ref), (qo, qo_ref)):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
 @pytest.mark.parametrize("rows", [5120, 3001])
 def test_weight_grads_multi_matches_float64(rows):
     """mh_weight_grads: the three layers' dW = g^T x and db = column sums of g of a policy-shaped MLP
