@@ -280,10 +280,10 @@ def layer_backward(dy, x, weight, y, act, need_x, need_w, need_b):
 # The whole 3-layer MLP forward as one launch (mh_mlp3_forward, csrc/mlp_fused.hip) where the
 # shape qualifies; MSACL_MLP3=0 restores the per-layer launches (A/B)
 _MLP3 = {"on": os.environ.get("MSACL_MLP3", "1") == "1",
-         # wide outputs (N3 a multiple of 64: the policy trunk): forward through the per-layer
-         # kernels (every CU on a column block) instead of the one-launch kernel, which re-reads the
-         # 256 x 256 weights per 16-row tile twice there; MSACL_MLP3_WIDE=1 takes the fused forward
-         "wide_fwd": os.environ.get("MSACL_MLP3_WIDE", "0") == "1"}
+         # wide outputs (N3 a multiple of 64: the policy trunk) through the one-launch kernel too
+         # (two row tiles per wave: 30.0 us standalone, the per-layer kernels 30.2; in the bench
+         # 1.114-1.125 vs 1.109-1.119 G env-steps/s); MSACL_MLP3_WIDE=0: the per-layer kernels
+         "wide_fwd": os.environ.get("MSACL_MLP3_WIDE", "1") == "1"}
 
 
 def _linear_act(x, W, b, act):

@@ -702,10 +702,20 @@ static bool deep_ok(const float* A, const float* B, const float* bias, int64_t M
 }
 
 // K splits: about 256 workgroups, slices of >= 2 chunks
+// workgroups a deep product aims for (MH_DEEP_WGS overrides 256 for A/B measurements)
+static int64_t deep_target() {
+  static const int64_t t = [] {
+    const char* e = getenv("MH_DEEP_WGS");
+    const int64_t v = e ? atoll(e) : 0;
+    return v > 0 ? v : 256;
+  }();
+  return t;
+}
+
 static int deep_splits(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = (M / 64) * ((N + 63) / 64);
   const int64_t chunks = (K + TK - 1) / TK;
-  int64_t S = (256 + tiles - 1) / tiles;
+  int64_t S = (deep_target() + tiles - 1) / tiles;
   if (S > chunks / 2) S = chunks / 2;
   if (S < 1) S = 1;
   const int64_t per = (chunks + S - 1) / S;

@@ -813,7 +813,9 @@ void k_sample_fused(FusedArgs a) {
         if (lane == 0) {
           const int nw = __popcll(m);
           a.emit_count[(int64_t)t * NW + gw] = nw;
+#ifndef MH_FUSED_EXP_NO_TS  // cost-attribution experiment only (the emission's totals stay 0)
           if (nw) __hip_atomic_fetch_add(a.ts_total + t, nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         }
         if (emit) a.emit_list[(int64_t)t * E + (int64_t)gw * 64 + __popcll(m & ((1ull << lane) - 1ull))] =
             lane | (emit_pos << 6);
@@ -859,18 +861,39 @@ void k_sample_fused(FusedArgs a) {
   // the per-lockstep window prefixes and the total into aux, with the store cursor they start
   // from; the cursor advanced past the horizon's windows; the counts re-zeroed for the next horizon
   __syncthreads();
+  __shared__ uint32_t s_last;
   if (threadIdx.x == 0) {
     __threadfence();
     const uint32_t arrived = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (arrived == gridDim.x - 1) {
-      int64_t run = 0;
-      int last = 0;
-      for (int t = 0; t < H; ++t) {
-        last = __hip_atomic_load(a.ts_total + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        a.aux[2 + t] = run;
-        run += last;
+    s_last = arrived == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (s_last && w == 0) {
+    // wave 0: 64 lockstep totals per round, loaded together, an inclusive wave scan, the
+    // exclusive prefixes stored and the totals re-zeroed (a lane-serial loop took one L2 round
+    // trip per lockstep at the kernel's tail)
+    __threadfence();
+    int64_t carry = 0;
+    int last = 0;
+    for (int t0 = 0; t0 < H; t0 += 64) {
+      const int t = t0 + lane;
+      const int v = t < H ? __hip_atomic_load(a.ts_total + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+      int64_t incl = v;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int64_t u = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += u;
+      }
+      if (t < H) {
+        a.aux[2 + t] = carry + incl - v;
         __hip_atomic_store(a.ts_total + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+      const int tl = (H - 1 - t0) < 63 ? (H - 1 - t0) : 63;  // this round's last valid lane
+      if (t0 + 64 >= H) last = __shfl(v, tl, 64);
+      carry += __shfl(incl, 63, 64);
+    }
+    if (lane == 0) {
+      const int64_t run = carry;
       a.aux[0] = run;
       if (a.cursor) {
         const int64_t M = a.capacity, c0 = a.cursor[0], c1 = a.cursor[1];
