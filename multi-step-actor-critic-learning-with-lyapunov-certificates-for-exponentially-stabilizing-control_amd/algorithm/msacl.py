@@ -348,6 +348,9 @@ class MSACL:
         # the trainer asks a device replay buffer for the batch's [obs | act] and [obs_0; obs2]
         # layouts too (gathered, not concatenated per update); MSACL_JOINT_BATCH=0: torch.cat (A/B)
         self.wants_joint_batch = (self.device.type == "cuda" and os.environ.get("MSACL_JOINT_BATCH", "1") == "1")
+        # the policy step's first policy forward reuses the Lyapunov step's (MSACL_REUSE_POLICY_FWD=0: off)
+        self._reuse_policy_fwd = os.environ.get("MSACL_REUSE_POLICY_FWD", "1") == "1"
+        self._pol_kept = None
         # the update's rsample noise drawn inside the policy-head kernel (Philox, a device counter);
         # MSACL_KERNEL_NOISE=0: torch's normal draw (A/B)
         self._kernel_noise = os.environ.get("MSACL_KERNEL_NOISE", "1") == "1"
@@ -545,7 +548,7 @@ class MSACL:
             main = torch.cuda.current_stream(self.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                loss_lya = self._lyapunov_update(data)
+                loss_lya = self._lyapunov_update(data, keep_policy=do_policy)
             loss_q, q1_mean, q2_mean = self._q_update(data, stats=do_policy)
             if do_target:
                 self._target_update()
@@ -560,7 +563,7 @@ class MSACL:
             side = self._seg_side_stream()
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                loss_lya = self._lyapunov_update(data, defer_step=True)
+                loss_lya = self._lyapunov_update(data, defer_step=True, keep_policy=do_policy)
             loss_q, q1_mean, q2_mean = self._q_update(data, defer_step=True, stats=do_policy)
             main.wait_stream(side)
             nets = self.networks
@@ -574,7 +577,7 @@ class MSACL:
             loss_q, q1_mean, q2_mean = self._q_update(data, stats=do_policy)
             if do_target:
                 self._target_update()
-            loss_lya = self._lyapunov_update(data)
+            loss_lya = self._lyapunov_update(data, keep_policy=do_policy)
         loss_policy = entropy = None
         if not do_policy:
             return loss_q, q1_mean, q2_mean, loss_lya, loss_policy, entropy
@@ -762,15 +765,27 @@ class MSACL:
             return s.loss_q[0], None, None
         return s.loss_q[0], q[0].mean(), q[1].mean()
 
-    def _lyapunov_update(self, data, defer_step=False):
+    def _lyapunov_update(self, data, defer_step=False, keep_policy=False):
+        """keep_policy: a policy step follows in this update: keep the policy forward's activations
+        (the policy step's first forward is this same evaluation: same rows, weights unchanged
+        until its optimiser step) for it (_pol_kept, MLP3Kept)."""
         obs, obs2, act, old_logp = data["obs"], data["obs2"], data["act"], data["logp"]
         B, n = old_logp.shape
         s = self._buf(B, n)
         head = self._head()
+        self._pol_kept = None
         with torch.no_grad():
             if head is not None:  # policy(obs) -> head + log_prob(act) in one launch
                 hi, lo, lsl, lsh = head
-                raw = self.networks.policy.policy(obs).contiguous()
+                kept = None
+                if keep_policy and self._reuse_policy_fwd:
+                    from ..apprfunc._fused import mlp3_forward_kept
+                    kept = mlp3_forward_kept(self.networks.policy.policy, obs.reshape(B * n, obs.shape[-1]))
+                if kept is not None:
+                    raw = kept[0]
+                    self._pol_kept = (obs.data_ptr(),) + tuple(kept[1:])
+                else:
+                    raw = self.networks.policy.policy(obs).contiguous()
                 logp = torch.empty(B, n, dtype=torch.float32, device=self.device)
                 _engine("policy_head", self.device, N.ptr(raw), None, None, N.ptr(act), N.ptr(hi), N.ptr(lo), B * n,
                         hi.numel(), 0, lsl, lsh, None, None, N.ptr(logp))
@@ -841,7 +856,17 @@ class MSACL:
         if head is not None:
             hi, lo, lsl, lsh = head
             A, Dd = hi.numel(), obs.shape[-1]
-            raw = nets.policy.policy(obs)
+            pk, self._pol_kept = self._pol_kept, None
+            if not reuse_adv and pk is not None and pk[0] == obs.data_ptr():
+                # the Lyapunov step's evaluation of this same forward (MLP3Kept: backward only)
+                from ..apprfunc._fused import MLP3Kept
+                (l1, l2, l3), acts = pk[2], pk[3]
+                cur = torch.cuda.current_stream(self.device)
+                for t in pk[1]:  # made on the Lyapunov branch's stream, read here after the join
+                    t.record_stream(cur)
+                raw = MLP3Kept.apply(obs.reshape(B * n, Dd), l1[0], l1[1], l2[0], l2[1], l3[0], l3[1], acts, pk[1])
+            else:
+                raw = nets.policy.policy(obs)
             eps = self._noise(raw)
             xq, new_act_logp, old_lp = _PolicyHead.apply(raw.reshape(B * n, 2 * A).contiguous(),
                                                          None if eps is None else eps.reshape(B * n, A).contiguous(),

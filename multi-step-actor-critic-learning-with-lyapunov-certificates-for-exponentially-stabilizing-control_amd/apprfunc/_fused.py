@@ -431,6 +431,39 @@ class MLP3(torch.autograd.Function):
         return dx, dW1, db1, dW2, db2, dW3, db3, None
 
 
+class MLP3Kept(torch.autograd.Function):
+    """MLP3 whose forward already ran (mlp3_forward with the activations kept, e.g. by an earlier
+    no-grad use of the same network on the same rows with the same weights): returns the kept
+    output, backward exactly as MLP3's. `kept` = (h1, h2, y)."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2, W3, b3, acts, kept):
+        h1, h2, y = kept
+        ctx.acts = acts
+        ctx.save_for_backward(x, W1, W2, W3, h1, h2, y)
+        return y.view_as(y)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return MLP3.backward(ctx, dy) + (None,)
+
+
+def mlp3_forward_kept(seq, x):
+    """(y, kept) of the MLP `seq` on x [rows][K1] through mh_mlp3_forward with h1 / h2 kept, for a
+    later MLP3Kept.apply(x, *params, acts, kept); None when the fused path does not take `seq`."""
+    if not (_MLP3["on"] and _GEMM_BACKEND["name"] != "blas" and x.is_cuda and x.dtype == torch.float32
+            and x.is_contiguous() and x.data_ptr() % 4 == 0):
+        return None
+    spec = mlp3_layers(seq)
+    if spec is None:
+        return None
+    (l1, l2, l3), acts = spec
+    if l3[0].shape[0] > 16 and not _MLP3["wide_fwd"]:
+        return None
+    y, h1, h2 = mlp3_forward(x, (l1, l2, l3), acts, True)
+    return y, (h1, h2, y), (l1, l2, l3), acts
+
+
 def mlp3_layers(seq):
     """((W1, b1), (W2, b2), (W3, b3)), (act ids) of an MLP [K1 <= 32, 256, 256, N3] that
     mh_mlp3_forward runs, else None."""

@@ -1,7 +1,7 @@
 #!/bin/bash
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest tests/test_gpu_fused_horizon.py tests/test_gpu_nstep.py -m gpu -x -q --timeout 300 --timeout-method thread -rf > gpurun_out/it9_tests.log 2>&1
+timeout -k 10 500 python -u -m pytest tests/test_gpu_fused_horizon.py tests/test_gpu_nstep.py tests/test_gpu_msacl.py tests/test_gpu_msacl_bench.py tests/test_gpu_mlp3.py tests/test_gpu_trainer.py -m gpu -x -q --timeout 300 --timeout-method thread -rf > gpurun_out/it9_tests.log 2>&1
 rc=$?; tail -2 gpurun_out/it9_tests.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do for v in build nots; do
   if [ $v = build ]; then L=""; else L="MSACL_HIP_LIB=exp_libs/sample_fused-$v/libmsacl_hip.so"; fi
