@@ -864,7 +864,8 @@ class MSACL:
                 cur = torch.cuda.current_stream(self.device)
                 for t in pk[1]:  # made on the Lyapunov branch's stream, read here after the join
                     t.record_stream(cur)
-                raw = MLP3Kept.apply(obs.reshape(B * n, Dd), l1[0], l1[1], l2[0], l2[1], l3[0], l3[1], acts, pk[1])
+                raw = MLP3Kept.apply(obs.reshape(B * n, Dd), l1[0], l1[1], l2[0], l2[1], l3[0], l3[1], acts,
+                                     pk[1]).view(B, n, 2 * A)  # (the [B, n, 2A] of policy.policy(obs))
             else:
                 raw = nets.policy.policy(obs)
             eps = self._noise(raw)
