@@ -7,8 +7,9 @@ import os
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "multi-step-actor-critic-learning-with-lyapunov-certificates-for-exponentially-stabilizing-control_amd",
                     "csrc")
-ROLLOUT_SOURCES = ("rollout.hip", "rollout.h", "env_math.h", "reset_draw.h", "philox.h", "capi.hip", "Makefile",
-                   "sample_fused.hip", "sample_fused.h", "policy_x3.h")
+# the kernels' own sources and build flags (the C ABI glue in capi.hip changes no kernel's traffic)
+ROLLOUT_SOURCES = ("rollout.hip", "env_math.h", "reset_draw.h", "philox.h", "Makefile",
+                   "sample_fused.hip", "sample_fused.h", "policy_x3.h", "policy_mlp.hip")
 
 
 def rollout_sources_sha(names=ROLLOUT_SOURCES) -> str:
