@@ -437,6 +437,20 @@ int mh_mlp3_forward_pair(const float* x, const float* x_b, int64_t rows, int32_t
                          int32_t act1, int32_t act2, int32_t act3, float* h1, float* h2, int64_t ldh, float* y,
                          float* y_b, int64_t ldy, int32_t groups, const int64_t* group_strides, void* stream);
 
+/* LyapunovValue (RL/apprfunc/mlp.py LyapunovValue: V(x) = sum_n MLP(x)_n^2, msacl.py:275-276) in the
+ * MLP's launches: mh_mlp3_forward (set A only) that also writes v [rows] = sum over the n_out
+ * outputs of y^2, in mh_square_sum's order (bit-identical); and its backward: mh_mlp3_backward's
+ * chain with the output gradient dy = dv[row] (2 y) formed in-kernel from the forward output y
+ * (mh_square_sum_backward's expression) and written to g3 [rows][ldy] for the weight gradients.
+ * n_out a multiple of 64. */
+int mh_mlp3_forward_sqsum(const float* x, int64_t rows, int32_t k1, int64_t ldx, const float* const* params,
+                          int32_t hidden, int32_t n_out, int32_t act1, int32_t act2, int32_t act3, float* h1,
+                          float* h2, int64_t ldh, float* y, int64_t ldy, float* v, void* stream);
+int mh_mlp3_backward_sqsum(const float* y, int64_t ldy, const float* dv, const float* h1, const float* h2, int64_t ldh,
+                           const float* W1, const float* W2, const float* W3, int64_t rows, int32_t k1, int32_t hidden,
+                           int32_t n_out, int32_t act1, int32_t act2, float* g3, float* g2, float* g1, int64_t ldg,
+                           float* dx, int64_t ldx, void* stream);
+
 /* The input-gradient chain of mh_mlp3_forward's network (its autograd backward, identity output
  * activation) in ONE launch: with dy [rows][ldy] the gradient of y,
  *   g2 = (dy W3) * act2'(h2),  g1 = (g2 W2) * act1'(h1),  dx = g1 W1

@@ -146,6 +146,10 @@ _PROTOS = {
                         + [c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mh_mlp3_forward_pair": (ctypes.c_int, [c_vp, c_vp, c_i64, c_i32, c_i64, c_vp, c_vp, c_i32, c_i32] + [c_i32] * 3
                              + [c_vp, c_vp, c_i64, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "mh_mlp3_forward_sqsum": (ctypes.c_int, [c_vp, c_i64, c_i32, c_i64, c_vp] + [c_i32] * 5
+                              + [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp]),
+    "mh_mlp3_backward_sqsum": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64]
+                               + [c_i32] * 5 + [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "mh_mlp3_backward": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64] + [c_i32] * 5
                          + [c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp]),
     "mh_weight_grads_workspace": (ctypes.c_int, [c_vp, c_i32, c_i64, ctypes.POINTER(c_i64)]),

@@ -283,7 +283,9 @@ _MLP3 = {"on": os.environ.get("MSACL_MLP3", "1") == "1",
          # wide outputs (N3 a multiple of 64: the policy trunk) through the one-launch kernel too
          # (two row tiles per wave: 30.0 us standalone, the per-layer kernels 30.2; in the bench
          # 1.114-1.125 vs 1.109-1.119 G env-steps/s); MSACL_MLP3_WIDE=0: the per-layer kernels
-         "wide_fwd": os.environ.get("MSACL_MLP3_WIDE", "1") == "1"}
+         "wide_fwd": os.environ.get("MSACL_MLP3_WIDE", "1") == "1",
+         # LyapunovValue's square sums inside the MLP's launches (MLP3SquareSum); 0: SquareSum (A/B)
+         "sqsum": os.environ.get("MSACL_MLP3_SQSUM", "1") == "1"}
 
 
 def _linear_act(x, W, b, act):
@@ -429,6 +431,87 @@ class MLP3(torch.autograd.Function):
             if need_h1:
                 dx, dW1, db1 = layer_backward(dh1, x, W1, h1, a1, nx, nW1, nb1)
         return dx, dW1, db1, dW2, db2, dW3, db3, None
+
+
+class MLP3SquareSum(torch.autograd.Function):
+    """LyapunovValue's V = sum(MLP(x)^2, -1) (mlp.py LyapunovValue) over a 3-layer MLP with a wide
+    output (N3 a multiple of 64): the forward is mh_mlp3_forward_sqsum (the square sums formed in
+    the MLP's launch, SquareSum's bits), the backward mh_mlp3_backward_sqsum (dy = dV 2y formed
+    in the chain's launch, SquareSum.backward's bits, kept for the weight gradients) plus
+    mh_weight_grads: the square-sum launch and its backward launch disappear."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2, W3, b3, acts):
+        N = _native()
+        M, K1 = x.shape
+        H, N3, dev = W2.shape[0], W3.shape[0], x.device
+        keep = any(ctx.needs_input_grad[:7])
+        e = lambda *sh: torch.empty(*sh, dtype=torch.float32, device=dev)  # noqa: E731
+        y, v = e(M, N3), e(M)
+        h1, h2 = (e(M, H), e(M, H)) if keep else (None, None)
+        ps = (ctypes.c_void_p * 6)(*[t.data_ptr() for t in (W1, b1, W2, b2, W3, b3)])
+        N.check(N.lib().mh_mlp3_forward_sqsum(N.ptr(x), M, K1, x.stride(0), ps, H, N3, acts[0], acts[1], acts[2],
+                                              N.ptr(h1), N.ptr(h2), H, N.ptr(y), N3, N.ptr(v), N.stream_of(dev)),
+                "mh_mlp3_forward_sqsum")
+        ctx.acts = acts
+        if keep:
+            ctx.save_for_backward(x, W1, W2, W3, h1, h2, y)
+        return v
+
+    @staticmethod
+    def backward(ctx, dv):
+        N = _native()
+        x, W1, W2, W3, h1, h2, y = ctx.saved_tensors
+        nx, nW1, nb1, nW2, nb2, nW3, nb3 = ctx.needs_input_grad[:7]
+        a1, a2, _a3 = ctx.acts
+        M, K1 = x.shape
+        H, N3, dev = W2.shape[0], W3.shape[0], x.device
+        e = lambda *sh: torch.empty(*sh, dtype=torch.float32, device=dev)  # noqa: E731
+        g3, g2, g1 = e(M, N3), e(M, H), e(M, H)
+        dx = e(M, K1) if nx else None
+        N.check(N.lib().mh_mlp3_backward_sqsum(N.ptr(y), N3, N.ptr(dv.contiguous()), N.ptr(h1), N.ptr(h2), H,
+                                               N.ptr(W1), N.ptr(W2), N.ptr(W3), M, K1, H, N3, a1, a2, N.ptr(g3),
+                                               N.ptr(g2), N.ptr(g1), H, N.ptr(dx), K1, N.stream_of(dev)),
+                "mh_mlp3_backward_sqsum")
+        out, prods = {}, []
+        for name, nw, nb, g, ld_g, xin, ld_x, n_out, n_in, W in (
+                ("3", nW3, nb3, g3, N3, h2, H, N3, H, W3), ("2", nW2, nb2, g2, H, h1, H, H, H, W2),
+                ("1", nW1, nb1, g1, H, x, K1, H, K1, W1)):
+            if not (nw or nb):
+                out[name] = (None, None)
+                continue
+            dw, db = e(n_out, n_in), (e(n_out) if nb else None)
+            if wgrad_ok(g, ld_g, xin, ld_x, n_out, n_in, M):
+                prods.append((g, ld_g, xin, ld_x, n_out, n_in, dw, db))
+                out[name] = (dw if nw else None, db)
+            else:
+                _, dw2, db2_ = layer_backward(g, xin, W, g, 0, False, nw, nb)
+                out[name] = (dw2, db2_)
+        if prods:
+            weight_grads(prods, M, dev)
+        return (dx, out["1"][0], out["1"][1], out["2"][0], out["2"][1], out["3"][0], out["3"][1], None)
+
+
+def square_sum_mlp(seq, x):
+    """V = sum(seq(x)^2, -1) through MLP3SquareSum when the fused path takes `seq` (a 3-layer MLP
+    with a wide identity output), else None (the caller runs seq and SquareSum)."""
+    if not (_MLP3["on"] and _MLP3["wide_fwd"] and _MLP3["sqsum"] and _GEMM_BACKEND["name"] != "blas" and x.is_cuda
+            and x.dtype == torch.float32):
+        return None
+    spec = mlp3_layers(seq)
+    if spec is None:
+        return None
+    (l1, l2, l3), acts = spec
+    if acts[2] != 0 or l3[0].shape[0] % 64 != 0:
+        return None
+    lead = x.shape[:-1]
+    h = x.reshape(-1, x.shape[-1])
+    if not h.is_contiguous():
+        h = h.contiguous()
+    if h.data_ptr() % 4:
+        return None
+    v = MLP3SquareSum.apply(h, l1[0], l1[1], l2[0], l2[1], l3[0], l3[1], acts)
+    return v.reshape(lead)
 
 
 class MLP3Kept(torch.autograd.Function):

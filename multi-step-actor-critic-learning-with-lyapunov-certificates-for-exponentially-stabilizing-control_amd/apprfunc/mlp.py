@@ -56,6 +56,11 @@ class LyapunovValue(nn.Module):
         self.lya = mlp([kw["input_dim"]] + list(kw["hidden_sizes"]) + [kw["output_dim"]], *_acts(kw))
 
     def forward(self, input_obs):
+        if input_obs.is_cuda and input_obs.dtype == torch.float32:
+            from ._fused import square_sum_mlp
+            v = square_sum_mlp(self.lya, input_obs)  # the square sums inside the MLP's launches
+            if v is not None:
+                return v
         y = self.lya(input_obs)
         if y.is_cuda and y.dtype == torch.float32:
             return SquareSum.apply(y)  # one launch each way (apprfunc/_fused.py)

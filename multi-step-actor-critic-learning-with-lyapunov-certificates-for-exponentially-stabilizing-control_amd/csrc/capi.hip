@@ -1102,6 +1102,61 @@ int mh_mlp3_backward(const float* dy, int64_t ldy, const float* h1, const float*
   return MH_OK;
 }
 
+int mh_mlp3_forward_sqsum(const float* x, int64_t rows, int32_t k1, int64_t ldx, const float* const* params,
+                          int32_t hidden, int32_t n_out, int32_t act1, int32_t act2, int32_t act3, float* h1,
+                          float* h2, int64_t ldh, float* y, int64_t ldy, float* v, void* stream) {
+  if (!params || !v) return fail(MH_EINVAL, "mh_mlp3_forward_sqsum: null operand");
+  if (n_out % 64 != 0) return fail(MH_EINVAL, "mh_mlp3_forward_sqsum: n_out must be a multiple of 64");
+  if (rows < 0) return fail(MH_EINVAL, "mh_mlp3_forward_sqsum: bad size");
+  if (rows == 0) return MH_OK;
+  if (!mh::mlp3_supported(rows, k1, hidden, n_out)) return fail(MH_EINVAL, "mh_mlp3_forward_sqsum: shape not supported");
+  for (int act : {act1, act2, act3})
+    if (act < 0 || act > 2) return fail(MH_EINVAL, "mh_mlp3_forward_sqsum: act must be 0, 1 or 2");
+  for (int i = 0; i < 6; ++i)
+    if (!params[i]) return fail(MH_EINVAL, "mh_mlp3_forward_sqsum: null operand");
+  if (!x || !y || ldx < k1 || ldy < n_out || ((h1 || h2) && ldh < hidden))
+    return fail(MH_EINVAL, "mh_mlp3_forward_sqsum: null operand or leading dimension too small");
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!al16(params[2]) || !al16(params[4]) || !al16(h1) || !al16(h2) || (ldh & 3))
+    return fail(MH_EINVAL, "mh_mlp3_forward_sqsum: W2, W3, h1, h2 must be 16-byte aligned");
+  mh::Mlp3Args a;
+  std::memset(&a, 0, sizeof(a));
+  a.x = x; a.M = rows; a.ldx = ldx; a.K1 = k1; a.H = hidden; a.N3 = n_out;
+  a.act1 = act1; a.act2 = act2; a.act3 = act3;
+  a.W1 = params[0]; a.b1 = params[1]; a.W2 = params[2]; a.b2 = params[3]; a.W3 = params[4]; a.b3 = params[5];
+  a.h1 = h1; a.h2 = h2; a.y = y; a.ldh = ldh; a.ldy = ldy;
+  a.sqsum = v;
+  MH_HIP(mh::launch_mlp3_forward(a, 1, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_mlp3_backward_sqsum(const float* y, int64_t ldy, const float* dv, const float* h1, const float* h2, int64_t ldh,
+                           const float* W1, const float* W2, const float* W3, int64_t rows, int32_t k1, int32_t hidden,
+                           int32_t n_out, int32_t act1, int32_t act2, float* g3, float* g2, float* g1, int64_t ldg,
+                           float* dx, int64_t ldx, void* stream) {
+  if (!dv || !g3) return fail(MH_EINVAL, "mh_mlp3_backward_sqsum: null operand");
+  if (n_out % 64 != 0) return fail(MH_EINVAL, "mh_mlp3_backward_sqsum: n_out must be a multiple of 64");
+  if (rows < 0) return fail(MH_EINVAL, "mh_mlp3_backward_sqsum: bad size");
+  if (rows == 0) return MH_OK;
+  if (!mh::mlp3_supported(rows, k1, hidden, n_out)) return fail(MH_EINVAL, "mh_mlp3_backward_sqsum: shape not supported");
+  if (act1 < 0 || act1 > 2 || act2 < 0 || act2 > 2) return fail(MH_EINVAL, "mh_mlp3_backward_sqsum: act must be 0, 1 or 2");
+  if (!y || !h1 || !h2 || !W1 || !W2 || !W3) return fail(MH_EINVAL, "mh_mlp3_backward_sqsum: null operand");
+  if (ldy < n_out || ldh < hidden || ((g1 || g2) && ldg < hidden) || (dx && ldx < k1))
+    return fail(MH_EINVAL, "mh_mlp3_backward_sqsum: leading dimension smaller than the matrix");
+  auto al16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (!al16(g1) || !al16(g2) || ((g1 || g2) && (ldg & 3)))
+    return fail(MH_EINVAL, "mh_mlp3_backward_sqsum: g1 / g2 must be 16-byte aligned (ldg a multiple of 4)");
+  mh::Mlp3BwdArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.dy = y; a.ldy = ldy; a.h1 = h1; a.h2 = h2; a.ldh = ldh;
+  a.W1 = W1; a.W2 = W2; a.W3 = W3; a.M = rows; a.K1 = k1; a.H = hidden; a.N3 = n_out;
+  a.act1 = act1; a.act2 = act2; a.groups = 1;
+  a.g2 = g2; a.g1 = g1; a.ldg = ldg; a.dx = dx; a.ldx = ldx;
+  a.sq_dv = dv; a.g3 = g3;
+  MH_HIP(mh::launch_mlp3_backward(a, (hipStream_t)stream));
+  return MH_OK;
+}
+
 static bool wgrad_specs(const mh_wgrad_t* products, int32_t n, std::vector<mh::WgradSpec>& v) {
   if (!products || n < 1 || n > 6) return false;
   v.resize(n);

@@ -346,6 +346,7 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
     }
   } else {
     // N3 = 64 c: wave w takes output columns [N3 / 4 * w, ...) in 16-column blocks of 64-wide passes
+    // (with sqsum: also into the free hs1 tile, N3 <= HID)
     for (int nb = wave * 64; nb < N3; nb += 256) {
       f32x4 acc[RT][4] = {};
       layer_cols<SH, HID / 16, RT>(hs2, wr3, nb, lane, acc);
@@ -359,9 +360,32 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int64_t row = m0 + 16 * rt + 4 * g + q;
-            if (row < a.M) a.y[row * a.ldy + n] = act_f(acc[rt][j][q] + bv, a.act3);
+            const float v = act_f(acc[rt][j][q] + bv, a.act3);
+            if (row < a.M) a.y[row * a.ldy + n] = v;
+            if (a.sqsum) hs1[(16 * rt + 4 * g + q) * SH + n] = v;
           }
         }
+    }
+    if (a.sqsum) {
+      // V = sum_n y^2 per row in k_square_sum's order (lane l: columns 4l .. 4l + 3 of each
+      // 256-column pass, in order; then the xor butterfly 32 .. 1): its bits
+      __syncthreads();
+      for (int rr = wave; rr < TR; rr += 4) {
+        float s = 0.0f;
+        for (int c0 = 0; c0 < N3; c0 += 256) {
+          const int cc = c0 + 4 * lane;
+          if (cc + 3 < N3) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(hs1 + rr * SH + cc);
+            s = s + v[0] * v[0];
+            s = s + v[1] * v[1];
+            s = s + v[2] * v[2];
+            s = s + v[3] * v[3];
+          }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s = s + __shfl_xor(s, off, 64);
+        if (lane == 0 && m0 + rr < a.M) a.sqsum[m0 + rr] = s;
+      }
     }
   }
 }
@@ -544,9 +568,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT == 1 ? 2
     if constexpr (NARROW) layer_cols_t_pre<HID / 16>(wr2, n0, lane, wb2);
     float hv2[RT][4][4];
     load_h_tile<RT>(h2, a.ldh, m0, a.M, n0, lane, hv2);
-    for (int i = tid; i < TR * N3p; i += 256) {
-      const int rr = i / N3p, k = i - rr * N3p;
-      gs3[rr * SH + k] = (m0 + rr < a.M && k < N3) ? dy[(m0 + rr) * a.ldy + k] : 0.0f;
+    if (a.sq_dv) {  // LyapunovValue: dy = dV (2 y) (k_square_sum_bwd's expression), kept in g3
+      for (int i = tid; i < TR * N3p; i += 256) {
+        const int rr = i / N3p, k = i - rr * N3p;
+        float v = 0.0f;
+        if (m0 + rr < a.M && k < N3) {
+          v = a.sq_dv[m0 + rr] * (2.0f * dy[(m0 + rr) * a.ldy + k]);
+          a.g3[(m0 + rr) * a.ldy + k] = v;
+        }
+        gs3[rr * SH + k] = v;
+      }
+    } else {
+      for (int i = tid; i < TR * N3p; i += 256) {
+        const int rr = i / N3p, k = i - rr * N3p;
+        gs3[rr * SH + k] = (m0 + rr < a.M && k < N3) ? dy[(m0 + rr) * a.ldy + k] : 0.0f;
+      }
     }
     __syncthreads();
     // dh2 = g3 W3 (contraction over W3's N3 rows), g2 = dh2 * act2'(h2)

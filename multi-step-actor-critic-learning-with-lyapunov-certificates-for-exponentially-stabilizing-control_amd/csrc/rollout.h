@@ -199,6 +199,9 @@ struct Mlp3Args {
   const float *x_b, *W1_b, *b1_b, *W2_b, *b2_b, *W3_b, *b3_b;
   float* y_b;
   int groups_a, groups_b;
+  // LyapunovValue's sum over the outputs of y^2 per row (N3 a multiple of 64), the square-sum
+  // kernel's order; null: not formed
+  float* sqsum;
 };
 // the fused 3-layer MLP input-gradient chain (mlp_fused.hip): g2 = (dy W3) * act2'(h2),
 // g1 = (g2 W2) * act1'(h1), dx = sum over groups of g1 W1 (dy is the gradient of the identity-
@@ -216,6 +219,10 @@ struct Mlp3BwdArgs {
   int64_t ldg, gs_g;
   float* dx;       // optional [M][ldx]
   int64_t ldx;
+  // LyapunovValue: dy = dv[row] (2 y) formed from the forward output y (ldy) and dv = dV instead
+  // of read (square-sum backward's expression), written to g3 ([M][ldy]) for the weight gradient
+  const float* sq_dv;
+  float* g3;
 };
 hipError_t launch_mlp3_backward(const Mlp3BwdArgs& a, hipStream_t st);
 // several weight gradients dw = g^T x, db = column sums of g in two launches (gemm.hip)

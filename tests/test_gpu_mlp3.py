@@ -260,3 +260,28 @@ def test_twin_weight_grads_fused_equals_per_layer():
             F._MLP3["on"] = True
     for u, v in zip(*res):
         torch.testing.assert_close(u, v, rtol=1e-4, atol=1e-5 * float(v.abs().max()))
+
+
+@pytest.mark.parametrize("M", [10240, 5376, 999])
+def test_lyapunov_square_sum_fused_equals_separate(M):
+    """LyapunovValue through MLP3SquareSum (mh_mlp3_forward_sqsum / mh_mlp3_backward_sqsum: the
+    square sums and dy = dV 2y inside the MLP's launches) vs the MLP's launches + SquareSum: V and
+    every gradient bit for bit."""
+    from msacl_amd.apprfunc.mlp import LyapunovValue
+    torch.manual_seed(5)
+    lya = LyapunovValue(input_dim=12, hidden_sizes=[256, 256], hidden_activation="tanh", output_dim=256,
+                        output_activation="linear").cuda()
+    x = torch.randn(M, 12, device="cuda")
+    dv = torch.randn(M, device="cuda")
+    outs = []
+    for fused in (True, False):
+        F._MLP3["sqsum"] = fused  # off: the same fused MLP launches, then SquareSum's two launches
+        try:
+            lya.zero_grad()
+            v = lya(x)
+            v.backward(dv)
+            outs.append([v.detach().clone()] + [p.grad.detach().clone() for p in lya.parameters()])
+        finally:
+            F._MLP3["sqsum"] = True
+    for a, b in zip(*outs):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
