@@ -36,10 +36,23 @@ def main():
 
     rows_out = []
     for M, K1, N3, keep, groups in ((5120, 16, 1, True, 2), (5120, 16, 1, False, 2), (10240, 12, 1, True, 1),
-                                    (5120, 12, 256, True, 1), (5120, 12, 1, True, 1)):
+                                    (5120, 12, 256, True, 1), (5120, 12, 1, True, 1), (10240, 12, 256, True, 1),
+                                    (5376, 12, 256, False, 1), (5120, 16, 1, True, 4)):
         layers = (lin(H, K1), lin(H, H), lin(N3, H))
         x = torch.randn(M, K1, device=dev)
-        if groups == 2:
+        if groups == 4:
+            # the critics and the target critics as the two network sets of one launch (forward_pair)
+            from msacl_amd.apprfunc._twin import TwinCritic
+            from msacl_amd.apprfunc.mlp import ActionValue
+            kw = dict(obs_dim=12, act_dim=4, hidden_sizes=[256, 256], hidden_activation="relu",
+                      output_activation="linear")
+            nets = [ActionValue(**kw).to(dev) for _ in range(4)]
+            tc, tt = TwinCritic.build(nets[0], nets[1]), TwinCritic.build(nets[2], nets[3])
+            xo = torch.randn(M, K1, device=dev)
+
+            def fwd():
+                tc.forward_pair(x, tt, xo)
+        elif groups == 2:
             # the twin critics' joint buffers: group q's operands at q x the strides
             W1 = torch.stack([layers[0][0]] * 2)
             b1 = torch.stack([layers[0][1]] * 2)
