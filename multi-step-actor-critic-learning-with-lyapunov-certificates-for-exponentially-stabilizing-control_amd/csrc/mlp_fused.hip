@@ -700,26 +700,49 @@ hipError_t launch_mlp3_backward(const Mlp3BwdArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// CU count of the (single) device this process drives, queried once (256 on the MI355X)
+static int64_t device_cus() {
+  static int cus = 0;
+  if (cus <= 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
 hipError_t launch_mlp3_forward(const Mlp3Args& a_in, int groups, hipStream_t st) {
   if (!mlp3_supported(a_in.M, a_in.K1, a_in.H, a_in.N3) || groups < 1 || a_in.groups_b < 0) return hipErrorInvalidValue;
   Mlp3Args a = a_in;
   a.groups_a = groups;
   groups += a.groups_b;
-  // two row tiles per wave: half the weight traffic per row (M = 5,120: 17.4 vs 22.4 us, though
-  // only 160 workgroups; 10,240: 29.9 vs 33.2; the policy trunk's N3 = 256: 30.0 vs 38.9;
-  // tools/mlp3_bench.py); MH_MLP_RT = 1 or 4 for the A/B
+  // Row tiles per wave (RT): a workgroup streams each weight matrix once per 16 RT rows, and
+  // costs about (10 + 10 RT) us at the Lyapunov shape (one per CU; two co-resident on a CU take
+  // 1.7x one), so the fastest grid is the fewest row tiles per workgroup that still fit one
+  // workgroup per CU: RT = 3 at 10,240 rows (40 vs 50 us at RT = 2 / 4), RT = 2 at 5,120 x 1 group,
+  // RT = 3 for the twin critics' 2 x 5,120 (24.9 vs 30.6 us), RT = 1 at 2,560 (13.7 vs 16.5).
+  // Beyond one per CU at RT = 4: RT = 3 while that is at most two per CU (20,480 rows: 76 vs 87),
+  // else RT = 2 (tools/mlp3_bench.py, tools/r04_rt3.sh, r04_rt3b.sh). MH_MLP_RT forces 1 / 2 / 3 / 4.
   static const int force_rt = [] {
     const char* e = getenv("MH_MLP_RT");
     return e ? atoi(e) : 0;
   }();
-  const int64_t tiles2 = (a.M + 31) / 32;
-  if (force_rt == 4) {
-    k_mlp3_fwd<4><<<dim3((unsigned)((a.M + 63) / 64), (unsigned)groups), 256, 0, st>>>(a);
-  } else if (force_rt != 1) {
-    k_mlp3_fwd<2><<<dim3((unsigned)tiles2, (unsigned)groups), 256, 0, st>>>(a);
-  } else {
-    const int64_t tiles = (a.M + TM - 1) / TM;
-    k_mlp3_fwd<1><<<dim3((unsigned)tiles, (unsigned)groups), 256, 0, st>>>(a);
+  int rt = force_rt;
+  if (rt < 1 || rt > 4) {
+    const int64_t cus = device_cus();
+    auto wgs = [&](int r) { return (a.M + 16 * r - 1) / (16 * r) * (int64_t)groups; };
+    rt = 0;
+    for (int r = 1; r <= 4 && !rt; ++r)
+      if (wgs(r) <= cus) rt = r;
+    if (!rt) rt = wgs(3) <= 2 * cus ? 3 : 2;
+  }
+  const unsigned gy = (unsigned)groups;
+  switch (rt) {
+    case 1: k_mlp3_fwd<1><<<dim3((unsigned)((a.M + 15) / 16), gy), 256, 0, st>>>(a); break;
+    case 3: k_mlp3_fwd<3><<<dim3((unsigned)((a.M + 47) / 48), gy), 256, 0, st>>>(a); break;
+    case 4: k_mlp3_fwd<4><<<dim3((unsigned)((a.M + 63) / 64), gy), 256, 0, st>>>(a); break;
+    default: k_mlp3_fwd<2><<<dim3((unsigned)((a.M + 31) / 32), gy), 256, 0, st>>>(a); break;
   }
   return hipGetLastError();
 }

@@ -23,6 +23,7 @@ from tools.gputime import time_launches  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--cases", default="", help="M,K1,N3,keep,groups;... (default: the bench's shapes)")
     a = ap.parse_args()
     import msacl_amd  # noqa: F401
     from msacl_amd.apprfunc import _fused as F
@@ -35,9 +36,11 @@ def main():
         return (torch.randn(n_out, n_in, device=dev) / n_in ** 0.5, torch.randn(n_out, device=dev) * 0.1)
 
     rows_out = []
-    for M, K1, N3, keep, groups in ((5120, 16, 1, True, 2), (5120, 16, 1, False, 2), (10240, 12, 1, True, 1),
+    cases = [tuple(int(v) for v in c.split(",")) for c in a.cases.split(";") if c]
+    for M, K1, N3, keep, groups in cases or ((5120, 16, 1, True, 2), (5120, 16, 1, False, 2), (10240, 12, 1, True, 1),
                                     (5120, 12, 256, True, 1), (5120, 12, 1, True, 1), (10240, 12, 256, True, 1),
                                     (5376, 12, 256, False, 1), (5120, 16, 1, True, 4)):
+        keep = bool(keep)
         layers = (lin(H, K1), lin(H, H), lin(N3, H))
         x = torch.randn(M, K1, device=dev)
         if groups == 4:
