@@ -465,6 +465,20 @@ int mh_mlp3_backward(const float* dy, int64_t ldy, const float* h1, const float*
                      int32_t act1, int32_t act2, float* g2, float* g1, int64_t ldg, float* dx, int64_t ldx,
                      int32_t groups, const int64_t* group_strides, void* stream);
 
+/* mh_mlp3_backward plus the output layer's gradients (n_out <= 16; the twin critics' q heads):
+ * dw3 [n_out][hidden] = dy^T h2 and, when non-NULL, db3 [n_out] = the column sums of dy, group q's
+ * at + q x gs_dw3 / gs_db3 floats. The chain launch forms each 16-row block's partials from the dy
+ * rows and h2 columns it already holds; one more launch adds them in block order (deterministic;
+ * the same bits as mh_head_backward's below 16,384 rows). workspace: the floats
+ * mh_mlp3_backward_w3_workspace reports. Replaces mh_mlp3_backward + mh_head_backward_grouped for
+ * TwinCritic.backward_weights (ActionValue's last nn.Linear, RL/apprfunc/mlp.py). */
+int mh_mlp3_backward_w3_workspace(int64_t rows, int32_t hidden, int32_t n_out, int32_t groups, int64_t* floats_out);
+int mh_mlp3_backward_w3(const float* dy, int64_t ldy, const float* h1, const float* h2, int64_t ldh, const float* W1,
+                        const float* W2, const float* W3, int64_t rows, int32_t k1, int32_t hidden, int32_t n_out,
+                        int32_t act1, int32_t act2, float* g2, float* g1, int64_t ldg, float* dx, int64_t ldx,
+                        int32_t groups, const int64_t* group_strides, float* dw3, float* db3, int64_t gs_dw3,
+                        int64_t gs_db3, float* workspace, void* stream);
+
 /* Several weight gradients of one backward (the three layers of an MLP, both twin critics') in two
  * launches: for each product, dw [n_out][n_in] = g^T x over `rows` and, when db is non-NULL,
  * db [n_out] = the column sums of g, with g [rows][ld_g] the layer's pre-activation gradient (as

@@ -152,6 +152,9 @@ _PROTOS = {
                                + [c_i32] * 5 + [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "mh_mlp3_backward": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64] + [c_i32] * 5
                          + [c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "mh_mlp3_backward_w3_workspace": (ctypes.c_int, [c_i64, c_i32, c_i32, c_i32, ctypes.POINTER(c_i64)]),
+    "mh_mlp3_backward_w3": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64] + [c_i32] * 5
+                            + [c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),
     "mh_weight_grads_workspace": (ctypes.c_int, [c_vp, c_i32, c_i64, ctypes.POINTER(c_i64)]),
     "mh_weight_grads": (ctypes.c_int, [c_vp, c_i32, c_i64, c_vp, c_vp]),
     "mh_stocha_head": (ctypes.c_int, [c_vp, c_i64, c_i32, c_f32, c_f32, c_vp, c_vp]),

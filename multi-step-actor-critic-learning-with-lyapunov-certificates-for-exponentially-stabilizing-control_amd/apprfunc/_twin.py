@@ -21,9 +21,14 @@ add the same f32 products in a different order.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
+
+# the q heads' weight gradients folded into the backward chain launch (mh_mlp3_backward_w3);
+# MSACL_FOLD_W3=0: the separate grouped head backward (the A/B and the bit-equality test)
+_FOLD_W3 = os.environ.get("MSACL_FOLD_W3", "1") == "1"
 
 
 def _native():
@@ -221,15 +226,26 @@ class TwinCritic:
             g2 = torch.empty(M, 2 * H, dtype=torch.float32, device=dev)
             g1 = torch.empty(M, 2 * H, dtype=torch.float32, device=dev)
             gs = (ctypes.c_int64 * 6)(M, H, H * K, H * H, H, H)
-            N.check(N.lib().mh_mlp3_backward(N.ptr(dq), 1, N.ptr(h1), N.ptr(h2), 2 * H, N.ptr(self.W1), N.ptr(self.W2),
-                                             N.ptr(self.W3), M, K, H, 1, 1, 1, N.ptr(g2), N.ptr(g1), 2 * H, None, K, 2,
-                                             gs, st), "mh_mlp3_backward (twin weights)")
-            n = ctypes.c_int64()
-            N.check(N.lib().mh_head_backward_workspace(M, 1, H, ctypes.byref(n)), "mh_head_backward_workspace")
-            wsh = self._workspace(("head", M), 2 * n.value)
-            N.check(N.lib().mh_head_backward_grouped(
-                N.ptr(dq), N.ptr(h2), N.ptr(self.W3), M, 1, H, 2 * H, 2 * H, 2, M, H, H, H, H, 1, None,
-                N.ptr(self.gW3), N.ptr(self.gb3), N.ptr(wsh), st), "mh_head_backward_grouped (dW3)")
+            if _FOLD_W3:
+                # the q heads' dW3 / db3 from the chain launch's own partials (+ one finish launch)
+                n = ctypes.c_int64()
+                N.check(N.lib().mh_mlp3_backward_w3_workspace(M, H, 1, 2, ctypes.byref(n)),
+                        "mh_mlp3_backward_w3_workspace")
+                wsh = self._workspace(("w3", M), n.value)
+                N.check(N.lib().mh_mlp3_backward_w3(
+                    N.ptr(dq), 1, N.ptr(h1), N.ptr(h2), 2 * H, N.ptr(self.W1), N.ptr(self.W2), N.ptr(self.W3), M, K, H,
+                    1, 1, 1, N.ptr(g2), N.ptr(g1), 2 * H, None, K, 2, gs, N.ptr(self.gW3), N.ptr(self.gb3), H, 1,
+                    N.ptr(wsh), st), "mh_mlp3_backward_w3 (twin weights)")
+            else:
+                N.check(N.lib().mh_mlp3_backward(N.ptr(dq), 1, N.ptr(h1), N.ptr(h2), 2 * H, N.ptr(self.W1),
+                                                 N.ptr(self.W2), N.ptr(self.W3), M, K, H, 1, 1, 1, N.ptr(g2), N.ptr(g1),
+                                                 2 * H, None, K, 2, gs, st), "mh_mlp3_backward (twin weights)")
+                n = ctypes.c_int64()
+                N.check(N.lib().mh_head_backward_workspace(M, 1, H, ctypes.byref(n)), "mh_head_backward_workspace")
+                wsh = self._workspace(("head", M), 2 * n.value)
+                N.check(N.lib().mh_head_backward_grouped(
+                    N.ptr(dq), N.ptr(h2), N.ptr(self.W3), M, 1, H, 2 * H, 2 * H, 2, M, H, H, H, H, 1, None,
+                    N.ptr(self.gW3), N.ptr(self.gb3), N.ptr(wsh), st), "mh_head_backward_grouped (dW3)")
             prods = [(g2[:, q * H:], 2 * H, h1[:, q * H:], 2 * H, H, H, self.gW2[q], self.gb2[q]) for q in range(2)]
             prods.append((g1, 2 * H, x, K, 2 * H, K, self.gW1, self.gb1))
             weight_grads(prods, M, dev)

@@ -1069,10 +1069,14 @@ int mh_mlp3_forward_pair(const float* x, const float* x_b, int64_t rows, int32_t
                            n_out, act1, act2, act3, h1, h2, ldh, y, ldy, groups, group_strides, second, stream);
 }
 
-int mh_mlp3_backward(const float* dy, int64_t ldy, const float* h1, const float* h2, int64_t ldh, const float* W1,
-                     const float* W2, const float* W3, int64_t rows, int32_t k1, int32_t hidden, int32_t n_out,
-                     int32_t act1, int32_t act2, float* g2, float* g1, int64_t ldg, float* dx, int64_t ldx,
-                     int32_t groups, const int64_t* group_strides, void* stream) {
+// mh_mlp3_backward, and with dw3 set (n_out <= 16) the output layer's weight / bias gradients from
+// the same launch's partials (Mlp3BwdArgs::pdw3) plus one k_head_finish launch
+static int mlp3_backward_impl(const float* dy, int64_t ldy, const float* h1, const float* h2, int64_t ldh,
+                              const float* W1, const float* W2, const float* W3, int64_t rows, int32_t k1,
+                              int32_t hidden, int32_t n_out, int32_t act1, int32_t act2, float* g2, float* g1,
+                              int64_t ldg, float* dx, int64_t ldx, int32_t groups, const int64_t* group_strides,
+                              float* dw3, float* db3, int64_t gs_dw3, int64_t gs_db3, float* workspace,
+                              void* stream) {
   if (rows < 0 || groups < 0) return fail(MH_EINVAL, "mh_mlp3_backward: bad size");
   if (rows == 0 || groups == 0) return MH_OK;
   if (!mh::mlp3_supported(rows, k1, hidden, n_out))
@@ -1098,8 +1102,47 @@ int mh_mlp3_backward(const float* dy, int64_t ldy, const float* h1, const float*
     if (g[5] & 3) return fail(MH_EINVAL, "mh_mlp3_backward: the g group stride must keep 16-byte alignment");
     a.gs_dy = g[0]; a.gs_h = g[1]; a.gs_W1 = g[2]; a.gs_W2 = g[3]; a.gs_W3 = g[4]; a.gs_g = g[5];
   }
+  const int64_t nblk = (rows + 15) / 16;
+  if (dw3) {
+    if (n_out > 16) return fail(MH_EINVAL, "mh_mlp3_backward_w3: the output-layer gradients need n_out <= 16");
+    if (!workspace) return fail(MH_EINVAL, "mh_mlp3_backward_w3: null workspace");
+    if (groups > 1 && (gs_dw3 < 0 || gs_db3 < 0)) return fail(MH_EINVAL, "mh_mlp3_backward_w3: negative group stride");
+    a.pdw3 = workspace;
+    a.pdb3 = db3 ? workspace + nblk * n_out * (int64_t)hidden : nullptr;
+    a.s_part3 = nblk * n_out * (int64_t)(hidden + 1);
+  } else if (db3) {
+    return fail(MH_EINVAL, "mh_mlp3_backward_w3: db3 without dw3");
+  }
   MH_HIP(mh::launch_mlp3_backward(a, (hipStream_t)stream));
+  if (dw3)
+    MH_HIP(mh::launch_head_finish(a.pdw3, a.pdb3, nblk, n_out, hidden, groups, a.s_part3, dw3, gs_dw3, db3, gs_db3,
+                                  (hipStream_t)stream));
   return MH_OK;
+}
+
+int mh_mlp3_backward(const float* dy, int64_t ldy, const float* h1, const float* h2, int64_t ldh, const float* W1,
+                     const float* W2, const float* W3, int64_t rows, int32_t k1, int32_t hidden, int32_t n_out,
+                     int32_t act1, int32_t act2, float* g2, float* g1, int64_t ldg, float* dx, int64_t ldx,
+                     int32_t groups, const int64_t* group_strides, void* stream) {
+  return mlp3_backward_impl(dy, ldy, h1, h2, ldh, W1, W2, W3, rows, k1, hidden, n_out, act1, act2, g2, g1, ldg, dx,
+                            ldx, groups, group_strides, nullptr, nullptr, 0, 0, nullptr, stream);
+}
+
+int mh_mlp3_backward_w3_workspace(int64_t rows, int32_t hidden, int32_t n_out, int32_t groups, int64_t* floats_out) {
+  if (rows < 0 || hidden <= 0 || n_out <= 0 || n_out > 16 || groups < 1 || !floats_out)
+    return fail(MH_EINVAL, "mh_mlp3_backward_w3_workspace: bad argument");
+  *floats_out = (rows + 15) / 16 * n_out * (int64_t)(hidden + 1) * groups;
+  return MH_OK;
+}
+
+int mh_mlp3_backward_w3(const float* dy, int64_t ldy, const float* h1, const float* h2, int64_t ldh, const float* W1,
+                        const float* W2, const float* W3, int64_t rows, int32_t k1, int32_t hidden, int32_t n_out,
+                        int32_t act1, int32_t act2, float* g2, float* g1, int64_t ldg, float* dx, int64_t ldx,
+                        int32_t groups, const int64_t* group_strides, float* dw3, float* db3, int64_t gs_dw3,
+                        int64_t gs_db3, float* workspace, void* stream) {
+  if (!dw3) return fail(MH_EINVAL, "mh_mlp3_backward_w3: null dw3");
+  return mlp3_backward_impl(dy, ldy, h1, h2, ldh, W1, W2, W3, rows, k1, hidden, n_out, act1, act2, g2, g1, ldg, dx,
+                            ldx, groups, group_strides, dw3, db3, gs_dw3, gs_db3, workspace, stream);
 }
 
 int mh_mlp3_forward_sqsum(const float* x, int64_t rows, int32_t k1, int64_t ldx, const float* const* params,

@@ -23,6 +23,8 @@
 // same f32 results as the per-layer kernels up to summation order.
 // Grouped launches (the twin critics, apprfunc/_twin.py): blockIdx.y = group q; every pointer is
 // advanced by q x its group stride (floats; 0 = shared).
+#include <cstring>
+
 #include "rollout.h"
 
 namespace mh {
@@ -535,6 +537,44 @@ __device__ __forceinline__ void grad_epilogue(const f32x4 (&acc)[RT][4], const f
     grad_epilogue_t<0, RT>(acc, hv, n0, lane, m0, M, out);
 }
 
+// The output layer's weight / bias gradient partials per 16-row block (Mlp3BwdArgs::pdw3) from the
+// staged output gradient (g3 rows, LDS) and this wave's 64 columns of h2 (hv, the MFMA C layout:
+// rows 4 g + q in lane group g): each lane gathers its column's 16 rows by shuffles and adds
+// g3[r][o] h2[r][n] over the block's rows in order, k_head_backward's expression and order.
+template <int RT>
+__device__ __forceinline__ void w3_partials(const float* gs3, const float (&hv)[RT][4][4], int N3, int n0, int lane,
+                                            int wave, int64_t m0, int64_t M, float* pdw, float* pdb) {
+  const int c = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int64_t r0 = m0 + 16 * rt;
+    if (r0 >= M) break;
+    const int nr = M - r0 < 16 ? (int)(M - r0) : 16;
+    const int64_t blk = r0 / 16;
+    const float* gr = gs3 + 16 * rt * SH;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float hc[16];
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg)
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) hc[4 * gg + qq] = __shfl(hv[rt][j][qq], c + 16 * gg, 64);
+      for (int o = 0; o < N3; ++o) {
+        float s = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (r < nr) s = s + gr[r * SH + o] * hc[r];
+        if (g == (o & 3)) pdw[(blk * N3 + o) * HID + n0 + 16 * j + c] = s;
+      }
+    }
+    if (pdb && wave == 0 && lane < N3) {
+      float s = 0.0f;
+      for (int r = 0; r < nr; ++r) s = s + gr[r * SH + lane];
+      pdb[blk * N3 + lane] = s;
+    }
+  }
+}
+
 // NARROW (N3 <= 16): the W2 product's weight ring is issued before the W3 product; the wide form
 // (N3 a multiple of 64) has no registers for that beside the W3 product's own ring. RT row tiles
 // of 16 per wave (the workgroup's 16 RT rows): each weight fragment feeds RT MFMAs.
@@ -595,6 +635,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT == 1 ? 2
       else
         layer_cols_t_n3<RT>(gs3, wr, N3, n0, lane, acc);
       grad_epilogue<RT>(acc, hv2, a.act2, n0, lane, m0, a.M, gs2);
+      if constexpr (NARROW) {
+        if (a.pdw3) w3_partials<RT>(gs3, hv2, N3, n0, lane, wave, m0, a.M, a.pdw3 + q * a.s_part3,
+                                    a.pdb3 ? a.pdb3 + q * a.s_part3 : nullptr);
+      }
     }
     __syncthreads();
     if (a.g2) store_tile(gs2, a.g2 + q * a.gs_g, a.ldg, m0, a.M, HID, TR);
@@ -719,14 +763,21 @@ hipError_t launch_mlp3_forward(const Mlp3Args& a_in, int groups, hipStream_t st)
   groups += a.groups_b;
   // Row tiles per wave (RT): a workgroup streams each weight matrix once per 16 RT rows, and
   // costs about (10 + 10 RT) us at the Lyapunov shape (one per CU; two co-resident on a CU take
-  // 1.7x one), so the fastest grid is the fewest row tiles per workgroup that still fit one
-  // workgroup per CU: RT = 3 at 10,240 rows (40 vs 50 us at RT = 2 / 4), RT = 2 at 5,120 x 1 group,
-  // RT = 3 for the twin critics' 2 x 5,120 (24.9 vs 30.6 us), RT = 1 at 2,560 (13.7 vs 16.5).
-  // Beyond one per CU at RT = 4: RT = 3 while that is at most two per CU (20,480 rows: 76 vs 87),
-  // else RT = 2 (tools/mlp3_bench.py, tools/r04_rt3.sh, r04_rt3b.sh). MH_MLP_RT forces 1 / 2 / 3 / 4.
+  // 1.7x one). Alone, the fastest grid is the fewest row tiles per workgroup that still fit one
+  // workgroup per CU (MH_MLP_RT=auto): RT = 3 at 10,240 rows (40 vs 50 us at RT = 2 / 4), RT = 3
+  // for the twin critics' 2 x 5,120 (24.9 vs 30.6 us), RT = 1 at 2,560 (13.7 vs 16.5)
+  // (tools/mlp3_bench.py, tools/r04_rt3.sh, r04_rt3b.sh). Inside the update, though, the critic and
+  // Lyapunov branches run these launches side by side, and RT = 3's 119 KB of LDS leaves no room
+  // for the other branch's workgroup on the CU (the critics + targets pair took 88 us there beside
+  // the Lyapunov forward at RT = 3 vs 49 us at RT = 2): the bench step is 1.2 % faster with RT = 2
+  // everywhere (1.120-1.127 vs 1.110-1.112 B env-steps/s, alternating runs on one box,
+  // tools/r04_iter13.sh), so RT = 2 (79 KB, two workgroups per CU) is the default.
+  // MH_MLP_RT = 1 / 2 / 3 / 4 forces, "auto" selects as above.
   static const int force_rt = [] {
     const char* e = getenv("MH_MLP_RT");
-    return e ? atoi(e) : 0;
+    if (!e) return 2;
+    if (std::strcmp(e, "auto") == 0) return 0;
+    return atoi(e);
   }();
   int rt = force_rt;
   if (rt < 1 || rt > 4) {
@@ -735,7 +786,7 @@ hipError_t launch_mlp3_forward(const Mlp3Args& a_in, int groups, hipStream_t st)
     rt = 0;
     for (int r = 1; r <= 4 && !rt; ++r)
       if (wgs(r) <= cus) rt = r;
-    if (!rt) rt = wgs(3) <= 2 * cus ? 3 : 2;
+    if (!rt) rt = 2;
   }
   const unsigned gy = (unsigned)groups;
   switch (rt) {

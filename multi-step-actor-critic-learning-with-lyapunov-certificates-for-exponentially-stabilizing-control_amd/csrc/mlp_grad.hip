@@ -311,6 +311,17 @@ hipError_t launch_head_backward_grouped(const float* dy, const float* x, const f
   return hipGetLastError();
 }
 
+hipError_t launch_head_finish(const float* pdw, const float* pdb, int64_t nblk, int n_out, int n_in, int groups,
+                              int64_t s_part, float* dw, int64_t s_dw, float* db, int64_t s_db, hipStream_t st) {
+  if (nblk <= 0 || n_out <= 0 || n_in <= 0 || groups <= 0 || groups > 65535 || !pdw || !dw || (db && !pdb))
+    return hipErrorInvalidValue;
+  const int64_t outs = n_out * (int64_t)n_in + (db ? n_out : 0);
+  k_head_finish<<<dim3((unsigned)((outs + 3) / 4), (unsigned)groups), 256, 0, st>>>(pdw, db ? pdb : nullptr, (int)nblk,
+                                                                                   n_out, n_in, dw, db, s_part, s_dw,
+                                                                                   s_db);
+  return hipGetLastError();
+}
+
 hipError_t launch_head_backward(const float* dy, const float* x, const float* W, int64_t M, int n_out, int n_in,
                                 float* dx, float* dw, float* db, float* workspace, hipStream_t st) {
   return launch_head_backward_grouped(dy, x, W, M, n_out, n_in, n_in, n_in, 1, 0, 0, 0, 0, 0, 0, dx, dw, db, workspace,

@@ -154,6 +154,9 @@ hipError_t launch_dx_narrow(const float* dy, const float* y, int act, const floa
 hipError_t launch_square_sum_bwd(const float* y, const float* g, int64_t rows, int cols, float* dy, hipStream_t st);
 hipError_t launch_head_backward(const float* dy, const float* x, const float* W, int64_t M, int n_out, int n_in,
                                 float* dx, float* dw, float* db, float* workspace, hipStream_t st);
+// dw = sum over blocks of pdw[b] (and db of pdb[b]) in block order, per group q at q x the strides
+hipError_t launch_head_finish(const float* pdw, const float* pdb, int64_t nblk, int n_out, int n_in, int groups,
+                              int64_t s_part, float* dw, int64_t s_dw, float* db, int64_t s_db, hipStream_t st);
 hipError_t launch_head_backward_grouped(const float* dy, const float* x, const float* W, int64_t M, int n_out,
                                         int n_in, int64_t ldx, int64_t lddx, int groups, int64_t s_dy, int64_t s_x,
                                         int64_t s_W, int64_t s_dx, int64_t s_dw, int64_t s_db, float* dx, float* dw,
@@ -223,6 +226,12 @@ struct Mlp3BwdArgs {
   // of read (square-sum backward's expression), written to g3 ([M][ldy]) for the weight gradient
   const float* sq_dv;
   float* g3;
+  // N3 <= 16 (optional): the output layer's weight / bias gradient partials of every 16-row block
+  // b, pdw3[b][N3][H] = sum over its rows (in order) of dy[r][o] h2[r][j] and pdb3[b][N3] = the
+  // rows' dy sums, group q's at q s_part3 (k_head_backward's partials, bit for bit below 16,384
+  // rows; summed by launch_head_finish)
+  float *pdw3, *pdb3;
+  int64_t s_part3;
 };
 hipError_t launch_mlp3_backward(const Mlp3BwdArgs& a, hipStream_t st);
 // several weight gradients dw = g^T x, db = column sums of g in two launches (gemm.hip)

@@ -262,6 +262,45 @@ def test_twin_weight_grads_fused_equals_per_layer():
         torch.testing.assert_close(u, v, rtol=1e-4, atol=1e-5 * float(v.abs().max()))
 
 
+@pytest.mark.parametrize("M", [5120, 1037, 16400])
+def test_twin_head_grads_folded_into_chain(M):
+    """The q heads' dW3 / db3 formed inside the chain launch (mh_mlp3_backward_w3) equal the
+    grouped head backward's bit for bit below 16,384 rows (same 16-row partials, same finish;
+    1,037: a ragged last block), agree with float64 at any size, and leave g1 / g2 unchanged."""
+    from msacl_amd.apprfunc import _twin as T
+    from msacl_amd.apprfunc.mlp import ActionValue
+    torch.manual_seed(M)
+    kw = dict(obs_dim=12, act_dim=4, hidden_sizes=[256, 256], hidden_activation="relu", output_activation="linear")
+    tc = T.TwinCritic.build(ActionValue(**kw).cuda(), ActionValue(**kw).cuda())
+    x = torch.randn(M, 16, device="cuda")
+    dq = torch.randn(2, M, device="cuda")
+    q, h1, h2 = tc.forward(x)
+    res = []
+    saved = T._FOLD_W3
+    for fold in (True, False):
+        T._FOLD_W3 = fold
+        try:
+            tc.backward_weights(x, dq, h1, h2)
+            torch.cuda.synchronize()
+            res.append([t.clone() for t in (tc.gW1, tc.gb1, tc.gW2, tc.gb2, tc.gW3, tc.gb3)])
+        finally:
+            T._FOLD_W3 = saved
+    exact = M < 16384
+    for u, v in zip(*res):
+        if exact:
+            torch.testing.assert_close(u, v, rtol=0, atol=0)
+        else:
+            torch.testing.assert_close(u, v, rtol=1e-5, atol=1e-6 * float(v.abs().max()))
+    D = lambda t: t.double().cpu().numpy()  # noqa: E731
+    gW3, gb3 = res[0][4], res[0][5]
+    for qn in range(2):
+        hq = D(h2[:, qn * 256:(qn + 1) * 256])
+        ref = D(dq[qn]) @ hq
+        tol = 2e-6 * M ** 0.5 * (np.abs(D(dq[qn])) @ np.abs(hq)) + 1e-6
+        assert np.all(np.abs(D(gW3[qn]).reshape(-1) - ref) <= tol)
+        assert abs(float(gb3[qn]) - D(dq[qn]).sum()) <= 2e-6 * M ** 0.5 * np.abs(D(dq[qn])).sum() + 1e-6
+
+
 @pytest.mark.parametrize("M", [10240, 5376, 999])
 def test_lyapunov_square_sum_fused_equals_separate(M):
     """LyapunovValue through MLP3SquareSum (mh_mlp3_forward_sqsum / mh_mlp3_backward_sqsum: the
