@@ -187,14 +187,20 @@ __global__ __launch_bounds__(256) void k_policy_head(const float* __restrict__ r
       e_draw = nv[i & 3];
       eps_out[r * A + i] = e_draw;
     }
-    __syncthreads();  // every lane of the workgroup has read ctr[0]
+    __syncthreads();  // every lane of the workgroup has read ctr[0] (its value consumed above)
+    // RELAXED arrival (optim.hip's Adam ticket): the only ordering needed is that every workgroup's
+    // read of ctr[0] returned before its arrival, and the read was consumed before the barrier. No
+    // data passes between workgroups, so no agent-scope fence / acquire-release (each an L2
+    // writeback + invalidate: the draw cost 12.5 us at 5,120 rows with them, tools/head_bench.py)
     if (threadIdx.x == 0) {
+#ifdef MH_REDUCE_FENCED  // A/B only: the former fenced arrival
       __threadfence();
+#endif
       const unsigned int arrived =
-          __hip_atomic_fetch_add(reinterpret_cast<unsigned int*>(ctr + 1), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(reinterpret_cast<unsigned int*>(ctr + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (arrived == gridDim.x - 1) {  // the last workgroup: every other has read the counter
         __hip_atomic_store(reinterpret_cast<unsigned int*>(ctr + 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(ctr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }

@@ -103,21 +103,39 @@ __device__ bool rows_reduce(double a, double b, double* part, unsigned int* arri
       x += sa[w];
       y += sb[w];
     }
+#ifdef MH_REDUCE_FENCED  // A/B only: the agent-scope fences (an L2 writeback + invalidate each)
     part[2 * blockIdx.x] = x;
     part[2 * blockIdx.x + 1] = y;
     __threadfence();
     last = atomicAdd(arrive, 1u) == gridDim.x - 1u;
+#else
+    // The partials as agent-scope atomic stores (written through to the device's coherence point,
+    // not left in this XCD's L2), complete (vmcnt(0)) before the relaxed arrival; the last
+    // workgroup reads them with agent-scope atomic loads. No fence: an agent-scope release /
+    // acquire writes back / invalidates the whole L2, which inside the update holds the other
+    // branch's dirty lines too (this launch took 25 us there with the fences).
+    __hip_atomic_store(part + 2 * blockIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(part + 2 * blockIdx.x + 1, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): both stores acknowledged
+    last = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
+#endif
   }
   __syncthreads();
   if (!last) return false;
+#ifdef MH_REDUCE_FENCED
   __threadfence();
-  // last workgroup: fixed-order total (lane-strided partials, then wave/LDS tree)
   const volatile double* vp = part;
+#define MH_PART(i) vp[i]
+#else
+#define MH_PART(i) __hip_atomic_load(part + (i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+#endif
+  // last workgroup: fixed-order total (lane-strided partials, then wave/LDS tree)
   double x = 0.0, y = 0.0;
   for (unsigned int g = threadIdx.x; g < gridDim.x; g += RTPB) {
-    x += vp[2 * g];
-    y += vp[2 * g + 1];
+    x += MH_PART(2 * g);
+    y += MH_PART(2 * g + 1);
   }
+#undef MH_PART
   x = wave_sum(x);
   y = wave_sum(y);
   __syncthreads();
@@ -134,7 +152,11 @@ __device__ bool rows_reduce(double a, double b, double* part, unsigned int* arri
   }
   *ta = X;
   *tb = Y;
+#ifdef MH_REDUCE_FENCED
   *arrive = 0u;
+#else
+  __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
   return true;
 }
 

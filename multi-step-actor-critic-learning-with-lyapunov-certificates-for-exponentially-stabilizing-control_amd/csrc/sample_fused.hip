@@ -47,6 +47,7 @@ namespace mh {
 struct PolicyLds {
   uint4* c0;            // W2 chunk buffers (PM_X3_FRAGS * 64 records each)
   uint4* c1;
+  uint4* c2;            // the third buffer (kTriple: chunks staged two phases ahead)
   const uint4* w3;      // fold operands [ob][s][split][lane]
   const float* b2;      // layer-2 bias, [256]
   const float* b3;      // layer-3 bias, [N3] (LDS: the pass epilogue's 16 bias reads stay off the memory path)
@@ -73,6 +74,20 @@ struct PolicyLds {
 constexpr bool kLoaders = true;
 #else
 constexpr bool kLoaders = false;
+#endif
+
+// Three W2 chunk buffers (MH_FUSED_TRIPLE): chunk c of the horizon's chunk sequence (8 per pass)
+// lives in buffer c % 3 and its DMA is issued two phases ahead, so the hand-off at a phase's start
+// waits only for a DMA issued ~2 phases earlier (vmcnt(8): the next chunk's 8 DMAs may still be in
+// flight). The LDS for it comes from the compacted layer-3 fold operands (W3's N3 <= 8 real rows
+// instead of 32 padded ones: 8 KB instead of 32 KB).
+#ifdef MH_FUSED_TRIPLE
+#ifdef MH_FUSED_LOADERS
+#error "MH_FUSED_TRIPLE is the policy-wave staging path: build it without MH_FUSED_LOADERS"
+#endif
+constexpr bool kTriple = true;
+#else
+constexpr bool kTriple = false;
 #endif
 
 // bounded LDS-counter wait (the same bound and error word as pol_sync). SLEEP: the loader waves
@@ -129,12 +144,19 @@ __device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
 // through mh_sample_horizon_errors) instead of hanging the device. (A split hand-off — "landed"
 // and "read" counters, the DMA wait and arrival late in the phase, the buffer-free wait before the
 // next DMA — measured 5 % slower on the fused kernel: 641-643 vs 606-617 us per horizon.)
-__device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_t* err, uint32_t limit) {
+__device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_t* err, uint32_t limit,
+                                         bool keep_next = false) {
 #ifdef MH_FUSED_EXP_NOSYNC  // cost-attribution experiment only (races: garbage logits)
   target += 4;
   return;
 #endif
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  // own DMAs of the chunk this phase reads landed: all of them (vmcnt(0)), or all but the next
+  // chunk's 8 (kTriple, vmcnt(8): memory operations complete in issue order for the counter)
+  static_assert(PM_X3_FRAGS / 4 == 8, "vmcnt(8) is one chunk's DMAs per policy wave");
+  if (keep_next)
+    __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8)
+  else
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   target += 4;
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   uint32_t spins = 0;
@@ -151,7 +173,9 @@ __device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_
 // the logits in LDS. `next`: stage chunk 0 of the following pass during the last phase.
 // LOAD: the W2 chunks are staged by loader waves (wait for `landed`, release each buffer); else
 // the four policy waves stage them themselves (pol_sync). D = 0: the observation width is Drt.
-template <int D, bool LOAD = kLoaders>
+// W3L: records per layer-3 fold fragment in LDS: 64 (one per lane) or 16 (compacted: the A
+// operand's rows l & 31 < 8 only, [half l >> 5][row]; the other lanes' rows are zero padding)
+template <int D, bool LOAD = kLoaders, int W3L = 64>
 __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int row0, bool next, uint32_t& target,
                             int pass_no = 0, int Drt = 0) {
   const int DD = D > 0 ? D : Drt;
@@ -245,14 +269,27 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
     constexpr int B = decltype(bufc)::value;
     uint4* cur_lds = B ? L.c1 : L.c0;
     uint4* nxt_lds = B ? L.c0 : L.c1;
-    const bool has_next = ib < PM_NB - 1 || next;
-    const int nib = (ib + 1) & (PM_NB - 1);
+    bool has_next = ib < PM_NB - 1 || next;
+    int nib = (ib + 1) & (PM_NB - 1);
+    bool keep_next = false;
+    if constexpr (kTriple) {
+      // chunk c = 8 pass + ib in buffer c % 3; this phase stages chunk c + 2 (W2 block ib + 2)
+      // (selects, not an indexed array: the pointers must stay provably LDS, or the ring reads
+      // become flat loads that wait for the DMAs in flight)
+      const int c = PM_NB * pass_no + ib, m = c % 3, mn = (c + 2) % 3;
+      cur_lds = m == 0 ? L.c0 : (m == 1 ? L.c1 : L.c2);
+      nxt_lds = mn == 0 ? L.c0 : (mn == 1 ? L.c1 : L.c2);
+      keep_next = ib + 1 < PM_NB || next;  // chunk c + 1's DMAs (issued last phase) may be in flight
+      has_next = ib + 2 < PM_NB || next;
+      nib = (ib + 2) & (PM_NB - 1);
+    }
     MH_STAMP(a, pass_no, 1 + 2 * ib);
     if constexpr (LOAD) {
       // chunk c = 8 pass + ib of the horizon: staged and published by the pass's loader waves
       wait_count(L.landed, 2u * (uint32_t)(PM_NB * pass_no + ib + 1), L.err, a.spin_limit);
     } else {
-      pol_sync(L.bar, target, L.err, a.spin_limit);  // chunk ib landed in every policy wave's share
+      // chunk ib landed in every policy wave's share
+      pol_sync(L.bar, target, L.err, a.spin_limit, keep_next);
     }
     MH_STAMP(a, pass_no, 2 + 2 * ib);
     const bool pipe = !fold;
@@ -363,7 +400,11 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
       if (fold && s == 1) {  // block ob's layer-3 operands (block ob - 1's last use was just above)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          w3f[q] = L.w3[(ob * 4 + q) * 64 + lane];
+          if constexpr (W3L == 64) {
+            w3f[q] = L.w3[(ob * 4 + q) * 64 + lane];
+          } else {
+            w3f[q] = (lane & 31) < 8 ? L.w3[(ob * 4 + q) * 16 + (lane >> 5) * 8 + (lane & 31)] : uint4{0u, 0u, 0u, 0u};
+          }
           // registers 4q .. 4q + 3 of block ob hold hidden units ob*32 + 8q + 4 (lane >> 5) + 0..3
           b2f[q] = *reinterpret_cast<const f32x4*>(L.b2 + ob * 32 + 8 * q + 4 * (lane >> 5));
         }
@@ -644,9 +685,13 @@ void k_sample_fused(FusedArgs a) {
   constexpr int D = Env::D, A = Env::A, S = Env::S, XS = Env::XS;
   constexpr int N3C = 2 * A;
   constexpr int F = rec_floats(D, A), CP = F / 4 + 1;
+  // the layer-3 fold operands compacted to W3's real rows when N3 <= 8 (kTriple's third buffer)
+  constexpr int W3L = (kTriple && N3C <= 8) ? 16 : 64;
+  static_assert(!kTriple || W3L == 16, "the third chunk buffer needs the compacted fold operands");
   __shared__ uint4 lds0[PM_X3_FRAGS * 64];
   __shared__ uint4 lds1[PM_X3_FRAGS * 64];
-  __shared__ uint4 lds_w3[PM_NB * 4 * 64];
+  __shared__ uint4 lds2[kTriple ? PM_X3_FRAGS * 64 : 1];
+  __shared__ uint4 lds_w3[PM_NB * 4 * W3L];
   __shared__ float lds_b2[PM_H];
   __shared__ float lds_b3[32];
   __shared__ uint4 lds_w1[PM_NB * 2 * 64];
@@ -688,10 +733,18 @@ void k_sample_fused(FusedArgs a) {
   if (pol) {
     const uint4* w3g = reinterpret_cast<const uint4*>(a.P + pm_off_w3x3(a.K1));
     constexpr int FOPW = PM_NB * 4 / 4;
+    if constexpr (W3L == 64) {
 #pragma unroll
-    for (int i = 0; i < FOPW; ++i) {
-      const int r = w * FOPW + i;
-      glds16(w3g + r * 64 + lane, &lds_w3[r * 64]);
+      for (int i = 0; i < FOPW; ++i) {
+        const int r = w * FOPW + i;
+        glds16(w3g + r * 64 + lane, &lds_w3[r * 64]);
+      }
+    } else {  // rows l & 31 < 8 of each fragment (the others are the zero padding of N3 <= 8)
+#pragma unroll
+      for (int i = 0; i < FOPW; ++i) {
+        const int r = w * FOPW + i;
+        if ((lane & 31) < 8) lds_w3[r * 16 + (lane >> 5) * 8 + (lane & 31)] = w3g[r * 64 + lane];
+      }
     }
     const uint4* w1g = reinterpret_cast<const uint4*>(a.P + pm_off_w1x3(a.K1));
 #pragma unroll
@@ -710,22 +763,27 @@ void k_sample_fused(FusedArgs a) {
     constexpr int FPW = PM_X3_FRAGS / 4;
 #pragma unroll
     for (int i = 0; i < FPW; ++i) glds16(W2g + (w * FPW + i) * 64 + lane, &lds0[(w * FPW + i) * 64]);
+    if constexpr (kTriple) {  // chunk 1 (W2 block 1) too: the first phase stages chunk 2
+#pragma unroll
+      for (int i = 0; i < FPW; ++i)
+        glds16(W2g + ((int64_t)PM_X3_FRAGS + w * FPW + i) * 64 + lane, &lds1[(w * FPW + i) * 64]);
+    }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's fold operands landed before the barrier
   }
   __syncthreads();
 
   if (pol) {
     // ================= policy waves: 2H passes (H1 first, then H0 / H1 alternating)
-    PolicyLds L{lds0, lds1, lds_w3, lds_b2, lds_b3, lds_w1, s_obs, s_lgt, &s_bar, a.err, &s_landed, &s_released};
+    PolicyLds L{lds0, lds1, lds2, lds_w3, lds_b2, lds_b3, lds_w1, s_obs, s_lgt, &s_bar, a.err, &s_landed, &s_released};
     uint32_t target = 0;
     const int total = 2 * H;
     int pass = 0;
     ++pass;
-    policy_pass<D>(a, L, w, FUSED_ENVS / 2 + w * 32, pass < total, target, pass - 1);
+    policy_pass<D, kLoaders, W3L>(a, L, w, FUSED_ENVS / 2 + w * 32, pass < total, target, pass - 1);
     __syncthreads();
     for (int t = 0; t < H; ++t) {
       ++pass;
-      policy_pass<D>(a, L, w, w * 32, pass < total, target, pass - 1);  // A(t): H0
+      policy_pass<D, kLoaders, W3L>(a, L, w, w * 32, pass < total, target, pass - 1);  // A(t): H0
       MH_STAMP(a, pass - 1, 18);
       __syncthreads();
 #ifdef MH_FUSED_EXP_SERIAL
@@ -733,7 +791,7 @@ void k_sample_fused(FusedArgs a) {
 #endif
       if (t < H - 1) {  // B(t): H1
         ++pass;
-        policy_pass<D>(a, L, w, FUSED_ENVS / 2 + w * 32, pass < total, target, pass - 1);
+        policy_pass<D, kLoaders, W3L>(a, L, w, FUSED_ENVS / 2 + w * 32, pass < total, target, pass - 1);
         MH_STAMP(a, pass - 1, 18);
       }
       __syncthreads();
@@ -773,7 +831,7 @@ void k_sample_fused(FusedArgs a) {
     const int NW = (int)((E + 63) / 64);
     const int gw = (int)(e / 64);
 #ifdef MH_FUSED_LOADERS
-    const PolicyLds LL{lds0, lds1, lds_w3, lds_b2, lds_b3, lds_w1, s_obs, s_lgt, &s_bar, a.err, &s_landed, &s_released};
+    const PolicyLds LL{lds0, lds1, lds2, lds_w3, lds_b2, lds_b3, lds_w1, s_obs, s_lgt, &s_bar, a.err, &s_landed, &s_released};
     const int npass = 2 * H;
 #endif
     float4* stage = s_stage[ew & 1];
