@@ -918,11 +918,21 @@ void k_sample_fused(FusedArgs a) {
   // ---- the emission's bookkeeping, by the last workgroup to finish (every lockstep count is in):
   // the per-lockstep window prefixes and the total into aux, with the store cursor they start
   // from; the cursor advanced past the horizon's windows; the counts re-zeroed for the next horizon
+  // The lockstep totals are agent-scope atomics (performed at the device's coherence point): each
+  // wave's adds complete (vmcnt(0)) before the workgroup's RELAXED arrival, and the last
+  // workgroup reads them with agent-scope atomic loads; nothing else passes between workgroups
+  // here (aux / cursor are read by the next launch), so no agent-scope fence (an L2 writeback +
+  // invalidate per workgroup at the kernel's tail). MH_FUSED_TAIL_FENCED: the former fences (A/B).
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();
   __shared__ uint32_t s_last;
   if (threadIdx.x == 0) {
+#ifdef MH_FUSED_TAIL_FENCED
     __threadfence();
     const uint32_t arrived = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    const uint32_t arrived = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
     s_last = arrived == gridDim.x - 1;
   }
   __syncthreads();
@@ -930,7 +940,9 @@ void k_sample_fused(FusedArgs a) {
     // wave 0: 64 lockstep totals per round, loaded together, an inclusive wave scan, the
     // exclusive prefixes stored and the totals re-zeroed (a lane-serial loop took one L2 round
     // trip per lockstep at the kernel's tail)
+#ifdef MH_FUSED_TAIL_FENCED
     __threadfence();
+#endif
     int64_t carry = 0;
     int last = 0;
     for (int t0 = 0; t0 < H; t0 += 64) {
@@ -961,7 +973,7 @@ void k_sample_fused(FusedArgs a) {
         a.cursor[2] += run;
         a.cursor[3] = last;  // windows of the horizon's last lockstep (the lockstep path's cursor[3])
       }
-      __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
