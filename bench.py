@@ -23,7 +23,7 @@ sys.path.insert(0, ROOT)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PEAK_F32_MFMA_TFS = 157.3  # MI355X dense f32 matrix peak (v_mfma_f32_*_f32)
 PEAK_F16_MFMA_TFS = 2500.0  # MI355X dense f16 matrix peak (v_mfma_f32_32x32x16_f16), MI355X_MICROARCH.md
-PMC_TRAFFIC = "r04_pmc_traffic_v2.json"  # the PMC summary of the current kernels (tools/pmc.sh + tools/pmc_summary.py)
+PMC_TRAFFIC = "r04_pmc_traffic_v3.json"  # the PMC summary of the current kernels (tools/pmc.sh + tools/pmc_summary.py)
 
 
 def parse():
@@ -239,21 +239,26 @@ def main():
     H = sampler.horizon
     noise_ptr = N.ptr(sampler._noise) if getattr(sampler, "_noise", None) is not None else None
 
+    # the emission launch alone on the timed region's LAST horizon (mh_sample_horizon_emit: it
+    # rewrites the same store rows, idempotent), i.e. at the trainer's own window count, before
+    # any diagnostic launch below moves the env state
+    t_emit_h = windows_emit = None
+    if fused_h:
+        win_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+
+        def k_emit_only():
+            N.lib().mh_sample_horizon_emit(h, H, ctypes.byref(buffer.ws), N.ptr(win_dev), st)
+
+        t_emit_h = time_launches(k_emit_only, reps) * 1e-3
+        windows_emit = int(win_dev.item())
+
     def k_fused():  # the fused horizon kernel alone (its windows are not emitted)
         N.lib().mh_sample_horizon(h, N.ptr(sampler._packed), sampler.envs.obs_dim, 2 * sampler.envs.act_dim,
                                   N.ptr(sampler.obs), H, None, noise_ptr, None, None, st)
 
-    def k_fused_emit():  # the sampler's horizon: the fused kernel + k_emit_scan + k_emit_cells into the store
-        N.lib().mh_sample_horizon(h, N.ptr(sampler._packed), sampler.envs.obs_dim, 2 * sampler.envs.act_dim,
-                                  N.ptr(sampler.obs), H, ctypes.byref(buffer.ws), noise_ptr, None, None, st)
-
-    t_fh = t_fhe = None
+    t_fh = None
     if fused_h:
         t_fh = time_launches(k_fused, 5) * 1e-3
-        w0 = int(buffer.cursor[2].item())
-        t_fhe = time_launches(k_fused_emit, 5, warm=0) * 1e-3
-        torch.cuda.synchronize()
-        windows_fh = (int(buffer.cursor[2].item()) - w0) / 5
     t_pol = time_launches(k_policy, reps) * 1e-3 if have_fused else None
     t_step = time_launches(k_roll, reps) * 1e-3
     win1 = int(buffer.cursor[2].item())
@@ -294,8 +299,7 @@ def main():
         # per f32-equivalent product) beside the env step; HBM traffic per horizon: the ring
         # records and the per-horizon state / observation load + store (W2 is re-read from L2)
         bytes_fh = a.envs * (H * F * 4 + 2 * (S * 4 + XS * 8 + 16) + 2 * D_ * 4)
-        bytes_win = windows_fh * bytes_window
-        t_emit_h = max(t_fhe - t_fh, 1e-9)
+        bytes_win = windows_emit * bytes_window
         kernels["sample_fused"] = {
             "avg_us_per_horizon": round(t_fh * 1e6, 2), "avg_us_per_lockstep": round(t_fh / H * 1e6, 3),
             "f16_mfma_TFLOPs": round(3 * flops_lockstep * H / t_fh / 1e12, 1),
@@ -303,10 +307,11 @@ def main():
             "hbm_bytes": bytes_fh, "GBps": round(bytes_fh / t_fh / 1e9, 1),
             "note": "k_sample_fused<Env>: the whole horizon (policy MLP + sample + env step + ring push for "
                     f"{H} locksteps) in one persistent launch, without its window emission"}
-        kernels["emit_horizon"] = {"avg_us": round(t_emit_h * 1e6, 2), "windows": windows_fh, "bytes": bytes_win,
+        kernels["emit_horizon"] = {"avg_us": round(t_emit_h * 1e6, 2), "windows": windows_emit, "bytes": bytes_win,
                                    "GBps": round(bytes_win / t_emit_h / 1e9, 1),
                                    "frac": round(bytes_win / t_emit_h / 1e9 / PEAK_HBM_GBS, 4),
-                                   "note": "k_emit_scan + k_emit_cells: the horizon's windows, ring -> replay store"}
+                                   "note": "k_emit_cells alone (mh_sample_horizon_emit) on the timed region's last "
+                                           "horizon: its windows, ring records -> replay store rows"}
     if t_pol is not None:
         flops = flops_lockstep
         # split-f16 arithmetic: every f32 product is 3 f16 MFMA products (hi.hi + hi.lo + lo.hi),

@@ -180,6 +180,14 @@ int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, i
                       int32_t horizon, const mh_window_store_t* store, const float* act_noise, float* act_out,
                       float* logp_out, void* stream);
 
+/* The emission launch of the last mh_sample_horizon alone, into `store` again: it reads the ring,
+ * the per-wave window lists and the header the fused kernel formed, and writes the same store
+ * rows (the cursor is not moved), so it is idempotent until the next horizon. A measurement
+ * entry (bench.py times the emission at the trainer's own window count with it); windows_out:
+ * optional DEVICE int64, the horizon's window count. */
+int mh_sample_horizon_emit(mh_env_t h, int32_t horizon, const mh_window_store_t* store, int64_t* windows_out,
+                           void* stream);
+
 /* Diagnostics of mh_sample_horizon: copies the handle's device error word (the number of bounded
  * intra-workgroup waits that timed out since mh_env_create; 0 when healthy) to int64 `out`, DEVICE
  * or pinned HOST memory (an async copy on `stream`). A timed-out wait means that horizon's logits,

@@ -98,6 +98,7 @@ _PROTOS = {
     "mh_sample_horizon_debug_logits": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "mh_sample_horizon": (ctypes.c_int, [c_vp, c_vp, c_i32, c_i32, c_vp, c_i32, ctypes.POINTER(WindowStore), c_vp,
                                          c_vp, c_vp, c_vp]),
+    "mh_sample_horizon_emit": (ctypes.c_int, [c_vp, c_i32, ctypes.POINTER(WindowStore), c_vp, c_vp]),
     "mh_rollout_traj_step": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(TrajStore), c_i32,
                                             c_vp, c_vp, c_vp]),
     "mh_policy_packed_size": (ctypes.c_int, [c_i32, ctypes.POINTER(c_i64)]),

@@ -391,6 +391,38 @@ int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, i
   return MH_OK;
 }
 
+int mh_sample_horizon_emit(mh_env_t h, int32_t horizon, const mh_window_store_t* store, int64_t* windows_out,
+                           void* stream) {
+  if (!h) return fail(MH_EINVAL, "mh_sample_horizon_emit: null handle");
+  if (!h->ring || !h->h_scan) return fail(MH_ESTATE, "mh_sample_horizon_emit: no horizon has been sampled");
+  if (horizon <= 0 || horizon > h->hcap) return fail(MH_EINVAL, "mh_sample_horizon_emit: bad horizon");
+  if (!store || store->capacity <= 0 || !store->cursor || !store->obs || !store->act || !store->rew ||
+      !store->cost || !store->obs2 || !store->done || !store->logp)
+    return fail(MH_EINVAL, "mh_sample_horizon_emit: incomplete window store");
+  mh::HorizonEmitArgs ea;
+  std::memset(&ea, 0, sizeof(ea));
+  ea.E = h->E;
+  ea.H = horizon;
+  ea.n = h->n;
+  ea.R = h->R;
+  ea.ring = h->ring;
+  ea.emit_count = h->h_count;
+  ea.emit_list = h->h_list;
+  ea.obs = store->obs;
+  ea.act = store->act;
+  ea.rew = store->rew;
+  ea.cost = store->cost;
+  ea.obs2 = store->obs2;
+  ea.done = store->done;
+  ea.logp = store->logp;
+  ea.capacity = store->capacity;
+  ea.aux = h->h_scan;
+  MH_HIP(mh::launch_emit_horizon(h->env_id, ea, (hipStream_t)stream));
+  if (windows_out)  // the horizon's window count (header word 0, formed by the fused kernel)
+    MH_HIP(hipMemcpyAsync(windows_out, h->h_scan, sizeof(int64_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return MH_OK;
+}
+
 int mh_sample_horizon_debug_logits(mh_env_t h, float* logits_out, float* obs_out) {
   if (!h) return fail(MH_EINVAL, "mh_sample_horizon_debug_logits: null handle");
   if ((logits_out == nullptr) != (obs_out == nullptr)) return fail(MH_EINVAL, "mh_sample_horizon_debug_logits: both or neither");

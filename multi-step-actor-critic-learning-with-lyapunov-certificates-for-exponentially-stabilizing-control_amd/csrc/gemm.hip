@@ -488,7 +488,7 @@ __global__ __launch_bounds__(256) void k_gemm_tall(GemmArgs g, int tiles_n) {
 // ------------------------------------------------------------------ deep products
 // C[M][N] = A^T B with A [K][M], B [K][N] and K >> M, N: the weight gradients g^T x of the
 // update's layers (M = N = 256, K = B x n = 5,120). The BLAS kernel for this shape runs 18.6 us.
-// Here the K range splits S ways (S x (M/64)(N/64) ~ 256 workgroups: S = 16 at 256 x 256) and
+// Here the K range splits S ways (S x (M/64)(N/64) ~ deep_target() workgroups: S = 8 at 256 x 256) and
 // each workgroup forms a 64 x 64 partial over its K slice:
 //   * 64-deep chunks of both operands staged through LDS as [k][64] rows (row-contiguous float4
 //     global loads: a quarter-wave reads 256 B of one k row), two chunks ahead in registers;
@@ -701,13 +701,17 @@ static bool deep_ok(const float* A, const float* B, const float* bias, int64_t M
          (K + TK) * ldb * 4 < ((int64_t)1 << 30);
 }
 
-// K splits: about 256 workgroups, slices of >= 2 chunks
-// workgroups a deep product aims for (MH_DEEP_WGS overrides 256 for A/B measurements)
+// K splits: about 128 workgroups per product, slices of >= 2 chunks. Workgroups a deep product
+// aims for (MH_DEEP_WGS overrides for A/B measurements): the weight gradients run beside the other
+// update branch's launches, where fewer, longer workgroups (less prologue / partial-tile work per
+// CU) win although alone 256 is as fast or faster: bench 1.154-1.161 B env-steps/s at 128 vs
+// 1.149-1.151 at 256, 1.139-1.141 at 96, 1.119 at 64; alone, the Lyapunov layers' 52.5 vs 54.7 us
+// and the critics' 28.1 vs 25.1 us (tools/r04_deepwgs.sh, r04_deepwgs2.sh)
 static int64_t deep_target() {
   static const int64_t t = [] {
     const char* e = getenv("MH_DEEP_WGS");
     const int64_t v = e ? atoll(e) : 0;
-    return v > 0 ? v : 256;
+    return v > 0 ? v : 128;
   }();
   return t;
 }

@@ -62,5 +62,6 @@ struct HorizonEmitArgs {
 
 
 hipError_t launch_sample_fused(int env_id, const FusedArgs& a, const HorizonEmitArgs& ea, hipStream_t st);
+hipError_t launch_emit_horizon(int env_id, const HorizonEmitArgs& ea, hipStream_t st);
 
 }  // namespace mh

@@ -1123,6 +1123,28 @@ static hipError_t launch_fused_t(const FusedArgs& a, const HorizonEmitArgs& ea, 
   return hipGetLastError();
 }
 
+// the emission launch alone (the last horizon's windows again: it reads the ring, the per-wave
+// lists and the fused kernel's header and writes the same store rows, so it is idempotent until
+// the next horizon; bench.py times it this way at the trainer's own window count)
+template <class Env>
+static hipError_t launch_emit_t(const HorizonEmitArgs& ea, hipStream_t st) {
+  k_emit_cells<Env::D, Env::A><<<(unsigned)fused_emit_cells(ea.E, ea.H), 256, 0, st>>>(ea);
+  return hipGetLastError();
+}
+
+hipError_t launch_emit_horizon(int env_id, const HorizonEmitArgs& ea, hipStream_t st) {
+  if (ea.obs == nullptr || ea.aux == nullptr) return hipErrorInvalidValue;
+  switch (env_id) {
+    case ENV_VANDERPOL: return launch_emit_t<VanderPol>(ea, st);
+    case ENV_PENDULUM: return launch_emit_t<Pendulum>(ea, st);
+    case ENV_DUCTEDFAN: return launch_emit_t<DuctedFan>(ea, st);
+    case ENV_TWOLINK: return launch_emit_t<TwoLink>(ea, st);
+    case ENV_SINGLETRACKCAR: return launch_emit_t<SingleTrackCar>(ea, st);
+    case ENV_QUADTRACKING: return launch_emit_t<QuadTracking>(ea, st);
+  }
+  return hipErrorInvalidValue;
+}
+
 hipError_t launch_sample_fused(int env_id, const FusedArgs& a, const HorizonEmitArgs& ea, hipStream_t st) {
   switch (env_id) {
     case ENV_VANDERPOL: return launch_fused_t<VanderPol>(a, ea, st);

@@ -100,6 +100,40 @@ def test_fused_horizon_with_exploration_noise(tmp_path):
         _assert_same(a, ba, b, bb, f"sample {it}")
 
 
+def test_emission_relaunch_rewrites_the_same_rows(tmp_path):
+    """mh_sample_horizon_emit (the emission launch alone, bench.py's timing of it) on the last
+    horizon rewrites exactly the rows that horizon's emission wrote — into a wiped store, bit for
+    bit, cursor untouched — and reports the horizon's window count."""
+    a, ba, b, bb = _pair("QuadTracking", 65536, 20, tmp_path, hover=True)
+    c0 = int(ba.cursor[2])
+    a.sample()
+    a.sample()  # the second horizon is the one re-emitted
+    torch.cuda.synchronize()
+    c_before = int(ba.cursor[2])
+    a.sample()
+    torch.cuda.synchronize()
+    won = int(ba.cursor[2]) - c_before
+    assert won > 0 and c0 >= 0
+    snap = {k: ba.n_step_buf[k].clone() for k in KEYS}
+    cur = ba.cursor.clone()
+    for k in KEYS:
+        ba.n_step_buf[k].fill_(-7.0)
+    wins = torch.zeros(1, dtype=torch.int64, device="cuda")
+    N.check(N.lib().mh_sample_horizon_emit(a._h, a.horizon, ctypes.byref(ba.ws), N.ptr(wins), N.stream_of()),
+            "mh_sample_horizon_emit")
+    torch.cuda.synchronize()
+    assert int(wins) == won
+    assert torch.equal(ba.cursor, cur)
+    M = ba.max_size
+    start = (int(cur[0]) - won) % M
+    rows = (start + torch.arange(won, device="cuda")) % M
+    for k in KEYS:
+        assert torch.equal(ba.n_step_buf[k][rows], snap[k][rows]), k
+    untouched = torch.ones(M, dtype=torch.bool, device="cuda")
+    untouched[rows] = False
+    assert bool((ba.n_step_buf["rew"][untouched] == -7.0).all())
+
+
 def test_fused_horizon_needs_reserved_rings():
     info = N.env_info("VanderPol")
     h = ctypes.c_void_p()
