@@ -239,7 +239,7 @@ def main():
     H = sampler.horizon
     noise_ptr = N.ptr(sampler._noise) if getattr(sampler, "_noise", None) is not None else None
 
-    # the emission launch alone on the timed region's LAST horizon (mh_sample_horizon_emit: it
+    # the emission launch alone on the last trainer step's horizon (mh_sample_horizon_emit: it
     # rewrites the same store rows, idempotent), i.e. at the trainer's own window count, before
     # any diagnostic launch below moves the env state
     t_emit_h = windows_emit = None
@@ -249,6 +249,8 @@ def main():
         def k_emit_only():
             N.lib().mh_sample_horizon_emit(h, H, ctypes.byref(buffer.ws), N.ptr(win_dev), st)
 
+        # (the window count swings from horizon to horizon, a few hundred to ~80 k: the init
+        # policy's episodes end together; the line reports the count this figure was taken at)
         t_emit_h = time_launches(k_emit_only, reps) * 1e-3
         windows_emit = int(win_dev.item())
 
@@ -310,7 +312,7 @@ def main():
         kernels["emit_horizon"] = {"avg_us": round(t_emit_h * 1e6, 2), "windows": windows_emit, "bytes": bytes_win,
                                    "GBps": round(bytes_win / t_emit_h / 1e9, 1),
                                    "frac": round(bytes_win / t_emit_h / 1e9 / PEAK_HBM_GBS, 4),
-                                   "note": "k_emit_cells alone (mh_sample_horizon_emit) on the timed region's last "
+                                   "note": "k_emit_cells alone (mh_sample_horizon_emit) on the last trainer step's "
                                            "horizon: its windows, ring records -> replay store rows"}
     if t_pol is not None:
         flops = flops_lockstep

@@ -4,6 +4,7 @@ autograd of the same nn.Linear + activation (RL/apprfunc/mlp.py:18-30), float64 
 Tolerance: each gradient within 2e-6 * sqrt(K) * (sum of |terms|) + 1e-6 of the float64 value
 (K = the summed dimension), the f32-accumulation bound the GEMM tests use."""
 import ctypes
+import os
 
 import pytest
 import torch
@@ -71,7 +72,10 @@ def test_linear_backward_plan_rejects():
         assert N.lib().mh_linear_backward_plan(*args, ctypes.byref(ok), ctypes.byref(ws)) == 0
         assert ok.value == 0, args
     assert N.lib().mh_linear_backward_plan(5120, 256, 256, 1, 1, 1, ctypes.byref(ok), ctypes.byref(ws)) == 0
-    assert ok.value == 1 and ws.value == 16 * 256 * 256 + 16 * 4 * 256  # dW partials + bias partials per split x column tile
+    # dW partials + bias partials per split x column tile: S = 8 splits (the deep products' target
+    # of 128 workgroups over 16 tiles of 64 x 64; MH_DEEP_WGS overrides it)
+    S = _deep_splits(256, 256, 5120)
+    assert ok.value == 1 and ws.value == S * 256 * 256 + S * 4 * 256
 
 
 @pytest.mark.parametrize("rows,n_in", [(5120, 12), (5120, 16), (10240, 12), (3001, 4), (5120, 60)])
@@ -92,11 +96,23 @@ def test_linear_backward_narrow_input_dw_db(rows, n_in, act):
     assert torch.equal(dw, dw2) and torch.equal(db, db2)
 
 
+def _deep_splits(M, N, K):
+    """gemm.hip deep_splits: about deep_target() workgroups (MH_DEEP_WGS, default 128) per product,
+    slices of >= 2 of the K range's 64-deep chunks."""
+    target = int(os.environ.get("MH_DEEP_WGS", "128"))
+    tiles = (M // 64) * ((N + 63) // 64)
+    chunks = -(-K // 64)
+    S = max(1, min(-(-target // tiles), chunks // 2))
+    per = -(-chunks // S)
+    return -(-chunks // per)
+
+
 def test_linear_backward_plan_narrow_input():
     ok, ws = ctypes.c_int32(), ctypes.c_int64()
     assert N.lib().mh_linear_backward_plan(5120, 256, 12, 0, 1, 1, ctypes.byref(ok), ctypes.byref(ws)) == 0
-    # S splits (about 256 workgroups over the 4 row tiles: 40, two 64-row chunks each) x (dW + one bias tile)
-    assert ok.value == 1 and ws.value == 40 * 256 * 12 + 40 * 1 * 256
+    # S splits (about deep_target() workgroups over the 4 row tiles) x (dW + one bias tile)
+    S = _deep_splits(256, 12, 5120)
+    assert ok.value == 1 and ws.value == S * 256 * 12 + S * 1 * 256
     for args in [(5120, 256, 12, 1, 1, 1), (5120, 256, 6, 0, 1, 1), (5120, 256, 68, 0, 1, 1)]:
         assert N.lib().mh_linear_backward_plan(*args, ctypes.byref(ok), ctypes.byref(ws)) == 0
         assert ok.value == 0, args
