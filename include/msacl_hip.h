@@ -473,6 +473,13 @@ int mh_mlp3_backward(const float* dy, int64_t ldy, const float* h1, const float*
                      int32_t act1, int32_t act2, float* g2, float* g1, int64_t ldg, float* dx, int64_t ldx,
                      int32_t groups, const int64_t* group_strides, void* stream);
 
+/* The fused forward's rows per workgroup for the mh_mlp3_forward* launches that follow (host
+ * state, read at launch, so also at graph capture): 0 = the default two 16-row tiles per wave;
+ * -1 = the fewest tiles that still give one workgroup per CU (the fastest grid for a launch that
+ * runs alone on the GPU, slower beside a concurrent branch: DESIGN 3.3); 1..4 fixed. The
+ * environment variable MH_MLP_RT overrides it. Bits do not depend on it. */
+int mh_mlp3_set_row_tiles(int32_t mode);
+
 /* mh_mlp3_backward plus the output layer's gradients (n_out <= 16; the twin critics' q heads):
  * dw3 [n_out][hidden] = dy^T h2 and, when non-NULL, db3 [n_out] = the column sums of dy, group q's
  * at + q x gs_dw3 / gs_db3 floats. The chain launch forms each 16-row block's partials from the dy

@@ -153,6 +153,7 @@ _PROTOS = {
                                + [c_i32] * 5 + [c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp]),
     "mh_mlp3_backward": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64] + [c_i32] * 5
                          + [c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp]),
+    "mh_mlp3_set_row_tiles": (ctypes.c_int, [c_i32]),
     "mh_mlp3_backward_w3_workspace": (ctypes.c_int, [c_i64, c_i32, c_i32, c_i32, ctypes.POINTER(c_i64)]),
     "mh_mlp3_backward_w3": (ctypes.c_int, [c_vp, c_i64, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64] + [c_i32] * 5
                             + [c_vp, c_vp, c_i64, c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp]),

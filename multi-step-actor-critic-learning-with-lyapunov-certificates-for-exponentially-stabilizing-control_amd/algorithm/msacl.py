@@ -350,6 +350,9 @@ class MSACL:
         self.wants_joint_batch = (self.device.type == "cuda" and os.environ.get("MSACL_JOINT_BATCH", "1") == "1")
         # the policy step's first policy forward reuses the Lyapunov step's (MSACL_REUSE_POLICY_FWD=0: off)
         self._reuse_policy_fwd = os.environ.get("MSACL_REUSE_POLICY_FWD", "1") == "1"
+        # later policy steps of an update (nothing beside them on the GPU) launch the critics'
+        # forward on the one-workgroup-per-CU grid (MSACL_POLICY_ALONE_RT=0: the default grid)
+        self._policy_alone_rt = os.environ.get("MSACL_POLICY_ALONE_RT", "1") == "1"
         self._pol_kept = None
         # the update's rsample noise drawn inside the policy-head kernel (Philox, a device counter);
         # MSACL_KERNEL_NOISE=0: torch's normal draw (A/B)
@@ -878,7 +881,16 @@ class MSACL:
             tc = self._twin_critics(B * n)
             if tc is not None:
                 from ..apprfunc._twin import TwinQ
-                q1, q2 = TwinQ.apply(xq.reshape(B * n, Dd + A), tc[0])
+                # the policy step's chain runs alone on the GPU (after the branches' join): the
+                # critics' forward takes the one-workgroup-per-CU grid (mh_mlp3_set_row_tiles)
+                alone = self._policy_alone_rt and reuse_adv
+                if alone:
+                    N.check(N.lib().mh_mlp3_set_row_tiles(-1), "mh_mlp3_set_row_tiles")
+                try:
+                    q1, q2 = TwinQ.apply(xq.reshape(B * n, Dd + A), tc[0])
+                finally:
+                    if alone:
+                        N.lib().mh_mlp3_set_row_tiles(0)
                 q1, q2 = q1.view(B, n), q2.view(B, n)
             else:
                 q1, q2 = self._twin_pair(lambda: nets.q1.q(xq).squeeze(-1), lambda: nets.q2.q(xq).squeeze(-1))

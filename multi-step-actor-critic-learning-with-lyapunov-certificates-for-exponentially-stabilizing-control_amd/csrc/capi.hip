@@ -1160,6 +1160,12 @@ int mh_mlp3_backward(const float* dy, int64_t ldy, const float* h1, const float*
                             ldx, groups, group_strides, nullptr, nullptr, 0, 0, nullptr, stream);
 }
 
+int mh_mlp3_set_row_tiles(int32_t mode) {
+  if (mode < -1 || mode > 4) return fail(MH_EINVAL, "mh_mlp3_set_row_tiles: mode must be -1, 0 or 1..4");
+  mh::mlp3_set_row_tiles(mode);
+  return MH_OK;
+}
+
 int mh_mlp3_backward_w3_workspace(int64_t rows, int32_t hidden, int32_t n_out, int32_t groups, int64_t* floats_out) {
   if (rows < 0 || hidden <= 0 || n_out <= 0 || n_out > 16 || groups < 1 || !floats_out)
     return fail(MH_EINVAL, "mh_mlp3_backward_w3_workspace: bad argument");

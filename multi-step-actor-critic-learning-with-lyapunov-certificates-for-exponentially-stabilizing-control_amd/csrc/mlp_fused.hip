@@ -744,6 +744,12 @@ hipError_t launch_mlp3_backward(const Mlp3BwdArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// the forward's row-tile mode for the launches that follow (mh_mlp3_set_row_tiles): 0 the default
+// (RT = 2), -1 the CU-count rule, 1 .. 4 fixed. Host state read at launch (and so at capture).
+static int g_row_tiles = 0;
+
+void mlp3_set_row_tiles(int mode) { g_row_tiles = mode; }
+
 // CU count of the (single) device this process drives, queried once (256 on the MI355X)
 static int64_t device_cus() {
   static int cus = 0;
@@ -775,11 +781,13 @@ hipError_t launch_mlp3_forward(const Mlp3Args& a_in, int groups, hipStream_t st)
   // MH_MLP_RT = 1 / 2 / 3 / 4 forces, "auto" selects as above.
   static const int force_rt = [] {
     const char* e = getenv("MH_MLP_RT");
-    if (!e) return 2;
+    if (!e) return -1;
     if (std::strcmp(e, "auto") == 0) return 0;
     return atoi(e);
   }();
-  int rt = force_rt;
+  // MH_MLP_RT wins; else the caller's mode (mh_mlp3_set_row_tiles: a launch it knows runs alone,
+  // such as the policy step's critic forward, takes the "auto" grid); else RT = 2
+  int rt = force_rt >= 0 ? force_rt : (g_row_tiles == 0 ? 2 : (g_row_tiles < 0 ? 0 : g_row_tiles));
   if (rt < 1 || rt > 4) {
     const int64_t cus = device_cus();
     auto wgs = [&](int r) { return (a.M + 16 * r - 1) / (16 * r) * (int64_t)groups; };

@@ -234,6 +234,7 @@ struct Mlp3BwdArgs {
   int64_t s_part3;
 };
 hipError_t launch_mlp3_backward(const Mlp3BwdArgs& a, hipStream_t st);
+void mlp3_set_row_tiles(int mode);
 // several weight gradients dw = g^T x, db = column sums of g in two launches (gemm.hip)
 struct WgradSpec {
   const float* g;

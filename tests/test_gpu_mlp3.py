@@ -262,6 +262,29 @@ def test_twin_weight_grads_fused_equals_per_layer():
         torch.testing.assert_close(u, v, rtol=1e-4, atol=1e-5 * float(v.abs().max()))
 
 
+@pytest.mark.parametrize("mode", [-1, 1, 3, 4])
+def test_forward_row_tile_modes_equal_default(mode):
+    """mh_mlp3_set_row_tiles changes only the grid (rows per workgroup), never the bits: the twin
+    critics' forward (2 x 5,120 rows and a ragged 1,037) under each mode equals the default."""
+    from msacl_amd.apprfunc._twin import TwinCritic
+    from msacl_amd.apprfunc.mlp import ActionValue
+    N = F._native()
+    torch.manual_seed(11)
+    kw = dict(obs_dim=12, act_dim=4, hidden_sizes=[256, 256], hidden_activation="relu", output_activation="linear")
+    tc = TwinCritic.build(ActionValue(**kw).cuda(), ActionValue(**kw).cuda())
+    for M in (5120, 1037):
+        x = torch.randn(M, 16, device="cuda")
+        ref = [t.clone() for t in tc.forward(x)]
+        N.check(N.lib().mh_mlp3_set_row_tiles(mode), "mh_mlp3_set_row_tiles")
+        try:
+            got = [t.clone() for t in tc.forward(x)]
+        finally:
+            N.lib().mh_mlp3_set_row_tiles(0)
+        for a, b in zip(got, ref):
+            torch.testing.assert_close(a, b, rtol=0, atol=0)
+    assert N.lib().mh_mlp3_set_row_tiles(5) != 0
+
+
 @pytest.mark.parametrize("M", [5120, 1037, 16400])
 def test_twin_head_grads_folded_into_chain(M):
     """The q heads' dW3 / db3 formed inside the chain launch (mh_mlp3_backward_w3) equal the
