@@ -260,7 +260,11 @@ def main():
 
     t_fh = None
     if fused_h:
-        t_fh = time_launches(k_fused, 5) * 1e-3
+        # one launch per measurement (each after the stream's spin), averaged: five back-to-back
+        # persistent MFMA launches ran ~10 % slower than the same kernel inside the trainer's
+        # steps (rocprofv3 average), where the update's launches sit between horizons
+        k_fused()
+        t_fh = sum(time_launches(k_fused, 1, warm=0) for _ in range(5)) / 5 * 1e-3
     t_pol = time_launches(k_policy, reps) * 1e-3 if have_fused else None
     t_step = time_launches(k_roll, reps) * 1e-3
     win1 = int(buffer.cursor[2].item())
