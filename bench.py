@@ -106,6 +106,16 @@ def main():
     local = D.local_device_index()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    # self-check of the launch: every rank joins one all-reduce of a ones tensor over the data-path
+    # backend (RCCL on the MI355X node); the count must equal --gpus, else the line is not valid
+    dist_backend = torch.distributed.get_backend() if world > 1 else None
+    ranks_seen = int(round(D.sum_over_ranks(1.0))) if world > 1 else 1
+    if ranks_seen != a.gpus or world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the process group has {world} ranks and an all-reduce over "
+              f"{dist_backend} counted {ranks_seen}", file=sys.stderr, flush=True)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        sys.exit(3)
     horizon = 20
     tmp = tempfile.mkdtemp(prefix=f"msacl_bench_r{rank}_")
     cfg = default_msacl_args(env_name=a.env, env_num=a.envs, env_seed=1 + rank * 1000003, seed=rank * 1000000,
@@ -389,6 +399,7 @@ def main():
                    "env": a.env, "envs_per_gpu": a.envs, "horizon": horizon, "n_step": n, "replay_batch": 256,
                    "policy": a.policy, "parallelism": f"dp{world}"},
         "roofline": roof,
+        "dist_backend": dist_backend, "rccl_ranks": ranks_seen,
         "kernels": kernels,
         "windows_per_step": round(windows_timed / a.steps, 1),
         "phases": phases,

@@ -184,9 +184,18 @@ int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, i
  * the per-wave window lists and the header the fused kernel formed, and writes the same store
  * rows (the cursor is not moved), so it is idempotent until the next horizon. A measurement
  * entry (bench.py times the emission at the trainer's own window count with it); windows_out:
- * optional DEVICE int64, the horizon's window count. */
+ * optional DEVICE int64, the horizon's window count. `horizon` must equal the last
+ * mh_sample_horizon's and `store` be the store it emitted into (same cursor), with no other
+ * stepping / resetting call on the handle since: MH_EINVAL / MH_ESTATE otherwise. */
 int mh_sample_horizon_emit(mh_env_t h, int32_t horizon, const mh_window_store_t* store, int64_t* windows_out,
                            void* stream);
+
+/* The window count of the handle's last mh_sample_horizon (the fused kernel's header aux[0], the
+ * windows the horizon completed, = the store cursor's advance of `total`), copied to int64 `out`
+ * (DEVICE or pinned HOST) on `stream`; valid until the next mh_sample_horizon on the handle. Lets
+ * the sampler report a horizon's window count lazily, without a cursor snapshot + subtraction
+ * launched around every horizon. */
+int mh_sample_horizon_windows(mh_env_t h, int64_t* out, void* stream);
 
 /* Diagnostics of mh_sample_horizon: copies the handle's device error word (the number of bounded
  * intra-workgroup waits that timed out since mh_env_create; 0 when healthy) to int64 `out`, DEVICE

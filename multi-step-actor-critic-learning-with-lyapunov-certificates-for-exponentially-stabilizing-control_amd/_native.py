@@ -2,7 +2,7 @@
 build, config 1: host_lib()).
 
 The library is built in-tree by `make -C csrc` (or __graft_entry__.build()) into
-csrc/build/libmsacl_hip.so. There is no CPU fallback anywhere in the product path: if the
+<repo>/lib/libmsacl_hip.so. There is no CPU fallback anywhere in the product path: if the
 library is missing or a call fails, this module raises.
 """
 from __future__ import annotations
@@ -11,7 +11,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("MSACL_HIP_LIB", os.path.join(_HERE, "csrc", "build", "libmsacl_hip.so"))
+_REPO = os.path.dirname(_HERE)
+LIB_PATH = os.environ.get("MSACL_HIP_LIB", os.path.join(_REPO, "lib", "libmsacl_hip.so"))
 
 ENV_IDS = {
     "VanderPol": 0,
@@ -90,6 +91,7 @@ _PROTOS = {
     "mh_env_set_action_noise": (ctypes.c_int, [c_vp, c_vp]),
     "mh_rollout_set_trace": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mh_nstep_reserve": (ctypes.c_int, [c_vp, c_i32]),
+    "mh_sample_horizon_windows": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "mh_sample_horizon_errors": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "mh_sample_horizon_set_spin_limit": (ctypes.c_int, [c_vp, ctypes.c_uint32]),
     "mh_env_get_counters": (ctypes.c_int, [c_vp, c_vp, c_vp]),
@@ -210,7 +212,7 @@ def exported_symbols():
 
 
 # ------------------------------------------------------------------ CPU build (config 1)
-HOST_LIB_PATH = os.environ.get("MSACL_HOST_LIB", os.path.join(_HERE, "csrc", "build", "libmsacl_host.so"))
+HOST_LIB_PATH = os.environ.get("MSACL_HOST_LIB", os.path.join(_REPO, "lib", "libmsacl_host.so"))
 _HOST_PROTOS = {
     "mhh_abi_version": (ctypes.c_int, []),
     "mhh_last_error": (ctypes.c_char_p, []),

@@ -457,6 +457,30 @@ class MSACL:
             self._noise_ctr = torch.zeros(2, dtype=torch.int64, device=self.device)
         return self._noise_seed, self._noise_ctr
 
+    def rng_state(self) -> dict:
+        """The algorithm's random state beyond its networks: the in-kernel rsample noise's seed and
+        device counter. The reference checkpoints only `networks.state_dict()` (its torch generator
+        restarts from the seed on resume); saving this as well lets a resumed run continue the
+        noise sequence instead of replaying it from the start."""
+        ctr = None if self._noise_ctr is None else self._noise_ctr.detach().cpu().clone()
+        return {"noise_seed": int(self._noise_seed), "noise_ctr": ctr}
+
+    def load_rng_state(self, state: dict) -> None:
+        """Restore rng_state(): the counter is written in place (captured update graphs hold its
+        address); a changed seed drops the captured graphs (the seed is a kernel argument)."""
+        seed = int(state["noise_seed"])
+        if seed != self._noise_seed and self._graphs:
+            from ._update_graph import release_graph
+            graphs, self._graphs = self._graphs, {}
+            for g, _o, _p in graphs.values():
+                release_graph(g)
+            self._warm = set()
+        self._noise_seed = seed
+        ctr = state.get("noise_ctr")
+        if ctr is not None:
+            _seed, dev_ctr = self._noise_rng()
+            dev_ctr.copy_(torch.as_tensor(ctr, dtype=torch.int64).to(dev_ctr.device))
+
     def _buf(self, B, n):
         key = (B, n)
         if key not in self._scratch:

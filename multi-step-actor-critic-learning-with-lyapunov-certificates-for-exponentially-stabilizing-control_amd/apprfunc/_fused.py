@@ -342,12 +342,16 @@ def weight_grads(products, rows, dev):
     for i, (g, ld_g, x, ld_x, n_out, n_in, dw, db) in enumerate(products):
         arr[i] = N.Wgrad(g.data_ptr(), ld_g, x.data_ptr(), ld_x, n_out, n_in, dw.data_ptr(),
                          db.data_ptr() if db is not None else None)
-    key = (dev, rows, tuple((p[4], p[5], p[1], p[3], p[7] is not None) for p in products))
-    ws = _WG_WS.get(key)
-    if ws is None:
+    # only the workspace SIZE is cached: the buffer itself comes from the caching allocator on the
+    # current stream for every call (under graph capture: the graph's pool), so two concurrent
+    # calls of one shape on different streams (the twin critics' q1 / q2) never share it
+    key = (rows, tuple((p[4], p[5], p[1], p[3], p[7] is not None) for p in products))
+    nws = _WG_WS.get(key)
+    if nws is None:
         f = ctypes.c_int64()
         N.check(N.lib().mh_weight_grads_workspace(arr, len(products), rows, ctypes.byref(f)), "mh_weight_grads_workspace")
-        ws = _WG_WS[key] = torch.empty(max(f.value, 1), dtype=torch.float32, device=dev)
+        nws = _WG_WS[key] = max(f.value, 1)
+    ws = torch.empty(nws, dtype=torch.float32, device=dev)
     N.check(N.lib().mh_weight_grads(arr, len(products), rows, N.ptr(ws), N.stream_of(dev)), "mh_weight_grads")
 
 
@@ -357,8 +361,11 @@ class MLP3(torch.autograd.Function):
     three layers' LinearAct backwards (layer_backward) on the kept activations."""
 
     @staticmethod
-    def forward(ctx, x, W1, b1, W2, b2, W3, b3, acts):
-        keep = any(ctx.needs_input_grad[:7])
+    def forward(ctx, x, W1, b1, W2, b2, W3, b3, acts, grad=True):
+        # h1 / h2 are written to HBM only when a backward can follow: `grad` is the caller's grad
+        # mode (Function.forward itself always runs without grad, and needs_input_grad is True
+        # under torch.no_grad() whenever the parameters require grad)
+        keep = grad and any(ctx.needs_input_grad[:7])
         if W3.shape[0] > 16 and not _MLP3["wide_fwd"]:
             h1 = _linear_act(x, W1, b1, acts[0])
             h2 = _linear_act(h1, W2, b2, acts[1])
@@ -386,7 +393,7 @@ class MLP3(torch.autograd.Function):
                                              N.ptr(W2), N.ptr(W3), M, K1, W2.shape[0], W3.shape[0], a1, a2, None,
                                              None, W2.shape[0], N.ptr(dx), K1, 1, None, N.stream_of(x.device)),
                     "mh_mlp3_backward")
-            return dx, None, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None
         if a3 == 0 and _MLP3["on"]:
             # the input-gradient chain in one launch (g2 / g1 kept for the weight gradients), then
             # every layer's weight / bias gradient in two more (mh_weight_grads); a product that
@@ -422,7 +429,7 @@ class MLP3(torch.autograd.Function):
                     out[name] = (dw2, db2_)
             if prods:
                 weight_grads(prods, M, dev)
-            return (dx, out["1"][0], out["1"][1], out["2"][0], out["2"][1], out["3"][0], out["3"][1], None)
+            return (dx, out["1"][0], out["1"][1], out["2"][0], out["2"][1], out["3"][0], out["3"][1], None, None)
         dh2, dW3, db3 = layer_backward(dy, h2, W3, y, a3, need_h2, nW3, nb3)
         dx = dW1 = db1 = dW2 = db2 = None
         if need_h2:
@@ -430,7 +437,7 @@ class MLP3(torch.autograd.Function):
             dh1, dW2, db2 = layer_backward(dh2, h1, W2, h2, a2, need_h1, nW2, nb2)
             if need_h1:
                 dx, dW1, db1 = layer_backward(dh1, x, W1, h1, a1, nx, nW1, nb1)
-        return dx, dW1, db1, dW2, db2, dW3, db3, None
+        return dx, dW1, db1, dW2, db2, dW3, db3, None, None
 
 
 class MLP3SquareSum(torch.autograd.Function):
@@ -441,11 +448,14 @@ class MLP3SquareSum(torch.autograd.Function):
     mh_weight_grads: the square-sum launch and its backward launch disappear."""
 
     @staticmethod
-    def forward(ctx, x, W1, b1, W2, b2, W3, b3, acts):
+    def forward(ctx, x, W1, b1, W2, b2, W3, b3, acts, grad=True):
         N = _native()
         M, K1 = x.shape
         H, N3, dev = W2.shape[0], W3.shape[0], x.device
-        keep = any(ctx.needs_input_grad[:7])
+        # h1 / h2 are written to HBM only when a backward can follow: `grad` is the caller's grad
+        # mode (Function.forward itself always runs without grad, and needs_input_grad is True
+        # under torch.no_grad() whenever the parameters require grad)
+        keep = grad and any(ctx.needs_input_grad[:7])
         e = lambda *sh: torch.empty(*sh, dtype=torch.float32, device=dev)  # noqa: E731
         y, v = e(M, N3), e(M)
         h1, h2 = (e(M, H), e(M, H)) if keep else (None, None)
@@ -489,7 +499,7 @@ class MLP3SquareSum(torch.autograd.Function):
                 out[name] = (dw2, db2_)
         if prods:
             weight_grads(prods, M, dev)
-        return (dx, out["1"][0], out["1"][1], out["2"][0], out["2"][1], out["3"][0], out["3"][1], None)
+        return (dx, out["1"][0], out["1"][1], out["2"][0], out["2"][1], out["3"][0], out["3"][1], None, None)
 
 
 def square_sum_mlp(seq, x):
@@ -510,7 +520,7 @@ def square_sum_mlp(seq, x):
         h = h.contiguous()
     if h.data_ptr() % 4:
         return None
-    v = MLP3SquareSum.apply(h, l1[0], l1[1], l2[0], l2[1], l3[0], l3[1], acts)
+    v = MLP3SquareSum.apply(h, l1[0], l1[1], l2[0], l2[1], l3[0], l3[1], acts, torch.is_grad_enabled())
     return v.reshape(lead)
 
 
@@ -528,7 +538,7 @@ class MLP3Kept(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        return MLP3.backward(ctx, dy) + (None,)
+        return MLP3.backward(ctx, dy)  # (its last None stands for `kept`)
 
 
 def mlp3_forward_kept(seq, x):
@@ -650,7 +660,7 @@ class MLP(nn.Sequential):
             spec = mlp3_layers(self)
             if spec is not None:
                 (l1, l2, l3), acts = spec
-                y = MLP3.apply(h, l1[0], l1[1], l2[0], l2[1], l3[0], l3[1], acts)
+                y = MLP3.apply(h, l1[0], l1[1], l2[0], l2[1], l3[0], l3[1], acts, torch.is_grad_enabled())
                 return y.reshape(*lead, y.shape[-1])
         mods = list(self)
         for i in range(0, len(mods), 2):

@@ -79,9 +79,16 @@ struct mh_env_s {
   int32_t* h_list = nullptr;        // [hcap][E]
   int64_t* h_scan = nullptr;        // the emission's bookkeeping (mh_nstep_reserve): aux [hcap + 2], then
                                     // int32 lockstep totals [hcap] + arrival count
+  int32_t* h_cpre = nullptr;        // [hcap][cells per lockstep]: per-cell window prefixes, only when a
+                                    // lockstep has more than FUSED_EMIT_SCAN_CELLS cells (k_emit_prefix)
   float* dbg_logits = nullptr;      // mh_sample_horizon_debug_logits: [H][E][2A] logits trace
   float* dbg_obs = nullptr;         //   and [H][E][D] pre-step observations
   uint32_t spin_limit = 0;          // mh_sample_horizon_set_spin_limit (0: the kernel's default)
+  // the last mh_sample_horizon that emitted into a store: its horizon and the store's cursor
+  // (mh_sample_horizon_emit replays exactly that emission; 0 / null once anything else stepped,
+  // reset or re-attached the handle: its rings and window lists no longer describe that horizon)
+  int emit_H = 0;
+  const int64_t* emit_cursor = nullptr;
   // deferred emission (mh_rollout_step_deferred): the last step's windows are not yet emitted
   bool pending = false;
   int parity = 0;                   // half of block_count / emit_list the next step writes
@@ -144,7 +151,7 @@ static void free_handle(mh_env_s* h) {
   for (hipEvent_t e : h->ev_pending) (void)hipEventDestroy(e);
   void* ptrs[] = {h->state, h->xstate, h->steps, h->tab, h->meta, h->ctr, h->ring, h->ring_len,
                   h->ring_pos, h->emit_rank, h->block_count, h->block_offset, h->emit_list, h->h_count,
-                  h->h_list, h->h_scan};
+                  h->h_list, h->h_scan, h->h_cpre};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete h;
@@ -279,8 +286,9 @@ int mh_nstep_reserve(mh_env_t h, int32_t ring_slots) {
   const int F = h->info.record_floats;
   // every buffer is allocated before anything is swapped: on failure the handle is unchanged
   float* ring = nullptr;
-  int32_t *cnt = nullptr, *lst = nullptr;
+  int32_t *cnt = nullptr, *lst = nullptr, *cpre = nullptr;
   int64_t* scan = nullptr;
+  const int64_t cells = (E + mh::FUSED_ENVS - 1) / mh::FUSED_ENVS;  // emission cells per lockstep
   hipError_t e = hipSuccess;
   if (new_ring) e = hipMalloc(&ring, sizeof(float) * E * ring_slots * F);
   if (e == hipSuccess) e = hipMalloc(&cnt, sizeof(int32_t) * hcap * ((E + 63) / 64));
@@ -290,9 +298,10 @@ int mh_nstep_reserve(mh_env_t h, int32_t ring_slots) {
   // horizons
   if (e == hipSuccess) e = hipMalloc(&scan, sizeof(int64_t) * (hcap + 2) + sizeof(int32_t) * (hcap + 2));
   if (e == hipSuccess) e = hipMemset(scan, 0, sizeof(int64_t) * (hcap + 2) + sizeof(int32_t) * (hcap + 2));
+  if (e == hipSuccess && cells > mh::FUSED_EMIT_SCAN_CELLS) e = hipMalloc(&cpre, sizeof(int32_t) * hcap * cells);
   if (e == hipSuccess && new_ring) e = hipMemset(ring, 0, sizeof(float) * E * ring_slots * F);
   if (e != hipSuccess) {
-    for (void* p : {(void*)ring, (void*)cnt, (void*)lst, (void*)scan})
+    for (void* p : {(void*)ring, (void*)cnt, (void*)lst, (void*)scan, (void*)cpre})
       if (p) (void)hipFree(p);
     (void)hipGetLastError();
     return fail(e == hipErrorOutOfMemory ? MH_ENOMEM : MH_EHIP, std::string("mh_nstep_reserve: ") + hipGetErrorString(e));
@@ -300,9 +309,11 @@ int mh_nstep_reserve(mh_env_t h, int32_t ring_slots) {
   (void)hipFree(h->h_count);
   (void)hipFree(h->h_list);
   (void)hipFree(h->h_scan);
+  (void)hipFree(h->h_cpre);
   h->h_count = cnt;
   h->h_list = lst;
   h->h_scan = scan;
+  h->h_cpre = cpre;
   h->hcap = hcap;
   if (new_ring) {  // every deque restarts empty over the new ring
     (void)hipFree(h->ring);
@@ -386,8 +397,11 @@ int mh_sample_horizon(mh_env_t h, const float* packed_policy, int32_t obs_dim, i
     ea.logp = store->logp;
     ea.capacity = store->capacity;
     ea.aux = h->h_scan;
+    ea.cell_pre = h->h_cpre;
   }
   MH_HIP(mh::launch_sample_fused(h->env_id, a, ea, (hipStream_t)stream));
+  h->emit_H = store ? horizon : 0;
+  h->emit_cursor = store ? store->cursor : nullptr;
   return MH_OK;
 }
 
@@ -399,6 +413,12 @@ int mh_sample_horizon_emit(mh_env_t h, int32_t horizon, const mh_window_store_t*
   if (!store || store->capacity <= 0 || !store->cursor || !store->obs || !store->act || !store->rew ||
       !store->cost || !store->obs2 || !store->done || !store->logp)
     return fail(MH_EINVAL, "mh_sample_horizon_emit: incomplete window store");
+  // the aux prefixes and window lists describe exactly the last horizon sampled into a store
+  if (h->emit_H == 0 || store->cursor != h->emit_cursor)
+    return fail(MH_ESTATE, "mh_sample_horizon_emit: no horizon was sampled into this store since the handle last "
+                           "stepped");
+  if (horizon != h->emit_H)
+    return fail(MH_EINVAL, "mh_sample_horizon_emit: horizon differs from the last sampled horizon");
   mh::HorizonEmitArgs ea;
   std::memset(&ea, 0, sizeof(ea));
   ea.E = h->E;
@@ -417,6 +437,7 @@ int mh_sample_horizon_emit(mh_env_t h, int32_t horizon, const mh_window_store_t*
   ea.logp = store->logp;
   ea.capacity = store->capacity;
   ea.aux = h->h_scan;
+  ea.cell_pre = h->h_cpre;
   MH_HIP(mh::launch_emit_horizon(h->env_id, ea, (hipStream_t)stream));
   if (windows_out)  // the horizon's window count (header word 0, formed by the fused kernel)
     MH_HIP(hipMemcpyAsync(windows_out, h->h_scan, sizeof(int64_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
@@ -428,6 +449,13 @@ int mh_sample_horizon_debug_logits(mh_env_t h, float* logits_out, float* obs_out
   if ((logits_out == nullptr) != (obs_out == nullptr)) return fail(MH_EINVAL, "mh_sample_horizon_debug_logits: both or neither");
   h->dbg_logits = logits_out;
   h->dbg_obs = obs_out;
+  return MH_OK;
+}
+
+int mh_sample_horizon_windows(mh_env_t h, int64_t* out, void* stream) {
+  if (!h || !out) return fail(MH_EINVAL, "mh_sample_horizon_windows: null handle / out");
+  if (!h->h_scan) return fail(MH_ESTATE, "mh_sample_horizon_windows: no horizon has been sampled");
+  MH_HIP(hipMemcpyAsync(out, h->h_scan, sizeof(int64_t), hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return MH_OK;
 }
 
@@ -660,6 +688,8 @@ static int rollout_impl(mh_env_t h, const float* logits, const float* act_in, co
 // Emission of the pending deferred step's windows (k_emit_fused on the half of the double
 // buffer that step wrote; the cursor snapshot in meta was written by its emitter waves).
 static int flush_pending(mh_env_t h, void* stream) {
+  h->emit_H = 0;  // every stepping / resetting entry point passes here: the last horizon is stale
+  h->emit_cursor = nullptr;
   if (!h->pending) return MH_OK;
   h->pending = false;
   const int pp = 1 - h->parity;  // half written by the pending step
@@ -706,6 +736,8 @@ int mh_rollout_step_deferred(mh_env_t h, const float* logits, const float* act_i
                              float* act_out, float* logp_out, void* stream) {
   if (!h) return fail(MH_EINVAL, "mh_rollout_step_deferred: null handle");
   if (!store) return fail(MH_EINVAL, "mh_rollout_step_deferred: null store (use mh_rollout_step)");
+  h->emit_H = 0;
+  h->emit_cursor = nullptr;
   // deferral needs the fused emission (E <= 1M envs) and at most `capacity` windows per step
   const bool ok = h->grid() <= mh::EMIT_FUSED_MAX_NB && h->E <= store->capacity;
   const bool same = h->pending && std::memcmp(&h->pstore, store, sizeof(*store)) == 0;

@@ -638,7 +638,6 @@ void k_policy_forward_x3(const float* __restrict__ P,
   const float* scal = P + pm_off_scal(K1);
   const PmScales scs = pm_scales(scal);
   const float isw1 = scs.isw[0], isw2 = scs.isw[1], isw3 = scs.isw[2], R1 = scs.R1, R2 = scs.R2;
-  const float one = 1.0f;
 
   // per lane: the 8 inputs k = 8 (lane >> 5) + j of env column lane & 31 (obs, then the
   // constant-1 bias input at k = D), scaled by 2^ex[0] and split; ex = the env's three exponents
@@ -692,10 +691,8 @@ void k_policy_forward_x3(const float* __restrict__ P,
   auto l1_split = [&](const f32x16& h, float rescale, f16x8* ph, f16x8* pl) {
     uint32_t hp[8], lp[8];
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {  // rescale (a power of two) commutes with the ReLU
-      const f32x2 y = f32x2{h[2 * p], h[2 * p + 1]} * f32x2{rescale, rescale};
-      split2h_pair(relu_raw(y.x), relu_raw(y.y), one, hp[p], lp[p]);
-    }
+    for (int p = 0; p < 8; ++p)  // rescale (a power of two) commutes with the ReLU
+      split2h_relu_scaled(h[2 * p], h[2 * p + 1], rescale, hp[p], lp[p]);
     ph[0] = __builtin_bit_cast(f16x8, uint4{hp[0], hp[1], hp[2], hp[3]});
     ph[1] = __builtin_bit_cast(f16x8, uint4{hp[4], hp[5], hp[6], hp[7]});
     pl[0] = __builtin_bit_cast(f16x8, uint4{lp[0], lp[1], lp[2], lp[3]});
@@ -738,17 +735,12 @@ void k_policy_forward_x3(const float* __restrict__ P,
   }
   for (; wg0 < ntiles; wg0 += per_round, t0 += per_round) {
     const bool more = wg0 + per_round < ntiles;
-    float k23[NT], sc3[NT];
+    float k23[NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      k23[t] = isw2 * pm_pow2(ex[t][2] - ex[t][1]);
-      sc3[t] = pm_pow2(ex[t][2]);
-    }
+    for (int t = 0; t < NT; ++t) k23[t] = isw2 * pm_pow2(ex[t][2] - ex[t][1]);
+    // layer 2 accumulates onto its bias b2 * sw2 * 2^ex1 (set in phase 0, once lds_b2 is visible);
+    // the H2 split is then relu(acc) * k23 (the fused sampler's expressions: the same bits)
     f32x16 acc[NT][PM_NB];
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int ob = 0; ob < PM_NB; ++ob) acc[t][ob] = f32x16{};
     // phase ib reads chunk ib from lds<ib & 1> and stages chunk ib + 1 into the other array
     auto phase = [&](auto bufc, int ib, bool fold) {
       constexpr int B = decltype(bufc)::value;
@@ -763,6 +755,20 @@ void k_policy_forward_x3(const float* __restrict__ P,
       __syncthreads();
       if (has_next) stage(nib, nxt_lds);
 #endif
+      if (ib == 0) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const float cb = pm_bias_unit(scs.sw[1], ex[t][1]);
+#pragma unroll
+          for (int ob = 0; ob < PM_NB; ++ob)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const f32x4 bq = __builtin_bit_cast(f32x4, lds_b2[(ob * 4 + q) * 64 + lane]);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) acc[t][ob][4 * q + j] = bq[j] * cb;
+            }
+        }
+      }
       // layer 1 of block ib + 1 is software-pipelined into this phase's MFMA stream (issued at
       // step 0, split at step 3, into a second operand set), so no wave idles on it at a barrier
       const bool pipe = !fold;
@@ -798,13 +804,9 @@ void k_policy_forward_x3(const float* __restrict__ P,
         }
 #endif
         uint4 w3f[4];
-        f32x4 b2f[4];
         if (fold && s == 1) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            w3f[q] = lds_w3[(ob * 4 + q) * 64 + lane];
-            b2f[q] = __builtin_bit_cast(f32x4, lds_b2[(ob * 4 + q) * 64 + lane]);
-          }
+          for (int q = 0; q < 4; ++q) w3f[q] = lds_w3[(ob * 4 + q) * 64 + lane];
         }
         const f16x8 wh = __builtin_bit_cast(f16x8, cur[0]);
         const f16x8 wl = __builtin_bit_cast(f16x8, cur[1]);
@@ -822,22 +824,9 @@ void k_policy_forward_x3(const float* __restrict__ P,
             // h2 * 2^e3 = relu(acc * (2^(e3 - e2) / sw2) + b2 * 2^e3): one packed fma per pair
             // (powers of two commute with the ReLU and with rounding)
             uint32_t hp[8], lp[8];
-            const f32x2 k2 = {k23[t], k23[t]}, s2 = {sc3[t], sc3[t]};
-#ifdef MH_X3_FOLDLITE
 #pragma unroll
-            for (int p = 0; p < 8; ++p) {
-              hp[p] = __float_as_uint(acc[t][ob][2 * p]);
-              lp[p] = __float_as_uint(acc[t][ob][2 * p + 1]);
-            }
-            if (k2.x == 12345.0f)
-#endif
-#pragma unroll
-            for (int p = 0; p < 8; ++p) {
-              const int r = 2 * p;
-              const f32x2 bs = f32x2{b2f[r >> 2][r & 3], b2f[r >> 2][(r & 3) + 1]} * s2;
-              const f32x2 y = __builtin_elementwise_fma(f32x2{acc[t][ob][r], acc[t][ob][r + 1]}, k2, bs);
-              split2h_pair(relu_raw(y.x), relu_raw(y.y), one, hp[p], lp[p]);
-            }
+            for (int p = 0; p < 8; ++p)
+              split2h_relu_scaled(acc[t][ob][2 * p], acc[t][ob][2 * p + 1], k23[t], hp[p], lp[p]);
             const f16x8 hh[2] = {__builtin_bit_cast(f16x8, uint4{hp[0], hp[1], hp[2], hp[3]}),
                                  __builtin_bit_cast(f16x8, uint4{hp[4], hp[5], hp[6], hp[7]})};
             const f16x8 hl[2] = {__builtin_bit_cast(f16x8, uint4{lp[0], lp[1], lp[2], lp[3]}),

@@ -110,5 +110,24 @@ __device__ __forceinline__ float relu_raw(float x) {
   asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(x));
   return r;
 }
+// The layer splits of the split-f16 MLP: hi = f16(relu(a k)), lo = f16(relu(a k) - hi) for a pair
+// (a, b), k a power of two (the layer's rescale; relu commutes with it). The products a k are
+// plain C++ (compiler-visible VALU): a and b are usually MFMA results, and an inline-asm reader of
+// an MFMA destination gets no hazard wait states from the compiler (the round-5 first cut fed them
+// straight to the asm max and read unfinished accumulators). Then split2h_pair's three-instruction
+// split with the fma_mix multiplier as the inline constant 1.0 (no register). 7 VALU per pair,
+// none of them packed-f32.
+__device__ __forceinline__ void split2h_relu_scaled(float a, float b, float k, uint32_t& hi, uint32_t& lo) {
+  const float ra = relu_raw(a * k), rb = relu_raw(b * k);
+  asm("v_cvt_pk_f16_f32 %0, %2, %3\n\t"
+      "v_fma_mixlo_f16 %1, %2, 1.0, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, 1.0, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(hi), "=&v"(lo)
+      : "v"(ra), "v"(rb));
+}
+// The layer-2 accumulator starts at the bias in the accumulator's units: b2 * sw2 * 2^ex1 (the
+// products are (W2 sw2)(H1 2^ex1)); cb = sw2 * 2^ex1 (a power of two: exact). The H2 split is then
+// split2h_relu_scaled(acc, k23), k23 = 2^(ex2 - ex1) / sw2.
+__device__ __forceinline__ float pm_bias_unit(float sw2, int ex1) { return sw2 * pm_pow2(ex1); }
 
 }  // namespace mh

@@ -48,6 +48,10 @@ constexpr int FUSED_ENVS = 256;   // envs per workgroup (one workgroup per CU)
 constexpr int FUSED_THREADS = 512;
 // (lockstep, 256-env block) cells of the horizon emission (one workgroup each)
 inline int64_t fused_emit_cells(int64_t E, int H) { return (int64_t)H * ((E + FUSED_ENVS - 1) / FUSED_ENVS); }
+// Above this many cells per lockstep (E > 262,144) a cell no longer sums the wave counts of every
+// earlier cell of its lockstep itself (O(cells^2) loads per lockstep): k_emit_prefix forms the
+// per-cell prefixes first (one workgroup per lockstep), into HorizonEmitArgs::cell_pre.
+constexpr int64_t FUSED_EMIT_SCAN_CELLS = 1024;
 
 struct HorizonEmitArgs {
   int64_t E;
@@ -58,6 +62,8 @@ struct HorizonEmitArgs {
   float *obs, *act, *rew, *cost, *obs2, *done, *logp;
   int64_t capacity;
   const int64_t* aux;  // FusedArgs::aux
+  int32_t* cell_pre;   // [H][cells] per-cell exclusive window prefixes within the lockstep (written by
+                       // k_emit_prefix when cells > FUSED_EMIT_SCAN_CELLS, else unused; may be null then)
 };
 
 

@@ -1,16 +1,16 @@
 // sample_fused.hip — the sampler's whole horizon (RL/trainer/sampler/base.py:118-222 run for
 // `sample_batch_size` lockstep steps) as ONE persistent kernel per sample(), for the default
-// StochaPolicy shape (256 x 256, D <= 15) and num_envs <= 256 x the CU count.
+// StochaPolicy shape (256 x 256, D <= 15).
 //
 // Why: the two-kernel lockstep (k_policy_forward_x3, MFMA-bound, then k_rollout, latency-bound
 // at one wave per SIMD) alternates two phases that each leave the other unit of every SIMD idle,
 // and every lockstep re-reads and re-writes the env state through the cache hierarchy. Here each
-// workgroup owns 256 envs for the whole horizon, one workgroup per CU, 8 waves:
-//   waves 0-3  policy waves: the split-f16 MLP (policy_x3.h, the same MFMA sequence as
-//              k_policy_forward_x3, so the same logits bit for bit), one 32-env tile per wave
-//              per pass, W2 streamed through LDS by LDS-DMA and shared by the four policy waves
-//              (they synchronise among themselves through an LDS counter, not s_barrier, so the
-//              env waves never wait on the policy's chunk handoffs);
+// workgroup owns 256 envs for the whole horizon, 8 waves:
+//   waves 0-3  policy waves: the split-f16 MLP (policy_x3.h, the same MFMA sequence on every
+//              accumulator as k_policy_forward_x3, so the same logits bit for bit), one 32-env
+//              tile per wave per pass, W2 streamed through LDS by LDS-DMA and shared by the four
+//              policy waves (they synchronise among themselves through an LDS counter, not
+//              s_barrier, so the env waves never wait on the policy's chunk handoffs);
 //   waves 4-7  env waves: one env per lane, the env's state (state, Rd_last, steps, Philox
 //              counter, deque length / position) kept in REGISTERS across the horizon; each
 //              lockstep samples the TanhGauss action, steps the env, autoresets and pushes the
@@ -22,8 +22,8 @@
 // with one workgroup barrier between phases; observations and logits pass through LDS only.
 // Windows: every full deque of lockstep t is recorded as (lane | oldest slot << 6) in a per-wave,
 // rank-ordered list; the rings hold n + H - 1 records (mh_nstep_reserve) so every window of the
-// horizon is still intact when k_emit_scan + k_emit_cells copy them, in the reference's order (lockstep
-// major, env index within a lockstep: base.py:178-213), into the replay store after the kernel.
+// horizon is still intact when k_emit_cells copies them, in the reference's order (lockstep major,
+// env index within a lockstep: base.py:178-213), into the replay store after the kernel.
 #include <type_traits>
 
 #include "policy_x3.h"
@@ -31,14 +31,10 @@
 #include "rollout.h"
 #include "sample_fused.h"
 
-#ifdef MH_FUSED_EXP_NO_MFMA  // experiment: the policy pass without its MFMAs (garbage logits)
+#ifdef MH_FUSED_EXP_NO_MFMA  // cost-attribution experiment: the policy pass without its MFMAs (garbage logits)
 #define MH_MFMA(a, b, c) (c)
 #else
 #define MH_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0)
-#endif
-
-#ifndef MH_FUSED_STATE_IN_REGS
-#define MH_FUSED_STATE_IN_REGS 1
 #endif
 
 namespace mh {
@@ -47,63 +43,16 @@ namespace mh {
 struct PolicyLds {
   uint4* c0;            // W2 chunk buffers (PM_X3_FRAGS * 64 records each)
   uint4* c1;
-  uint4* c2;            // the third buffer (kTriple: chunks staged two phases ahead)
-  const uint4* w3;      // fold operands [ob][s][split][lane]
+  uint32_t c0_lds;      // their LDS byte addresses (the chunk DMA's M0 values)
+  uint32_t c1_lds;
+  const uint4* w3;      // layer-3 operands [ob][s][split][lane]
   const float* b2;      // layer-2 bias, [256]
-  const float* b3;      // layer-3 bias, [N3] (LDS: the pass epilogue's 16 bias reads stay off the memory path)
   const uint4* w1;      // layer-1 fragments [blk][split][lane] (LDS: no memory loads inside a pass)
   const float* obs;     // [256][D] observations of the workgroup's envs
   float* lgt;           // [256][N3] logits out
-  uint32_t* bar;        // policy-wave barrier counter (default chunk staging)
+  uint32_t* bar;        // policy-wave barrier counter
   int64_t* err;         // device error word (bounded waits that timed out)
-  uint32_t* landed;     // loader path: chunk c of the horizon is in LDS once landed >= 2 (c + 1)
-  uint32_t* released;   // loader path: chunk c's buffer is free again once released >= 4 (c + 1)
 };
-
-// W2 chunk staging. Default: each policy wave issues its share of the pass's chunk DMAs itself
-// (LDS-DMA, two buffers, a policy-wave barrier per chunk).
-// MH_FUSED_LOADERS: the chunks are staged by LOADER waves instead: in each pass the env waves of
-// the half that is not stepping (they would otherwise wait at the pass's closing barrier) issue the
-// pass's chunk DMAs, wait for them to land and publish each chunk through an LDS counter; the
-// policy waves only wait for that counter and release each buffer after their last read of it, so
-// their instruction stream carries no LDS-DMA issue and no policy wave waits for the others. It
-// measured SLOWER on MI355X (QuadTracking, 65,536 envs, 20 lock-steps: 637-641 us per horizon vs
-// 585-595 us for the default; profiles/r04_fused_loader_ab.jsonl): the loader half's polling and
-// the extra LDS-counter round trips cost more than the policy waves' DMA issue slots.
-#ifdef MH_FUSED_LOADERS
-constexpr bool kLoaders = true;
-#else
-constexpr bool kLoaders = false;
-#endif
-
-// Three W2 chunk buffers (MH_FUSED_TRIPLE): chunk c of the horizon's chunk sequence (8 per pass)
-// lives in buffer c % 3 and its DMA is issued two phases ahead, so the hand-off at a phase's start
-// waits only for a DMA issued ~2 phases earlier (vmcnt(8): the next chunk's 8 DMAs may still be in
-// flight). The LDS for it comes from the compacted layer-3 fold operands (W3's N3 <= 8 real rows
-// instead of 32 padded ones: 8 KB instead of 32 KB).
-#ifdef MH_FUSED_TRIPLE
-#ifdef MH_FUSED_LOADERS
-#error "MH_FUSED_TRIPLE is the policy-wave staging path: build it without MH_FUSED_LOADERS"
-#endif
-constexpr bool kTriple = true;
-#else
-constexpr bool kTriple = false;
-#endif
-
-// bounded LDS-counter wait (the same bound and error word as pol_sync). SLEEP: the loader waves
-// poll with s_sleep between reads (they share each SIMD and the LDS with a policy wave, and wait
-// for a phase's worth of MFMAs); the policy waves poll back to back (their data is normally there)
-template <bool SLEEP = false>
-__device__ __forceinline__ void wait_count(uint32_t* ctr, uint32_t target, int64_t* err, uint32_t limit) {
-  uint32_t spins = 0;
-  while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
-    if (SLEEP) __builtin_amdgcn_s_sleep(2);
-    if (++spins >= limit) {
-      if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(err, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-  }
-}
 
 // 16-byte LDS-DMA (global_load_lds_dwordx4: this lane's 16 bytes at gsrc -> LDS lds_dst + 16 lane) as
 // inline asm, M0 written in the same statement (cdna_hip_programming.md's recipe). Not the builtin:
@@ -123,15 +72,56 @@ __device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
                : "memory");
 }
 
+// The same DMA with the global address as an SGPR base + a 32-bit VGPR offset (the saddr form):
+// the per-piece address arithmetic is scalar (the 64-bit VGPR form spent two v_lshl_add_u64 per
+// piece), M0 = the wave-uniform LDS byte address of the piece.
+__device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32_t lds_addr) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(lds_addr)
+               : "memory");
+}
+
 #ifdef MH_FUSED_EXP_STAMPS
 // diagnostic build only: lane 0 of policy wave w of workgroup b < 4 stores s_memtime at slot `slot`
-// of pass `pass` into the debug-logits buffer (reinterpreted as uint64 [4 wg][4 wave][64 pass][32])
+// of pass `pass` into the debug-logits buffer (reinterpreted as uint64 [4 wg][4 wave][64 pass][32]).
+// (Each stamp is a global store: the next vmcnt(0) — the hand-off's — waits for it, so the
+// "sync" segments read long; MH_FUSED_EXP_TACC has no such artefact.)
 #define MH_STAMP(a, pass, slot)                                                                      \
   do {                                                                                               \
     if (blockIdx.x < 4 && (threadIdx.x & 63) == 0 && (a).lgt_out) {                                  \
       const uint64_t t_ = __builtin_amdgcn_s_memtime();                                              \
       reinterpret_cast<uint64_t*>((a).lgt_out)[((blockIdx.x * 4 + (threadIdx.x >> 6)) * 64 + (pass)) * 32 + (slot)] = t_; \
     }                                                                                                \
+  } while (0)
+#elif defined(MH_FUSED_EXP_TACC)
+// diagnostic build only: s_memtime deltas summed per segment kind in registers (no memory traffic
+// inside the horizon), stored once at the end: [wg 4][policy wave 4][8] uint64 in the debug-logits
+// buffer. Kinds: 0 prologue, 1 hand-offs, 2 phases 0..6, 3 phase 7 layer 2 + splits, 4 layer 3,
+// 5 logits store + pass barrier, 6 between passes.
+struct TAcc {
+  uint64_t t[8];
+  uint64_t last;
+};
+__device__ __forceinline__ void tacc_add(TAcc& c, int kind) {
+  const uint64_t now = __builtin_amdgcn_s_memtime();
+  const uint64_t d = now - c.last;
+  c.last = now;
+  if (kind == 0) c.t[0] += d;
+  else if (kind == 1) c.t[1] += d;
+  else if (kind == 2) c.t[2] += d;
+  else if (kind == 3) c.t[3] += d;
+  else if (kind == 4) c.t[4] += d;
+  else if (kind == 5) c.t[5] += d;
+  else c.t[6] += d;
+}
+// slot -> the kind of the segment it closes (MH_STAMP's slots)
+#define MH_STAMP(a, pass, slot)                                                                      \
+  do {                                                                                               \
+    const int s_ = (slot);                                                                           \
+    tacc_add(g_tacc, s_ == 0 ? 6 : s_ == 1 ? 0 : s_ == 17 ? 3 : s_ == 19 ? 4 : s_ == 18 ? 5 :        \
+                         ((s_ & 1) == 0 ? 1 : 2));                                                    \
   } while (0)
 #else
 #define MH_STAMP(a, pass, slot) \
@@ -141,22 +131,16 @@ __device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
 
 // the four policy waves' barrier: own LDS-DMA landed (vmcnt(0)), arrive, wait for all four. The
 // wait is bounded (~1e9 cycles): a wave that gives up records it in *err (read by the tests
-// through mh_sample_horizon_errors) instead of hanging the device. (A split hand-off — "landed"
-// and "read" counters, the DMA wait and arrival late in the phase, the buffer-free wait before the
-// next DMA — measured 5 % slower on the fused kernel: 641-643 vs 606-617 us per horizon.)
-__device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_t* err, uint32_t limit,
-                                         bool keep_next = false) {
+// through mh_sample_horizon_errors) instead of hanging the device. Measured and rejected (DESIGN
+// §3.2): a split hand-off (separate "landed" / "buffer read" counters, 641-643 vs 606-617 us per
+// horizon), loader waves staging the chunks (637-641 vs 585-595 us), three chunk buffers with the
+// DMA two phases ahead (645-656 vs 621-625 us).
+__device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_t* err, uint32_t limit) {
 #ifdef MH_FUSED_EXP_NOSYNC  // cost-attribution experiment only (races: garbage logits)
   target += 4;
   return;
 #endif
-  // own DMAs of the chunk this phase reads landed: all of them (vmcnt(0)), or all but the next
-  // chunk's 8 (kTriple, vmcnt(8): memory operations complete in issue order for the counter)
-  static_assert(PM_X3_FRAGS / 4 == 8, "vmcnt(8) is one chunk's DMAs per policy wave");
-  if (keep_next)
-    __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8)
-  else
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's share of the chunk landed in LDS
   target += 4;
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   uint32_t spins = 0;
@@ -168,16 +152,65 @@ __device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_
   }
 }
 
+// Splits of two accumulator values into the next layer's (hi, lo) f16 operands (policy_x3.h
+// split2h_relu_scaled: no packed-f32 VALU — beside MFMAs a v_pk_mul_f32 / v_pk_fma_f32 costs ~22
+// cycles more than the two scalar instructions it replaces, MI355X_MICROARCH.md constants):
+//   layer 1: relu(h) * rs     (rs = 2^(ex1 - ex0) / sw1; b1 rides in the MFMA as a constant input)
+//   layer 2: relu(acc) * k23  (k23 = 2^(ex2 - ex1) / sw2; acc started at b2 * sw2 * 2^ex1)
+// k_policy_forward_x3 uses the same expressions: the same bits.
+
+// The layer-3 pair schedule of the last phase (all compile-time). H2 block fb (pairs 8 fb .. 8 fb +
+// 7, pair p = accumulator registers 2p, 2p + 1) is final after step 2 fb + 1 of the last phase; its
+// pairs are split from step 2 fb + 2 on (its MFMAs retired: no VALU waits on the matrix pipe),
+// at most FOLD_K2 per layer-2 step; the rest during the layer-3 MFMAs, at most FOLD_K3 per
+// layer-3 block but always every pair of the block the next layer-3 MFMA reads.
+constexpr int FOLD_K2 = 2;
+constexpr int FOLD_K3 = 6;
+constexpr int fold_done_l2(int st) {  // pairs split after layer-2 steps 0 .. st
+  int done = 0;
+  for (int t = 0; t <= st; ++t) {
+    const int ready = t >= 2 ? 8 * ((t - 2) / 2 + 1) : 0;
+    const int take = ready - done < FOLD_K2 ? ready - done : FOLD_K2;
+    done += take > 0 ? take : 0;
+  }
+  return done;
+}
+constexpr int fold_done_l3(int fb) {  // pairs split before layer-3 block fb's MFMAs (fb = -1: after layer 2)
+  int done = fold_done_l2(2 * PM_NB - 1);
+  for (int b = 0; b <= fb; ++b) {
+    int want = done + FOLD_K3;
+    if (want < 8 * (b + 1)) want = 8 * (b + 1);
+    if (want > 8 * PM_NB) want = 8 * PM_NB;
+    done = want;
+  }
+  return done;
+}
+
 // One pass: the 32-env tile `row0 .. row0 + 31` (workgroup-local rows) of policy wave pw through
-// all three layers; k_policy_forward_x3<1, 8>'s per-tile sequence with the observation rows and
-// the logits in LDS. `next`: stage chunk 0 of the following pass during the last phase.
-// LOAD: the W2 chunks are staged by loader waves (wait for `landed`, release each buffer); else
-// the four policy waves stage them themselves (pol_sync). D = 0: the observation width is Drt.
-// W3L: records per layer-3 fold fragment in LDS: 64 (one per lane) or 16 (compacted: the A
-// operand's rows l & 31 < 8 only, [half l >> 5][row]; the other lanes' rows are zero padding)
-template <int D, bool LOAD = kLoaders, int W3L = 64>
+// all three layers (k_policy_forward_x3<1, 8>'s per-tile MFMA sequence) with the observation rows
+// and the logits in LDS. `next`: stage chunk 0 of the following pass during the last phase.
+// D = 0: the observation width is Drt.
+//   phases 0 .. 6: layer 2's input block ib (chunk ib) into all eight H2 blocks; layer 1 of block
+//     ib + 1 pipelined into the phase (issued at step 0, split over steps 3 .. 10);
+//   phase 7: chunk 7 into the H2 blocks, each finished block split (bias, ReLU, rescale, f16 hi /
+//     lo) two steps later beside the remaining layer-2 MFMAs, then layer 3 as one MFMA run over
+//     the split blocks (k_policy_forward_x3's layer-3 order: block 0 .. 7, k-step 0, 1, products
+//     lo·hi, hi·lo, hi·hi) with the remaining splits beside it.
+// The chunk DMA for the next phase is issued one 1-KB piece per step (steps 0 .. 7) rather than all
+// at once: a piece's issue costs a policy wave 60-185 cycles, eight in a row idle the matrix pipe.
+#ifdef MH_FUSED_EXP_TACC
+#define MH_TACC_PARAM , TAcc& g_tacc
+#define MH_TACC_ARG , g_tacc
+#else
+#define MH_TACC_PARAM
+#define MH_TACC_ARG
+#endif
+// N3 = 2A <= 8 (compile-time: the logits rows are stored without per-row branches); b3r: the
+// layer-3 bias of the outputs this lane stores (rows 4 (lane >> 5) + 0..3), held in registers.
+template <int D, int N3>
 __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int row0, bool next, uint32_t& target,
-                            int pass_no = 0, int Drt = 0) {
+                            const float (&b3r)[4], int pass_no MH_TACC_PARAM, int Drt = 0) {
+  static_assert(N3 >= 1 && N3 <= 8, "the fused sampler's policy head has 2A <= 8 outputs");
   const int DD = D > 0 ? D : Drt;
   MH_STAMP(a, pass_no, 0);
   (void)pass_no;
@@ -186,22 +219,22 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
 #endif
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
   constexpr int FPW = PM_X3_FRAGS / 4;  // W2 fragments each policy wave stages per chunk
+  static_assert(FPW <= 2 * PM_NB, "one DMA piece per step");
   const int lane = threadIdx.x & 63;
-  const int K1 = a.K1, N3 = a.N3;
+  const int K1 = a.K1;
   const float* P = a.P;
   const uint4* W2g = reinterpret_cast<const uint4*>(P + pm_off_w2x3(K1));
   const PmScales scs = pm_scales(P + pm_off_scal(K1));
   const float isw1 = scs.isw[0], isw2 = scs.isw[1], isw3 = scs.isw[2], R1 = scs.R1, R2 = scs.R2;
-  const float one = 1.0f;
 
-  auto stage = [&](int ib, uint4* dstbuf) {
+  // piece i (1 KB) of this wave's share of chunk ib into the chunk buffer at LDS address dst
+  const uint32_t voff = (uint32_t)lane * 16u;
+  auto stage_piece = [&](int ib, uint32_t dst, int i) {
 #ifdef MH_FUSED_EXP_NODMA  // cost-attribution experiment only (stale chunks)
     if (a.H > 0) return;
 #endif
-    const uint4* src = W2g + ((int64_t)ib * PM_X3_FRAGS + pw * FPW) * 64;
-    asm volatile("" : "+s"(src));
-#pragma unroll
-    for (int i = 0; i < FPW; ++i) glds16(src + i * 64 + lane, &dstbuf[(pw * FPW + i) * 64]);
+    const uint4* src = W2g + ((int64_t)ib * PM_X3_FRAGS + pw * FPW + i) * 64;
+    glds16s(src, voff, dst + (uint32_t)(pw * FPW + i) * 1024u);
   };
   auto l1_mfma = [&](const uint4* wf, const f16x8& xh, const f16x8& xl) {
     const f16x8 wh = __builtin_bit_cast(f16x8, wf[0]), wl = __builtin_bit_cast(f16x8, wf[1]);
@@ -211,17 +244,8 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
     h = MH_MFMA(wh, xh, h);
     return h;
   };
-  auto l1_split = [&](const f32x16& h, float rescale, f16x8* ph, f16x8* pl) {
-    uint32_t hp[8], lp[8];
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const f32x2 y = f32x2{h[2 * p], h[2 * p + 1]} * f32x2{rescale, rescale};
-      split2h_pair(relu_raw(y.x), relu_raw(y.y), one, hp[p], lp[p]);
-    }
-    ph[0] = __builtin_bit_cast(f16x8, uint4{hp[0], hp[1], hp[2], hp[3]});
-    ph[1] = __builtin_bit_cast(f16x8, uint4{hp[4], hp[5], hp[6], hp[7]});
-    pl[0] = __builtin_bit_cast(f16x8, uint4{lp[0], lp[1], lp[2], lp[3]});
-    pl[1] = __builtin_bit_cast(f16x8, uint4{lp[4], lp[5], lp[6], lp[7]});
+  auto pack8 = [](const uint32_t* p) {
+    return __builtin_bit_cast(f16x8, uint4{p[0], p[1], p[2], p[3]});
   };
 
   // observations of env column lane & 31 (inputs k = 8 (lane >> 5) + j; the constant-1 bias input
@@ -252,101 +276,64 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
       xol[j] = lo;
     }
   }
+  const float rs1 = pm_pow2(ex[1] - ex[0]) * isw1;
   f16x8 xh[2], xl[2];
   uint4 w1c[2];
+  f32x16 hn;  // layer 1 of the next block, issued ahead of the hand-off that precedes its split
   {
     const uint4 w10[2] = {L.w1[lane], L.w1[64 + lane]};
     w1c[0] = L.w1[(1 * 2 + 0) * 64 + lane];
     w1c[1] = L.w1[(1 * 2 + 1) * 64 + lane];
-    l1_split(l1_mfma(w10, xoh, xol), pm_pow2(ex[1] - ex[0]) * isw1, xh, xl);
-  }
-  const float k23 = isw2 * pm_pow2(ex[2] - ex[1]), sc3 = pm_pow2(ex[2]);
-  f32x16 acc[PM_NB];
+    const f32x16 h = l1_mfma(w10, xoh, xol);
+    hn = l1_mfma(w1c, xoh, xol);  // block 1 (split during phase 0)
+    uint32_t hp[8], lp[8];
 #pragma unroll
-  for (int ob = 0; ob < PM_NB; ++ob) acc[ob] = f32x16{};
+    for (int p = 0; p < 8; ++p) split2h_relu_scaled(h[2 * p], h[2 * p + 1], rs1, hp[p], lp[p]);
+    xh[0] = pack8(hp);
+    xh[1] = pack8(hp + 4);
+    xl[0] = pack8(lp);
+    xl[1] = pack8(lp + 4);
+  }
+  const float k23 = isw2 * pm_pow2(ex[2] - ex[1]);
+  const float cb = pm_bias_unit(scs.sw[1], ex[1]);
+  f32x16 acc[PM_NB];
+  f32x4 b2n[4];  // the next block's layer-2 bias (phase 0: the accumulators start at b2 * cb)
+  auto load_b2 = [&](int ob) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) b2n[q] = *reinterpret_cast<const f32x4*>(L.b2 + ob * 32 + 8 * q + 4 * (lane >> 5));
+  };
 
-  auto phase = [&](auto bufc, int ib, bool fold) {
-    constexpr int B = decltype(bufc)::value;
-    uint4* cur_lds = B ? L.c1 : L.c0;
-    uint4* nxt_lds = B ? L.c0 : L.c1;
-    bool has_next = ib < PM_NB - 1 || next;
-    int nib = (ib + 1) & (PM_NB - 1);
-    bool keep_next = false;
-    if constexpr (kTriple) {
-      // chunk c = 8 pass + ib in buffer c % 3; this phase stages chunk c + 2 (W2 block ib + 2)
-      // (selects, not an indexed array: the pointers must stay provably LDS, or the ring reads
-      // become flat loads that wait for the DMAs in flight)
-      const int c = PM_NB * pass_no + ib, m = c % 3, mn = (c + 2) % 3;
-      cur_lds = m == 0 ? L.c0 : (m == 1 ? L.c1 : L.c2);
-      nxt_lds = mn == 0 ? L.c0 : (mn == 1 ? L.c1 : L.c2);
-      keep_next = ib + 1 < PM_NB || next;  // chunk c + 1's DMAs (issued last phase) may be in flight
-      has_next = ib + 2 < PM_NB || next;
-      nib = (ib + 2) & (PM_NB - 1);
-    }
-    MH_STAMP(a, pass_no, 1 + 2 * ib);
-    if constexpr (LOAD) {
-      // chunk c = 8 pass + ib of the horizon: staged and published by the pass's loader waves
-      wait_count(L.landed, 2u * (uint32_t)(PM_NB * pass_no + ib + 1), L.err, a.spin_limit);
+  // the three split products of one layer-2 step into H2 block ob (k-step s of the phase's block);
+  // `first`: the block's first step (phase 0, s = 0) accumulates onto its bias b2 * cb (registers
+  // 4q .. 4q + 3 of block ob hold hidden units ob*32 + 8q + 4 (lane >> 5) + 0..3)
+  auto l2_step = [&](int ob, int s, const uint4* cur, bool first) {
+    const f16x8 wh = __builtin_bit_cast(f16x8, cur[0]);
+    const f16x8 wl = __builtin_bit_cast(f16x8, cur[1]);
+    f32x16 acc_ob;
+    if (first) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc_ob[r] = b2n[r >> 2][r & 3] * cb;
     } else {
-      // chunk ib landed in every policy wave's share
-      pol_sync(L.bar, target, L.err, a.spin_limit, keep_next);
+      acc_ob = acc[ob];
     }
+    acc_ob = MH_MFMA(wl, xh[s], acc_ob);
+    acc_ob = MH_MFMA(wh, xl[s], acc_ob);
+    acc_ob = MH_MFMA(wh, xh[s], acc_ob);
+    acc[ob] = acc_ob;
+  };
+
+  // ---- phases 0 .. PM_NB - 2: input block ib; chunk ib + 1 staged, layer 1 of block ib + 1
+  auto phase = [&](auto bufc, auto firstc, int ib) {
+    constexpr int B = decltype(bufc)::value;
+    constexpr bool FIRST = decltype(firstc)::value;  // phase 0: the accumulators start at zero
+    uint4* cur_lds = B ? L.c1 : L.c0;
+    const uint32_t nxt_lds = B ? L.c0_lds : L.c1_lds;
+    MH_STAMP(a, pass_no, 1 + 2 * ib);
+    pol_sync(L.bar, target, L.err, a.spin_limit);  // chunk ib landed in every policy wave's share
     MH_STAMP(a, pass_no, 2 + 2 * ib);
-    const bool pipe = !fold;
-    f32x16 hn;
+    if constexpr (FIRST) load_b2(0);
     uint32_t l1hp[8], l1lp[8];  // the next block's layer-1 split, pair by pair
     const uint4* Lc = cur_lds + lane;
-    uint4 w3f[4];
-    f32x4 b2f[4];
-    // H2 block fb final: bias, ReLU, rescale, split, layer 3, one half (ks: registers 8 ks ..
-    // 8 ks + 7, hidden units 16 ks + ... of the block) per call. Blocks and halves are folded in
-    // the order (fb, ks) = (0, 0), (0, 1), (1, 0), ...: k_policy_forward_x3's layer-3 order
-    // (block 0: both halves split before its registers become the layer-3 accumulator acc[0])
-    auto split_half = [&](int fb, int ks, f16x8& hh, f16x8& hl) {
-      uint32_t hp[4], lp[4];
-      const f32x2 k2 = {k23, k23}, s2 = {sc3, sc3};
-#pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        const int r = 8 * ks + 2 * p;
-        const f32x2 bs = f32x2{b2f[r >> 2][r & 3], b2f[r >> 2][(r & 3) + 1]} * s2;
-        const f32x2 y = __builtin_elementwise_fma(f32x2{acc[fb][r], acc[fb][r + 1]}, k2, bs);
-        split2h_pair(relu_raw(y.x), relu_raw(y.y), one, hp[p], lp[p]);
-      }
-      hh = __builtin_bit_cast(f16x8, uint4{hp[0], hp[1], hp[2], hp[3]});
-      hl = __builtin_bit_cast(f16x8, uint4{lp[0], lp[1], lp[2], lp[3]});
-    };
-    auto fold_mfma = [&](f32x16 o, int ks, const f16x8& hh, const f16x8& hl) {
-      const f16x8 vh = __builtin_bit_cast(f16x8, w3f[2 * ks]);
-      const f16x8 vl = __builtin_bit_cast(f16x8, w3f[2 * ks + 1]);
-      o = MH_MFMA(vl, hh, o);
-      o = MH_MFMA(vh, hl, o);
-      o = MH_MFMA(vh, hh, o);
-      return o;
-    };
-    auto fold_half = [&](int fb, int ks) {
-      if (fb == 0) {
-        if (ks == 1) return;  // block 0 whole at its first fold step
-        f16x8 h0, l0, h1, l1;
-        split_half(0, 0, h0, l0);
-        split_half(0, 1, h1, l1);
-        acc[0] = fold_mfma(fold_mfma(f32x16{}, 0, h0, l0), 1, h1, l1);
-        return;
-      }
-      f16x8 hh, hl;
-      split_half(fb, ks, hh, hl);
-      acc[0] = fold_mfma(acc[0], ks, hh, hl);
-    };
-    // this step's three block MFMAs interleaved with the fold half's split VALU (one wave per SIMD:
-    // VALU between MFMAs overlaps them; the compiler otherwise issues the MFMAs first, then ~40
-    // dependent VALU with the matrix pipe idle), then the fold half's three MFMAs
-    auto fold_sched = [&]() {
-#pragma unroll
-      for (int g = 0; g < 3; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);  // VALU
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
-    };
     uint4 ring[3][2];
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
@@ -360,99 +347,145 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
 #pragma unroll
         for (int p = 0; p < 2; ++p) ring[(st + 2) % 3][p] = Lc[((st + 2) * 2 + p) * 64];
       }
-      const uint4* cur = ring[st % 3];
-      if (pipe && st == 0) hn = l1_mfma(w1c, xoh, xol);
       // the next chunk's DMA into the other buffer (every policy wave finished reading it in the
-      // previous phase: the pol_sync above), issued after this phase's first W1 use
-      if constexpr (!LOAD) {
-        if (st == 0 && has_next) stage(nib, nxt_lds);
-      }
-      if (pipe && st == 0) {
-        if (ib + 2 < PM_NB) {
-          w1c[0] = L.w1[((ib + 2) * 2 + 0) * 64 + lane];
-          w1c[1] = L.w1[((ib + 2) * 2 + 1) * 64 + lane];
-        }
-      }
-      // the next block's layer-1 split, one register pair per step over steps 3..10 (the
-      // split's VALU between this phase's MFMAs instead of ~60 VALU in one step: one wave per SIMD)
-      if (pipe && st >= 3 && st < 11) {
-        const int p = st - 3;
-        const float rs = pm_pow2(ex[1] - ex[0]) * isw1;
-        const f32x2 y = f32x2{hn[2 * p], hn[2 * p + 1]} * f32x2{rs, rs};
-        split2h_pair(relu_raw(y.x), relu_raw(y.y), one, l1hp[p], l1lp[p]);
-      }
-      const f16x8 wh = __builtin_bit_cast(f16x8, cur[0]);
-      const f16x8 wl = __builtin_bit_cast(f16x8, cur[1]);
-      {
-        f32x16 acc_ob = acc[ob];
-        acc_ob = MH_MFMA(wl, xh[s], acc_ob);
-        acc_ob = MH_MFMA(wh, xl[s], acc_ob);
-        acc_ob = MH_MFMA(wh, xh[s], acc_ob);
-        acc[ob] = acc_ob;
-      }
-      // H2 block ob - 1 (final since the previous step) folded into layer 3 during block ob's two
-      // steps, one half per step: its split waits on MFMAs issued a step earlier and overlaps
-      // this step's block-ob MFMAs
-      if (fold && ob > 0) {
-        fold_half(ob - 1, s);
-        fold_sched();
-      }
-      if (fold && s == 1) {  // block ob's layer-3 operands (block ob - 1's last use was just above)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if constexpr (W3L == 64) {
-            w3f[q] = L.w3[(ob * 4 + q) * 64 + lane];
-          } else {
-            w3f[q] = (lane & 31) < 8 ? L.w3[(ob * 4 + q) * 16 + (lane >> 5) * 8 + (lane & 31)] : uint4{0u, 0u, 0u, 0u};
-          }
-          // registers 4q .. 4q + 3 of block ob hold hidden units ob*32 + 8q + 4 (lane >> 5) + 0..3
-          b2f[q] = *reinterpret_cast<const f32x4*>(L.b2 + ob * 32 + 8 * q + 4 * (lane >> 5));
-        }
-      }
-#ifdef MH_FUSED_EXP_FOLD_NOSB  // experiment: the compiler may interleave the fold phase's steps
-      if (!fold) __builtin_amdgcn_sched_barrier(0);
+      // previous phase: the pol_sync above), one piece per step
+#ifdef MH_FUSED_EXP_DMA_BURST  // experiment: the whole share at step 0 (the round-4 placement)
+      if (st == 0)
+        for (int i = 0; i < FPW; ++i) stage_piece(ib + 1, nxt_lds, i);
 #else
-      __builtin_amdgcn_sched_barrier(0);
+      if (st < FPW) stage_piece(ib + 1, nxt_lds, st);
 #endif
+      if (st == 0 && ib + 2 < PM_NB) {
+        w1c[0] = L.w1[((ib + 2) * 2 + 0) * 64 + lane];
+        w1c[1] = L.w1[((ib + 2) * 2 + 1) * 64 + lane];
+      }
+      // the next block's layer-1 split, one register pair per step over steps 3..10 (its VALU
+      // between this phase's MFMAs)
+      if (st >= 3 && st < 11) {
+        const int p = st - 3;
+        split2h_relu_scaled(hn[2 * p], hn[2 * p + 1], rs1, l1hp[p], l1lp[p]);
+      }
+      l2_step(ob, s, ring[st % 3], FIRST && s == 0);
+      if (FIRST && s == 0 && ob + 1 < PM_NB) load_b2(ob + 1);  // the next block's bias, a step ahead
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // VALU
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
-    if constexpr (LOAD) {
-      // every fragment of this chunk is in registers (step 15's MFMAs consumed the last reads): the
-      // buffer may be overwritten by the loaders
-      if (lane == 0) __hip_atomic_fetch_add(L.released, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    if (fold) {
-      fold_half(PM_NB - 1, 0);
-      fold_half(PM_NB - 1, 1);
-    }
-    if (pipe) {  // (l1_split's packing of the pairs)
-      xh[0] = __builtin_bit_cast(f16x8, uint4{l1hp[0], l1hp[1], l1hp[2], l1hp[3]});
-      xh[1] = __builtin_bit_cast(f16x8, uint4{l1hp[4], l1hp[5], l1hp[6], l1hp[7]});
-      xl[0] = __builtin_bit_cast(f16x8, uint4{l1lp[0], l1lp[1], l1lp[2], l1lp[3]});
-      xl[1] = __builtin_bit_cast(f16x8, uint4{l1lp[4], l1lp[5], l1lp[6], l1lp[7]});
-    }
+    xh[0] = pack8(l1hp);
+    xh[1] = pack8(l1hp + 4);
+    xl[0] = pack8(l1lp);
+    xl[1] = pack8(l1lp + 4);
+    // layer 1 of block ib + 2 before the next hand-off: its MFMAs keep the matrix pipe busy while
+    // the wave waits there (its split runs in the next phase)
+    if (ib + 2 < PM_NB) hn = l1_mfma(w1c, xoh, xol);
   };
   using B0 = std::integral_constant<int, 0>;
   using B1 = std::integral_constant<int, 1>;
+  using F0 = std::integral_constant<bool, false>;
+  using F1 = std::integral_constant<bool, true>;
+  phase(B0{}, F1{}, 0);
+  phase(B1{}, F0{}, 1);
 #pragma unroll 1
-  for (int ib = 0; ib < PM_NB - 2; ib += 2) {
-    phase(B0{}, ib, false);
-    phase(B1{}, ib + 1, false);
+  for (int ib = 2; ib < PM_NB - 2; ib += 2) {
+    phase(B0{}, F0{}, ib);
+    phase(B1{}, F0{}, ib + 1);
   }
-  phase(B0{}, PM_NB - 2, false);
-#ifdef MH_FUSED_EXP_NOFOLD  // cost-attribution experiment: no layer 3 (garbage logits)
-  phase(B1{}, PM_NB - 1, false);
-#else
-  phase(B1{}, PM_NB - 1, true);
-#endif
+  phase(B0{}, F0{}, PM_NB - 2);
+
+  // ---- phase PM_NB - 1 (chunk 7, buffer 1): the last layer-2 input block, the H2 splits, layer 3
+  f32x16 o3 = {};
+  {
+    constexpr int ib = PM_NB - 1;
+    (void)ib;
+    MH_STAMP(a, pass_no, 1 + 2 * ib);
+    pol_sync(L.bar, target, L.err, a.spin_limit);
+    MH_STAMP(a, pass_no, 2 + 2 * ib);
+    const uint4* Lc = L.c1 + lane;
+    uint4 ring[3][2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      ring[0][p] = Lc[p * 64];
+      ring[1][p] = Lc[(2 + p) * 64];
+    }
+    uint32_t hs[PM_NB][8], ls[PM_NB][8];  // split H2 blocks: pair p of block fb -> (hs, ls)[fb][p]
+    // pair q = 8 fb + p: registers 2p, 2p + 1 of block fb (the bias is already in the accumulator)
+    auto split_pair = [&](int q) {
+      const int fb = q >> 3, p = q & 7, r = 2 * p;
+      split2h_relu_scaled(acc[fb][r], acc[fb][r + 1], k23, hs[fb][p], ls[fb][p]);
+    };
+    // (pairs split in layer-2 step st: [fold_done_l2(st - 1), fold_done_l2(st)))
+#pragma unroll
+    for (int st = 0; st < 2 * PM_NB; ++st) {
+      const int ob = st >> 1, s = st & 1;
+      const int q0 = st == 0 ? 0 : fold_done_l2(st - 1), q1 = fold_done_l2(st);
+      if (st + 2 < 2 * PM_NB) {
+#pragma unroll
+        for (int p = 0; p < 2; ++p) ring[(st + 2) % 3][p] = Lc[((st + 2) * 2 + p) * 64];
+      }
+      if (next && st < FPW) stage_piece(0, L.c0_lds, st);  // chunk 0 of the next pass
+      l2_step(ob, s, ring[st % 3], false);
+#pragma unroll
+      for (int q = q0; q < q1; ++q) split_pair(q);
+      // the split VALU between the step's three MFMAs, not bunched after them
+#pragma unroll
+      for (int g = 0; g < 3; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 2 * FOLD_K2, 0);  // VALU (6 per pair)
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    MH_STAMP(a, pass_no, 17);
+    // layer 3: o3 = W3 H2 over the split blocks, k_policy_forward_x3's order; the layer-3 operands
+    // read one block ahead, the remaining splits (and their biases, one block ahead) beside the MFMAs
+    uint4 w3f[2][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) w3f[0][q] = L.w3[q * 64 + lane];
+#pragma unroll
+    for (int fb = 0; fb < PM_NB; ++fb) {
+      const int q0 = fold_done_l3(fb - 1), q1 = fold_done_l3(fb);
+      if (fb + 1 < PM_NB) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w3f[(fb + 1) & 1][q] = L.w3[((fb + 1) * 4 + q) * 64 + lane];
+      }
+#pragma unroll
+      for (int q = q0; q < q1; ++q) split_pair(q);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const f16x8 vh = __builtin_bit_cast(f16x8, w3f[fb & 1][2 * ks]);
+        const f16x8 vl = __builtin_bit_cast(f16x8, w3f[fb & 1][2 * ks + 1]);
+        const f16x8 hh = pack8(&hs[fb][4 * ks]), hl = pack8(&ls[fb][4 * ks]);
+        o3 = MH_MFMA(vl, hh, o3);
+        o3 = MH_MFMA(vh, hl, o3);
+        o3 = MH_MFMA(vh, hh, o3);
+      }
+#pragma unroll
+      for (int g = 0; g < 6; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                       // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, FOLD_K3, 0);  // VALU (6 per pair)
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
   // logits rows (registers r hold output pm_row(r, lane) of env column lane & 31), the same
   // expression as k_policy_forward_x3's store
-  MH_STAMP(a, pass_no, 17);
+  MH_STAMP(a, pass_no, 19);
+  // (registers r >= 4 hold outputs >= 8 >= N3: padding). One 16-byte (N3 = 8, 4) or 4-byte (N3 = 2)
+  // stores per lane instead of 16 branches, each waiting on its own bias read.
   const float iu = isw3 * pm_pow2(-ex[2]);
   const int row = row0 + (lane & 31);
+  const int o0 = 4 * (lane >> 5);
+  float v[4];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int oo = pm_row(r, lane);
-    if (oo < N3) L.lgt[row * N3 + oo] = acc[0][r] * iu + L.b3[oo];
+  for (int r = 0; r < 4; ++r) v[r] = o3[r] * iu + b3r[r];
+  if constexpr (N3 % 4 == 0) {
+    if (o0 < N3) *reinterpret_cast<float4*>(L.lgt + row * N3 + o0) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (o0 + r < N3) L.lgt[row * N3 + o0 + r] = v[r];
   }
 }
 
@@ -463,10 +496,6 @@ struct EnvLane {  // one env's persistent state, held in registers across the ho
   double xs[Env::XS > 0 ? Env::XS : 1];
   int k, len, pos;
   uint32_t ctr;
-#ifdef MH_FUSED_EXP_CHECK_OBS  // experiment: the observation this lane wrote to LDS, kept
-  float keep[Env::D];
-  int have;
-#endif
 };
 
 // One lockstep of one env (lane) — k_rollout<Env, true>'s arithmetic: TanhGauss sample from the
@@ -488,14 +517,6 @@ __device__ __forceinline__ void env_lockstep(const FusedArgs& a, EnvLane<Env>& v
     float lgt[2 * A];
 #pragma unroll
     for (int i = 0; i < 2 * A; ++i) lgt[i] = lg_row[i];
-#ifdef MH_FUSED_EXP_CHECK_OBS
-    if (v.have) {
-      bool bad = false;
-#pragma unroll
-      for (int i = 0; i < D; ++i) bad = bad || (__float_as_uint(obs_row[i]) != __float_as_uint(v.keep[i]));
-      if (bad) __hip_atomic_fetch_add(a.err + 0, (int64_t)(1 << 20), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#endif
 #ifdef MH_FUSED_EXP_STAMPS
     if (false) {
 #else
@@ -507,13 +528,8 @@ __device__ __forceinline__ void env_lockstep(const FusedArgs& a, EnvLane<Env>& v
       for (int i = 0; i < D; ++i) a.obs_out[((int64_t)t * a.E + e) * D + i] = obs_row[i];
     }
     // the record's pre-step observation goes to the stage now: not held across the env step
-#ifdef MH_FUSED_DIRECT_RING
-#pragma unroll
-    for (int i = 0; i < D; ++i) rec[i] = obs_row[i];
-#else
 #pragma unroll
     for (int i = 0; i < D; ++i) srec[i] = obs_row[i];
-#endif
     const float noise = a.act_noise ? a.act_noise[t] : 0.0f;
     double rowv[Env::ROWN > 0 ? Env::ROWN : 1];
     if constexpr (Env::ROWN > 0) {
@@ -555,13 +571,11 @@ __device__ __forceinline__ void env_lockstep(const FusedArgs& a, EnvLane<Env>& v
       }
       logp = (lg - lt) - a.log_half_sum;
     }
-#ifndef MH_FUSED_EXP_NO_TRACE
     if (a.act_out) {
 #pragma unroll
       for (int i = 0; i < A; ++i) a.act_out[((int64_t)t * a.E + e) * A + i] = u[i];
     }
     if (a.logp_out) a.logp_out[(int64_t)t * a.E + e] = logp;
-#endif
     float obs2[D], r;
     if constexpr (Env::ROWN > 0)
       Env::step_row(v.s, v.xs, rowv, u, obs2, &r);
@@ -592,11 +606,6 @@ __device__ __forceinline__ void env_lockstep(const FusedArgs& a, EnvLane<Env>& v
     v.ctr = v.ctr + 1u;
 #pragma unroll
     for (int i = 0; i < D; ++i) obs_row[i] = obsn[i];
-#ifdef MH_FUSED_EXP_CHECK_OBS
-#pragma unroll
-    for (int i = 0; i < D; ++i) v.keep[i] = obsn[i];
-    v.have = 1;
-#endif
 #pragma unroll
     for (int i = 0; i < A; ++i) rec[D + i] = u[i];
 #pragma unroll
@@ -615,14 +624,6 @@ __device__ __forceinline__ void env_lockstep(const FusedArgs& a, EnvLane<Env>& v
     emit_pos = v.pos - n < 0 ? v.pos - n + R : v.pos - n;
     if (done) v.len = 0;
   }
-#ifdef MH_FUSED_DIRECT_RING  // experiment: each lane stores its own record (no LDS transposition)
-  if (live) {
-    float4* dst = reinterpret_cast<float4*>(a.ring + (e * a.R + wpos) * (int64_t)F);
-#pragma unroll
-    for (int i = 0; i < F / 4; ++i) dst[i] = make_float4(rec[4 * i], rec[4 * i + 1], rec[4 * i + 2], rec[4 * i + 3]);
-  }
-  return;
-#endif
   // ring record: transposed through this wave's LDS staging so each store instruction writes
   // whole records (k_rollout's ring store); its first D floats (obs0) are already there
 #pragma unroll
@@ -653,30 +654,6 @@ __device__ __forceinline__ void env_lockstep(const FusedArgs& a, EnvLane<Env>& v
 }
 
 // ------------------------------------------------------------------ loader waves
-#ifdef MH_FUSED_LOADERS
-// Loader wave l (0, 1) of pass p: stages chunks 8 p + 1 .. 8 p + 7 of the horizon and chunk 0 of
-// the next pass (chunk 8 p + 8), each into buffer c & 1 once the policy waves released the chunk
-// two before it, its half of the 32 pieces, then publishes it. Returns after the last chunk
-// landed, so nothing is in flight across the pass's closing barrier.
-__device__ void load_pass(const FusedArgs& a, const PolicyLds& L, int p, int npass, int l) {
-  constexpr int HALF = PM_X3_FRAGS / 2;  // pieces (1 KB each) per loader wave per chunk
-  const int lane = threadIdx.x & 63;
-  const uint4* W2g = reinterpret_cast<const uint4*>(a.P + pm_off_w2x3(a.K1));
-  const int last = p + 1 < npass ? PM_NB : PM_NB - 1;
-  for (int i = 1; i <= last; ++i) {
-    const uint32_t c = (uint32_t)(PM_NB * p + i);
-    wait_count<true>(L.released, c >= 2 ? 4u * (c - 1) : 0u, L.err, a.spin_limit);  // chunk c - 2's buffer free
-    const int ib = i & (PM_NB - 1);
-    uint4* dst = (c & 1) ? L.c1 : L.c0;
-    const uint4* src = W2g + ((int64_t)ib * PM_X3_FRAGS + l * HALF) * 64;
-    asm volatile("" : "+s"(src));
-#pragma unroll
-    for (int f = 0; f < HALF; ++f) glds16(src + f * 64 + lane, &dst[(l * HALF + f) * 64]);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's pieces are in LDS
-    if (lane == 0) __hip_atomic_fetch_add(L.landed, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-}
-#endif
 
 // ------------------------------------------------------------------ the kernel
 template <class Env>
@@ -685,38 +662,21 @@ void k_sample_fused(FusedArgs a) {
   constexpr int D = Env::D, A = Env::A, S = Env::S, XS = Env::XS;
   constexpr int N3C = 2 * A;
   constexpr int F = rec_floats(D, A), CP = F / 4 + 1;
-  // the layer-3 fold operands compacted to W3's real rows when N3 <= 8 (kTriple's third buffer)
-  constexpr int W3L = (kTriple && N3C <= 8) ? 16 : 64;
-  static_assert(!kTriple || W3L == 16, "the third chunk buffer needs the compacted fold operands");
   __shared__ uint4 lds0[PM_X3_FRAGS * 64];
   __shared__ uint4 lds1[PM_X3_FRAGS * 64];
-  __shared__ uint4 lds2[kTriple ? PM_X3_FRAGS * 64 : 1];
-  __shared__ uint4 lds_w3[PM_NB * 4 * W3L];
+  __shared__ uint4 lds_w3[PM_NB * 4 * 64];
   __shared__ float lds_b2[PM_H];
-  __shared__ float lds_b3[32];
   __shared__ uint4 lds_w1[PM_NB * 2 * 64];
   __shared__ float s_obs[FUSED_ENVS * D];
   __shared__ float s_lgt[FUSED_ENVS * N3C];
-#ifdef MH_FUSED_DIRECT_RING
-  __shared__ float4 s_stage[2][1];
-#else
   __shared__ float4 s_stage[2][64 * CP];
-#endif
   __shared__ int s_spos[2][64];
   __shared__ uint32_t s_bar;
-  __shared__ uint32_t s_landed, s_released;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int64_t E = a.E;
   const int64_t base = (int64_t)blockIdx.x * FUSED_ENVS;
   const int H = a.H;
-#ifdef MH_FUSED_EXP_PAD_SCRATCH  // experiment: a larger private segment per lane
-  {
-    volatile float pad[MH_FUSED_EXP_PAD_SCRATCH];
-    pad[lane % MH_FUSED_EXP_PAD_SCRATCH] = 0.0f;
-    if (a.H < 0) a.obs[0] = pad[(lane + 1) % MH_FUSED_EXP_PAD_SCRATCH];
-  }
-#endif
 
   // ---- prologue: the workgroup's observations into LDS (rows past E: zeros), the policy's
   // fold operands and layer-2 bias, chunk 0 of W2
@@ -726,25 +686,15 @@ void k_sample_fused(FusedArgs a) {
   }
   if (threadIdx.x == 0) {
     s_bar = 0u;
-    s_landed = 2u;  // chunk 0 of the first pass: staged by the prologue below (both "loader" halves)
-    s_released = 0u;
   }
   const bool pol = w < 4;
   if (pol) {
     const uint4* w3g = reinterpret_cast<const uint4*>(a.P + pm_off_w3x3(a.K1));
     constexpr int FOPW = PM_NB * 4 / 4;
-    if constexpr (W3L == 64) {
 #pragma unroll
-      for (int i = 0; i < FOPW; ++i) {
-        const int r = w * FOPW + i;
-        glds16(w3g + r * 64 + lane, &lds_w3[r * 64]);
-      }
-    } else {  // rows l & 31 < 8 of each fragment (the others are the zero padding of N3 <= 8)
-#pragma unroll
-      for (int i = 0; i < FOPW; ++i) {
-        const int r = w * FOPW + i;
-        if ((lane & 31) < 8) lds_w3[r * 16 + (lane >> 5) * 8 + (lane & 31)] = w3g[r * 64 + lane];
-      }
+    for (int i = 0; i < FOPW; ++i) {
+      const int r = w * FOPW + i;
+      glds16(w3g + r * 64 + lane, &lds_w3[r * 64]);
     }
     const uint4* w1g = reinterpret_cast<const uint4*>(a.P + pm_off_w1x3(a.K1));
 #pragma unroll
@@ -758,53 +708,59 @@ void k_sample_fused(FusedArgs a) {
       const int r = q & 15, l = ((q >> 4) & 1) * 32, ob = q >> 5;
       lds_b2[ob * 32 + pm_row(r, l)] = b2p[((int64_t)ob * 64 + l) * 16 + r];
     }
-    if (threadIdx.x < 32) lds_b3[threadIdx.x] = (int)threadIdx.x < a.N3 ? a.P[pm_off_b3(a.K1) + threadIdx.x] : 0.0f;
     const uint4* W2g = reinterpret_cast<const uint4*>(a.P + pm_off_w2x3(a.K1));
     constexpr int FPW = PM_X3_FRAGS / 4;
 #pragma unroll
     for (int i = 0; i < FPW; ++i) glds16(W2g + (w * FPW + i) * 64 + lane, &lds0[(w * FPW + i) * 64]);
-    if constexpr (kTriple) {  // chunk 1 (W2 block 1) too: the first phase stages chunk 2
-#pragma unroll
-      for (int i = 0; i < FPW; ++i)
-        glds16(W2g + ((int64_t)PM_X3_FRAGS + w * FPW + i) * 64 + lane, &lds1[(w * FPW + i) * 64]);
-    }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // this wave's fold operands landed before the barrier
   }
   __syncthreads();
 
   if (pol) {
     // ================= policy waves: 2H passes (H1 first, then H0 / H1 alternating)
-    PolicyLds L{lds0, lds1, lds2, lds_w3, lds_b2, lds_b3, lds_w1, s_obs, s_lgt, &s_bar, a.err, &s_landed, &s_released};
+    const uint32_t lds0_addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds0;
+    const uint32_t lds1_addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds1;
+    PolicyLds L{lds0, lds1, lds0_addr, lds1_addr, lds_w3, lds_b2, lds_w1, s_obs, s_lgt, &s_bar, a.err};
+    // the layer-3 bias of the rows this lane stores (4 (lane >> 5) + r; zero past N3)
+    float b3r[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = 4 * (lane >> 5) + r;
+      b3r[r] = o < N3C ? a.P[pm_off_b3(a.K1) + o] : 0.0f;
+    }
     uint32_t target = 0;
     const int total = 2 * H;
+#ifdef MH_FUSED_EXP_TACC
+    TAcc g_tacc{};
+    g_tacc.last = __builtin_amdgcn_s_memtime();
+#endif
     int pass = 0;
     ++pass;
-    policy_pass<D, kLoaders, W3L>(a, L, w, FUSED_ENVS / 2 + w * 32, pass < total, target, pass - 1);
+    policy_pass<D, N3C>(a, L, w, FUSED_ENVS / 2 + w * 32, pass < total, target, b3r, pass - 1 MH_TACC_ARG);
     __syncthreads();
     for (int t = 0; t < H; ++t) {
       ++pass;
-      policy_pass<D, kLoaders, W3L>(a, L, w, w * 32, pass < total, target, pass - 1);  // A(t): H0
+      policy_pass<D, N3C>(a, L, w, w * 32, pass < total, target, b3r, pass - 1 MH_TACC_ARG);  // A(t): H0
       MH_STAMP(a, pass - 1, 18);
       __syncthreads();
-#ifdef MH_FUSED_EXP_SERIAL
-      __syncthreads();
-#endif
       if (t < H - 1) {  // B(t): H1
         ++pass;
-        policy_pass<D, kLoaders, W3L>(a, L, w, FUSED_ENVS / 2 + w * 32, pass < total, target, pass - 1);
+        policy_pass<D, N3C>(a, L, w, FUSED_ENVS / 2 + w * 32, pass < total, target, b3r, pass - 1 MH_TACC_ARG);
         MH_STAMP(a, pass - 1, 18);
       }
       __syncthreads();
-#ifdef MH_FUSED_EXP_SERIAL
-      __syncthreads();
-#endif
     }
+#ifdef MH_FUSED_EXP_TACC
+    if (blockIdx.x < 4 && lane == 0 && a.lgt_out) {
+      uint64_t* o = reinterpret_cast<uint64_t*>(a.lgt_out) + (blockIdx.x * 4 + w) * 8;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) o[k] = g_tacc.t[k];
+      o[7] = (uint64_t)total;
+    }
+#endif
     __builtin_amdgcn_s_waitcnt(0x0F70);
   } else {
 #ifdef MH_FUSED_EXP_NO_ENV  // cost-attribution experiment only
-#ifdef MH_FUSED_LOADERS
-#error "MH_FUSED_EXP_NO_ENV removes the loader waves: build it without MH_FUSED_LOADERS"
-#endif
     if (false)
 #endif
     {
@@ -815,10 +771,7 @@ void k_sample_fused(FusedArgs a) {
     const int64_t e = base + row;
     const bool live = e < E;
     EnvLane<Env> v;
-#ifdef MH_FUSED_EXP_CHECK_OBS
-    v.have = 0;
-#endif
-    if (MH_FUSED_STATE_IN_REGS && live) {
+    if (live) {
 #pragma unroll
       for (int i = 0; i < S; ++i) v.s[i] = a.state[(int64_t)i * E + e];
 #pragma unroll
@@ -830,75 +783,34 @@ void k_sample_fused(FusedArgs a) {
     }
     const int NW = (int)((E + 63) / 64);
     const int gw = (int)(e / 64);
-#ifdef MH_FUSED_LOADERS
-    const PolicyLds LL{lds0, lds1, lds2, lds_w3, lds_b2, lds_b3, lds_w1, s_obs, s_lgt, &s_bar, a.err, &s_landed, &s_released};
-    const int npass = 2 * H;
-#endif
     float4* stage = s_stage[ew & 1];
     int* spos = s_spos[ew & 1];
     auto step = [&](int t) {
       bool emit;
       int emit_pos;
-#if !MH_FUSED_STATE_IN_REGS
-      // the env's state through the cache hierarchy each lockstep (what k_rollout does): held in
-      // registers across the horizon instead, the Quad step's live set spills
-      if (live) {
-#pragma unroll
-        for (int i = 0; i < S; ++i) v.s[i] = a.state[(int64_t)i * E + e];
-#pragma unroll
-        for (int i = 0; i < XS; ++i) v.xs[i] = a.xstate[(int64_t)i * E + e];
-        v.k = a.steps[e];
-        v.ctr = a.ctr[e];
-        v.len = a.ring_len[e];
-        v.pos = a.ring_pos[e];
-      }
-#endif
       env_lockstep<Env>(a, v, e, live, t, s_lgt + row * N3C, s_obs + row * D, stage, spos, emit, emit_pos);
-#if !MH_FUSED_STATE_IN_REGS
-      if (live) {
-#pragma unroll
-        for (int i = 0; i < S; ++i) a.state[(int64_t)i * E + e] = v.s[i];
-#pragma unroll
-        for (int i = 0; i < XS; ++i) a.xstate[(int64_t)i * E + e] = v.xs[i];
-        a.steps[e] = v.k;
-        a.ctr[e] = v.ctr;
-        a.ring_len[e] = v.len;
-        a.ring_pos[e] = v.pos;
-      }
-#endif
       const unsigned long long m = __ballot(emit);
       if (base + ew * 64 < E) {
         if (lane == 0) {
           const int nw = __popcll(m);
           a.emit_count[(int64_t)t * NW + gw] = nw;
-#ifndef MH_FUSED_EXP_NO_TS  // cost-attribution experiment only (the emission's totals stay 0)
           if (nw) __hip_atomic_fetch_add(a.ts_total + t, nw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
         }
         if (emit) a.emit_list[(int64_t)t * E + (int64_t)gw * 64 + __popcll(m & ((1ull << lane) - 1ull))] =
             lane | (emit_pos << 6);
       }
     };
-#ifdef MH_FUSED_LOADERS
-    if (half == 0) load_pass(a, LL, 0, npass, ew & 1);  // the policy's first pass (H1): H0's waves load
-#endif
     __syncthreads();  // the policy's first pass (H1)
     // phases A(t) (half H1 steps) and B(t) (half H0 steps), one call site for the step's body; the
     // other half's waves stage the pass's W2 chunks (phase ph runs policy pass ph + 1)
     for (int ph = 0; ph < 2 * H; ++ph) {
-#ifdef MH_FUSED_EXP_SERIAL  // experiment: env steps never overlap a policy pass
-      __syncthreads();
-#endif
       if ((ph & 1) == (half ^ 1)) {
         step(ph >> 1);
       } else {
-#ifdef MH_FUSED_LOADERS
-        if (ph + 1 < npass) load_pass(a, LL, ph + 1, npass, ew & 1);
-#endif
       }
       __syncthreads();
     }
-    if (MH_FUSED_STATE_IN_REGS && live) {
+    if (live) {
 #pragma unroll
       for (int i = 0; i < S; ++i) a.state[(int64_t)i * E + e] = v.s[i];
 #pragma unroll
@@ -922,17 +834,12 @@ void k_sample_fused(FusedArgs a) {
   // wave's adds complete (vmcnt(0)) before the workgroup's RELAXED arrival, and the last
   // workgroup reads them with agent-scope atomic loads; nothing else passes between workgroups
   // here (aux / cursor are read by the next launch), so no agent-scope fence (an L2 writeback +
-  // invalidate per workgroup at the kernel's tail). MH_FUSED_TAIL_FENCED: the former fences (A/B).
+  // invalidate per workgroup at the kernel's tail).
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();
   __shared__ uint32_t s_last;
   if (threadIdx.x == 0) {
-#ifdef MH_FUSED_TAIL_FENCED
-    __threadfence();
-    const uint32_t arrived = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-#else
     const uint32_t arrived = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
     s_last = arrived == gridDim.x - 1;
   }
   __syncthreads();
@@ -940,9 +847,6 @@ void k_sample_fused(FusedArgs a) {
     // wave 0: 64 lockstep totals per round, loaded together, an inclusive wave scan, the
     // exclusive prefixes stored and the totals re-zeroed (a lane-serial loop took one L2 round
     // trip per lockstep at the kernel's tail)
-#ifdef MH_FUSED_TAIL_FENCED
-    __threadfence();
-#endif
     int64_t carry = 0;
     int last = 0;
     for (int t0 = 0; t0 < H; t0 += 64) {
@@ -1018,6 +922,41 @@ __device__ __forceinline__ void emit_rows_lds(float* dst, const float* row, floa
   __builtin_amdgcn_wave_barrier();
 }
 
+// Per-cell exclusive window prefixes of each lockstep (one 1024-thread workgroup per lockstep): the
+// cells' window counts (four wave counts each), a block scan, the prefixes into cell_pre. Used
+// only when a lockstep has more than FUSED_EMIT_SCAN_CELLS cells.
+__global__ __launch_bounds__(1024) void k_emit_prefix(HorizonEmitArgs a) {
+  const int NW = (int)((a.E + 63) / 64);
+  const int NBK = (NW + 3) / 4;
+  const int ts = blockIdx.x;
+  const int32_t* cnt = a.emit_count + (int64_t)ts * NW;
+  int32_t* out = a.cell_pre + (int64_t)ts * NBK;
+  const int per = (NBK + 1023) / 1024;
+  const int c0 = threadIdx.x * per, c1 = c0 + per < NBK ? c0 + per : NBK;
+  int sum = 0;
+  for (int c = c0; c < c1; ++c)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sum += 4 * c + q < NW ? cnt[4 * c + q] : 0;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int incl = sum;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int u = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += u;
+  }
+  __shared__ int wsum[16];
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  int before = 0;
+  for (int v = 0; v < wave; ++v) before += wsum[v];
+  int run = before + incl - sum;
+  for (int c = c0; c < c1; ++c) {
+    out[c] = run;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) run += 4 * c + q < NW ? cnt[4 * c + q] : 0;
+  }
+}
+
 template <int D, int A>
 __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
   constexpr int F = rec_floats(D, A);
@@ -1034,7 +973,9 @@ __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
     s_hdr[1] = a.aux[1];
     s_hdr[2] = a.aux[2 + ts];
   }
-  {  // the wave counts of the lockstep's cells before b
+  if (NBK > FUSED_EMIT_SCAN_CELLS) {  // k_emit_prefix formed the cell's prefix
+    if (threadIdx.x < 4) s_pre[threadIdx.x] = threadIdx.x == 0 ? a.cell_pre[(int64_t)ts * NBK + b] : 0;
+  } else {  // the wave counts of the lockstep's cells before b (at most 4 * FUSED_EMIT_SCAN_CELLS)
     int part = 0;
     for (int i = threadIdx.x; i < 4 * b; i += 256) part += cnt[i];
 #pragma unroll
@@ -1113,23 +1054,27 @@ __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
 }
 
 // ------------------------------------------------------------------ launchers
+// the emission launch alone (the last horizon's windows again: it reads the ring, the per-wave
+// lists and the fused kernel's header and writes the same store rows, so it is idempotent until
+// the next horizon; bench.py times it this way at the trainer's own window count)
+template <class Env>
+static hipError_t launch_emit_t(const HorizonEmitArgs& ea, hipStream_t st) {
+  if ((ea.E + FUSED_ENVS - 1) / FUSED_ENVS > FUSED_EMIT_SCAN_CELLS) {
+    if (ea.cell_pre == nullptr) return hipErrorInvalidValue;
+    k_emit_prefix<<<ea.H, 1024, 0, st>>>(ea);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  }
+  k_emit_cells<Env::D, Env::A><<<(unsigned)fused_emit_cells(ea.E, ea.H), 256, 0, st>>>(ea);
+  return hipGetLastError();
+}
+
 template <class Env>
 static hipError_t launch_fused_t(const FusedArgs& a, const HorizonEmitArgs& ea, hipStream_t st) {
   const int grid = (int)((a.E + FUSED_ENVS - 1) / FUSED_ENVS);
   k_sample_fused<Env><<<grid, FUSED_THREADS, 0, st>>>(a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || ea.obs == nullptr) return e;
-  k_emit_cells<Env::D, Env::A><<<(unsigned)fused_emit_cells(a.E, a.H), 256, 0, st>>>(ea);
-  return hipGetLastError();
-}
-
-// the emission launch alone (the last horizon's windows again: it reads the ring, the per-wave
-// lists and the fused kernel's header and writes the same store rows, so it is idempotent until
-// the next horizon; bench.py times it this way at the trainer's own window count)
-template <class Env>
-static hipError_t launch_emit_t(const HorizonEmitArgs& ea, hipStream_t st) {
-  k_emit_cells<Env::D, Env::A><<<(unsigned)fused_emit_cells(ea.E, ea.H), 256, 0, st>>>(ea);
-  return hipGetLastError();
+  return launch_emit_t<Env>(ea, st);
 }
 
 hipError_t launch_emit_horizon(int env_id, const HorizonEmitArgs& ea, hipStream_t st) {

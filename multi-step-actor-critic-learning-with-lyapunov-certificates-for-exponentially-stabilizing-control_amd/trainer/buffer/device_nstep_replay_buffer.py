@@ -24,16 +24,25 @@ KEYS = ("obs", "act", "rew", "cost", "obs2", "done", "logp")
 
 class DeviceWindowBatch:
     """What the HIP sampler's sample() returns: windows already emitted into `store_owner`
-    (when bound) or into the sampler's staging store. `count` is a device int64 scalar."""
+    (when bound) or into the sampler's staging store. `count` is a device int64 scalar, or None
+    with `count_fn` given: the count is then read on demand (the fused horizon's header holds it
+    until the sampler's next horizon, which first calls resolve() on a batch still unresolved)."""
 
-    def __init__(self, sampler, store_owner, count, first_total=None):
+    def __init__(self, sampler, store_owner, count, first_total=None, count_fn=None):
         self.sampler = sampler
         self.store_owner = store_owner
         self.count = count
         self.first_total = first_total
+        self._count_fn = count_fn
+
+    def resolve(self):
+        if self.count is None:
+            self.count = self._count_fn()
+            self._count_fn = None
+        return self.count
 
     def __len__(self):
-        return int(self.count.item())
+        return int(self.resolve().item())
 
 
 class DeviceNstepReplayBuffer:

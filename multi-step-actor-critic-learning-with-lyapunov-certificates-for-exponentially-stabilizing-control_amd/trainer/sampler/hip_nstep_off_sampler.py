@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import ctypes
 import time
+import weakref
 
 import torch
 import torch.nn as nn
@@ -94,6 +95,7 @@ class HipNstepOffSampler:
         self._graph = None
         self._graph_key = None
         self._eager_calls = 0
+        self._last_batch = None  # weakref to the last fused horizon's batch (its count unread)
 
     # ------------------------------------------------------------------ reference API
     def get_total_sample_num(self) -> int:
@@ -261,10 +263,27 @@ class HipNstepOffSampler:
             drain_pending_handles()  # env handles released by a finaliser during the capture
         return self._graph
 
+    def _window_count(self):
+        """The last horizon's window count (mh_sample_horizon_windows), a fresh device int64."""
+        out = torch.empty(1, dtype=torch.int64, device=self.device)
+        N.check(N.lib().mh_sample_horizon_windows(self._h, N.ptr(out), N.stream_of(self.device)),
+                "mh_sample_horizon_windows")
+        return out[0]
+
     def _sample(self):
         self._handle()
         store = self._target()
-        before = store.cursor[2].clone()
+        fused_h = self._fused_horizon_ok(self._fused_layers() is not None)
+        if fused_h:
+            # the window count stays in the fused kernel's header until the next horizon: a batch
+            # that still holds it unread copies it out first (no launches on the usual path, where
+            # the trainer drops the batch right after add_batch)
+            prev = self._last_batch() if self._last_batch is not None else None
+            if prev is not None:
+                prev.resolve()
+            before = None
+        else:
+            before = store.cursor[2].clone()
         with torch.no_grad():
             if self.use_graph and self._eager_calls >= 1 and not getattr(self, "_timing", False):
                 self._graph_for(store).replay()
@@ -275,6 +294,10 @@ class HipNstepOffSampler:
                     torch.cuda._sleep(int(getattr(self, "_timing_spin_cycles", 20_000_000)))
                 self._horizon(store)
                 self._eager_calls += 1
+        if fused_h:
+            batch = DeviceWindowBatch(self, store, None, count_fn=self._window_count)
+            self._last_batch = weakref.ref(batch)
+            return batch
         return DeviceWindowBatch(self, store, store.cursor[2] - before)
 
     def sample(self):

@@ -4,10 +4,9 @@ csrc/Makefile compiles sample_fused.hip with -fno-slp-vectorize: with the env st
 code SLP-vectorised into packed-FP32 instructions (v_pk_mul / v_pk_add / v_pk_fma _f32) running on
 the env waves beside the policy waves' MFMAs, QuadTracking produced run-to-run different results in
 lanes 48-63 (tools/probes/variants_det.sh). The guard must not rest on the flag
-alone: the policy pass uses packed-f32 arithmetic on purpose (its split / rescale pairs, identical
-in every instantiation), so every env's k_sample_fused<Env> must contain exactly the same number of
-packed-f32 instructions — any env-step code the compiler packs shows up as an excess in that env's
-kernel.
+alone. Since round 5 the policy pass has no packed-f32 arithmetic either (its split / rescale
+pairs are scalar: beside MFMAs a v_pk_fma_f32 costs ~22 cycles more than two v_fma_f32), so no
+k_sample_fused<Env> may contain a single packed-f32 instruction.
 """
 import os
 import re
@@ -47,5 +46,9 @@ def test_env_step_code_of_the_fused_kernel_is_not_packed(tmp_path):
         if name and "k_sample_fused" in name and re.search(r"\bv_pk_(mul|add|fma)_f32\b", line):
             counts[name] = counts.get(name, 0) + 1
     per_env = {e: sum(c for n, c in counts.items() if e in n) for e in ENVS}
-    assert all(per_env[e] > 0 for e in ENVS), per_env  # the policy pass's own packed arithmetic
-    assert len(set(per_env.values())) == 1, f"packed-f32 env-step code in the fused kernel: {per_env}"
+    assert any("k_sample_fused" in n for n in _kernels(asm)), "no k_sample_fused in the code object"
+    assert all(v == 0 for v in per_env.values()), f"packed-f32 code in the fused kernel: {per_env}"
+
+
+def _kernels(asm):
+    return [m.group(1) for m in re.finditer(r"^[0-9a-f]+ <(.*)>:", asm, re.M)]

@@ -74,8 +74,10 @@ def _assert_same(a, ba, b, bb, where):
 
 CASES = [(nm, 65536, 20, False) for nm in OE.ENVS] + [("QuadTracking", 65536, 20, True), ("QuadTracking", 4000, 20, False),
                                                      ("DuctedFan", 300, 3, False), ("TwoLink", 777, 5, False),
-                                                     # > 8,192 emission cells: k_emit_scan runs several rounds
-                                                     ("VanderPol", 200000, 20, False)]
+                                                     # 782 cells per lockstep: each cell sums the earlier cells' counts
+                                                     ("VanderPol", 200000, 20, False),
+                                                     # 1,172 cells per lockstep (> FUSED_EMIT_SCAN_CELLS): k_emit_prefix
+                                                     ("VanderPol", 300000, 20, False)]
 
 
 @pytest.mark.parametrize("name,E,n,hover", CASES, ids=[f"{c[0]}-{c[1]}-n{c[2]}{'-hover' if c[3] else ''}" for c in CASES])
@@ -132,6 +134,11 @@ def test_emission_relaunch_rewrites_the_same_rows(tmp_path):
     untouched = torch.ones(M, dtype=torch.bool, device="cuda")
     untouched[rows] = False
     assert bool((ba.n_step_buf["rew"][untouched] == -7.0).all())
+    # only that horizon can be re-emitted: another horizon length, or any stepping / resetting
+    # call on the handle since (here mh_rollout_flush), is refused without a launch
+    assert N.lib().mh_sample_horizon_emit(a._h, a.horizon - 1, ctypes.byref(ba.ws), None, N.stream_of()) != 0
+    N.check(N.lib().mh_rollout_flush(a._h, N.stream_of()), "mh_rollout_flush")
+    assert N.lib().mh_sample_horizon_emit(a._h, a.horizon, ctypes.byref(ba.ws), None, N.stream_of()) != 0
 
 
 def test_fused_horizon_needs_reserved_rings():
