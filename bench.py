@@ -253,14 +253,26 @@ def main():
     # rewrites the same store rows, idempotent), i.e. at the trainer's own window count, before
     # any diagnostic launch below moves the env state
     t_emit_h = windows_emit = None
+    emit_extra_steps = 0
     if fused_h:
         win_dev = torch.zeros(1, dtype=torch.int64, device=dev)
 
         def k_emit_only():
-            N.lib().mh_sample_horizon_emit(h, H, ctypes.byref(buffer.ws), N.ptr(win_dev), st)
+            N.check(N.lib().mh_sample_horizon_emit(h, H, ctypes.byref(buffer.ws), N.ptr(win_dev), st),
+                    "mh_sample_horizon_emit")
 
-        # (the window count swings from horizon to horizon, a few hundred to ~80 k: the init
-        # policy's episodes end together; the line reports the count this figure was taken at)
+        # (the window count swings from horizon to horizon, 0 to ~1.3 M: the episodes of the init
+        # policy end together, and the hover policy's all reach the step limit in the same lockstep
+        # and emit nothing for n locksteps; the line reports the count this figure was taken at).
+        # A horizon with fewer than 1 % of its E x H env-steps as windows says nothing about HBM:
+        # a few more sampler steps (diagnostics, after the timed region) until one has more.
+        k_emit_only()
+        torch.cuda.synchronize()
+        while int(win_dev.item()) < a.envs * horizon // 100 and emit_extra_steps < 60:
+            buffer.add_batch(sampler.sample()[0])
+            emit_extra_steps += 1
+            k_emit_only()
+            torch.cuda.synchronize()
         t_emit_h = time_launches(k_emit_only, reps) * 1e-3
         windows_emit = int(win_dev.item())
 
@@ -326,8 +338,10 @@ def main():
         kernels["emit_horizon"] = {"avg_us": round(t_emit_h * 1e6, 2), "windows": windows_emit, "bytes": bytes_win,
                                    "GBps": round(bytes_win / t_emit_h / 1e9, 1),
                                    "frac": round(bytes_win / t_emit_h / 1e9 / PEAK_HBM_GBS, 4),
-                                   "note": "k_emit_cells alone (mh_sample_horizon_emit) on the last trainer step's "
-                                           "horizon: its windows, ring records -> replay store rows"}
+                                   "extra_sampler_steps": emit_extra_steps,
+                                   "note": "k_emit_cells alone (mh_sample_horizon_emit) on the last sampled horizon "
+                                           "(the last trainer step's, or the first later one with >= 1 % of its "
+                                           "env-steps as windows): its windows, ring records -> replay store rows"}
     if t_pol is not None:
         flops = flops_lockstep
         # split-f16 arithmetic: every f32 product is 3 f16 MFMA products (hi.hi + hi.lo + lo.hi),

@@ -197,7 +197,12 @@ def lib():
                 f"`make -C {os.path.join(_HERE, 'csrc')}` (or __graft_entry__.build()). "
                 "There is no CPU fallback.")
         L = ctypes.CDLL(LIB_PATH)
+        # A/B runs load older builds through MSACL_HIP_LIB: an entry point they lack is left
+        # unbound there (a call then raises); the in-tree library must export every one
+        ab = "MSACL_HIP_LIB" in os.environ
         for name, (res, args) in _PROTOS.items():
+            if ab and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

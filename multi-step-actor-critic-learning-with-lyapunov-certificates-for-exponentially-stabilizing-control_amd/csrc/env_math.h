@@ -355,14 +355,12 @@ struct TwoLink {
     double Cq2 = (double)C21 * (double)dq1 + 0.0 * (double)dq2;
     double b1 = ((double)u[0] - Cq1) - (double)G1;
     double b2 = ((double)u[1] - Cq2) - (double)G2;
-    // LU with partial pivoting on the first column (getrf), then forward/back substitution
-    double a11 = M11, a12 = M12, a21 = M21, a22 = M22;
-    if (fabs(a21) > fabs(a11)) {
-      double t;
-      t = a11; a11 = a21; a21 = t;
-      t = a12; a12 = a22; a22 = t;
-      t = b1; b1 = b2; b2 = t;
-    }
+    // LU of the 2 x 2 mass matrix (getrf), then forward/back substitution. getrf pivots on the
+    // larger |entry| of the first column, and for this arm that is always M11: M11 = 5/3 + c2 and
+    // M21 = M12 = 1/3 + c2 / 2 give M11 - |M21| >= 1/2 for every c2 in [-1, 1] (a margin no f32
+    // rounding of the entries can close), so the row swap never happens and is not coded (its
+    // compare and six f64 selects were ~7 % of the step's VALU at 4 M envs).
+    const double a11 = M11, a12 = M12, a21 = M21, a22 = M22;
     const double i11 = rcp64(a11);
     double l21 = a21 * i11;
     double u22 = a22 - l21 * a12;

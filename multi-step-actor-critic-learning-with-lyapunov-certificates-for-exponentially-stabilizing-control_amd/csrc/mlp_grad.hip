@@ -71,7 +71,12 @@ __global__ __launch_bounds__(256) void k_act_grad_colsum(const float* __restrict
     store_g();
     return;
   }
-  // fused finish: publish this chunk's sums write-through, count arrivals per column group
+  // fused finish: publish this chunk's sums write-through, count arrivals per column group.
+  // Memory-model basis (LLVM AMDGPUUsage, "Memory Model GFX942" code sequences, which gfx950
+  // follows): the agent-scope atomic store is written through to the coherence point and is
+  // performed when `s_waitcnt vmcnt(0)` returns; the arrival follows the workgroup barrier in
+  // program order; the finishing chunk reads the sums with agent-scope atomic loads (`sc1`) from
+  // the coherence point: no release / acquire fence (MI355X_MICROARCH.md, sc1 hand-off row 1).
   if (ty == 0 && n < N)
     __hip_atomic_store(partial + (int64_t)blockIdx.y * N + n, csum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -114,6 +114,13 @@ __device__ bool rows_reduce(double a, double b, double* part, unsigned int* arri
     // workgroup reads them with agent-scope atomic loads. No fence: an agent-scope release /
     // acquire writes back / invalidates the whole L2, which inside the update holds the other
     // branch's dirty lines too (this launch took 25 us there with the fences).
+    // Memory-model basis (LLVM AMDGPUUsage, "Memory Model GFX942" code sequences, which gfx950
+    // follows): an agent-scope atomic store is a `global_store ... sc1`, written through to the
+    // coherence point; `s_waitcnt vmcnt(0)` returns only once it is performed there, and the
+    // relaxed arrival is issued after that wait in program order. The last workgroup reads the
+    // partials with agent-scope atomic loads (`sc1`: from the coherence point, not a stale L1/L2
+    // line), so it sees them without an acquire (MI355X_MICROARCH.md, "Hand-offs measured with
+    // sc1 loads", row 1).
     __hip_atomic_store(part + 2 * blockIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(part + 2 * blockIdx.x + 1, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): both stores acknowledged

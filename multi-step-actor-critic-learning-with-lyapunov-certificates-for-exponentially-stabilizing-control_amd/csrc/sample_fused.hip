@@ -33,6 +33,22 @@
 
 #ifdef MH_FUSED_EXP_NO_MFMA  // cost-attribution experiment: the policy pass without its MFMAs (garbage logits)
 #define MH_MFMA(a, b, c) (c)
+#elif defined(MH_FUSED_EXP_MFMA16)
+// clock experiment (garbage logits): each 32x32x16 product replaced by two v_mfma_f32_16x16x32_f16
+// of the same flops into two quarters of the accumulator (the DVFS give-back of the shape)
+namespace mh {
+typedef float f32x4e __attribute__((ext_vector_type(4)));
+template <class V, class A>
+__device__ __forceinline__ V mfma16_pair(const A& a, const A& b, V c) {
+  f32x4e lo = {c[0], c[1], c[2], c[3]}, hi = {c[4], c[5], c[6], c[7]};
+  lo = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, lo, 0, 0, 0);
+  hi = __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, hi, 0, 0, 0);
+  c[0] = lo[0]; c[1] = lo[1]; c[2] = lo[2]; c[3] = lo[3];
+  c[4] = hi[0]; c[5] = hi[1]; c[6] = hi[2]; c[7] = hi[3];
+  return c;
+}
+}  // namespace mh
+#define MH_MFMA(a, b, c) mfma16_pair(a, b, c)
 #else
 #define MH_MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0)
 #endif
@@ -835,6 +851,13 @@ void k_sample_fused(FusedArgs a) {
   // workgroup reads them with agent-scope atomic loads; nothing else passes between workgroups
   // here (aux / cursor are read by the next launch), so no agent-scope fence (an L2 writeback +
   // invalidate per workgroup at the kernel's tail).
+  // Memory-model basis (LLVM AMDGPUUsage, "Memory Model GFX942" code sequences, which gfx950
+  // follows): the lockstep totals are agent-scope atomic RMWs, performed at the coherence point;
+  // `s_waitcnt vmcnt(0)` returns once every one of this workgroup's adds is performed (each
+  // storing wave waits before the barrier), and the relaxed arrival is issued after the barrier in
+  // program order; the last workgroup reads the totals with agent-scope atomic loads (`sc1`, from
+  // the coherence point), so it needs no acquire (MI355X_MICROARCH.md, "Hand-offs measured with sc1
+  // loads", row 1). aux / cursor are published to the next launch by the kernel boundary.
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   __syncthreads();
   __shared__ uint32_t s_last;

@@ -6,12 +6,13 @@
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG=multi-step-actor-critic-learning-with-lyapunov-certificates-for-exponentially-stabilizing-control_amd
-SRCS="rollout capi msacl_kernels per gae policy_mlp mlp_grad optim dist_kernels gemm"
+SRCS="rollout sample_fused capi msacl_kernels per gae policy_mlp mlp_grad optim dist_kernels gemm mlp_fused"
 build_dir() {  # $1 = csrc dir, $2 = include dir, $3 = out dir
   mkdir -p "$3"
   ( cd "$1" && for f in $SRCS; do
       [ -f $f.hip ] || continue
-      /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
+      x=""; [ $f = sample_fused ] && x="-fno-slp-vectorize"  # as the Makefile
+      /opt/rocm/bin/hipcc $x -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
         -I"$2" -I. ${EXTRA_FLAGS} -c $f.hip -o "$3/$f.o" & done; wait
     /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$3/libmsacl_hip.so" "$3"/*.o )
 }

@@ -45,6 +45,13 @@ def row(kernel, env, units, unit_name, bytes_per_unit, ms, **extra):
     return r
 
 
+# SURVEY §8(d)'s algorithmic bytes per env-step (minimal f32 SoA: read state + step counter +
+# action, write state + step counter + real_next_obs + reward + cost + term + trunc; Quad with
+# Rd_last in f64), the figure the >= 40 % per-kernel HBM bar is quoted on
+SURVEY_BYTES = {"VanderPol": 46, "Pendulum": 46, "DuctedFan": 98, "TwoLink": 74, "SingleTrackCar": 110,
+                "QuadTracking": 370}
+
+
 def env_step_bytes(info):
     S, XS, D, A = info.state_dim, info.xstate_dim, info.obs_dim, info.act_dim
     # read state/xstate/step + action; write state/xstate/step + obs + real_next_obs + reward + term + trunc
@@ -74,7 +81,9 @@ def bench_env_step(name, E, reps, dev):
                                 N.ptr(trunc), st)
 
         ms = time_launches(fn, reps)
-        return row("env_step", name, E, "env_steps", env_step_bytes(info), ms)
+        sb = SURVEY_BYTES[name]
+        return row("env_step", name, E, "env_steps", env_step_bytes(info), ms, survey_bytes_per_unit=sb,
+                   survey_frac=round(E * sb / (ms * 1e-3) / 1e9 / PEAK, 4))
     finally:
         torch.cuda.synchronize()
         N.lib().mh_env_destroy(h)
