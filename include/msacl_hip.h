@@ -597,6 +597,22 @@ int mh_msacl_q_target(const float* q1, const float* q2, const float* q1t, const 
                       int32_t n, float* backup, float* dq1, float* dq2, float* loss_out,
                       float* abs_td, void* stream);
 
+/* mh_msacl_q_target plus the logged critic means (msacl.py:211-222, q1.mean() / q2.mean()):
+ * q_means [2] (nullable) receives mean(q1), mean(q2) from the same pass and the same fixed-order
+ * float64 reduction as the loss, in place of two separate mean reductions. */
+int mh_msacl_q_target_stats(const float* q1, const float* q2, const float* q1t, const float* q2t,
+                            const float* next_logp, const float* rew, const float* done,
+                            const float* log_alpha, const float* weight, float gamma, int32_t B,
+                            int32_t n, float* backup, float* dq1, float* dq2, float* loss_out,
+                            float* abs_td, float* q_means, void* stream);
+
+/* The seven logged scalars of model_update (msacl.py:211-222) packed in one launch:
+ * out [7] = {entropy, exp(log_alpha), q_means[0], q_means[1], loss_q, loss_lya, loss_policy};
+ * every input is a one-element device scalar (q_means: two). */
+int mh_msacl_tb_pack(const float* entropy, const float* log_alpha, const float* q_means,
+                     const float* loss_q, const float* loss_lya, const float* loss_policy, float* out,
+                     void* stream);
+
 /* _lyapunov_update certificate (msacl.py:279-332). Inputs: logp (policy log-prob of the
  * stored actions), old_logp, V(obs) lya_obs, V(obs2) lya_obs2, obs/obs2 [B][n][D].
  * Coefficients c (start_obs_norm_coef), w (lya_diff_coef), s (start_lya_coef) are [n].

@@ -280,7 +280,7 @@ class _Scratch:
         # dq1 | dq2 as the two halves of one buffer: the twin critics' grouped backward reads both
         self.dq_both = f(2, B, n)
         self.dq1, self.dq2 = self.dq_both[0], self.dq_both[1]
-        self.abs_td, self.loss_q = f(B), f(1)
+        self.abs_td, self.loss_q, self.q_means = f(B), f(1), f(2)
         self.is_clip, self.esl, self.lya_diff, self.loss_lya = f(B, n), f(B, n), f(B), f(1)
         # dV | dV2 as the two halves of one buffer: the two Lyapunov evaluations run as one batch
         self.dV_both = f(2 * B, n)
@@ -622,9 +622,22 @@ class MSACL:
                 adam_steps(nets.policy_optimizer, nets.alpha_optimizer)
                 self._alpha_clamp()
         # the logged scalars (msacl.py:211-222), stacked inside the update (model_update snapshots them)
-        tb = torch.stack([entropy, self.networks.log_alpha.detach().exp(), q1_mean, q2_mean, loss_q, loss_lya,
-                          loss_policy])
+        tb = self._tb_pack(entropy, q1_mean, q2_mean, loss_q, loss_lya, loss_policy)
         return loss_q, q1_mean, q2_mean, loss_lya, loss_policy, entropy, tb
+
+    def _tb_pack(self, entropy, q1_mean, q2_mean, loss_q, loss_lya, loss_policy):
+        """The logged scalars (msacl.py:211-222) as one [7] tensor: one launch on a HIP device
+        when the critic means are the q-target kernel's (adjacent in its scratch), torch.stack
+        otherwise."""
+        la = self.networks.log_alpha.detach()
+        parts = (entropy, loss_q, loss_lya, loss_policy)
+        if (self.device.type == "cuda" and q2_mean.data_ptr() == q1_mean.data_ptr() + 4
+                and all(t.numel() == 1 and t.dtype == torch.float32 for t in parts)):
+            tb = torch.empty(7, dtype=torch.float32, device=self.device)
+            _engine("msacl_tb_pack", self.device, N.ptr(entropy), N.ptr(la), N.ptr(q1_mean), N.ptr(loss_q),
+                    N.ptr(loss_lya), N.ptr(loss_policy), N.ptr(tb))
+            return tb
+        return torch.stack([entropy, la.exp(), q1_mean, q2_mean, loss_q, loss_lya, loss_policy])
 
     # ------------------------------------------------------------------ HIP-graph replay
     def _graphable(self):
@@ -741,12 +754,8 @@ class MSACL:
 
         (q1, q1t), (q2, q2t) = self._twin_pair(critic1, critic2)
         weight = data.get("weight") if self.per_flag else None
-        _engine(
-            "msacl_q_target", self.device,
-            N.ptr(q1.detach().contiguous()), N.ptr(q2.detach().contiguous()), N.ptr(q1t), N.ptr(q2t),
-            N.ptr(next_logp.contiguous()), N.ptr(rew), N.ptr(done), N.ptr(self.networks.log_alpha.detach()),
-            N.ptr(weight.contiguous() if weight is not None else None), float(self.gamma), B, n, N.ptr(s.backup),
-            N.ptr(s.dq1), N.ptr(s.dq2), N.ptr(s.loss_q), N.ptr(s.abs_td))
+        means = self._q_target(q1.detach().contiguous(), q2.detach().contiguous(), q1t, q2t, next_logp, rew, done,
+                               weight, B, n, s, stats)
         self.networks.q1_optimizer.zero_grad()
         self.networks.q2_optimizer.zero_grad()
         torch.autograd.backward([q1, q2], [s.dq1, s.dq2])
@@ -757,8 +766,23 @@ class MSACL:
             self.last_priority = s.abs_td.clone()
         if not stats:  # iterations without a policy step log nothing (model_update returns None)
             return s.loss_q[0], None, None
-        # views of the scratch / fresh means, read by model_update right after the update
+        if means is not None:  # the kernel's means (scratch views, read by model_update right after)
+            return s.loss_q[0], means[0], means[1]
         return s.loss_q[0], q1.detach().mean(), q2.detach().mean()
+
+    def _q_target(self, q1, q2, q1t, q2t, next_logp, rew, done, weight, B, n, s, stats):
+        """The backup / twin-MSE kernel (msacl.py:242-257). On a HIP device with stats wanted it
+        also writes the logged critic means into s.q_means (one pass, no extra reductions) and
+        returns that buffer; otherwise None (the caller takes the means itself)."""
+        args = (N.ptr(q1), N.ptr(q2), N.ptr(q1t), N.ptr(q2t), N.ptr(next_logp.contiguous()), N.ptr(rew), N.ptr(done),
+                N.ptr(self.networks.log_alpha.detach()), N.ptr(weight.contiguous() if weight is not None else None),
+                float(self.gamma), B, n, N.ptr(s.backup), N.ptr(s.dq1), N.ptr(s.dq2), N.ptr(s.loss_q),
+                N.ptr(s.abs_td))
+        if stats and self.device.type == "cuda":
+            _engine("msacl_q_target_stats", self.device, *args, N.ptr(s.q_means))
+            return s.q_means
+        _engine("msacl_q_target", self.device, *args)
+        return None
 
     def _q_update_twin(self, tc, data, xa, xq2, next_logp, s, defer_step, stats):
         """_q_update with both critics (and both targets) as one grouped network each
@@ -776,12 +800,7 @@ class MSACL:
             q, h1, h2 = twin.forward(xa2)
             qt, _, _ = twin_t.forward(xq2f, keep=False)
         weight = data.get("weight") if self.per_flag else None
-        _engine(
-            "msacl_q_target", self.device,
-            N.ptr(q[0]), N.ptr(q[1]), N.ptr(qt[0]), N.ptr(qt[1]),
-            N.ptr(next_logp.contiguous()), N.ptr(rew), N.ptr(done), N.ptr(self.networks.log_alpha.detach()),
-            N.ptr(weight.contiguous() if weight is not None else None), float(self.gamma), B, n, N.ptr(s.backup),
-            N.ptr(s.dq1), N.ptr(s.dq2), N.ptr(s.loss_q), N.ptr(s.abs_td))
+        means = self._q_target(q[0], q[1], qt[0], qt[1], next_logp, rew, done, weight, B, n, s, stats)
         twin.backward_weights(xa2, s.dq_both.view(2, M), h1, h2)  # binds q1 / q2 .grad
         if not defer_step:
             D.allreduce_grads(list(self.networks.q1.parameters()) + list(self.networks.q2.parameters()))
@@ -790,6 +809,8 @@ class MSACL:
             self.last_priority = s.abs_td.clone()
         if not stats:
             return s.loss_q[0], None, None
+        if means is not None:
+            return s.loss_q[0], means[0], means[1]
         return s.loss_q[0], q[0].mean(), q[1].mean()
 
     def _lyapunov_update(self, data, defer_step=False, keep_policy=False):

@@ -48,7 +48,7 @@ constexpr int RPB = 4;             // rows (wavefronts) per workgroup
 constexpr int RTPB = RPB * 64;
 
 struct RowScratch {
-  double* part = nullptr;          // [cap][2] per-workgroup partial sums
+  double* part = nullptr;          // [cap][4] per-workgroup partial sums (2 or 4 used)
   unsigned int* arrive = nullptr;  // arrival counter (0 between launches)
   int64_t cap = 0;
 };
@@ -68,7 +68,7 @@ hipError_t row_scratch(int slot, int64_t blocks, RowScratch** out) {
     r.arrive = nullptr;
     r.cap = 0;
     const int64_t cap = blocks < 4096 ? 4096 : blocks;
-    e = hipMalloc(&r.part, sizeof(double) * 2 * cap);
+    e = hipMalloc(&r.part, sizeof(double) * 4 * cap);
     if (e == hipSuccess) e = hipMalloc(&r.arrive, sizeof(unsigned int));
     if (e == hipSuccess) e = hipMemset(r.arrive, 0, sizeof(unsigned int));
     if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -84,28 +84,31 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-// Sum (a, b) over the workgroup, publish the partials, and let the last workgroup total them.
-// Returns true in thread 0 of the last workgroup with the batch sums in *ta, *tb.
-__device__ bool rows_reduce(double a, double b, double* part, unsigned int* arrive, double* ta, double* tb) {
-  __shared__ double sa[RPB], sb[RPB];
+// Sum v[0..K) over the workgroup, publish the partials, and let the last workgroup total them.
+// Returns true in thread 0 of the last workgroup with the batch sums in t[0..K).
+template <int K>
+__device__ bool rows_reduce(const double (&v)[K], double* part, unsigned int* arrive, double (&t)[K]) {
+  __shared__ double sv[K][RPB];
   __shared__ bool last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  a = wave_sum(a);
-  b = wave_sum(b);
+  double w[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) w[j] = wave_sum(v[j]);
   if (lane == 0) {
-    sa[wave] = a;
-    sb[wave] = b;
+#pragma unroll
+    for (int j = 0; j < K; ++j) sv[j][wave] = w[j];
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double x = 0.0, y = 0.0;
-    for (int w = 0; w < RPB; ++w) {
-      x += sa[w];
-      y += sb[w];
+    double x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      x[j] = 0.0;
+      for (int q = 0; q < RPB; ++q) x[j] += sv[j][q];
     }
 #ifdef MH_REDUCE_FENCED  // A/B only: the agent-scope fences (an L2 writeback + invalidate each)
-    part[2 * blockIdx.x] = x;
-    part[2 * blockIdx.x + 1] = y;
+#pragma unroll
+    for (int j = 0; j < K; ++j) part[K * blockIdx.x + j] = x[j];
     __threadfence();
     last = atomicAdd(arrive, 1u) == gridDim.x - 1u;
 #else
@@ -121,9 +124,10 @@ __device__ bool rows_reduce(double a, double b, double* part, unsigned int* arri
     // partials with agent-scope atomic loads (`sc1`: from the coherence point, not a stale L1/L2
     // line), so it sees them without an acquire (MI355X_MICROARCH.md, "Hand-offs measured with
     // sc1 loads", row 1).
-    __hip_atomic_store(part + 2 * blockIdx.x, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(part + 2 * blockIdx.x + 1, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): both stores acknowledged
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      __hip_atomic_store(part + K * blockIdx.x + j, x[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): every store acknowledged
     last = __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
 #endif
   }
@@ -137,28 +141,29 @@ __device__ bool rows_reduce(double a, double b, double* part, unsigned int* arri
 #define MH_PART(i) __hip_atomic_load(part + (i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
 #endif
   // last workgroup: fixed-order total (lane-strided partials, then wave/LDS tree)
-  double x = 0.0, y = 0.0;
+  double x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = 0.0;
   for (unsigned int g = threadIdx.x; g < gridDim.x; g += RTPB) {
-    x += MH_PART(2 * g);
-    y += MH_PART(2 * g + 1);
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] += MH_PART(K * g + j);
   }
 #undef MH_PART
-  x = wave_sum(x);
-  y = wave_sum(y);
+#pragma unroll
+  for (int j = 0; j < K; ++j) x[j] = wave_sum(x[j]);
   __syncthreads();
   if (lane == 0) {
-    sa[wave] = x;
-    sb[wave] = y;
+#pragma unroll
+    for (int j = 0; j < K; ++j) sv[j][wave] = x[j];
   }
   __syncthreads();
   if (threadIdx.x != 0) return false;
-  double X = 0.0, Y = 0.0;
-  for (int w = 0; w < RPB; ++w) {
-    X += sa[w];
-    Y += sb[w];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    double X = 0.0;
+    for (int q = 0; q < RPB; ++q) X += sv[j][q];
+    t[j] = X;
   }
-  *ta = X;
-  *tb = Y;
 #ifdef MH_REDUCE_FENCED
   *arrive = 0u;
 #else
@@ -172,14 +177,14 @@ __global__ __launch_bounds__(RTPB) void k_q_target(const float* q1, const float*
                                                    const float* q2t, const float* nlogp, const float* rew,
                                                    const float* done, const float* log_alpha, const float* weight,
                                                    float gamma, int B, int n, float* backup, float* dq1,
-                                                   float* dq2, float* loss_out, float* abs_td, double* part,
-                                                   unsigned int* arrive) {
+                                                   float* dq2, float* loss_out, float* abs_td, float* q_means,
+                                                   double* part, unsigned int* arrive) {
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * RPB + (threadIdx.x >> 6);
   const float alpha = expf(*log_alpha);
   const int64_t N = (int64_t)B * n;
   const float inv = (float)(1.0 / (double)N);
-  double acc1 = 0.0, acc2 = 0.0, atd = 0.0;
+  double acc1 = 0.0, acc2 = 0.0, atd = 0.0, sq1 = 0.0, sq2 = 0.0;
   if (b < B) {
     const float wb = weight ? weight[b] : 1.0f;
     for (int k = lane; k < n; k += 64) {
@@ -193,13 +198,25 @@ __global__ __launch_bounds__(RTPB) void k_q_target(const float* q1, const float*
       if (dq1) dq1[i] = 2.0f * e1 * inv * wb;
       if (dq2) dq2[i] = 2.0f * e2 * inv * wb;
       atd += 0.5 * (fabs((double)q1[i] - (double)bk) + fabs((double)q2[i] - (double)bk));
+      sq1 += (double)q1[i];
+      sq2 += (double)q2[i];
     }
     atd = wave_sum(atd);
     if (abs_td && lane == 0) abs_td[b] = (float)(atd / n);
   }
-  double s1, s2;
-  if (rows_reduce(acc1, acc2, part, arrive, &s1, &s2) && loss_out)
-    loss_out[0] = (float)(s1 / (double)N) + (float)(s2 / (double)N);
+  // the loss sums, plus the q1 / q2 sums when the logged means are wanted (msacl.py:211-222)
+  if (q_means) {
+    double t[4];
+    if (rows_reduce<4>({acc1, acc2, sq1, sq2}, part, arrive, t)) {
+      if (loss_out) loss_out[0] = (float)(t[0] / (double)N) + (float)(t[1] / (double)N);
+      q_means[0] = (float)(t[2] / (double)N);
+      q_means[1] = (float)(t[3] / (double)N);
+    }
+  } else {
+    double t[2];
+    if (rows_reduce<2>({acc1, acc2}, part, arrive, t) && loss_out)
+      loss_out[0] = (float)(t[0] / (double)N) + (float)(t[1] / (double)N);
+  }
 }
 
 // --------------------------------------------------- Lyapunov certificate (msacl.py:279-332)
@@ -286,9 +303,9 @@ __global__ __launch_bounds__(RTPB) void k_lyapunov(const float* logp, const floa
       diff_acc = (double)rowsum;
     }
   }
-  double sb, sd;
-  if (rows_reduce(bound_acc, diff_acc, part, arrive, &sb, &sd) && loss_out)
-    loss_out[0] = (float)(sb / (double)N) * pos_scale + (float)(sd / (double)B) * diff_scale;
+  double t[2];
+  if (rows_reduce<2>({bound_acc, diff_acc}, part, arrive, t) && loss_out)
+    loss_out[0] = (float)(t[0] / (double)N) * pos_scale + (float)(t[1] / (double)B) * diff_scale;
 }
 
 // ------------------------------------------------ stability advantage (msacl.py:383-399)
@@ -498,6 +515,21 @@ __global__ __launch_bounds__(TPB) void k_policy_objective_step(
   if (alpha_grad && threadIdx.x == 0) alpha_grad[0] = (entropy[0] - target_entropy) * expf(log_alpha[0]);
 }
 
+// ------------------------------------------------------- logged scalars (msacl.py:211-222)
+// [entropy, alpha, q1_mean, q2_mean, loss_q, loss_lya, loss_policy] in one launch (in place of
+// an exp, a stack and the copy model_update snapshots).
+__global__ void k_tb_pack(const float* entropy, const float* log_alpha, const float* q_means, const float* loss_q,
+                          const float* loss_lya, const float* loss_policy, float* out) {
+  if (threadIdx.x != 0) return;
+  out[0] = entropy[0];
+  out[1] = expf(log_alpha[0]);
+  out[2] = q_means[0];
+  out[3] = q_means[1];
+  out[4] = loss_q[0];
+  out[5] = loss_lya[0];
+  out[6] = loss_policy[0];
+}
+
 thread_local std::string g_merr;
 
 }  // namespace
@@ -510,10 +542,10 @@ thread_local std::string g_merr;
 
 extern "C" {
 
-int mh_msacl_q_target(const float* q1, const float* q2, const float* q1t, const float* q2t,
-                      const float* next_logp, const float* rew, const float* done, const float* log_alpha,
-                      const float* weight, float gamma, int32_t B, int32_t n, float* backup, float* dq1,
-                      float* dq2, float* loss_out, float* abs_td, void* stream) {
+int mh_msacl_q_target_stats(const float* q1, const float* q2, const float* q1t, const float* q2t,
+                            const float* next_logp, const float* rew, const float* done, const float* log_alpha,
+                            const float* weight, float gamma, int32_t B, int32_t n, float* backup, float* dq1,
+                            float* dq2, float* loss_out, float* abs_td, float* q_means, void* stream) {
   if (!q1 || !q2 || !q1t || !q2t || !next_logp || !rew || !done || !log_alpha || !backup || B <= 0 || n <= 0)
     return MH_EINVAL;
   const int64_t nb = ((int64_t)B + RPB - 1) / RPB;
@@ -521,8 +553,24 @@ int mh_msacl_q_target(const float* q1, const float* q2, const float* q1t, const 
   if (row_scratch(0, nb, &rs) != hipSuccess) return MH_EHIP;
   k_q_target<<<(unsigned)nb, RTPB, 0, (hipStream_t)stream>>>(q1, q2, q1t, q2t, next_logp, rew, done, log_alpha,
                                                              weight, gamma, B, n, backup, dq1, dq2, loss_out, abs_td,
-                                                             rs->part, rs->arrive);
+                                                             q_means, rs->part, rs->arrive);
   MH_CHECK_LAUNCH("q_target");
+  return MH_OK;
+}
+
+int mh_msacl_q_target(const float* q1, const float* q2, const float* q1t, const float* q2t,
+                      const float* next_logp, const float* rew, const float* done, const float* log_alpha,
+                      const float* weight, float gamma, int32_t B, int32_t n, float* backup, float* dq1,
+                      float* dq2, float* loss_out, float* abs_td, void* stream) {
+  return mh_msacl_q_target_stats(q1, q2, q1t, q2t, next_logp, rew, done, log_alpha, weight, gamma, B, n, backup,
+                                 dq1, dq2, loss_out, abs_td, nullptr, stream);
+}
+
+int mh_msacl_tb_pack(const float* entropy, const float* log_alpha, const float* q_means, const float* loss_q,
+                     const float* loss_lya, const float* loss_policy, float* out, void* stream) {
+  if (!entropy || !log_alpha || !q_means || !loss_q || !loss_lya || !loss_policy || !out) return MH_EINVAL;
+  k_tb_pack<<<1, 64, 0, (hipStream_t)stream>>>(entropy, log_alpha, q_means, loss_q, loss_lya, loss_policy, out);
+  MH_CHECK_LAUNCH("tb_pack");
   return MH_OK;
 }
 
