@@ -174,8 +174,7 @@ def main():
         buffer.add_batch(samples)
         torch.cuda.synchronize()
         tb_ = time.perf_counter()
-        rs = trainer._replay_batch()  # as the trainer does (into the update graph's static inputs)
-        alg.model_update(rs, trainer.iteration)
+        trainer.replay_and_update()  # as step() does (the draw inside the replayed update graph)
         trainer.iteration += 1
         torch.cuda.synchronize()
         ph_s += tb_ - ta
@@ -198,7 +197,8 @@ def main():
         return name
 
     wrapped = [(trainer, timed(trainer, "_sample")), (trainer, timed(trainer, "_replay_batch")),
-               (alg, timed(alg, "model_update")), (buffer, timed(buffer, "add_batch"))]
+               (alg, timed(alg, "model_update")), (alg, timed(alg, "model_update_drawn")),
+               (buffer, timed(buffer, "add_batch"))]
     torch.cuda.synchronize()
     th0 = time.perf_counter()
     for _ in range(k_host):

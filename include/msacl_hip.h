@@ -582,6 +582,24 @@ int mh_replay_gather_joint(const mh_window_store_t* store, int32_t n_step, int32
 int mh_replay_sample_indices(const mh_window_store_t* store, uint64_t seed, uint64_t counter,
                              int64_t batch, int64_t* idx_out, void* stream);
 
+/* mh_replay_sample_indices keyed by a DEVICE draw counter: draw_state [2] int64 (0-initialised;
+ * [0] the counter, [1] the launch's arrival ticket, 0 between launches). Draw k of a buffer uses
+ * counter k and advances draw_state[0] by one inside the launch, so the call can be captured in a
+ * HIP graph and replayed (each replay is the next draw); same indices as
+ * mh_replay_sample_indices(..., counter = k, ...). */
+int mh_replay_sample_indices_dev(const mh_window_store_t* store, uint64_t seed, int64_t* draw_state,
+                                 int64_t batch, int64_t* idx_out, void* stream);
+
+/* The replay draw and mh_replay_gather_joint in ONE launch (nstep_replay_buffer.py:136-148):
+ * the indices are drawn inside the gather from (seed, draw_state[0]) exactly as
+ * mh_replay_sample_indices_dev draws them, written to idx_out (nullable), and the counter is
+ * advanced by the launch. Graph-capturable (the window count is read from store->cursor). */
+int mh_replay_draw_gather(const mh_window_store_t* store, int32_t n_step, int32_t obs_dim,
+                          int32_t act_dim, uint64_t seed, int64_t* draw_state, int64_t batch,
+                          int64_t* idx_out, float* out_obs, float* out_act, float* out_rew,
+                          float* out_cost, float* out_obs2, float* out_done, float* out_logp,
+                          float* out_obs_act, float* out_v_in, void* stream);
+
 /* ---- MSACL target / certificate kernels (RL/algorithm/msacl.py), all [B][n] float32 ---- */
 
 /* _q_update backup + twin MSE (msacl.py:242-257):
@@ -612,6 +630,14 @@ int mh_msacl_q_target_stats(const float* q1, const float* q2, const float* q1t, 
 int mh_msacl_tb_pack(const float* entropy, const float* log_alpha, const float* q_means,
                      const float* loss_q, const float* loss_lya, const float* loss_policy, float* out,
                      void* stream);
+
+/* mh_msacl_tb_pack into slot ctr[0] % slots of ring [slots][8] (element 7 = the low 32 bits of
+ * ctr[0], as float bits: the reader checks that the slot still holds its update), then
+ * ctr[0] += 1. Inside a replayed update graph this keeps each update's logged scalars readable for
+ * `slots` further updates with no copy out of the graph's output. */
+int mh_msacl_tb_pack_ring(const float* entropy, const float* log_alpha, const float* q_means,
+                          const float* loss_q, const float* loss_lya, const float* loss_policy, float* ring,
+                          int64_t* ctr, int32_t slots, void* stream);
 
 /* _lyapunov_update certificate (msacl.py:279-332). Inputs: logp (policy log-prob of the
  * stored actions), old_logp, V(obs) lya_obs, V(obs2) lya_obs2, obs/obs2 [B][n][D].

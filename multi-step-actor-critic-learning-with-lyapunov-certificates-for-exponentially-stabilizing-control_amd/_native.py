@@ -175,9 +175,13 @@ _PROTOS = {
     "mh_replay_gather_joint": (ctypes.c_int, [ctypes.POINTER(WindowStore), c_i32, c_i32, c_i32, c_vp, c_i64]
                                + [c_vp] * 10),
     "mh_replay_sample_indices": (ctypes.c_int, [ctypes.POINTER(WindowStore), c_u64, c_u64, c_i64, c_vp, c_vp]),
+    "mh_replay_sample_indices_dev": (ctypes.c_int, [ctypes.POINTER(WindowStore), c_u64, c_vp, c_i64, c_vp, c_vp]),
+    "mh_replay_draw_gather": (ctypes.c_int, [ctypes.POINTER(WindowStore), c_i32, c_i32, c_i32, c_u64, c_vp, c_i64]
+                              + [c_vp] * 10 + [c_vp]),
     "mh_msacl_q_target": (ctypes.c_int, [c_vp] * 9 + [c_f32, c_i32, c_i32] + [c_vp] * 5 + [c_vp]),
     "mh_msacl_q_target_stats": (ctypes.c_int, [c_vp] * 9 + [c_f32, c_i32, c_i32] + [c_vp] * 6 + [c_vp]),
     "mh_msacl_tb_pack": (ctypes.c_int, [c_vp] * 7 + [c_vp]),
+    "mh_msacl_tb_pack_ring": (ctypes.c_int, [c_vp] * 8 + [c_i32, c_vp]),
     "mh_msacl_lyapunov": (ctypes.c_int, [c_vp] * 9 + [c_f32] * 4 + [c_i32] * 3 + [c_vp] * 6 + [c_vp]),
     "mh_msacl_stability_adv": (ctypes.c_int, [c_vp] * 4 + [c_i32, c_i32, c_vp, c_vp, c_vp]),
     "mh_msacl_ppo_clip": (ctypes.c_int, [c_vp, c_vp, c_vp, c_f64, c_f32, c_i32, c_vp, c_vp, c_vp, c_vp]),

@@ -103,6 +103,9 @@ def _stacked(a, b):
     return torch.cat([a, b], 0)
 
 
+_TB_SLOTS = 256  # policy updates a tb dict stays readable for (the device ring of logged scalars)
+
+
 class LazyTbInfo(Mapping):
     """model_update's tb dict (msacl.py:211-222) over a device tensor of its seven scalars: the
     values are read back (one transfer, a host sync) on first access, alg_time then being the
@@ -112,12 +115,17 @@ class LazyTbInfo(Mapping):
     KEYS = ("MSACL/entropy-RL iter", "MSACL/alpha-RL iter", "MSACL/q1_mean-RL iter", "MSACL/q2_mean-RL iter",
             tb_tags["loss_critic"], tb_tags["loss_lyapunov"], tb_tags["loss_actor"])
 
-    def __init__(self, vals: torch.Tensor, start: float):
-        self._vals, self._start, self._d = vals, start, None
+    def __init__(self, vals: torch.Tensor, start: float, gen=None):
+        self._vals, self._start, self._d, self._gen = vals, start, None, gen
 
     def _dict(self):
         if self._d is None:
-            v = self._vals.tolist()
+            h = self._vals.cpu()
+            if self._gen is not None:  # a ring slot (MSACL._tb_pack): it must still hold this update
+                tag = int(h.view(torch.int32)[7]) & 0xFFFFFFFF
+                if tag != self._gen & 0xFFFFFFFF:
+                    raise RuntimeError(f"MSACL tb dict read after {_TB_SLOTS} later policy updates reused its slot")
+            v = h[:7].tolist()
             self._d = dict(zip(self.KEYS, v))
             self._d[tb_tags["alg_time"]] = (time.time() - self._start) * 1000
             self._vals = None
@@ -375,6 +383,11 @@ class MSACL:
         self._static_shapes = None
         self._graphs = {}
         self._warm = set()
+        # the logged scalars of each policy update land in a device ring (mh_msacl_tb_pack_ring)
+        # keyed by a device generation counter that the host mirrors (_tb_gen)
+        self._tb_ring = None
+        self._tb_ctr = None
+        self._tb_gen = 0
 
     def close(self):
         """Release the captured update graphs, their static inputs, the scratch buffers and the
@@ -507,13 +520,36 @@ class MSACL:
             outs = self._graph_update(data, flags)
         else:
             outs = self._update_body(data, *flags)
+        return self._update_result(outs, flags, data, start)
+
+    def model_update_drawn(self, draw, global_iteration: int):
+        """model_update with the replay draw inside the replayed update: `draw(out)` gathers the
+        next batch into the static inputs `out` (DeviceNstepReplayBuffer.sample_batch(B, out=out):
+        one launch keyed by the buffer's device draw counter), and runs as the first node of the
+        captured graph instead of as separate launches before it. Only valid once replay_inputs()
+        returns the static inputs (the trainer checks); same batches, same results as
+        model_update(buffer.sample_batch(B, out=replay_inputs(B))) in the same order."""
+        start = time.time()
+        if self.anneal_lr or self._static is None:
+            raise RuntimeError("model_update_drawn needs the replayed update's static inputs (replay_inputs)")
+        flags = (global_iteration % self.target_network_frequency == 0, global_iteration % self.policy_frequency == 0)
+        outs = self._graph_update(None, flags, draw=draw)
+        return self._update_result(outs, flags, self._static, start)
+
+    def _update_result(self, outs, flags, data, start):
         tb_info = None
         if flags[1]:
             # the logged scalars (msacl.py:211-222), stacked on the device inside the update and
             # snapshotted here (the next replay overwrites the graph's output); read back only when
             # the caller reads the dict (the trainer: on logging iterations), so an update leaves
             # no host sync behind and the next sampling is enqueued while it still runs
-            tb_info = LazyTbInfo(outs[-1].clone(), start)
+            tb = outs[-1]
+            if tb is self._tb_ring:  # this update's slot of the ring (no copy out of the graph)
+                gen = self._tb_gen
+                self._tb_gen += 1
+                tb_info = LazyTbInfo(tb[gen % _TB_SLOTS], start, gen)
+            else:
+                tb_info = LazyTbInfo(tb.clone(), start)
         if self.per_flag:
             return tb_info, data.get("idx"), self.last_priority
         return tb_info
@@ -633,10 +669,13 @@ class MSACL:
         parts = (entropy, loss_q, loss_lya, loss_policy)
         if (self.device.type == "cuda" and q2_mean.data_ptr() == q1_mean.data_ptr() + 4
                 and all(t.numel() == 1 and t.dtype == torch.float32 for t in parts)):
-            tb = torch.empty(7, dtype=torch.float32, device=self.device)
-            _engine("msacl_tb_pack", self.device, N.ptr(entropy), N.ptr(la), N.ptr(q1_mean), N.ptr(loss_q),
-                    N.ptr(loss_lya), N.ptr(loss_policy), N.ptr(tb))
-            return tb
+            if self._tb_ring is None:  # (first policy update: eager, before any capture)
+                self._tb_ring = torch.zeros(_TB_SLOTS, 8, dtype=torch.float32, device=self.device)
+                self._tb_ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
+                self._tb_gen = 0
+            _engine("msacl_tb_pack_ring", self.device, N.ptr(entropy), N.ptr(la), N.ptr(q1_mean), N.ptr(loss_q),
+                    N.ptr(loss_lya), N.ptr(loss_policy), N.ptr(self._tb_ring), N.ptr(self._tb_ctr), _TB_SLOTS)
+            return self._tb_ring
         return torch.stack([entropy, la.exp(), q1_mean, q2_mean, loss_q, loss_lya, loss_policy])
 
     # ------------------------------------------------------------------ HIP-graph replay
@@ -659,11 +698,16 @@ class MSACL:
             return None
         return st
 
-    def _graph_update(self, data, flags):
+    def _graph_update(self, data, flags, draw=None):
         """Replay the whole update (~250 launches) as one HIP graph (with data parallelism: a
         chain of graphs cut at the gradient all-reduces, utils/dist.py GraphSegments). The first
         call per branch (even/odd iteration) runs eagerly on the static inputs (lazy BLAS / Adam
-        state init), the second captures, later calls only copy the new batch in and replay."""
+        state init), the second captures, later calls only copy the new batch in and replay.
+        draw (model_update_drawn): the batch is gathered into the static inputs by draw(static),
+        eagerly or as part of the capture, instead of being passed in."""
+        if draw is not None:  # (its own graphs: a replay must draw exactly when its capture did)
+            return self._graph_run(flags + ("drawn",),
+                                   lambda: (draw(self._static), self._update_body(self._static, *flags))[1])
         shapes = tuple((k, tuple(v.shape)) for k, v in sorted(data.items()) if torch.is_tensor(v))
         if self._static is None or self._static_shapes != shapes:
             self._static = {k: v.clone() for k, v in data.items() if torch.is_tensor(v)}
@@ -681,22 +725,26 @@ class MSACL:
         for k, v in self._static.items():
             if data[k].data_ptr() != v.data_ptr():
                 v.copy_(data[k])
-        if flags not in self._warm:
-            self._warm.add(flags)
-            return self._update_body(self._static, *flags)
-        if flags not in self._graphs:
+        return self._graph_run(flags, lambda: self._update_body(self._static, *flags))
+
+    def _graph_run(self, key, body):
+        """body() eagerly on the branch's first call, captured on its second, replayed after."""
+        if key not in self._warm:
+            self._warm.add(key)
+            return body()
+        if key not in self._graphs:
             if self._segmented():
                 g = D.GraphSegments()
                 with D.capturing(g):
-                    outs = self._update_body(self._static, *flags)
+                    outs = body()
                     prio = self.last_priority
             else:
                 g = torch.cuda.CUDAGraph()
                 with D.cuda_graph(g):
-                    outs = self._update_body(self._static, *flags)
+                    outs = body()
                     prio = self.last_priority
-            self._graphs[flags] = (g, outs, prio)
-        g, outs, prio = self._graphs[flags]
+            self._graphs[key] = (g, outs, prio)
+        g, outs, prio = self._graphs[key]
         g.replay()
         self.last_priority = prio
         return outs

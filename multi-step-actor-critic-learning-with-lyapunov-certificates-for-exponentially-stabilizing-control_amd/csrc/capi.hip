@@ -1482,4 +1482,37 @@ int mh_replay_sample_indices(const mh_window_store_t* store, uint64_t seed, uint
   return MH_OK;
 }
 
+int mh_replay_sample_indices_dev(const mh_window_store_t* store, uint64_t seed, int64_t* draw_state, int64_t batch,
+                                 int64_t* idx_out, void* stream) {
+  if (!store || !store->cursor || !draw_state || !idx_out)
+    return fail(MH_EINVAL, "mh_replay_sample_indices_dev: null arg");
+  MH_HIP(mh::launch_sample_idx_dev(store->cursor, seed, draw_state, batch, idx_out, (hipStream_t)stream));
+  return MH_OK;
+}
+
+int mh_replay_draw_gather(const mh_window_store_t* store, int32_t n_step, int32_t obs_dim, int32_t act_dim,
+                          uint64_t seed, int64_t* draw_state, int64_t batch, int64_t* idx_out, float* out_obs,
+                          float* out_act, float* out_rew, float* out_cost, float* out_obs2, float* out_done,
+                          float* out_logp, float* out_obs_act, float* out_v_in, void* stream) {
+  if (!store || !store->cursor || !draw_state) return fail(MH_EINVAL, "mh_replay_draw_gather: null store/state");
+  if (batch <= 0) return fail(MH_EINVAL, "mh_replay_draw_gather: batch must be positive");
+  mh::GatherArgs g;
+  g.idx = nullptr;
+  g.batch = batch;
+  g.n = n_step;
+  g.D = obs_dim;
+  g.A = act_dim;
+  g.s_obs = store->obs; g.s_act = store->act; g.s_rew = store->rew; g.s_cost = store->cost;
+  g.s_obs2 = store->obs2; g.s_done = store->done; g.s_logp = store->logp;
+  g.o_obs = out_obs; g.o_act = out_act; g.o_rew = out_rew; g.o_cost = out_cost;
+  g.o_obs2 = out_obs2; g.o_done = out_done; g.o_logp = out_logp;
+  g.o_obs_act = out_obs_act; g.o_v_in = out_v_in;
+  g.cursor = store->cursor;
+  g.seed = seed;
+  g.draw = draw_state;
+  g.idx_out = idx_out;
+  MH_HIP(mh::launch_gather(g, (hipStream_t)stream));
+  return MH_OK;
+}
+
 }  // extern "C"

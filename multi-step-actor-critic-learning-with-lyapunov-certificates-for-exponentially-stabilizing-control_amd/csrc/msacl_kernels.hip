@@ -530,6 +530,26 @@ __global__ void k_tb_pack(const float* entropy, const float* log_alpha, const fl
   out[6] = loss_policy[0];
 }
 
+// the same seven scalars into slot ctr % slots of a ring [slots][8] (element 7: the low 32 bits of
+// the generation ctr, as float bits), ctr advanced: a replayed graph's logged values stay readable
+// until `slots` later updates without a copy out of the graph's output
+__global__ void k_tb_pack_ring(const float* entropy, const float* log_alpha, const float* q_means,
+                               const float* loss_q, const float* loss_lya, const float* loss_policy, float* ring,
+                               int64_t* ctr, int slots) {
+  if (threadIdx.x != 0) return;
+  const int64_t gen = ctr[0];
+  float* out = ring + (gen % slots) * 8;
+  out[0] = entropy[0];
+  out[1] = expf(log_alpha[0]);
+  out[2] = q_means[0];
+  out[3] = q_means[1];
+  out[4] = loss_q[0];
+  out[5] = loss_lya[0];
+  out[6] = loss_policy[0];
+  out[7] = __uint_as_float((uint32_t)(uint64_t)gen);
+  ctr[0] = gen + 1;
+}
+
 thread_local std::string g_merr;
 
 }  // namespace
@@ -564,6 +584,17 @@ int mh_msacl_q_target(const float* q1, const float* q2, const float* q1t, const 
                       float* dq2, float* loss_out, float* abs_td, void* stream) {
   return mh_msacl_q_target_stats(q1, q2, q1t, q2t, next_logp, rew, done, log_alpha, weight, gamma, B, n, backup,
                                  dq1, dq2, loss_out, abs_td, nullptr, stream);
+}
+
+int mh_msacl_tb_pack_ring(const float* entropy, const float* log_alpha, const float* q_means, const float* loss_q,
+                          const float* loss_lya, const float* loss_policy, float* ring, int64_t* ctr, int32_t slots,
+                          void* stream) {
+  if (!entropy || !log_alpha || !q_means || !loss_q || !loss_lya || !loss_policy || !ring || !ctr || slots <= 0)
+    return MH_EINVAL;
+  k_tb_pack_ring<<<1, 64, 0, (hipStream_t)stream>>>(entropy, log_alpha, q_means, loss_q, loss_lya, loss_policy, ring,
+                                                    ctr, slots);
+  MH_CHECK_LAUNCH("tb_pack_ring");
+  return MH_OK;
 }
 
 int mh_msacl_tb_pack(const float* entropy, const float* log_alpha, const float* q_means, const float* loss_q,

@@ -106,6 +106,13 @@ struct GatherArgs {
   // rows (the critics' input), o_v_in [batch + batch n][D] = obs(b, 0) rows then the obs2 rows (the
   // Lyapunov network's batch of the stability advantage)
   float *o_obs_act, *o_v_in;
+  // in-kernel draw (draw != null: idx is ignored): idx[b] = the (seed, b, draw[0]) index into the
+  // store's [0, cursor[1]) windows, written to idx_out (nullable); the last workgroup to finish
+  // advances draw[0] (draw[1] is its arrival ticket, 0 between launches)
+  const int64_t* cursor = nullptr;
+  uint64_t seed = 0;
+  int64_t* draw = nullptr;
+  int64_t* idx_out = nullptr;
 };
 
 hipError_t launch_rollout(int env_id, const StepArgs& a, hipStream_t st);
@@ -262,6 +269,8 @@ hipError_t launch_emit(const EmitArgs& a, hipStream_t st);
 hipError_t launch_gather(const GatherArgs& a, hipStream_t st);
 hipError_t launch_sample_idx(const int64_t* cursor, uint64_t seed, uint64_t counter, int64_t batch,
                              int64_t* idx, hipStream_t st);
+hipError_t launch_sample_idx_dev(const int64_t* cursor, uint64_t seed, int64_t* draw, int64_t batch, int64_t* idx,
+                                 hipStream_t st);
 hipError_t launch_transpose_f32(const float* src, float* dst, int W, int64_t E, bool to_aos, hipStream_t st);
 hipError_t launch_transpose_f64(const double* src, double* dst, int W, int64_t E, bool to_aos, hipStream_t st);
 

@@ -805,29 +805,70 @@ __global__ __launch_bounds__(256) void k_emit_fused(EmitArgs a) {
 }
 
 // --------------------------------------------------------------- replay gather / indices
+// The replay draw (np.random.randint at nstep_replay_buffer.py:138): window b of draw `counter`
+// is the (seed, b, counter) Philox draw modulo the store's window count.
+__device__ __forceinline__ int64_t draw_index(uint64_t seed, int64_t b, uint64_t counter, int64_t size) {
+  const Rng r = make_rng(seed, (uint64_t)b, counter);
+  const u32x4 q = r.draw(7);
+  const uint64_t v = ((uint64_t)q.x << 32) | q.y;
+  return size > 0 ? (int64_t)(v % (uint64_t)size) : 0;
+}
+
+// the window index of batch row b: the caller's idx, or the in-kernel draw (cached per thread: a
+// thread's grid-stride elements change row rarely)
+struct RowIndex {
+  const int64_t* idx;
+  uint64_t seed, counter;
+  int64_t size, last_b = -1, last = 0;
+  __device__ int64_t operator()(int64_t b) {
+    if (idx) return idx[b];
+    if (b != last_b) {
+      last = draw_index(seed, b, counter, size);
+      last_b = b;
+    }
+    return last;
+  }
+};
+
+// Last-workgroup arrival of an in-kernel draw: advances the counter once every workgroup has
+// READ it. Each thread's counter read was consumed (into its RowIndex) before the barrier, and
+// thread 0 arrives after the barrier; no data is handed between workgroups, so a relaxed arrival
+// suffices (the same argument as k_adam_multi's step counter, optim.hip). The next launch reads
+// the new counter across the kernel boundary.
+__device__ __forceinline__ void draw_arrive(int64_t* draw, uint64_t counter, unsigned int total) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned int* ticket = reinterpret_cast<unsigned int*>(draw + 1);
+    const unsigned int done = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == total - 1u) {
+      draw[0] = (int64_t)(counter + 1);
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // Replay gather: blockIdx.y selects one of the 7 arrays; each thread copies 16-B vectors of
 // the sampled rows (a row of one array is n * width contiguous floats), grid-stride over
 // batch x row-vectors, so every lane moves useful bytes regardless of the field width.
 template <typename V>
-__device__ __forceinline__ void gather_rows(const float* src, float* dst, const int64_t* idx, int64_t batch,
-                                            int64_t len) {
+__device__ __forceinline__ void gather_rows(const float* src, float* dst, RowIndex& ix, int64_t batch, int64_t len) {
   const int64_t v = len * (int64_t)sizeof(float) / (int64_t)sizeof(V);
   const V* s = reinterpret_cast<const V*>(src);
   V* d = reinterpret_cast<V*>(dst);
   const int64_t total = batch * v;
   for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
     const int64_t b = q / v, i = q - b * v;
-    d[q] = s[idx[b] * v + i];
+    d[q] = s[ix(b) * v + i];
   }
 }
 
 // the joint layouts: element-wise (D + A and D are small), rows of the windows at idx
-__device__ __forceinline__ void gather_joint(const GatherArgs& a) {
+__device__ __forceinline__ void gather_joint(const GatherArgs& a, RowIndex& ix) {
   const int64_t n = a.n, D = a.D, A = a.A;
   if (blockIdx.y == 7) {
     const int64_t W = D + A, total = a.batch * n * W;
     for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
-      const int64_t row = q / W, c = q - row * W, b = row / n, t = row - b * n, w = a.idx[b];
+      const int64_t row = q / W, c = q - row * W, b = row / n, t = row - b * n, w = ix(b);
       a.o_obs_act[q] = c < D ? a.s_obs[(w * n + t) * D + c] : a.s_act[(w * n + t) * A + (c - D)];
     }
   } else {
@@ -835,18 +876,18 @@ __device__ __forceinline__ void gather_joint(const GatherArgs& a) {
     for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
       const int64_t row = q / D, c = q - row * D;
       if (row < a.batch) {
-        a.o_v_in[q] = a.s_obs[(a.idx[row] * n) * D + c];
+        a.o_v_in[q] = a.s_obs[(ix(row) * n) * D + c];
       } else {
         const int64_t r = row - a.batch, b = r / n, t = r - b * n;
-        a.o_v_in[q] = a.s_obs2[(a.idx[b] * n + t) * D + c];
+        a.o_v_in[q] = a.s_obs2[(ix(b) * n + t) * D + c];
       }
     }
   }
 }
 
-__global__ __launch_bounds__(256) void k_gather(GatherArgs a) {
+__device__ __forceinline__ void gather_body(const GatherArgs& a, RowIndex& ix) {
   if (blockIdx.y >= 7) {
-    if ((blockIdx.y == 7 && a.o_obs_act) || (blockIdx.y == 8 && a.o_v_in)) gather_joint(a);
+    if ((blockIdx.y == 7 && a.o_obs_act) || (blockIdx.y == 8 && a.o_v_in)) gather_joint(a, ix);
     return;
   }
   const float* src;
@@ -861,25 +902,54 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs a) {
     case 5: src = a.s_done; dst = a.o_done; w = 1; break;
     default: src = a.s_logp; dst = a.o_logp; w = 1; break;
   }
+  if (blockIdx.y == 0 && a.idx_out) {  // the drawn indices (one writer per row)
+    for (int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x; b < a.batch; b += (int64_t)gridDim.x * 256)
+      a.idx_out[b] = ix(b);
+  }
   if (!dst) return;
   const int64_t len = (int64_t)a.n * w;
   if (len % 4 == 0)
-    gather_rows<float4>(src, dst, a.idx, a.batch, len);
+    gather_rows<float4>(src, dst, ix, a.batch, len);
   else if (len % 2 == 0)
-    gather_rows<float2>(src, dst, a.idx, a.batch, len);
+    gather_rows<float2>(src, dst, ix, a.batch, len);
   else
-    gather_rows<float>(src, dst, a.idx, a.batch, len);
+    gather_rows<float>(src, dst, ix, a.batch, len);
+}
+
+constexpr int GATHER_LDS_ROWS = 2048;  // in-kernel draws of batches up to this size go through LDS
+
+__global__ __launch_bounds__(256) void k_gather(GatherArgs a) {
+  __shared__ int64_t sidx[GATHER_LDS_ROWS];
+  RowIndex ix;
+  ix.idx = a.draw ? nullptr : a.idx;
+  ix.seed = a.seed;
+  ix.counter = a.draw ? (uint64_t)a.draw[0] : 0u;
+  ix.size = a.draw ? a.cursor[1] : 0;
+  if (a.draw && a.batch <= GATHER_LDS_ROWS) {
+    // every workgroup draws the whole batch once (one Philox draw per row) into LDS: the copy
+    // loops then read indices like the caller-supplied path
+    for (int b = threadIdx.x; b < a.batch; b += 256) sidx[b] = draw_index(ix.seed, b, ix.counter, ix.size);
+    __syncthreads();
+    ix.idx = sidx;
+  }
+  gather_body(a, ix);
+  if (a.draw) draw_arrive(a.draw, ix.counter, gridDim.x * gridDim.y);
 }
 
 __global__ __launch_bounds__(256) void k_sample_idx(const int64_t* cursor, uint64_t seed, uint64_t counter,
                                                    int64_t batch, int64_t* idx) {
   const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (b >= batch) return;
-  const int64_t size = cursor[1];
-  const Rng r = make_rng(seed, (uint64_t)b, counter);
-  const u32x4 q = r.draw(7);
-  const uint64_t v = ((uint64_t)q.x << 32) | q.y;
-  idx[b] = size > 0 ? (int64_t)(v % (uint64_t)size) : 0;
+  idx[b] = draw_index(seed, b, counter, cursor[1]);
+}
+
+// the same draw keyed by the device counter draw[0], advanced by the launch
+__global__ __launch_bounds__(256) void k_sample_idx_dev(const int64_t* cursor, uint64_t seed, int64_t* draw,
+                                                       int64_t batch, int64_t* idx) {
+  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t counter = (uint64_t)draw[0];
+  if (b < batch) idx[b] = draw_index(seed, b, counter, cursor[1]);
+  draw_arrive(draw, counter, gridDim.x);
 }
 
 // --------------------------------------------------------------- state transposes
@@ -991,6 +1061,12 @@ hipError_t launch_sample_idx(const int64_t* cursor, uint64_t seed, uint64_t coun
                              int64_t* idx, hipStream_t st) {
   if (batch <= 0) return hipSuccess;
   k_sample_idx<<<(int)((batch + 255) / 256), 256, 0, st>>>(cursor, seed, counter, batch, idx);
+  return hipGetLastError();
+}
+hipError_t launch_sample_idx_dev(const int64_t* cursor, uint64_t seed, int64_t* draw, int64_t batch, int64_t* idx,
+                                 hipStream_t st) {
+  if (batch <= 0) return hipSuccess;
+  k_sample_idx_dev<<<(int)((batch + 255) / 256), 256, 0, st>>>(cursor, seed, draw, batch, idx);
   return hipGetLastError();
 }
 hipError_t launch_transpose_f32(const float* src, float* dst, int W, int64_t E, bool to_aos, hipStream_t st) {

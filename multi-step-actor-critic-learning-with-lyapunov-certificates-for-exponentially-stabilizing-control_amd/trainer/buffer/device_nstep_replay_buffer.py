@@ -61,8 +61,17 @@ class DeviceNstepReplayBuffer:
         self.cursor = torch.zeros(4, dtype=torch.int64, device=self.device)  # ptr, size, total, last
         self.ws = N.WindowStore(*[ctypes.c_void_p(self.n_step_buf[k].data_ptr()) for k in KEYS],
                                 M, ctypes.c_void_p(self.cursor.data_ptr()))
-        self._draws = 0
+        # the replay draw counter lives on the device ([counter, arrival ticket]): a draw can then
+        # be captured in the update's graph and replayed (mh_replay_draw_gather)
+        self._draw_state = torch.zeros(2, dtype=torch.int64, device=self.device)
         self._idx = None
+
+    graph_draw = True  # sample_batch(B, out=...) is one capturable launch (the trainer's drawn update)
+
+    @property
+    def draws(self):
+        """Replay draws made so far (reads the device counter: a host sync)."""
+        return int(self._draw_state[0].item())
 
     # ------------------------------------------------------------------ size / memory
     @property
@@ -135,9 +144,9 @@ class DeviceNstepReplayBuffer:
     # ------------------------------------------------------------------ reads
     def sample_indices(self, batch_size):
         idx = torch.empty(batch_size, dtype=torch.int64, device=self.device)
-        N.check(N.lib().mh_replay_sample_indices(ctypes.byref(self.ws), self.seed, self._draws, batch_size,
-                                                 N.ptr(idx), N.stream_of(self.device)), "mh_replay_sample_indices")
-        self._draws += 1
+        N.check(N.lib().mh_replay_sample_indices_dev(ctypes.byref(self.ws), self.seed, N.ptr(self._draw_state),
+                                                     batch_size, N.ptr(idx), N.stream_of(self.device)),
+                "mh_replay_sample_indices_dev")
         return idx
 
     def _fits(self, out, B):
@@ -165,6 +174,17 @@ class DeviceNstepReplayBuffer:
         otherwise into fresh tensors. joint (or `out` holding them): also the update's joint
         layouts "obs_act" = [obs | act] and "v_in" = [obs[:, 0]; obs2 rows] (mh_replay_gather_joint)."""
         B = int(idx.numel())
+        dst = self._destinations(B, out, joint)
+        n, D, A = self.n_step, self.obsv_dim, self.act_dim
+        idx = idx.to(self.device, torch.int64).contiguous()
+        N.check(N.lib().mh_replay_gather_joint(ctypes.byref(self.ws), n, D, A, N.ptr(idx), B,
+                                               *[N.ptr(dst[k]) for k in KEYS], N.ptr(dst.get("obs_act")),
+                                               N.ptr(dst.get("v_in")), N.stream_of(self.device)),
+                "mh_replay_gather_joint")
+        return dst
+
+    def _destinations(self, B, out, joint):
+        """The gather's destination tensors: `out`'s when it fits, fresh ones otherwise."""
         n, D, A = self.n_step, self.obsv_dim, self.act_dim
         e = lambda *s: torch.empty(*s, dtype=torch.float32, device=self.device)  # noqa: E731
         js = self._joint_shapes(B)
@@ -180,17 +200,18 @@ class DeviceNstepReplayBuffer:
                    "done": e(B, n), "logp": e(B, n)}
             if joint:
                 dst.update({k: e(*shp) for k, shp in js.items()})
-        idx = idx.to(self.device, torch.int64).contiguous()
-        N.check(N.lib().mh_replay_gather_joint(ctypes.byref(self.ws), n, D, A, N.ptr(idx), B,
-                                               *[N.ptr(dst[k]) for k in KEYS], N.ptr(dst.get("obs_act")),
-                                               N.ptr(dst.get("v_in")), N.stream_of(self.device)),
-                "mh_replay_gather_joint")
         return dst
 
     def sample_batch(self, batch_size: int, out=None, joint=False) -> dict:
         """nstep_replay_buffer.py:136-148. `out` (optional): destination tensors (gather); joint:
         add the update's joint layouts (gather)."""
-        idx = self.sample_indices(batch_size)
         if out is None and not joint:
-            return self.gather(idx)  # (the 1-step ReplayBuffer's gather takes idx only)
-        return self.gather(idx, out, joint)
+            return self.gather(self.sample_indices(batch_size))  # (the 1-step ReplayBuffer's gather takes idx only)
+        # the draw and the gather in one launch (the draw counter advanced on the device)
+        dst = self._destinations(batch_size, out, joint)
+        n, D, A = self.n_step, self.obsv_dim, self.act_dim
+        N.check(N.lib().mh_replay_draw_gather(ctypes.byref(self.ws), n, D, A, self.seed, N.ptr(self._draw_state),
+                                              batch_size, None, *[N.ptr(dst[k]) for k in KEYS],
+                                              N.ptr(dst.get("obs_act")), N.ptr(dst.get("v_in")),
+                                              N.stream_of(self.device)), "mh_replay_draw_gather")
+        return dst

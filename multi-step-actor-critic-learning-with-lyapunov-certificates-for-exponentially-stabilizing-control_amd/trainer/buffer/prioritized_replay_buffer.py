@@ -15,6 +15,8 @@ from .device_nstep_replay_buffer import DeviceNstepReplayBuffer
 
 
 class PrioritizedReplayBuffer(DeviceNstepReplayBuffer):
+    graph_draw = False  # the proportional draw (host draw counter) and the tree stay outside the graph
+
     def __init__(self, **kwargs):
         super().__init__(**kwargs)
         self.alpha = float(kwargs.get("per_alpha", 0.6))

@@ -19,6 +19,8 @@ __all__ = ["ReplayBuffer"]
 
 
 class ReplayBuffer(DeviceNstepReplayBuffer):
+    graph_draw = False  # 1-step transitions: the trainers draw and gather eagerly
+
     def __init__(self, **kwargs):
         kw = dict(kwargs)
         kw["n_step"] = 1

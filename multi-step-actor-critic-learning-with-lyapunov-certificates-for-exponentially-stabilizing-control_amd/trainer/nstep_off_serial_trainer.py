@@ -95,6 +95,27 @@ class NstepOffSerialTrainer:
             return self.buffer.sample_batch(self.replay_batch_size, joint=True)
         return self.buffer.sample_batch(self.replay_batch_size)
 
+    def _drawn_update(self):
+        """The replay draw runs inside the algorithm's replayed update (the buffer's one-launch
+        draw + gather captured as the graph's first node): graph replay under way, a plain
+        device buffer (its draw counter on the device), no PER, no overlapped sampling (that
+        orders the next sampling after an eager gather)."""
+        return (not self.per_flag and not self._overlap_next() and getattr(self.buffer, "graph_draw", False)
+                and hasattr(self.alg, "model_update_drawn")
+                and self.alg.replay_inputs(self.replay_batch_size) is not None)
+
+    def _update(self, replay_samples):
+        """alg.model_update on the drawn batch, or with the draw inside the replay (None)."""
+        if replay_samples is None:
+            B, buf = self.replay_batch_size, self.buffer
+            return self.alg.model_update_drawn(lambda out: buf.sample_batch(B, out=out), self.iteration)
+        return self.alg.model_update(replay_samples, self.iteration)
+
+    def replay_and_update(self):
+        """The replay draw and the update of one step (step()'s middle part, for measurements)."""
+        rs = None if self._drawn_update() else self._replay_batch()
+        return self._update(rs)
+
     def _overlap_next(self):
         """Sampling of iteration + 1 may run beside this iteration's update."""
         return (self.overlap and self.iteration % self.policy_frequency != 0
@@ -110,7 +131,7 @@ class NstepOffSerialTrainer:
                 sampler_samples, sampler_tb_dict = self._sample()
             self.buffer.add_batch(sampler_samples)
             self.sampler_tb_dict.add_average(sampler_tb_dict)
-        replay_samples = self._replay_batch()
+        replay_samples = None if self._drawn_update() else self._replay_batch()
         if self._overlap_next():
             if self._side is None:
                 self._side = torch.cuda.Stream(device=torch.device(self.sample_device))
@@ -125,12 +146,12 @@ class NstepOffSerialTrainer:
             if alg_tb_dict is not None and self.iteration % self.log_save_interval == 0 and self.is_main:
                 add_scalars(alg_tb_dict, self.writer, step=self.iteration)
         elif self.iteration % self.policy_frequency == 0:
-            alg_tb_dict = self.alg.model_update(replay_samples, self.iteration)
+            alg_tb_dict = self._update(replay_samples)
             if self.iteration % self.log_save_interval == 0 and self.is_main:
                 print("Iter = ", self.iteration, "save training data!")
                 add_scalars(alg_tb_dict, self.writer, step=self.iteration)
         else:
-            self.alg.model_update(replay_samples, self.iteration)
+            self._update(replay_samples)
         self.networks.eval()
         if self.iteration % self.log_save_interval == 0:
             check = getattr(self.sampler, "check_errors", None)  # device sampler health (every rank)

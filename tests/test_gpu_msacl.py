@@ -49,6 +49,52 @@ def test_q_target_kernel(B, n, weighted):
     np.testing.assert_allclose(out[4].cpu().numpy(), td, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("B,n", [(256, 20), (7, 70)])
+def test_q_target_stats_kernel(B, n):
+    """mh_msacl_q_target_stats: the same backup / gradients / loss bits as mh_msacl_q_target, plus
+    the logged critic means (msacl.py:211-222) from the same float64 reduction (rtol 1e-6 vs numpy
+    float64 means rounded to float32)."""
+    rng = np.random.default_rng(B * n)
+    f = lambda *s: rng.standard_normal(s).astype(np.float32)  # noqa: E731
+    q1, q2, q1t, q2t, nlp, rew = f(B, n) + 3, f(B, n) - 1, f(B, n), f(B, n), f(B, n), f(B, n)
+    done = (rng.uniform(size=(B, n)) < 0.1).astype(np.float32)
+    ins = [N.ptr(dev(a)) for a in (q1, q2, q1t, q2t, nlp, rew, done)] + [N.ptr(dev([np.float32(0.3)])), None]
+    outs = [[torch.empty(B, n, device="cuda") for _ in range(3)] + [torch.empty(1, device="cuda"),
+                                                                   torch.empty(B, device="cuda")] for _ in range(2)]
+    means = torch.full((2,), float("nan"), device="cuda")
+    N.check(N.lib().mh_msacl_q_target(*ins, 0.99, B, n, *[N.ptr(o) for o in outs[0]], N.stream_of()), "q")
+    N.check(N.lib().mh_msacl_q_target_stats(*ins, 0.99, B, n, *[N.ptr(o) for o in outs[1]], N.ptr(means),
+                                            N.stream_of()), "q stats")
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    np.testing.assert_allclose(means.cpu().numpy(), [np.float32(q1.astype(np.float64).mean()),
+                                                     np.float32(q2.astype(np.float64).mean())], rtol=1e-6)
+
+
+def test_tb_ring_slots(monkeypatch):
+    """The policy updates' logged scalars go to a device ring (mh_msacl_tb_pack_ring, no copy out
+    of the replayed graph): a tb dict read within the ring's depth equals the eager update's, and
+    one read after its slot was reused raises instead of returning another update's values."""
+    import msacl_amd.algorithm.msacl as M
+    monkeypatch.setattr(M, "_TB_SLOTS", 2)
+    g = np.load(os.path.join(G, "msacl_update.npz"))
+    B, n = int(g["cfg_B"]), int(g["cfg_n"])
+    data = {k: torch.as_tensor(g["in_" + k], device="cuda") for k in ("obs", "act", "rew", "cost", "obs2", "done", "logp")}
+    tbs = {}
+    for mode in (True, False):
+        torch.manual_seed(0)
+        alg = M.MSACL(**_msacl_kwargs(B, n), alg_use_graph=mode)
+        alg.networks.load_state_dict({k[5:]: torch.as_tensor(g[k]) for k in g.files if k.startswith("init/")})
+        tbs[mode] = [alg.model_update(data, it) for it in range(8)][::2]
+        assert alg._tb_ring.shape == (2, 8)
+    for mode in (True, False):
+        with pytest.raises(RuntimeError, match="reused its slot"):
+            tbs[mode][0]["Loss/Critic loss-RL iter"]
+    for k in tbs[False][-1]:
+        if "time" not in k.lower():
+            np.testing.assert_allclose(tbs[True][-1][k], tbs[False][-1][k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
 @pytest.mark.parametrize("B,n,D", [(256, 20, 12), (33, 5, 2), (5, 100, 6)])
 def test_lyapunov_kernel(B, n, D):
     rng = np.random.default_rng(B * n)

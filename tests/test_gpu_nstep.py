@@ -157,6 +157,48 @@ def test_replay_gather_joint_layouts():
     assert out["v_in"].shape == (6 + 6 * n, D)
 
 
+def test_device_draw_counter_and_one_launch_draw_gather():
+    """The replay draw keyed by the buffer's DEVICE counter (mh_replay_sample_indices_dev) equals
+    the host-counter entry at the same counters; the one-launch draw + gather
+    (mh_replay_draw_gather, sample_batch with out / joint) equals the draw followed by the gather,
+    bit for bit; and a captured draw + gather replays as the NEXT draw each time (the counter is
+    advanced inside the launch), which is what lets the trainer put it inside the update graph."""
+    import ctypes
+    import msacl_amd._native as N
+    path = os.path.join(G, "nstep_DuctedFan.npz")
+    g, buf, total, _ = _run_trace(path)
+    B = 300  # > 256: two workgroups share the counter's arrival ticket
+    st = N.stream_of(buf.device)
+
+    def host_draw(k):
+        ref = torch.empty(B, dtype=torch.int64, device="cuda")
+        N.check(N.lib().mh_replay_sample_indices(ctypes.byref(buf.ws), buf.seed, k, B, N.ptr(ref), st), "draw")
+        return ref
+    for k in range(3):
+        got = buf.sample_indices(B)
+        assert torch.equal(got, host_draw(k)), k
+    assert buf.draws == 3
+    ref = buf.gather(host_draw(3), joint=True)
+    got = buf.sample_batch(B, joint=True)
+    assert set(got) == set(ref)
+    for k in ref:
+        assert torch.equal(got[k], ref[k]), k
+    assert buf.draws == 4
+    static = {k: torch.full_like(v, float("nan")) for k, v in got.items()}
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        buf.sample_batch(B, out=static)
+    assert buf.draws == 4  # capture runs nothing
+    for k in (4, 5):
+        graph.replay()
+        ref = buf.gather(host_draw(k), joint=True)
+        for key in ref:
+            assert torch.equal(static[key], ref[key]), (k, key)
+        assert buf.draws == k + 1
+    del graph
+
+
 def n_of(g):
     return int(g["n_step"])
 
