@@ -23,7 +23,7 @@ sys.path.insert(0, ROOT)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PEAK_F32_MFMA_TFS = 157.3  # MI355X dense f32 matrix peak (v_mfma_f32_*_f32)
 PEAK_F16_MFMA_TFS = 2500.0  # MI355X dense f16 matrix peak (v_mfma_f32_32x32x16_f16), MI355X_MICROARCH.md
-PMC_TRAFFIC = "r04_pmc_traffic_v3.json"  # the PMC summary of the current kernels (tools/pmc.sh + tools/pmc_summary.py)
+PMC_TRAFFIC = "r05_pmc_traffic_v1.json"  # the PMC summary of the current kernels (tools/pmc.sh + tools/pmc_summary.py)
 
 
 def parse():
@@ -254,6 +254,7 @@ def main():
     # any diagnostic launch below moves the env state
     t_emit_h = windows_emit = None
     emit_extra_steps = 0
+    emit_seen, emit_seen_cursor = [], []
     if fused_h:
         win_dev = torch.zeros(1, dtype=torch.int64, device=dev)
 
@@ -268,11 +269,15 @@ def main():
         # a few more sampler steps (diagnostics, after the timed region) until one has more.
         k_emit_only()
         torch.cuda.synchronize()
-        while int(win_dev.item()) < a.envs * horizon // 100 and emit_extra_steps < 60:
+        emit_seen = [int(win_dev.item())]
+        while emit_seen[-1] < a.envs * horizon // 100 and emit_extra_steps < 60:
+            c_before = int(buffer.cursor[2].item())
             buffer.add_batch(sampler.sample()[0])
             emit_extra_steps += 1
             k_emit_only()
             torch.cuda.synchronize()
+            emit_seen.append(int(win_dev.item()))
+            emit_seen_cursor.append(int(buffer.cursor[2].item()) - c_before)
         t_emit_h = time_launches(k_emit_only, reps) * 1e-3
         windows_emit = int(win_dev.item())
 
@@ -339,6 +344,7 @@ def main():
                                    "GBps": round(bytes_win / t_emit_h / 1e9, 1),
                                    "frac": round(bytes_win / t_emit_h / 1e9 / PEAK_HBM_GBS, 4),
                                    "extra_sampler_steps": emit_extra_steps,
+                                   "windows_seen": emit_seen[:12], "windows_seen_cursor": emit_seen_cursor[:12],
                                    "note": "k_emit_cells alone (mh_sample_horizon_emit) on the last sampled horizon "
                                            "(the last trainer step's, or the first later one with >= 1 % of its "
                                            "env-steps as windows): its windows, ring records -> replay store rows"}
