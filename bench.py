@@ -147,6 +147,24 @@ def main():
 
     for _ in range(a.warmup):
         one_step()
+    # the horizon emission alone (k_emit_cells via mh_sample_horizon_emit) on the last warm-up
+    # step's horizon, before the timed region: it rewrites the same store rows (idempotent) and
+    # moves no env state, and the window count is then one of the trainer's own steps (after the
+    # timed region the init policy's episodes have mostly become short and horizons emit ~1 k)
+    from tools.gputime import time_launches
+    trainer.finish_pending()
+    emit_diag = None
+    if (hasattr(sampler, "_pack_policy") and getattr(sampler, "_fused_horizon_ok", None)
+            and sampler._fused_horizon_ok(bool(sampler._pack_policy()))):
+        h_e, st_e = sampler.envs.handle(), N.stream_of(dev)
+        win_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+
+        def k_emit_only():
+            N.check(N.lib().mh_sample_horizon_emit(h_e, sampler.horizon, ctypes.byref(buffer.ws), N.ptr(win_dev),
+                                                   st_e), "mh_sample_horizon_emit")
+        k_emit_only()
+        torch.cuda.synchronize()
+        emit_diag = (time_launches(k_emit_only, 20) * 1e-3, int(win_dev.item()))
     win0 = int(buffer.cursor[2].item())
     if world > 1:
         torch.distributed.barrier()
@@ -249,37 +267,7 @@ def main():
     H = sampler.horizon
     noise_ptr = N.ptr(sampler._noise) if getattr(sampler, "_noise", None) is not None else None
 
-    # the emission launch alone on the last trainer step's horizon (mh_sample_horizon_emit: it
-    # rewrites the same store rows, idempotent), i.e. at the trainer's own window count, before
-    # any diagnostic launch below moves the env state
-    t_emit_h = windows_emit = None
-    emit_extra_steps = 0
-    emit_seen, emit_seen_cursor = [], []
-    if fused_h:
-        win_dev = torch.zeros(1, dtype=torch.int64, device=dev)
-
-        def k_emit_only():
-            N.check(N.lib().mh_sample_horizon_emit(h, H, ctypes.byref(buffer.ws), N.ptr(win_dev), st),
-                    "mh_sample_horizon_emit")
-
-        # (the window count swings from horizon to horizon, 0 to ~1.3 M: the episodes of the init
-        # policy end together, and the hover policy's all reach the step limit in the same lockstep
-        # and emit nothing for n locksteps; the line reports the count this figure was taken at).
-        # A horizon with fewer than 1 % of its E x H env-steps as windows says nothing about HBM:
-        # a few more sampler steps (diagnostics, after the timed region) until one has more.
-        k_emit_only()
-        torch.cuda.synchronize()
-        emit_seen = [int(win_dev.item())]
-        while emit_seen[-1] < a.envs * horizon // 100 and emit_extra_steps < 60:
-            c_before = int(buffer.cursor[2].item())
-            buffer.add_batch(sampler.sample()[0])
-            emit_extra_steps += 1
-            k_emit_only()
-            torch.cuda.synchronize()
-            emit_seen.append(int(win_dev.item()))
-            emit_seen_cursor.append(int(buffer.cursor[2].item()) - c_before)
-        t_emit_h = time_launches(k_emit_only, reps) * 1e-3
-        windows_emit = int(win_dev.item())
+    t_emit_h, windows_emit = emit_diag if emit_diag is not None else (None, None)
 
     def k_fused():  # the fused horizon kernel alone (its windows are not emitted)
         N.lib().mh_sample_horizon(h, N.ptr(sampler._packed), sampler.envs.obs_dim, 2 * sampler.envs.act_dim,
@@ -332,7 +320,6 @@ def main():
         # per f32-equivalent product) beside the env step; HBM traffic per horizon: the ring
         # records and the per-horizon state / observation load + store (W2 is re-read from L2)
         bytes_fh = a.envs * (H * F * 4 + 2 * (S * 4 + XS * 8 + 16) + 2 * D_ * 4)
-        bytes_win = windows_emit * bytes_window
         kernels["sample_fused"] = {
             "avg_us_per_horizon": round(t_fh * 1e6, 2), "avg_us_per_lockstep": round(t_fh / H * 1e6, 3),
             "f16_mfma_TFLOPs": round(3 * flops_lockstep * H / t_fh / 1e12, 1),
@@ -340,14 +327,14 @@ def main():
             "hbm_bytes": bytes_fh, "GBps": round(bytes_fh / t_fh / 1e9, 1),
             "note": "k_sample_fused<Env>: the whole horizon (policy MLP + sample + env step + ring push for "
                     f"{H} locksteps) in one persistent launch, without its window emission"}
+    if fused_h and t_emit_h is not None:
+        bytes_win = windows_emit * bytes_window
         kernels["emit_horizon"] = {"avg_us": round(t_emit_h * 1e6, 2), "windows": windows_emit, "bytes": bytes_win,
                                    "GBps": round(bytes_win / t_emit_h / 1e9, 1),
                                    "frac": round(bytes_win / t_emit_h / 1e9 / PEAK_HBM_GBS, 4),
-                                   "extra_sampler_steps": emit_extra_steps,
-                                   "windows_seen": emit_seen[:12], "windows_seen_cursor": emit_seen_cursor[:12],
-                                   "note": "k_emit_cells alone (mh_sample_horizon_emit) on the last sampled horizon "
-                                           "(the last trainer step's, or the first later one with >= 1 % of its "
-                                           "env-steps as windows): its windows, ring records -> replay store rows"}
+                                   "note": "k_emit_cells alone (mh_sample_horizon_emit) on the last warm-up step's "
+                                           "horizon, before the timed region: its windows, ring records -> replay "
+                                           "store rows"}
     if t_pol is not None:
         flops = flops_lockstep
         # split-f16 arithmetic: every f32 product is 3 f16 MFMA products (hi.hi + hi.lo + lo.hi),
