@@ -934,6 +934,8 @@ int mh_head_backward(const float* dy, const float* x, const float* W, int64_t ro
   return MH_OK;
 }
 
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
 static int adam_multi_impl(const mh_adam_tensor_t* tensors, int32_t n, double lr, const double* lrs, double beta1,
                            double beta2, double eps, uint32_t* ticket, void* stream) {
   if (n < 0 || (n > 0 && (!tensors || !ticket))) return fail(MH_EINVAL, "mh_adam_multi: bad argument");
@@ -950,7 +952,12 @@ static int adam_multi_impl(const mh_adam_tensor_t* tensors, int32_t n, double lr
       L.m[k] = t.exp_avg;
       L.v[k] = t.exp_avg_sq;
       L.step[k] = t.step;
-      L.start[k + 1] = L.start[k] + t.numel;
+      // float4 units when every array of the tensor allows them, single elements otherwise
+      const bool vec = t.numel % 4 == 0 && aligned16(t.param) && aligned16(t.grad) && aligned16(t.exp_avg) &&
+                       aligned16(t.exp_avg_sq);
+      L.vec[k] = vec ? 1 : 0;
+      L.numel[k] = t.numel;
+      L.start[k + 1] = L.start[k] + (vec ? t.numel / 4 : t.numel);
       L.lr[k] = lrs ? lrs[base + k] : lr;
     }
     MH_HIP(mh::launch_adam_multi(L, beta1, beta2, eps, ticket, (hipStream_t)stream));
@@ -980,7 +987,10 @@ int mh_polyak_multi(const mh_polyak_tensor_t* tensors, int32_t n, double polyak,
         return fail(MH_EINVAL, "mh_polyak_multi: null pointer or negative size in the tensor list");
       L.t[k] = t.target;
       L.s[k] = t.source;
-      L.start[k + 1] = L.start[k] + t.numel;
+      const bool vec = t.numel % 4 == 0 && aligned16(t.target) && aligned16(t.source);
+      L.vec[k] = vec ? 1 : 0;
+      L.numel[k] = t.numel;
+      L.start[k + 1] = L.start[k] + (vec ? t.numel / 4 : t.numel);
     }
     MH_HIP(mh::launch_polyak_multi(L, polyak, (hipStream_t)stream));
   }

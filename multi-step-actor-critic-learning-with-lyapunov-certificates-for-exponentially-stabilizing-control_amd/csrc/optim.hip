@@ -19,6 +19,15 @@
 
 namespace mh {
 
+// one element of the Adam update (the same float32 expressions for every layout)
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float w1, float w2, float fb2,
+                                          float bc2, float step_size, float feps) {
+  m = m + w1 * (g - m);  // exp_avg.lerp_(grad, 1 - beta1)
+  v = fb2 * v + w2 * (g * g);
+  const float denom = sqrtf(v) / bc2 + feps;
+  p = p - step_size * m / denom;
+}
+
 __global__ __launch_bounds__(256) void k_adam_multi(AdamList L, double b1, double b2, double eps,
                                                     uint32_t* __restrict__ ticket) {
   // the scalars as PyTorch forms them from the Python floats: (1 - beta) and the bias
@@ -35,18 +44,33 @@ __global__ __launch_bounds__(256) void k_adam_multi(AdamList L, double b1, doubl
   const float w1 = (float)(1.0 - b1), w2 = (float)(1.0 - b2);
   const float fb2 = (float)b2, feps = (float)eps;
   const int64_t total = L.start[L.n];
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    int k = 0;
-    while (k + 1 < L.n && i >= L.start[k + 1]) ++k;  // <= MH_ADAM_MAX_TENSORS, uniform mostly
-    const int64_t j = i - L.start[k];
-    const float g = L.g[k][j];
-    float m = L.m[k][j], v = L.v[k][j];
-    m = m + w1 * (g - m);  // exp_avg.lerp_(grad, 1 - beta1)
-    v = fb2 * v + w2 * (g * g);
-    const float denom = sqrtf(v) / s_bc2[k] + feps;
-    L.p[k][j] = L.p[k][j] - s_step_size[k] * m / denom;
-    L.m[k][j] = m;
-    L.v[k][j] = v;
+  // work units: 4-element vectors of the tensors that allow them (16-byte aligned, numel % 4 ==
+  // 0), single elements of the rest; a thread's grid-stride units only move forward through the
+  // tensor list, so its tensor index is carried from one unit to the next
+  int k = 0;
+  for (int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x; u < total; u += (int64_t)gridDim.x * 256) {
+    while (k + 1 < L.n && u >= L.start[k + 1]) ++k;
+    const int64_t j = u - L.start[k];
+    const float ss = s_step_size[k], bc2 = s_bc2[k];
+    if (L.vec[k]) {
+      float4 p = reinterpret_cast<const float4*>(L.p[k])[j];
+      const float4 g = reinterpret_cast<const float4*>(L.g[k])[j];
+      float4 m = reinterpret_cast<const float4*>(L.m[k])[j];
+      float4 v = reinterpret_cast<const float4*>(L.v[k])[j];
+      adam_elem(p.x, g.x, m.x, v.x, w1, w2, fb2, bc2, ss, feps);
+      adam_elem(p.y, g.y, m.y, v.y, w1, w2, fb2, bc2, ss, feps);
+      adam_elem(p.z, g.z, m.z, v.z, w1, w2, fb2, bc2, ss, feps);
+      adam_elem(p.w, g.w, m.w, v.w, w1, w2, fb2, bc2, ss, feps);
+      reinterpret_cast<float4*>(L.p[k])[j] = p;
+      reinterpret_cast<float4*>(L.m[k])[j] = m;
+      reinterpret_cast<float4*>(L.v[k])[j] = v;
+    } else {
+      float p = L.p[k][j], m = L.m[k][j], v = L.v[k][j];
+      adam_elem(p, L.g[k][j], m, v, w1, w2, fb2, bc2, ss, feps);
+      L.p[k][j] = p;
+      L.m[k][j] = m;
+      L.v[k][j] = v;
+    }
   }
   // the last workgroup to finish advances every step counter. The arrival count is RELAXED: the
   // only ordering needed is that every workgroup has READ the old count before the last one
@@ -58,7 +82,7 @@ __global__ __launch_bounds__(256) void k_adam_multi(AdamList L, double b1, doubl
   if (threadIdx.x == 0) {
     const uint32_t done = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (done == gridDim.x - 1) {
-      for (int k = 0; k < L.n; ++k) *L.step[k] = s_t[k];
+      for (int q = 0; q < L.n; ++q) *L.step[q] = s_t[q];
       *ticket = 0u;
     }
   }
@@ -78,12 +102,22 @@ hipError_t launch_adam_multi(const AdamList& L, double b1, double b2, double eps
 // over a tensor list in one launch (PyTorch: three multi-tensor kernels per network).
 __global__ __launch_bounds__(256) void k_polyak_multi(PolyakList L, float a, float b) {
   const int64_t total = L.start[L.n];
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    int k = 0;
-    while (k + 1 < L.n && i >= L.start[k + 1]) ++k;
-    const int64_t j = i - L.start[k];
-    const float t = L.t[k][j] * a;
-    L.t[k][j] = t + L.s[k][j] * b;
+  int k = 0;  // (units as in k_adam_multi; the tensor index carried forward)
+  for (int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x; u < total; u += (int64_t)gridDim.x * 256) {
+    while (k + 1 < L.n && u >= L.start[k + 1]) ++k;
+    const int64_t j = u - L.start[k];
+    if (L.vec[k]) {
+      float4 t = reinterpret_cast<const float4*>(L.t[k])[j];
+      const float4 s = reinterpret_cast<const float4*>(L.s[k])[j];
+      t.x = t.x * a + s.x * b;
+      t.y = t.y * a + s.y * b;
+      t.z = t.z * a + s.z * b;
+      t.w = t.w * a + s.w * b;
+      reinterpret_cast<float4*>(L.t[k])[j] = t;
+    } else {
+      const float t = L.t[k][j] * a;
+      L.t[k][j] = t + L.s[k][j] * b;
+    }
   }
 }
 

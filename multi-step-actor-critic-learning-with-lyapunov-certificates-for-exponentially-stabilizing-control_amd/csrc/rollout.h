@@ -183,14 +183,18 @@ struct AdamList {  // one optimiser's tensors, passed by value in the kernel arg
   float* m[ADAM_MAX_TENSORS];
   float* v[ADAM_MAX_TENSORS];
   float* step[ADAM_MAX_TENSORS];
-  int64_t start[ADAM_MAX_TENSORS + 1];  // prefix sums of the element counts
+  int64_t start[ADAM_MAX_TENSORS + 1];  // prefix sums of the work units (4-element vectors or elements)
   double lr[ADAM_MAX_TENSORS];           // each tensor's learning rate (one launch may step several optimisers)
+  int64_t numel[ADAM_MAX_TENSORS];
+  int vec[ADAM_MAX_TENSORS];             // 1: the tensor is stepped as float4 units (aligned, numel % 4 == 0)
   int n;
 };
 struct PolyakList {
   float* t[ADAM_MAX_TENSORS];
   const float* s[ADAM_MAX_TENSORS];
-  int64_t start[ADAM_MAX_TENSORS + 1];
+  int64_t start[ADAM_MAX_TENSORS + 1];  // prefix sums of the work units, as in AdamList
+  int64_t numel[ADAM_MAX_TENSORS];
+  int vec[ADAM_MAX_TENSORS];
   int n;
 };
 // the fused 3-layer MLP forward (mlp_fused.hip)

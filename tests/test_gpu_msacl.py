@@ -71,6 +71,55 @@ def test_q_target_stats_kernel(B, n):
                                                      np.float32(q2.astype(np.float64).mean())], rtol=1e-6)
 
 
+def test_kernel_noise_state_round_trip():
+    """The update's in-kernel rsample noise (Philox keyed by (seed, row, a device counter)):
+    each update advances the counter; restoring networks + optimisers + rng_state() replays an
+    update bit for bit, and restoring everything BUT the rng state gives different noise and so a
+    different update (the counter is part of the algorithm's saved state)."""
+    import copy
+    from msacl_amd.algorithm.msacl import MSACL
+    g = np.load(os.path.join(G, "msacl_update.npz"))
+    B, n = int(g["cfg_B"]), int(g["cfg_n"])
+    data = {k: torch.as_tensor(g["in_" + k], device="cuda") for k in ("obs", "act", "rew", "cost", "obs2", "done", "logp")}
+    alg = MSACL(**_msacl_kwargs(B, n), alg_use_graph=False)
+    alg.networks.load_state_dict({k[5:]: torch.as_tensor(g[k]) for k in g.files if k.startswith("init/")})
+    nets = alg.networks
+    opts = [nets.q1_optimizer, nets.q2_optimizer, nets.lyapunov_optimizer, nets.policy_optimizer, nets.alpha_optimizer]
+    alg.model_update(data, 1)
+    st = alg.rng_state()
+    assert st["noise_ctr"] is not None, "the in-kernel noise path is off"
+    sd = {k: v.detach().clone() for k, v in nets.state_dict().items()}
+    osd = [copy.deepcopy(o.state_dict()) for o in opts]
+
+    def update():
+        tb = alg.model_update(data, 0)
+        torch.cuda.synchronize()
+        return {k: v for k, v in dict(tb).items() if "time" not in k.lower()}, \
+            {k: v.detach().clone() for k, v in nets.state_dict().items()}
+
+    def restore(rng):
+        nets.load_state_dict(sd)
+        for o, s in zip(opts, osd):
+            o.load_state_dict(copy.deepcopy(s))
+        if rng:
+            alg.load_rng_state(st)
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)  # (library split-K GEMMs: no atomics)
+    try:
+        tb_a, p_a = update()
+        assert not torch.equal(alg.rng_state()["noise_ctr"], st["noise_ctr"])  # the update advanced it
+        restore(True)
+        tb_b, p_b = update()
+        restore(False)  # the counter keeps going: new noise
+        tb_c, p_c = update()
+    finally:
+        torch.use_deterministic_algorithms(prev)
+    assert tb_a == tb_b
+    for k in p_a:
+        assert torch.equal(p_a[k], p_b[k]), k
+    assert any(not torch.equal(p_a[k], p_c[k]) for k in p_a)
+
+
 def test_tb_ring_slots(monkeypatch):
     """The policy updates' logged scalars go to a device ring (mh_msacl_tb_pack_ring, no copy out
     of the replayed graph): a tb dict read within the ring's depth equals the eager update's, and
