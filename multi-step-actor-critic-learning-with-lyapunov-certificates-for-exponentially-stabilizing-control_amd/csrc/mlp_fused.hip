@@ -39,12 +39,18 @@ constexpr int SH = HID + 4;   // LDS row stride of a hidden tile (floats): rows 
 constexpr int K1P = 32;       // first-layer K padded
 constexpr int SX = K1P + 4;
 #ifndef MH_MLP_PF
-#define MH_MLP_PF 4
+#define MH_MLP_PF 2
 #endif
 #ifndef MH_MLP_PFT
 #define MH_MLP_PFT 3
 #endif
-constexpr int PF = MH_MLP_PF;  // weight groups in the load ring: PF - 1 in flight behind the MFMAs
+// weight groups in the load ring: PF - 1 in flight behind the MFMAs. One group ahead (PF = 2) is
+// the fastest at the update's shapes (round 5, tools/r05_pf_probe.sh, r05_pf_bench.sh): a group's
+// MFMAs (32 at two row tiles, ~1 k cycles) cover its loads' L2 latency, and every deeper ring was
+// slower (PF = 4 / 5 / 6 / 8: +3 / +5 / +7 / +15 % on the 10,240-row forward): each load touches
+// 16 half-used 128-byte lines whose other halves the NEXT group reads, and with more groups in
+// flight those lines are evicted from the vector L1 before that read
+constexpr int PF = MH_MLP_PF;
 
 // The load ring is enforced with scheduling barriers: left to itself the scheduler regroups the
 // fully unrolled loop and waits on each group's loads right after issuing them (one L2 latency per
