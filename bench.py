@@ -183,20 +183,32 @@ def main():
 
     trainer.finish_pending()
 
-    # ---- phase split (diagnostic, after the timed region): sample() vs replay sample + update
-    ph_s = ph_u = 0.0
-    for _ in range(2):
-        torch.cuda.synchronize()
-        ta = time.perf_counter()
-        samples, _ = sampler.sample()
-        buffer.add_batch(samples)
-        torch.cuda.synchronize()
-        tb_ = time.perf_counter()
-        trainer.replay_and_update()  # as step() does (the draw inside the replayed update graph)
-        trainer.iteration += 1
-        torch.cuda.synchronize()
-        ph_s += tb_ - ta
-        ph_u += time.perf_counter() - tb_
+    # ---- phase split (diagnostic, after the timed region): sample() vs replay sample + update,
+    # each synchronised, over PH_PAIRS (policy-free, policy) step pairs; per pair the two steps'
+    # mean, and the median over the pairs (single pairs swing by +-10 % on one box)
+    PH_PAIRS = 8
+    pair_s, pair_u, u_by_kind = [], [], {True: [], False: []}
+    for _ in range(PH_PAIRS):
+        ps = pu = 0.0
+        for _ in range(2):
+            torch.cuda.synchronize()
+            ta = time.perf_counter()
+            samples, _ = sampler.sample()
+            buffer.add_batch(samples)
+            torch.cuda.synchronize()
+            tb_ = time.perf_counter()
+            policy_step = trainer.iteration % trainer.policy_frequency == 0
+            trainer.replay_and_update()  # as step() does (the draw inside the replayed update graph)
+            trainer.iteration += 1
+            torch.cuda.synchronize()
+            ps += tb_ - ta
+            du = time.perf_counter() - tb_
+            pu += du
+            u_by_kind[policy_step].append(du)
+        pair_s.append(ps)
+        pair_u.append(pu)
+    med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+    ph_s, ph_u = med(pair_s), med(pair_u)
     # host enqueue rate: the host time of trainer steps without a sync (it only blocks when the
     # device queue is full or a call waits) against the same steps' wall time: equal = host-bound
     k_host = 6
@@ -227,6 +239,9 @@ def main():
     for obj, name in wrapped:
         delattr(obj, name)
     phases = {"sample_ms": round(ph_s / 2 * 1e3, 3), "replay_and_update_ms": round(ph_u / 2 * 1e3, 3),
+              "replay_and_update_ms_policy_free_policy": [round(med(u_by_kind[False]) * 1e3, 3),
+                                                          round(med(u_by_kind[True]) * 1e3, 3)],
+              "phase_pairs": PH_PAIRS,
               "sampler_only_env_steps_per_s": round(a.envs * horizon / (ph_s / 2), 1),
               "update_to_data_ratio": round(1.0 / (a.envs * horizon), 9),
               "host_enqueue_ms_per_step": round((th1 - th0) / k_host * 1e3, 3),
