@@ -7,7 +7,7 @@ mkdir -p "$ROOT/gpurun_out"
 for rep in 1 2; do
   for v in base $VARIANTS; do
     lib="$ROOT/exp_libs/$v/libmsacl_hip.so"; [ $v = base ] && lib=""
-    MSACL_HIP_LIB=${lib:-$ROOT/multi-step-actor-critic-learning-with-lyapunov-certificates-for-exponentially-stabilizing-control_amd/csrc/build/libmsacl_hip.so} \
+    MSACL_HIP_LIB=${lib:-$ROOT/lib/libmsacl_hip.so} \
       timeout -k 10 120 python "$ROOT/tools/kernel_bench.py" --envs ${ENVS:-SingleTrackCar} --sizes ${SIZES:-4194304} \
       --skip gather,msacl,gae,policy,rollout --reps 20 > "$ROOT/gpurun_out/carv_run.log" 2>&1 || { tail -20 "$ROOT/gpurun_out/carv_run.log"; exit 1; }
     grep '"env_step"' "$ROOT/gpurun_out/carv_run.log" | sed "s/^{/{\"variant\": \"$v\", /" | tee -a "$ROOT/gpurun_out/carv.jsonl" | cut -c1-200
