@@ -476,7 +476,9 @@ __global__ __launch_bounds__(256, 1) void k_policy_forward_x6(const float* __res
 // read two steps ahead) with 32 instead of 48 fragments per chunk and half the MFMAs; layer 1 is
 // 3 MFMAs per 32-row block (K = 16 covers obs + bias for D <= 15); layer 3 is folded into the
 // last phase: output block ob's accumulators are final after its step (ob, 1), go through bias,
-// ReLU and the split, and into 2 x 3 MFMAs against W3x3 staged once per kernel in LDS.
+// ReLU and the split, and into 2 x 3 16x16x32 MFMAs against W3x3 staged once per kernel in LDS
+// (policy_x3.h pm_l3_row_half: N3 <= 8, the policy head 2A of every env; wider heads take the
+// f32 kernel).
 // The raw magnitudes behind the scales: [0] max |W1, b1|, [1] max |W2|, [2] max |W3|,
 // [3] R1 = max_k (sum_j |W1[k][j]| + |b1[k]|), [4] R2 = max_o (sum_k |W2[o][k]| + |b2[o]|).
 // PM_SC_WG workgroups of 16 waves, one row of W2 per wave and pass (a float4 per lane, wave
@@ -598,10 +600,10 @@ __global__ __launch_bounds__(256) void k_policy_pack_x3(const float* __restrict_
     } else if (q < n2 + n1) {
       const int blk = (int)(f >> 1), k = 8 * (l >> 5) + j, row = blk * 32 + (l & 31);
       v = k < D ? W1[(int64_t)row * D + k] * sw1 : (k == D ? b1[row] * sw1 : 0.0f);
-    } else {
-      const int s = (int)((f >> 1) & 1), ob = (int)(f >> 2), o = l & 31;
+    } else {  // the 16x16x32 A operand (policy_x3.h pm_l3_row_half): row l & 15, k-group l >> 4
+      const int s = (int)((f >> 1) & 1), ob = (int)(f >> 2), o = l & 7;
       const int k = ob * 32 + (j & 3) + 8 * (j >> 2) + 16 * s + 4 * (l >> 5);
-      v = o < N3 ? W3[(int64_t)o * PM_H + k] * sw3 : 0.0f;
+      v = pm_l3_row_half(l) && o < N3 ? W3[(int64_t)o * PM_H + k] * sw3 : 0.0f;
     }
     _Float16 hi, lo;
     split2h(v, hi, lo);
@@ -619,7 +621,7 @@ void k_policy_forward_x3(const float* __restrict__ P,
                                                              int K1, float* __restrict__ logits) {
   typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
   constexpr int FPW = PM_X3_FRAGS / WAVES;  // W2x3 fragments each wave stages per chunk
-  constexpr int FOPW = 2 * PM_NB * 4 / (2 * WAVES);  // fold-operand records per wave (per array)
+  constexpr int FOPW = PM_NB * 4 / WAVES;  // fold-operand records per wave (per array)
   // two distinct LDS arrays (not one [2][...]): with the buffer known at compile time in every
   // phase, alias analysis proves the next chunk's LDS-DMA writes disjoint from this phase's
   // ds_reads, so the reads do not wait for the staging to land
@@ -831,17 +833,20 @@ void k_policy_forward_x3(const float* __restrict__ P,
                                  __builtin_bit_cast(f16x8, uint4{hp[4], hp[5], hp[6], hp[7]})};
             const f16x8 hl[2] = {__builtin_bit_cast(f16x8, uint4{lp[0], lp[1], lp[2], lp[3]}),
                                  __builtin_bit_cast(f16x8, uint4{lp[4], lp[5], lp[6], lp[7]})};
-            // layer 3's accumulator lives in acc[t][0] once block 0 has been folded (its
-            // registers are free from then on), so it needs no registers of its own
+            // layer 3 on 16x16x32 (policy_x3.h pm_l3_row_half); its accumulator lives in registers
+            // 0..3 of acc[t][0] once block 0 has been folded (free from then on)
             f32x16 o = ob == 0 ? f32x16{} : acc[t][0];
+            f32x4 o3 = {o[0], o[1], o[2], o[3]};
 #pragma unroll
             for (int ks = 0; ks < 2; ++ks) {
               const f16x8 vh = __builtin_bit_cast(f16x8, w3f[2 * ks]);
               const f16x8 vl = __builtin_bit_cast(f16x8, w3f[2 * ks + 1]);
-              o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, hh[ks], o, 0, 0, 0);
-              o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, hl[ks], o, 0, 0, 0);
-              o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, hh[ks], o, 0, 0, 0);
+              o3 = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, hh[ks], o3, 0, 0, 0);
+              o3 = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, hl[ks], o3, 0, 0, 0);
+              o3 = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, hh[ks], o3, 0, 0, 0);
             }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[i] = o3[i];
             acc[t][0] = o;
           }
         }
@@ -868,33 +873,26 @@ void k_policy_forward_x3(const float* __restrict__ P,
     }
     phase(B0{}, PM_NB - 2, false);
     phase(B1{}, PM_NB - 1, true);
-    // logits: o3 holds out^T (rows = outputs, row(r, lane); column = env lane & 31), in units of
-    // sw3 * 2^ex[2]
+    // logits: registers 0..3 of acc[t][0] hold outputs 4 ((lane >> 4) & 1) + i of env column
+    // pm_l3_env(lane), in units of sw3 * 2^ex[2] of that env (its exponents live on that env's lane)
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const int64_t b = (t0 + t) * 32 + (lane & 31);
-      const float iu = isw3 * pm_pow2(-ex[t][2]);
-      if (t0 + t < ntiles && b < E) {
+      const int e = pm_l3_env(lane);
+      const float iu = __shfl(isw3 * pm_pow2(-ex[t][2]), e);
+      const int o0 = 4 * ((lane >> 4) & 1);
+      const int64_t b = (t0 + t) * 32 + e;
+      if (t0 + t < ntiles && b < E && o0 < N3) {
         if ((N3 & 3) == 0) {
-          // registers 4q..4q+3 are the env's consecutive outputs 8q + 4 (lane >> 5) + 0..3: one
-          // 16-byte store each, so a wave writes its 32 rows as whole lines (4-byte stores at the
-          // row stride wrote every line 4 times: PMC WRITE_SIZE 9.5x the logits' bytes)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int o0 = 8 * q + 4 * (lane >> 5);
-            if (o0 < N3) {
-              const float4 bb = *reinterpret_cast<const float4*>(b3 + o0);
-              *reinterpret_cast<float4*>(logits + b * N3 + o0) =
-                  make_float4(acc[t][0][4 * q] * iu + bb.x, acc[t][0][4 * q + 1] * iu + bb.y,
-                              acc[t][0][4 * q + 2] * iu + bb.z, acc[t][0][4 * q + 3] * iu + bb.w);
-            }
-          }
+          // one 16-byte store per lane (whole lines: 4-byte stores at the row stride wrote every
+          // line 4 times, PMC WRITE_SIZE 9.5x the logits' bytes)
+          const float4 bb = *reinterpret_cast<const float4*>(b3 + o0);
+          *reinterpret_cast<float4*>(logits + b * N3 + o0) =
+              make_float4(acc[t][0][0] * iu + bb.x, acc[t][0][1] * iu + bb.y, acc[t][0][2] * iu + bb.z,
+                          acc[t][0][3] * iu + bb.w);
         } else {
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int oo = pm_row(r, lane);
-            if (oo < N3) logits[b * N3 + oo] = acc[t][0][r] * iu + b3[oo];
-          }
+          for (int i = 0; i < 4; ++i)
+            if (o0 + i < N3) logits[b * N3 + o0 + i] = acc[t][0][i] * iu + b3[o0 + i];
         }
       }
     }
@@ -931,7 +929,8 @@ hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2,
   if (reinterpret_cast<uintptr_t>(W2) & 15) return hipErrorInvalidValue;  // k_policy_scales: 16-byte rows
   const int64_t total = pm_off_w2x6(K1);
   const int grid = (int)((total + 255) / 256 < 1024 ? (total + 255) / 256 : 1024);
-  const bool split_only = policy_mode() == 2 && D <= 15;  // the default kernel reads only b2 / b3 in f32
+  // the default kernel (split-f16, layer 3 on 8 + 8 output rows) reads only b2 / b3 in f32
+  const bool split_only = policy_mode() == 2 && D <= 15 && N3 <= 8;
   if (!split_only) {
     k_policy_pack<<<grid, 256, 0, st>>>(W1, b1, W2, b2, W3, b3, D, N3, K1, P);
     if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
@@ -962,7 +961,7 @@ static hipError_t launch_fwd_t(const float* P, const float* obs, int64_t E, int 
   const int64_t want = (tiles + 3) / 4;
   const int grid = (int)(want < cus ? want : cus);
   const int mode = policy_mode();
-  if (D <= 15 && mode == 2) {  // K = 16 holds the observation and the bias input
+  if (D <= 15 && N3 <= 8 && mode == 2) {  // K = 16 holds the observation and the bias input
     // default (round 4): one wave per SIMD with 2 tiles (k_policy_forward_x3<2, 4>, 512 registers,
     // nothing spilled); MH_POLICY_WAVES=8: two waves per SIMD with 1 tile each, whose 256-register
     // budget spilled 32 VGPRs to scratch in every phase — the 9x WRITE_SIZE of the logits' bytes

@@ -42,8 +42,10 @@ __host__ __device__ constexpr int64_t pm_off_w2x6(int K1) { return (pm_off_b3(K1
 //   W1x3 [blk 8][split 2][lane 64][8 f16]        W1[blk*32 + (l & 31)][8 (l >> 5) + j] * sw1,
 //                                                b1 at k = D (constant-1 input), 0 beyond
 //   W2x3 [ib 8][ob 8][s 2][split 2][lane 64][8 f16]   the W2x6 k order, * sw2
-//   W3x3 [ob 8][s 2][split 2][lane 64][8 f16]    W3[l & 31][ob*32 + (j & 3) + 8 (j >> 2) + 16 s + 4 (l >> 5)]
-//                                                * sw3 (0 for rows >= N3)
+//   W3x3 [ob 8][s 2][split 2][lane 64][8 f16]    the A operand of layer 3 on v_mfma_f32_16x16x32_f16
+//                                                (N3 <= 8): row m = l & 15, k-group g = l >> 4 holds
+//                                                W3[m & 7][ob*32 + (j & 3) + 8 (j >> 2) + 16 s + 4 (g >> 1)] * sw3
+//                                                when (m < 8) == (g even), else 0 (pm_l3_row_half)
 constexpr int PM_X3_FRAGS = 32;                                      // W2x3 fragments per chunk
 constexpr int64_t PM_X3_FLOATS = (int64_t)PM_NB * PM_X3_FRAGS * 64 * 4;
 constexpr int64_t PM_X3_W1_FLOATS = (int64_t)PM_NB * 2 * 64 * 4;
@@ -129,5 +131,17 @@ __device__ __forceinline__ void split2h_relu_scaled(float a, float b, float k, u
 // products are (W2 sw2)(H1 2^ex1)); cb = sw2 * 2^ex1 (a power of two: exact). The H2 split is then
 // split2h_relu_scaled(acc, k23), k23 = 2^(ex2 - ex1) / sw2.
 __device__ __forceinline__ float pm_bias_unit(float sw2, int ex1) { return sw2 * pm_pow2(ex1); }
+
+// Layer 3 on v_mfma_f32_16x16x32_f16 without moving the H2 split across lanes. The split of
+// k-step s of an H2 block is, read as that MFMA's B operand (lane l = column l & 15, k-group
+// g = l >> 4), env l & 31's eight units of row half l >> 5: k-groups 0 and 2 belong to env
+// column n = l & 15 and groups 1 and 3 to env 16 + n. W3x3 puts the weights of the even groups in
+// output rows 0..7 and those of the odd groups in rows 8..15 (zeros elsewhere), so the 16x16
+// result holds outputs 0..7 of env n in rows 0..7 and of env 16 + n in rows 8..15 — every row
+// real for N3 = 8, where a 32x32x16 tile pads 32 rows — and lane l ends up with outputs
+// 4 ((l >> 4) & 1) + i of env pm_l3_env(l). Per block 2 k-steps x 3 products (lo·hi, hi·lo,
+// hi·hi) on one accumulator.
+__device__ __forceinline__ int pm_l3_env(int lane) { return 16 * (lane >> 5) + (lane & 15); }
+__host__ __device__ constexpr bool pm_l3_row_half(int lane) { return ((lane & 15) < 8) == (((lane >> 4) & 1) == 0); }
 
 }  // namespace mh

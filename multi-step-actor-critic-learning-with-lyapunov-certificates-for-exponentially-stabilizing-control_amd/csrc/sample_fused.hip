@@ -61,7 +61,7 @@ struct PolicyLds {
   uint4* c1;
   uint32_t c0_lds;      // their LDS byte addresses (the chunk DMA's M0 values)
   uint32_t c1_lds;
-  const uint4* w3;      // layer-3 operands [ob][s][split][lane]
+  const uint4* w3;      // layer-3 operands [ob][s][split][lane] (16x16x32 A fragments)
   const float* b2;      // layer-2 bias, [256]
   const uint4* w1;      // layer-1 fragments [blk][split][lane] (LDS: no memory loads inside a pass)
   const float* obs;     // [256][D] observations of the workgroup's envs
@@ -180,8 +180,14 @@ __device__ __forceinline__ void pol_sync(uint32_t* bar, uint32_t& target, int64_
 // pairs are split from step 2 fb + 2 on (its MFMAs retired: no VALU waits on the matrix pipe),
 // at most FOLD_K2 per layer-2 step; the rest during the layer-3 MFMAs, at most FOLD_K3 per
 // layer-3 block but always every pair of the block the next layer-3 MFMA reads.
-constexpr int FOLD_K2 = 2;
-constexpr int FOLD_K3 = 6;
+#ifndef MH_FOLD_K2  // (overridable for A/B builds, tools/src_variants.sh)
+#define MH_FOLD_K2 2
+#endif
+#ifndef MH_FOLD_K3
+#define MH_FOLD_K3 6
+#endif
+constexpr int FOLD_K2 = MH_FOLD_K2;
+constexpr int FOLD_K3 = MH_FOLD_K3;
 constexpr int fold_done_l2(int st) {  // pairs split after layer-2 steps 0 .. st
   int done = 0;
   for (int t = 0; t <= st; ++t) {
@@ -209,9 +215,9 @@ constexpr int fold_done_l3(int fb) {  // pairs split before layer-3 block fb's M
 //   phases 0 .. 6: layer 2's input block ib (chunk ib) into all eight H2 blocks; layer 1 of block
 //     ib + 1 pipelined into the phase (issued at step 0, split over steps 3 .. 10);
 //   phase 7: chunk 7 into the H2 blocks, each finished block split (bias, ReLU, rescale, f16 hi /
-//     lo) two steps later beside the remaining layer-2 MFMAs, then layer 3 as one MFMA run over
-//     the split blocks (k_policy_forward_x3's layer-3 order: block 0 .. 7, k-step 0, 1, products
-//     lo·hi, hi·lo, hi·hi) with the remaining splits beside it.
+//     lo) two steps later beside the remaining layer-2 MFMAs, then layer 3 as one 16x16x32 MFMA
+//     run over the split blocks (policy_x3.h pm_l3_row_half; k_policy_forward_x3's layer-3 order:
+//     block 0 .. 7, k-step 0, 1, products lo·hi, hi·lo, hi·hi) with the remaining splits beside it.
 // The chunk DMA for the next phase is issued one 1-KB piece per step (steps 0 .. 7) rather than all
 // at once: a piece's issue costs a policy wave 60-185 cycles, eight in a row idle the matrix pipe.
 #ifdef MH_FUSED_EXP_TACC
@@ -412,7 +418,7 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
   phase(B0{}, F0{}, PM_NB - 2);
 
   // ---- phase PM_NB - 1 (chunk 7, buffer 1): the last layer-2 input block, the H2 splits, layer 3
-  f32x16 o3 = {};
+  f32x4 o3 = {};  // layer 3: outputs 4 ((lane >> 4) & 1) + i of env pm_l3_env(lane)
   {
     constexpr int ib = PM_NB - 1;
     (void)ib;
@@ -454,8 +460,8 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
       __builtin_amdgcn_sched_barrier(0);
     }
     MH_STAMP(a, pass_no, 17);
-    // layer 3: o3 = W3 H2 over the split blocks, k_policy_forward_x3's order; the layer-3 operands
-    // read one block ahead, the remaining splits (and their biases, one block ahead) beside the MFMAs
+    // layer 3 on 16x16x32 (policy_x3.h pm_l3_row_half; k_policy_forward_x3's order): o3 = W3 H2 over
+    // the split blocks; the layer-3 operands read one block ahead, the remaining splits beside the MFMAs
     uint4 w3f[2][4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) w3f[0][q] = L.w3[q * 64 + lane];
@@ -473,26 +479,26 @@ __device__ void policy_pass(const FusedArgs& a, const PolicyLds& L, int pw, int 
         const f16x8 vh = __builtin_bit_cast(f16x8, w3f[fb & 1][2 * ks]);
         const f16x8 vl = __builtin_bit_cast(f16x8, w3f[fb & 1][2 * ks + 1]);
         const f16x8 hh = pack8(&hs[fb][4 * ks]), hl = pack8(&ls[fb][4 * ks]);
-        o3 = MH_MFMA(vl, hh, o3);
-        o3 = MH_MFMA(vh, hl, o3);
-        o3 = MH_MFMA(vh, hh, o3);
+        o3 = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, hh, o3, 0, 0, 0);
+        o3 = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, hl, o3, 0, 0, 0);
+        o3 = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, hh, o3, 0, 0, 0);
       }
 #pragma unroll
       for (int g = 0; g < 6; ++g) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                       // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, FOLD_K3, 0);  // VALU (6 per pair)
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);        // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, FOLD_K3, 0);  // VALU
       }
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  // logits rows (registers r hold output pm_row(r, lane) of env column lane & 31), the same
-  // expression as k_policy_forward_x3's store
+  // logits rows, the same expression as k_policy_forward_x3's store: lane l stores outputs
+  // 4 ((l >> 4) & 1) + i of env pm_l3_env(l) — one 16-byte (N3 = 8, 4) or 4-byte (N3 = 2, 6) store
+  // per lane — with that env's unit 2^-ex[2] / sw3 from the env's own lane
   MH_STAMP(a, pass_no, 19);
-  // (registers r >= 4 hold outputs >= 8 >= N3: padding). One 16-byte (N3 = 8, 4) or 4-byte (N3 = 2)
-  // stores per lane instead of 16 branches, each waiting on its own bias read.
-  const float iu = isw3 * pm_pow2(-ex[2]);
-  const int row = row0 + (lane & 31);
-  const int o0 = 4 * (lane >> 5);
+  const int erow = pm_l3_env(lane);
+  const float iu = __shfl(isw3 * pm_pow2(-ex[2]), erow);
+  const int row = row0 + erow;
+  const int o0 = 4 * ((lane >> 4) & 1);
   float v[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) v[r] = o3[r] * iu + b3r[r];
@@ -737,11 +743,11 @@ void k_sample_fused(FusedArgs a) {
     const uint32_t lds0_addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds0;
     const uint32_t lds1_addr = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds1;
     PolicyLds L{lds0, lds1, lds0_addr, lds1_addr, lds_w3, lds_b2, lds_w1, s_obs, s_lgt, &s_bar, a.err};
-    // the layer-3 bias of the rows this lane stores (4 (lane >> 5) + r; zero past N3)
+    // the layer-3 bias of the rows this lane stores (4 ((lane >> 4) & 1) + r; zero past N3)
     float b3r[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int o = 4 * (lane >> 5) + r;
+      const int o = 4 * ((lane >> 4) & 1) + r;
       b3r[r] = o < N3C ? a.P[pm_off_b3(a.K1) + o] : 0.0f;
     }
     uint32_t target = 0;
