@@ -288,7 +288,7 @@ int mh_nstep_reserve(mh_env_t h, int32_t ring_slots) {
   float* ring = nullptr;
   int32_t *cnt = nullptr, *lst = nullptr, *cpre = nullptr;
   int64_t* scan = nullptr;
-  const int64_t cells = (E + mh::FUSED_ENVS - 1) / mh::FUSED_ENVS;  // emission cells per lockstep
+  const int64_t cells = mh::fused_emit_cells_per_lockstep(E);  // emission cells per lockstep
   hipError_t e = hipSuccess;
   if (new_ring) e = hipMalloc(&ring, sizeof(float) * E * ring_slots * F);
   if (e == hipSuccess) e = hipMalloc(&cnt, sizeof(int32_t) * hcap * ((E + 63) / 64));

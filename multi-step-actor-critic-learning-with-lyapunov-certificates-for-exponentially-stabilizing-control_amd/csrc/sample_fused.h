@@ -46,12 +46,20 @@ constexpr uint32_t FUSED_SPIN_LIMIT = 1u << 26;
 
 constexpr int FUSED_ENVS = 256;   // envs per workgroup (one workgroup per CU)
 constexpr int FUSED_THREADS = 512;
-// (lockstep, 256-env block) cells of the horizon emission (one workgroup each)
-inline int64_t fused_emit_cells(int64_t E, int H) { return (int64_t)H * ((E + FUSED_ENVS - 1) / FUSED_ENVS); }
-// Above this many cells per lockstep (E > 262,144) a cell no longer sums the wave counts of every
-// earlier cell of its lockstep itself (O(cells^2) loads per lockstep): k_emit_prefix forms the
-// per-cell prefixes first (one workgroup per lockstep), into HorizonEmitArgs::cell_pre.
-constexpr int64_t FUSED_EMIT_SCAN_CELLS = 1024;
+// (lockstep, FUSED_EMIT_CW x 64-env block) cells of the horizon emission (one workgroup each)
+// 16 waves (1,024 envs) per cell: 5 -> 1.25 k workgroups per 65,536-env horizon, one round of
+// them on the chip; k_emit_cells alone 21.6 vs 24.3 us for 23,040 windows against 4 waves per cell
+// (profiles/r05_emit_cell_width_ab.txt)
+#ifndef MH_EMIT_CW
+#define MH_EMIT_CW 16
+#endif
+constexpr int FUSED_EMIT_CW = MH_EMIT_CW;  // 64-env waves per emission cell
+inline int64_t fused_emit_cells_per_lockstep(int64_t E) { return ((E + 63) / 64 + FUSED_EMIT_CW - 1) / FUSED_EMIT_CW; }
+inline int64_t fused_emit_cells(int64_t E, int H) { return (int64_t)H * fused_emit_cells_per_lockstep(E); }
+// Above this many 64-env waves per lockstep (E > 262,144) a cell no longer sums the wave counts
+// of every earlier cell of its lockstep itself (O(cells^2) loads per lockstep): k_emit_prefix forms
+// the per-cell prefixes first (one workgroup per lockstep), into HorizonEmitArgs::cell_pre.
+constexpr int64_t FUSED_EMIT_SCAN_CELLS = 4096 / FUSED_EMIT_CW;
 
 struct HorizonEmitArgs {
   int64_t E;

@@ -915,7 +915,7 @@ void k_sample_fused(FusedArgs a) {
 // Every window of the horizon, in the reference's order (lockstep major; env index within a
 // lockstep: base.py:178-213), into the store rows after the cursor (FIFO wrap; windows older than
 // the last `capacity` of this horizon are skipped as overwritten), in ONE launch: k_emit_cells, a
-// workgroup per (lockstep, 256-env block) cell. A cell's first store row is its exclusive window
+// workgroup per (lockstep, FUSED_EMIT_CW x 64-env block) cell. A cell's first store row is its exclusive window
 // prefix: the lockstep's prefix (aux, formed at the end of the fused kernel from per-lockstep
 // totals its waves summed with integer atomic adds: order-free) plus the wave counts of the cells
 // before it in its lockstep (at most E / 64 counts, reduced by the workgroup). The fused kernel's
@@ -955,8 +955,9 @@ __device__ __forceinline__ void emit_rows_lds(float* dst, const float* row, floa
 // cells' window counts (four wave counts each), a block scan, the prefixes into cell_pre. Used
 // only when a lockstep has more than FUSED_EMIT_SCAN_CELLS cells.
 __global__ __launch_bounds__(1024) void k_emit_prefix(HorizonEmitArgs a) {
+  constexpr int CW = FUSED_EMIT_CW;
   const int NW = (int)((a.E + 63) / 64);
-  const int NBK = (NW + 3) / 4;
+  const int NBK = (NW + CW - 1) / CW;
   const int ts = blockIdx.x;
   const int32_t* cnt = a.emit_count + (int64_t)ts * NW;
   int32_t* out = a.cell_pre + (int64_t)ts * NBK;
@@ -965,7 +966,7 @@ __global__ __launch_bounds__(1024) void k_emit_prefix(HorizonEmitArgs a) {
   int sum = 0;
   for (int c = c0; c < c1; ++c)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) sum += 4 * c + q < NW ? cnt[4 * c + q] : 0;
+    for (int q = 0; q < CW; ++q) sum += CW * c + q < NW ? cnt[CW * c + q] : 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int incl = sum;
 #pragma unroll
@@ -982,20 +983,25 @@ __global__ __launch_bounds__(1024) void k_emit_prefix(HorizonEmitArgs a) {
   for (int c = c0; c < c1; ++c) {
     out[c] = run;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) run += 4 * c + q < NW ? cnt[4 * c + q] : 0;
+    for (int q = 0; q < CW; ++q) run += CW * c + q < NW ? cnt[CW * c + q] : 0;
   }
 }
 
 template <int D, int A>
 __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
   constexpr int F = rec_floats(D, A);
+  constexpr int CW = FUSED_EMIT_CW;
   __shared__ float stage[4][64 * D];
   __shared__ int s_pre[4];
   const int NW = (int)((a.E + 63) / 64);
-  const int NBK = (NW + 3) / 4;
+  const int NBK = (NW + CW - 1) / CW;
   const int64_t c = blockIdx.x;
   const int ts = (int)(c / NBK), b = (int)(c - (int64_t)ts * NBK);
   const int32_t* cnt = a.emit_count + (int64_t)ts * NW;
+  // the cell's own wave counts, issued with the header and prefix loads (unconditional, clamped)
+  int cv[CW];
+#pragma unroll
+  for (int q = 0; q < CW; ++q) cv[q] = cnt[CW * b + q < NW ? CW * b + q : NW - 1];
   __shared__ int64_t s_hdr[3];
   if (threadIdx.x == 0) {  // one lane reads the shared header (every workgroup reads the same line)
     s_hdr[0] = a.aux[0];
@@ -1004,9 +1010,9 @@ __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
   }
   if (NBK > FUSED_EMIT_SCAN_CELLS) {  // k_emit_prefix formed the cell's prefix
     if (threadIdx.x < 4) s_pre[threadIdx.x] = threadIdx.x == 0 ? a.cell_pre[(int64_t)ts * NBK + b] : 0;
-  } else {  // the wave counts of the lockstep's cells before b (at most 4 * FUSED_EMIT_SCAN_CELLS)
+  } else {  // the wave counts of the lockstep's cells before b (at most CW * FUSED_EMIT_SCAN_CELLS)
     int part = 0;
-    for (int i = threadIdx.x; i < 4 * b; i += 256) part += cnt[i];
+    for (int i = threadIdx.x; i < CW * b; i += 256) part += cnt[i];
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) part += __shfl_xor(part, off, 64);
     if ((threadIdx.x & 63) == 0) s_pre[threadIdx.x >> 6] = part;
@@ -1015,13 +1021,11 @@ __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
   const int64_t total = s_hdr[0], base = s_hdr[1], M = a.capacity;
   const int64_t g0 = s_hdr[2] + (int64_t)(s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3]);
   const int64_t start = total > M ? total - M : 0;  // older windows are overwritten this horizon
-  int pre[5], cv[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) cv[q] = cnt[4 * b + q < NW ? 4 * b + q : NW - 1];  // unconditional loads
+  int pre[CW + 1];
   pre[0] = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) pre[q + 1] = pre[q] + (4 * b + q < NW ? cv[q] : 0);
-  const int nwin = pre[4];
+  for (int q = 0; q < CW; ++q) pre[q + 1] = pre[q] + (CW * b + q < NW ? cv[q] : 0);
+  const int nwin = pre[CW];
   const int n = a.n, R = a.R;
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // wave-strided chunks of 64 records (every lane of a wave takes part in each chunk, so the
@@ -1036,9 +1040,15 @@ __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
       const int64_t g = g0 + w;
       valid = g >= start;
       if (valid) {
-        const int q = (w >= pre[1]) + (w >= pre[2]) + (w >= pre[3]);
-        const int gw = 4 * b + q;
-        const int packed = a.emit_list[(int64_t)ts * a.E + (int64_t)gw * 64 + (w - pre[q])];
+        int q = 0, pq = 0;  // the wave holding window w and its first window (selects: no indexed registers)
+#pragma unroll
+        for (int k = 1; k < CW; ++k) {
+          const bool past = w >= pre[k];
+          q += past;
+          pq = past ? pre[k] : pq;
+        }
+        const int gw = CW * b + q;
+        const int packed = a.emit_list[(int64_t)ts * a.E + (int64_t)gw * 64 + (w - pq)];
         const int64_t e = (int64_t)gw * 64 + (packed & 63);
         int slot = (packed >> 6) + j;
         slot = slot >= R ? slot - R : slot;
@@ -1088,7 +1098,7 @@ __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
 // the next horizon; bench.py times it this way at the trainer's own window count)
 template <class Env>
 static hipError_t launch_emit_t(const HorizonEmitArgs& ea, hipStream_t st) {
-  if ((ea.E + FUSED_ENVS - 1) / FUSED_ENVS > FUSED_EMIT_SCAN_CELLS) {
+  if (fused_emit_cells_per_lockstep(ea.E) > FUSED_EMIT_SCAN_CELLS) {
     if (ea.cell_pre == nullptr) return hipErrorInvalidValue;
     k_emit_prefix<<<ea.H, 1024, 0, st>>>(ea);
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;

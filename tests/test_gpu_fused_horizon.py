@@ -74,9 +74,11 @@ def _assert_same(a, ba, b, bb, where):
 
 CASES = [(nm, 65536, 20, False) for nm in OE.ENVS] + [("QuadTracking", 65536, 20, True), ("QuadTracking", 4000, 20, False),
                                                      ("DuctedFan", 300, 3, False), ("TwoLink", 777, 5, False),
-                                                     # 782 cells per lockstep: each cell sums the earlier cells' counts
+                                                     # 3,125 waves (196 cells of 16) per lockstep: each cell sums the
+                                                     # earlier cells' counts
                                                      ("VanderPol", 200000, 20, False),
-                                                     # 1,172 cells per lockstep (> FUSED_EMIT_SCAN_CELLS): k_emit_prefix
+                                                     # 4,688 waves per lockstep (293 cells > FUSED_EMIT_SCAN_CELLS):
+                                                     # k_emit_prefix
                                                      ("VanderPol", 300000, 20, False)]
 
 
