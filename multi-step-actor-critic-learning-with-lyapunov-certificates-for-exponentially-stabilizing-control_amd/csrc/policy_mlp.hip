@@ -481,57 +481,50 @@ __global__ __launch_bounds__(256, 1) void k_policy_forward_x6(const float* __res
 // f32 kernel).
 // The raw magnitudes behind the scales: [0] max |W1, b1|, [1] max |W2|, [2] max |W3|,
 // [3] R1 = max_k (sum_j |W1[k][j]| + |b1[k]|), [4] R2 = max_o (sum_k |W2[o][k]| + |b2[o]|).
-// PM_SC_WG workgroups of 16 waves, one row of W2 per wave and pass (a float4 per lane, wave
-// max / sum by butterflies), W1 row / W3 column of the same hidden unit on its lane 0; each
-// workgroup stores its five maxima to the partial slots scal[8 + 5 wg + q] with plain stores
-// (no atomics: 256 workgroups combining by atomic max on five words serialised at the L2, 17.5
-// us; one workgroup alone took 11 us); k_policy_pack_x3 reduces the partials.
-constexpr int PM_SC_WG = 8;
-__global__ __launch_bounds__(1024) void k_policy_scales(const float* __restrict__ W1, const float* __restrict__ b1,
-                                                        const float* __restrict__ W2, const float* __restrict__ b2,
-                                                        const float* __restrict__ W3, int D, int N3, int K1,
-                                                        float* __restrict__ P) {
-  __shared__ float red[5][16];
+// PM_SC_WG workgroups of 8 waves, one row of W2 per wave (a float4 per lane, wave max / sum by
+// butterflies), W1 row / W3 column of the same hidden unit on its lanes; each workgroup stores its
+// five maxima to the partial slots scal[8 + 5 wg + q] with plain stores (no atomics: 256 workgroups
+// combining by atomic max on five words serialised at the L2, 17.5 us; one workgroup alone took
+// 11 us, 8 workgroups of 16 waves with two rows per wave 6.5 us); k_policy_pack_x3 reduces them.
+__global__ __launch_bounds__(512) void k_policy_scales(const float* __restrict__ W1, const float* __restrict__ b1,
+                                                       const float* __restrict__ W2, const float* __restrict__ b2,
+                                                       const float* __restrict__ W3, int D, int N3, int K1,
+                                                       float* __restrict__ P) {
+  static_assert(PM_SC_WG * 8 == PM_H, "one W2 row per wave");
+  __shared__ float red[5][8];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  float v[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-  for (int row = blockIdx.x * (PM_H / PM_SC_WG) + wv; row < (blockIdx.x + 1) * (PM_H / PM_SC_WG); row += 16) {
-    const float4 x = reinterpret_cast<const float4*>(W2 + (int64_t)row * PM_H)[lane];
-    const float a = fabsf(x.x), b = fabsf(x.y), c = fabsf(x.z), d = fabsf(x.w);
-    float m2 = fmaxf(fmaxf(a, b), fmaxf(c, d)), s2 = (a + b) + (c + d);
-    // hidden unit `row`: its W1 row on lanes j < D, its W3 column on lanes 32 + o, o < N3 — one
-    // load per lane, all in flight together (a serial per-element loop on one lane waited out
-    // ~40 L2 latencies per wave: 12 us for the kernel)
-    const int j = lane & 31;
-    const float u1 = lane < 32 && j < D ? fabsf(W1[(int64_t)row * D + j]) : 0.0f;
-    const float u3 = lane >= 32 && j < N3 ? fabsf(W3[(int64_t)j * PM_H + row]) : 0.0f;
-    float m1 = u1, r1 = u1, m3 = u3;
+  const int row = blockIdx.x * 8 + wv;
+  const float4 x = reinterpret_cast<const float4*>(W2 + (int64_t)row * PM_H)[lane];
+  // hidden unit `row`: its W1 row on lanes j < D, its W3 column on lanes 32 + o, o < N3 — one
+  // load per lane, all in flight together (a serial per-element loop on one lane waited out
+  // ~40 L2 latencies per wave: 12 us for the kernel)
+  const int j = lane & 31;
+  const float u1 = lane < 32 && j < D ? fabsf(W1[(int64_t)row * D + j]) : 0.0f;
+  const float u3 = lane >= 32 && j < N3 ? fabsf(W3[(int64_t)j * PM_H + row]) : 0.0f;
+  const float bb1 = fabsf(b1[row]), bb2 = fabsf(b2[row]);
+  const float a = fabsf(x.x), b = fabsf(x.y), c = fabsf(x.z), d = fabsf(x.w);
+  float m2 = fmaxf(fmaxf(a, b), fmaxf(c, d)), s2 = (a + b) + (c + d);
+  float m1 = u1, r1 = u1, m3 = u3;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      m2 = fmaxf(m2, __shfl_xor(m2, off, 64));
-      s2 += __shfl_xor(s2, off, 64);
-      m1 = fmaxf(m1, __shfl_xor(m1, off, 64));
-      r1 += __shfl_xor(r1, off, 64);
-      m3 = fmaxf(m3, __shfl_xor(m3, off, 64));
-    }
-    const float bb = fabsf(b1[row]);
-    v[0] = fmaxf(v[0], fmaxf(m1, bb));
-    v[1] = fmaxf(v[1], m2);
-    v[2] = fmaxf(v[2], m3);
-    v[3] = fmaxf(v[3], r1 + bb);
-    v[4] = fmaxf(v[4], s2 + fabsf(b2[row]));
+  for (int off = 32; off > 0; off >>= 1) {
+    m2 = fmaxf(m2, __shfl_xor(m2, off, 64));
+    s2 += __shfl_xor(s2, off, 64);
+    m1 = fmaxf(m1, __shfl_xor(m1, off, 64));
+    r1 += __shfl_xor(r1, off, 64);
+    m3 = fmaxf(m3, __shfl_xor(m3, off, 64));
   }
-#pragma unroll
-  for (int q = 0; q < 5; ++q)
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v[q] = fmaxf(v[q], __shfl_xor(v[q], off, 64));
   if (lane == 0) {
-#pragma unroll
-    for (int q = 0; q < 5; ++q) red[q][wv] = v[q];
+    red[0][wv] = fmaxf(m1, bb1);
+    red[1][wv] = m2;
+    red[2][wv] = m3;
+    red[3][wv] = r1 + bb1;
+    red[4][wv] = s2 + bb2;
   }
   __syncthreads();
   if (threadIdx.x < 5) {
     float m = 0.0f;
-    for (int w = 0; w < 16; ++w) m = fmaxf(m, red[threadIdx.x][w]);
+#pragma unroll
+    for (int w = 0; w < 8; ++w) m = fmaxf(m, red[threadIdx.x][w]);
     P[pm_off_scal(K1) + 8 + 5 * blockIdx.x + threadIdx.x] = m;
   }
 }
@@ -543,6 +536,7 @@ __device__ __forceinline__ void pm_reduce_scales(float* P, int K1, float* out5) 
   float* scal = P + pm_off_scal(K1);
   if (threadIdx.x < 5) {
     float m = 0.0f;
+#pragma unroll
     for (int w = 0; w < PM_SC_WG; ++w) m = fmaxf(m, scal[8 + 5 * w + threadIdx.x]);
     s5[threadIdx.x] = m;
     if (blockIdx.x == 0) scal[threadIdx.x] = m;
@@ -552,63 +546,89 @@ __device__ __forceinline__ void pm_reduce_scales(float* P, int K1, float* out5) 
   for (int q = 0; q < 5; ++q) out5[q] = s5[q];
 }
 
-// One thread per packed f16 of W2x3, W1x3 and W3x3.
+// The split-f16 operands, one thread per (fragment pair, lane): the lane's eight weights of a
+// fragment (two 16-byte runs of a W2 / W3 row, or eight W1 entries), scaled by the layer's power
+// of two and split, stored as the hi and the lo fragment's 16-byte records (the split index is
+// the fragment index's low bit in every region). Fragment pairs: W2x3 PM_NB * 16 (pair P: k-step
+// P & 1, output block (P >> 1) % PM_NB, input block P / (2 PM_NB)), W1x3 PM_NB (pair = block),
+// W3x3 PM_NB * 2 (k-step P & 1, output block P >> 1).
 // with_bias: also the f32 layer-2 / layer-3 bias regions the split-f16 forward reads (k_policy_pack's
 // layout), so the default kernel needs no f32 pack launch
+constexpr int PM_X3_PAIRS_W2 = PM_NB * 16, PM_X3_PAIRS_W1 = PM_NB, PM_X3_PAIRS_W3 = PM_NB * 2;
+constexpr int PM_X3_PACK_THREADS = (PM_X3_PAIRS_W2 + PM_X3_PAIRS_W1 + PM_X3_PAIRS_W3) * 64;
+static_assert(PM_X3_PAIRS_W2 * 2 * 64 * 4 == PM_X3_FLOATS && PM_X3_PAIRS_W1 * 2 * 64 * 4 == PM_X3_W1_FLOATS &&
+                  PM_X3_PAIRS_W3 * 2 * 64 * 4 == PM_X3_W3_FLOATS,
+              "fragment pairs cover the split regions");
 __global__ __launch_bounds__(256) void k_policy_pack_x3(const float* __restrict__ W1, const float* __restrict__ b1,
                                                         const float* __restrict__ W2, const float* __restrict__ b2,
                                                         const float* __restrict__ W3, const float* __restrict__ b3,
                                                         int D, int N3, int K1, int with_bias, float* __restrict__ P) {
-  float raw5[5];
-  pm_reduce_scales(P, K1, raw5);
-  const PmScales sc = pm_scales(raw5);
-  const float sw1 = sc.sw[0], sw2 = sc.sw[1], sw3 = sc.sw[2];
-  constexpr int64_t n2 = PM_X3_FLOATS * 2, n1 = PM_X3_W1_FLOATS * 2, n3 = PM_X3_W3_FLOATS * 2;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int l = t & 63, pr = t >> 6;
+  // the weights first (independent of the scales): their loads and the partial-scale loads of
+  // pm_reduce_scales are in flight together
+  float x[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  int region = -1, idx = 0;
+  if (pr < PM_X3_PAIRS_W2) {
+    const int s = pr & 1, ob = (pr >> 1) % PM_NB, ib = pr / (2 * PM_NB);
+    const int k0 = ib * 32 + 16 * s + 4 * (l >> 5);  // elements j: k0 + (j & 3) + 8 (j >> 2)
+    const float* src = W2 + (int64_t)(ob * 32 + (l & 31)) * PM_H + k0;
+    const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 8);
+    x[0] = x0.x; x[1] = x0.y; x[2] = x0.z; x[3] = x0.w; x[4] = x1.x; x[5] = x1.y; x[6] = x1.z; x[7] = x1.w;
+    region = 1;
+    idx = pr;
+  } else if (pr < PM_X3_PAIRS_W2 + PM_X3_PAIRS_W1) {
+    const int blk = pr - PM_X3_PAIRS_W2, row = blk * 32 + (l & 31);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * (l >> 5) + j;
+      x[j] = k < D ? W1[(int64_t)row * D + k] : (k == D ? b1[row] : 0.0f);
+    }
+    region = 0;
+    idx = blk;
+  } else if (pr < PM_X3_PAIRS_W2 + PM_X3_PAIRS_W1 + PM_X3_PAIRS_W3) {
+    // the 16x16x32 A operand (policy_x3.h pm_l3_row_half): row l & 15, k-group l >> 4
+    const int p3 = pr - PM_X3_PAIRS_W2 - PM_X3_PAIRS_W1;
+    const int s = p3 & 1, ob = p3 >> 1, o = l & 7;
+    if (pm_l3_row_half(l) && o < N3) {
+      const float* src = W3 + (int64_t)o * PM_H + ob * 32 + 16 * s + 4 * (l >> 5);
+      const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 8);
+      x[0] = x0.x; x[1] = x0.y; x[2] = x0.z; x[3] = x0.w; x[4] = x1.x; x[5] = x1.y; x[6] = x1.z; x[7] = x1.w;
+    }
+    region = 2;
+    idx = p3;
+  }
   if (with_bias) {  // b2 as [blk][lane][16] (pm_row order) and b3 (N3 values, zero padded)
-    const int64_t nb2 = pm_off_w3(K1) - pm_off_b2(K1);
-    for (int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x; o < nb2 + 32; o += (int64_t)gridDim.x * 256) {
+    const int nb2 = (int)(pm_off_w3(K1) - pm_off_b2(K1));
+    for (int o = t; o < nb2 + 32; o += gridDim.x * 256) {
       if (o < nb2) {
-        const int r = (int)(o % 16), l = (int)((o / 16) % 64), blk = (int)(o / (16 * 64));
-        P[pm_off_b2(K1) + o] = b2[blk * 32 + pm_row(r, l)];
+        const int r = o % 16, ll = (o / 16) % 64, blk = o / (16 * 64);
+        P[pm_off_b2(K1) + o] = b2[blk * 32 + pm_row(r, ll)];
       } else {
-        const int i = (int)(o - nb2);
+        const int i = o - nb2;
         P[pm_off_b3(K1) + i] = i < N3 ? b3[i] : 0.0f;
       }
     }
   }
-  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n2 + n1 + n3; q += (int64_t)gridDim.x * 256) {
-    float v;
-    int64_t r;
-    _Float16* dst;
-    if (q < n2) {
-      r = q;
-      dst = reinterpret_cast<_Float16*>(P + pm_off_w2x3(K1));
-    } else if (q < n2 + n1) {
-      r = q - n2;
-      dst = reinterpret_cast<_Float16*>(P + pm_off_w1x3(K1));
-    } else {
-      r = q - n2 - n1;
-      dst = reinterpret_cast<_Float16*>(P + pm_off_w3x3(K1));
-    }
-    const int j = (int)(r & 7), l = (int)((r >> 3) & 63);
-    const int64_t f = r >> 9;  // fragment index
-    const int split = (int)(f & 1);
-    if (q < n2) {
-      const int s = (int)((f >> 1) & 1), ob = (int)((f >> 2) % PM_NB), ib = (int)(f / (4 * PM_NB));
-      const int k = ib * 32 + (j & 3) + 8 * (j >> 2) + 16 * s + 4 * (l >> 5);
-      v = W2[(int64_t)(ob * 32 + (l & 31)) * PM_H + k] * sw2;
-    } else if (q < n2 + n1) {
-      const int blk = (int)(f >> 1), k = 8 * (l >> 5) + j, row = blk * 32 + (l & 31);
-      v = k < D ? W1[(int64_t)row * D + k] * sw1 : (k == D ? b1[row] * sw1 : 0.0f);
-    } else {  // the 16x16x32 A operand (policy_x3.h pm_l3_row_half): row l & 15, k-group l >> 4
-      const int s = (int)((f >> 1) & 1), ob = (int)(f >> 2), o = l & 7;
-      const int k = ob * 32 + (j & 3) + 8 * (j >> 2) + 16 * s + 4 * (l >> 5);
-      v = pm_l3_row_half(l) && o < N3 ? W3[(int64_t)o * PM_H + k] * sw3 : 0.0f;
-    }
-    _Float16 hi, lo;
-    split2h(v, hi, lo);
-    dst[r] = split ? lo : hi;
+  float raw5[5];
+  pm_reduce_scales(P, K1, raw5);  // (a workgroup barrier: every thread of the workgroup reaches it)
+  if (region < 0) return;
+  const PmScales sc = pm_scales(raw5);
+  const float sw = sc.sw[region];
+  uint4* dst = reinterpret_cast<uint4*>(P + (region == 1 ? pm_off_w2x3(K1) : region == 0 ? pm_off_w1x3(K1)
+                                                                                          : pm_off_w3x3(K1))) +
+               (int64_t)idx * 128;
+  uint32_t hw[4], lw[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    _Float16 h0, l0, h1, l1;
+    split2h(x[2 * q] * sw, h0, l0);
+    split2h(x[2 * q + 1] * sw, h1, l1);
+    hw[q] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+    lw[q] = (uint32_t)__builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
   }
+  dst[l] = uint4{hw[0], hw[1], hw[2], hw[3]};       // fragment 2 idx: hi
+  dst[64 + l] = uint4{lw[0], lw[1], lw[2], lw[3]};  // fragment 2 idx + 1: lo
 }
 
 // WAVES = 4 (one wave per SIMD, NT = 2 tiles each) or 8 (two waves per SIMD, NT = 1: the
@@ -926,7 +946,8 @@ static int policy_mode() {
 hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2, const float* b2, const float* W3,
                               const float* b3, int D, int N3, float* P, hipStream_t st) {
   const int K1 = D / 2 + 1;  // ceil((D + 1) / 2): observation + the bias input
-  if (reinterpret_cast<uintptr_t>(W2) & 15) return hipErrorInvalidValue;  // k_policy_scales: 16-byte rows
+  // k_policy_scales / k_policy_pack_x3 read 16-byte runs of W2 and W3 rows
+  if ((reinterpret_cast<uintptr_t>(W2) | reinterpret_cast<uintptr_t>(W3)) & 15) return hipErrorInvalidValue;
   const int64_t total = pm_off_w2x6(K1);
   const int grid = (int)((total + 255) / 256 < 1024 ? (total + 255) / 256 : 1024);
   // the default kernel (split-f16, layer 3 on 8 + 8 output rows) reads only b2 / b3 in f32
@@ -939,10 +960,10 @@ hipError_t launch_policy_pack(const float* W1, const float* b1, const float* W2,
     k_policy_pack_x6<<<(int)(PM_X6_FLOATS * 2 / 256), 256, 0, st>>>(W2, K1, P);
     if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
   }
-  k_policy_scales<<<PM_SC_WG, 1024, 0, st>>>(W1, b1, W2, b2, W3, D, N3, K1, P);
+  k_policy_scales<<<PM_SC_WG, 512, 0, st>>>(W1, b1, W2, b2, W3, D, N3, K1, P);
   if (hipGetLastError() != hipSuccess) return hipErrorLaunchFailure;
-  k_policy_pack_x3<<<(int)((PM_X3_FLOATS + PM_X3_W1_FLOATS + PM_X3_W3_FLOATS) * 2 / 256), 256, 0, st>>>(
-      W1, b1, W2, b2, W3, b3, D, N3, K1, split_only ? 1 : 0, P);
+  k_policy_pack_x3<<<(PM_X3_PACK_THREADS + 255) / 256, 256, 0, st>>>(W1, b1, W2, b2, W3, b3, D, N3, K1,
+                                                                     split_only ? 1 : 0, P);
   return hipGetLastError();
 }
 

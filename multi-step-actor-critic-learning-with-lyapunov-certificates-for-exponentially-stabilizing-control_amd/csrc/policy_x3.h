@@ -56,7 +56,9 @@ __host__ __device__ constexpr int64_t pm_off_w3x3(int K1) { return pm_off_w1x3(K
 // scalars: the raw layer magnitudes of k_policy_scales (pm_scales() derives sw1..3 and the bounds
 // |H1| <= R1 max(1, max |obs|), |H2| <= R2 max(1, |H1|))
 __host__ __device__ constexpr int64_t pm_off_scal(int K1) { return pm_off_w3x3(K1) + PM_X3_W3_FLOATS; }
-__host__ __device__ constexpr int64_t pm_packed_floats(int K1) { return pm_off_scal(K1) + 64; }
+// [0..4] the final magnitudes, [8 + 5 wg + q] k_policy_scales' per-workgroup partials
+constexpr int PM_SC_WG = 32;  // k_policy_scales workgroups (8 waves, one W2 row per wave)
+__host__ __device__ constexpr int64_t pm_packed_floats(int K1) { return pm_off_scal(K1) + (8 + 5 * PM_SC_WG + 63) / 64 * 64; }
 
 __device__ __forceinline__ int pm_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
