@@ -850,37 +850,60 @@ __device__ __forceinline__ void draw_arrive(int64_t* draw, uint64_t counter, uns
 // Replay gather: blockIdx.y selects one of the 7 arrays; each thread copies 16-B vectors of
 // the sampled rows (a row of one array is n * width contiguous floats), grid-stride over
 // batch x row-vectors, so every lane moves useful bytes regardless of the field width.
+// (launch_gather bounds the batch so every per-launch element count fits 32 bits: the index
+// arithmetic is unsigned 32-bit, its divisions a few instructions instead of a 64-bit expansion)
 template <typename V>
 __device__ __forceinline__ void gather_rows(const float* src, float* dst, RowIndex& ix, int64_t batch, int64_t len) {
-  const int64_t v = len * (int64_t)sizeof(float) / (int64_t)sizeof(V);
+  const uint32_t v = (uint32_t)(len * (int64_t)sizeof(float) / (int64_t)sizeof(V));
   const V* s = reinterpret_cast<const V*>(src);
   V* d = reinterpret_cast<V*>(dst);
-  const int64_t total = batch * v;
-  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
-    const int64_t b = q / v, i = q - b * v;
-    d[q] = s[ix(b) * v + i];
+  const uint32_t total = (uint32_t)batch * v;
+  for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < total; q += gridDim.x * 256) {
+    const uint32_t b = q / v, i = q - b * v;
+    d[q] = s[ix(b) * (int64_t)v + i];
   }
 }
 
 // the joint layouts: element-wise (D + A and D are small), rows of the windows at idx
 __device__ __forceinline__ void gather_joint(const GatherArgs& a, RowIndex& ix) {
-  const int64_t n = a.n, D = a.D, A = a.A;
+  const uint32_t n = (uint32_t)a.n, D = (uint32_t)a.D, A = (uint32_t)a.A, B = (uint32_t)a.batch;
+  // GJ elements per thread and round, every source address formed and loaded before the first
+  // store (a plain grid-stride loop waited out one random store-row load per element)
+  constexpr int GJ = 4;
+  const uint32_t stride = gridDim.x * 256;
   if (blockIdx.y == 7) {
-    const int64_t W = D + A, total = a.batch * n * W;
-    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
-      const int64_t row = q / W, c = q - row * W, b = row / n, t = row - b * n, w = ix(b);
-      a.o_obs_act[q] = c < D ? a.s_obs[(w * n + t) * D + c] : a.s_act[(w * n + t) * A + (c - D)];
+    const uint32_t W = D + A, total = B * n * W;
+    for (uint32_t q0 = blockIdx.x * 256 + threadIdx.x; q0 < total; q0 += GJ * stride) {
+      float v[GJ];
+#pragma unroll
+      for (int u = 0; u < GJ; ++u) {
+        const uint32_t q = q0 + u * stride;
+        const uint32_t qq = q < total ? q : total - 1;
+        const uint32_t row = qq / W, c = qq - row * W, b = row / n, t = row - b * n;
+        const int64_t wr = ix(b) * (int64_t)n + t;  // the store row
+        v[u] = c < D ? a.s_obs[wr * D + c] : a.s_act[wr * A + (c - D)];
+      }
+#pragma unroll
+      for (int u = 0; u < GJ; ++u)
+        if (q0 + u * stride < total) a.o_obs_act[q0 + u * stride] = v[u];
     }
   } else {
-    const int64_t total = (a.batch + a.batch * n) * D;
-    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < total; q += (int64_t)gridDim.x * 256) {
-      const int64_t row = q / D, c = q - row * D;
-      if (row < a.batch) {
-        a.o_v_in[q] = a.s_obs[(ix(row) * n) * D + c];
-      } else {
-        const int64_t r = row - a.batch, b = r / n, t = r - b * n;
-        a.o_v_in[q] = a.s_obs2[(ix(b) * n + t) * D + c];
+    const uint32_t total = (B + B * n) * D;
+    for (uint32_t q0 = blockIdx.x * 256 + threadIdx.x; q0 < total; q0 += GJ * stride) {
+      float v[GJ];
+#pragma unroll
+      for (int u = 0; u < GJ; ++u) {
+        const uint32_t q = q0 + u * stride;
+        const uint32_t qq = q < total ? q : total - 1;
+        const uint32_t row = qq / D, c = qq - row * D;
+        const bool first = row < B;
+        const uint32_t r = first ? row : row - B, b = first ? r : r / n, t = first ? 0 : r - b * n;
+        const float* src = first ? a.s_obs : a.s_obs2;
+        v[u] = src[(ix(b) * (int64_t)n + t) * D + c];
       }
+#pragma unroll
+      for (int u = 0; u < GJ; ++u)
+        if (q0 + u * stride < total) a.o_v_in[q0 + u * stride] = v[u];
     }
   }
 }
@@ -1052,6 +1075,8 @@ hipError_t launch_emit_fused(int env_id, const EmitArgs& a, hipStream_t st) {
 }
 hipError_t launch_gather(const GatherArgs& a, hipStream_t st) {
   if (a.batch <= 0) return hipSuccess;
+  // the kernel's element counts are 32-bit (joint layouts: (batch + batch n) D and batch n (D + A))
+  if (a.batch * ((int64_t)a.n + 1) * ((int64_t)a.D + a.A) >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
   const int64_t vec = (a.batch * (int64_t)a.n * (a.D > a.A ? a.D : a.A) + 1023) / 1024;  // float4s of the widest array
   const int gx = (int)(vec < 1 ? 1 : (vec > 2048 ? 2048 : vec));
   k_gather<<<dim3(gx, (a.o_obs_act || a.o_v_in) ? 9 : 7), 256, 0, st>>>(a);
