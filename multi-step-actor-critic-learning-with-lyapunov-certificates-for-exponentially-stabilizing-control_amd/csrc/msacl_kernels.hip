@@ -27,16 +27,19 @@ constexpr int TPB = 1024;  // one workgroup; 16 wavefronts
 // torch.maximum / torch.minimum backward: ties split the gradient in half.
 __device__ __forceinline__ float relu_grad(float a) { return a > 0.0f ? 1.0f : (a == 0.0f ? 0.5f : 0.0f); }
 
+// Workgroup sum of one double per thread, the same value returned to every thread: a butterfly
+// within each wavefront, then the 16 wave totals added in wave order by every thread (two
+// barriers; the 10-level LDS tree it replaces held 10 barriers per sum). `sh` needs TPB / 64 + 1
+// entries. Deterministic: a fixed order for a fixed launch shape.
 __device__ double block_sum(double v, double* sh) {
-  const int t = threadIdx.x;
-  sh[t] = v;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
   __syncthreads();
-  for (int off = TPB / 2; off > 0; off >>= 1) {
-    if (t < off) sh[t] += sh[t + off];
-    __syncthreads();
-  }
-  double r = sh[0];
-  __syncthreads();
+  double r = 0.0;
+#pragma unroll
+  for (int w = 0; w < TPB / 64; ++w) r += sh[w];
+  __syncthreads();  // sh is reused by the next sum
   return r;
 }
 
@@ -509,8 +512,8 @@ __global__ __launch_bounds__(TPB) void k_policy_objective_step(
     dq1[i] = a == bq ? gg / 2.0f : (a > bq ? 0.0f : gg);
     dq2[i] = a == bq ? gg / 2.0f : (a < bq ? 0.0f : gg);
     dlogp[i] = (-gg) * alpha;
-    const int64_t b = i / n;
-    dlp_new[i] = (i - b * n) == 0 ? (-(g1 * d_ratio[b])) * ratio[b] : 0.0f;
+    const int b = (int)i / n;  // (N = B n < 2^31)
+    dlp_new[i] = ((int)i - b * n) == 0 ? (-(g1 * d_ratio[b])) * ratio[b] : 0.0f;
   }
   if (alpha_grad && threadIdx.x == 0) alpha_grad[0] = (entropy[0] - target_entropy) * expf(log_alpha[0]);
 }
