@@ -613,9 +613,12 @@ class MSACL:
             with torch.cuda.stream(side):
                 loss_lya = self._lyapunov_update(data, keep_policy=do_policy)
             loss_q, q1_mean, q2_mean = self._q_update(data, stats=do_policy)
+            main.wait_stream(side)
+            # the target update after the join: a graph whose last node sits on a side queue makes
+            # the next graph launch wait ~20 us for its completion instead of ~5 us (kernel trace,
+            # profiles/r05_update_tail_ab.txt); the Polyak step reads only the stepped critics
             if do_target:
                 self._target_update()
-            main.wait_stream(side)
         elif self._segmented() and self.concurrent and self.device.type == "cuda":
             # data parallel: the two backward passes still run as parallel branches, and their
             # gradients are averaged by ONE all-reduce at the join (one graph cut instead of two,
