@@ -228,7 +228,7 @@ def main():
 
     wrapped = [(trainer, timed(trainer, "_sample")), (trainer, timed(trainer, "_replay_batch")),
                (alg, timed(alg, "model_update")), (alg, timed(alg, "model_update_drawn")),
-               (buffer, timed(buffer, "add_batch"))]
+               (buffer, timed(buffer, "add_batch")), (trainer, timed(trainer, "_graph_step"))]
     torch.cuda.synchronize()
     th0 = time.perf_counter()
     for _ in range(k_host):

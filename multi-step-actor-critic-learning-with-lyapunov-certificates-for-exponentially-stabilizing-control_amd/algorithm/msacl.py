@@ -536,6 +536,26 @@ class MSACL:
         outs = self._graph_update(None, flags, draw=draw)
         return self._update_result(outs, flags, self._static, start)
 
+    def drawn_step_parts(self, draw, global_iteration: int):
+        """model_update_drawn as parts for a trainer-level graph that also holds the sampling
+        before it (NstepOffSerialTrainer._graph_step): (key, body, post), or None until this
+        branch's eager first run happened (through model_update_drawn) or when the update is not
+        one graph (annealed learning rates, data-parallel segments). body() -> outs: the draw and
+        the update, exactly what the drawn graph captures; post(outs, start) -> model_update's
+        return value."""
+        if self.anneal_lr or self._static is None or self._segmented():
+            return None
+        flags = (global_iteration % self.target_network_frequency == 0, global_iteration % self.policy_frequency == 0)
+        if flags + ("drawn",) not in self._warm:
+            return None
+        key = flags + (self._static["rew"].data_ptr(),)
+
+        def body():
+            draw(self._static)
+            return self._update_body(self._static, *flags)
+
+        return key, body, lambda outs, start: self._update_result(outs, flags, self._static, start)
+
     def _update_result(self, outs, flags, data, start):
         tb_info = None
         if flags[1]:

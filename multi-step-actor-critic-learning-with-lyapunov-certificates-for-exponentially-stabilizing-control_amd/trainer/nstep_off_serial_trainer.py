@@ -79,6 +79,9 @@ class NstepOffSerialTrainer:
                         and hasattr(self.sampler, "bind_store"))
         self._side = None
         self._pending = None
+        # one graph per iteration kind holding the sampling AND the update (_graph_step)
+        self.graph_step = bool(kwargs.get("trainer_graph_step", os.environ.get("MSACL_GRAPH_STEP", "1") != "0"))
+        self._step_graphs = {}
         self.start_time = time.time()
 
     def _sample(self):
@@ -121,7 +124,59 @@ class NstepOffSerialTrainer:
         return (self.overlap and self.iteration % self.policy_frequency != 0
                 and (self.iteration + 1) % self.sample_interval == 0 and self.iteration + 1 <= self.max_iteration)
 
+    def _graph_step(self):
+        """The iteration's sampling and update replayed as ONE HIP graph instead of two (the
+        sampler's and the update's): the graph-to-graph transition between them (~9 us on the
+        device) becomes a kernel boundary inside the graph. Applies once both parts were run
+        eagerly (sampler: its first horizon; update: each branch's first call) to the plain
+        drawn-update path (sampling every iteration, no PER, no overlapped sampling, sampler time
+        not synchronised). The captured work is exactly the two graphs' in their order.
+        -> (True, model_update's return value), or None to take the separate calls."""
+        if (not self.graph_step or self.sample_interval != 1 or self._pending is not None or self.per_flag
+                or not self._drawn_update() or getattr(self.sampler, "device", None) != getattr(self.alg, "device", None)):
+            return None
+        sparts, aparts = getattr(self.sampler, "step_graph_parts", None), getattr(self.alg, "drawn_step_parts", None)
+        if sparts is None or aparts is None:
+            return None
+        sp = sparts()
+        if sp is None:
+            return None
+        B, buf = self.replay_batch_size, self.buffer
+        ap = aparts(lambda out: buf.sample_batch(B, out=out), self.iteration)
+        if ap is None:
+            return None
+        skey, pre, sbody, spost = sp
+        akey, abody, apost = ap
+        key = (skey, akey)
+        pre()
+        t0, start = time.perf_counter(), time.time()
+        ent = self._step_graphs.get(key)
+        if ent is None:
+            # graphs of an older sampler key (other policy / observation buffers) are dead
+            self._step_graphs = {k: v for k, v in self._step_graphs.items() if k[0] == skey}
+            g = torch.cuda.CUDAGraph()
+            with D.cuda_graph(g):
+                sbody()
+                outs = abody()
+            ent = self._step_graphs[key] = (g, outs)
+        g, outs = ent
+        self.networks.train()
+        g.replay()
+        samples, stb = spost(t0)
+        self.buffer.add_batch(samples)
+        self.sampler_tb_dict.add_average(stb)
+        return True, apost(outs, start)
+
     def step(self):
+        graphed = self._graph_step()
+        if graphed is not None:
+            alg_tb_dict = graphed[1]
+            if (self.iteration % self.policy_frequency == 0 and self.iteration % self.log_save_interval == 0
+                    and self.is_main):
+                print("Iter = ", self.iteration, "save training data!")
+                add_scalars(alg_tb_dict, self.writer, step=self.iteration)
+            self._step_tail()
+            return
         if self.iteration % self.sample_interval == 0:
             if self._pending is not None:  # enqueued on the side stream during the last update
                 sampler_samples, sampler_tb_dict = self._pending
@@ -152,6 +207,9 @@ class NstepOffSerialTrainer:
                 add_scalars(alg_tb_dict, self.writer, step=self.iteration)
         else:
             self._update(replay_samples)
+        self._step_tail()
+
+    def _step_tail(self):
         self.networks.eval()
         if self.iteration % self.log_save_interval == 0:
             check = getattr(self.sampler, "check_errors", None)  # device sampler health (every rank)
@@ -203,6 +261,7 @@ class NstepOffSerialTrainer:
         fin = getattr(self, "finish_pending", None)
         if fin is not None:
             fin()
+        self._step_graphs = {}  # (their captured work references the parts' device buffers)
         for part in (self.sampler, self.alg, self.evaluator):
             close = getattr(part, "close", None)
             if close is not None:

@@ -300,6 +300,40 @@ class HipNstepOffSampler:
             return batch
         return DeviceWindowBatch(self, store, store.cursor[2] - before)
 
+    def step_graph_parts(self):
+        """The pieces of one graphed sample() for a trainer-level graph that also holds the update
+        after it (NstepOffSerialTrainer._graph_step): (key, pre, body, post), or None while that
+        does not apply (eager horizons still due, per-kernel timing, a synchronised sampler time,
+        no fused horizon, or no bound store). key: what the capture depends on (as the sampler
+        graph's key); pre(): host work before the replay; body(): the horizon, exactly what the
+        sampler graph captures; post(t0) -> sample()'s return value after the replay."""
+        if (self._h is None or not self.use_graph or self._eager_calls < 1 or getattr(self, "_timing", False)
+                or self.sync_timing or self._bound is None):
+            return None
+        if not self._fused_horizon_ok(self._fused_layers() is not None):
+            return None
+        store = self._bound
+        key = (id(store), id(self.networks.policy), tuple(p.data_ptr() for p in self.networks.policy.parameters()),
+               self.obs.data_ptr())
+
+        def pre():
+            # the previous horizon's window count lives in the fused kernel's header until this one
+            prev = self._last_batch() if self._last_batch is not None else None
+            if prev is not None:
+                prev.resolve()
+            self.total_sample_number += self.sample_batch_size
+
+        def body():
+            with torch.no_grad():
+                self._horizon(store)
+
+        def post(t0):
+            batch = DeviceWindowBatch(self, store, None, count_fn=self._window_count)
+            self._last_batch = weakref.ref(batch)
+            return batch, {tb_tags["sampler_time"]: (time.perf_counter() - t0) * 1000}
+
+        return key, pre, body, post
+
     def sample(self):
         """-> (DeviceWindowBatch, {sampler_time ms}) (base.py:308-323)."""
         self.total_sample_number += self.sample_batch_size

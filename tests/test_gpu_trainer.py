@@ -193,3 +193,52 @@ def test_gather_into_update_inputs_equals_copy(tmp_path, monkeypatch, buffer_nam
         assert torch.equal(a[0][k], b[0][k]), k
     if a[1] is not None:
         assert torch.equal(a[1], b[1])
+
+
+@pytest.mark.parametrize("env_name", ["QuadTracking", "DuctedFan"])
+def test_graphed_step_equals_separate_graphs(tmp_path, env_name):
+    """trainer_graph_step (the iteration's sampling and update replayed as one graph, active with
+    an unsynchronised sampler time) gives bit-identical networks, window store, replay cursor,
+    sampler state and logged scalars to the sampler graph + update graph pair (deterministic GEMM
+    mode, as above)."""
+    prev = torch.are_deterministic_algorithms_enabled()
+    torch.use_deterministic_algorithms(True, warn_only=True)
+
+    def run(graph_step, sub):
+        torch.manual_seed(0)
+        args = default_msacl_args(env_name=env_name, env_num=4096, buffer_warm_size=3000, buffer_max_size=60000,
+                                  max_iteration=9, eval_interval=10 ** 6, log_save_interval=10 ** 6,
+                                  apprfunc_save_interval=10 ** 6, save_folder=str(tmp_path / sub), seed=0,
+                                  num_eval_episode=1, sampler_sync_timing=False, trainer_graph_step=graph_step)
+        args, alg, sampler, buffer, evaluator, trainer = build_pipeline(args)
+        used = []
+        orig = trainer._graph_step
+
+        def spy():
+            r = orig()
+            used.append(r is not None)
+            return r
+        trainer._graph_step = spy
+        while trainer.iteration <= trainer.max_iteration:
+            trainer.step()
+            trainer.iteration += 1
+        torch.cuda.synchronize()
+        sd = {k: v.detach().cpu().clone() for k, v in alg.networks.state_dict().items()}
+        store = {k: v.cpu().clone() for k, v in buffer.n_step_buf.items()}
+        ring = alg._tb_ring.cpu().clone() if getattr(alg, "_tb_ring", None) is not None else None  # logged scalars
+        out = (sd, store, buffer.cursor.cpu().clone(), sampler.obs.cpu().clone(), used, ring)
+        trainer.close()
+        return out
+
+    try:
+        a = run(True, "a")
+        b = run(False, "b")
+    finally:
+        torch.use_deterministic_algorithms(prev)
+    assert any(a[4]) and not any(b[4])  # the graphed step really ran (and never in the reference run)
+    for k in a[0]:
+        assert torch.equal(a[0][k], b[0][k]), k
+    for k in a[1]:
+        assert torch.equal(a[1][k], b[1][k]), k
+    assert torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
+    assert a[5] is not None and torch.equal(a[5], b[5])
