@@ -380,11 +380,26 @@ __device__ __forceinline__ void policy_loss_body(const float* q1, const float* q
                                                  double* sh) {
   const float alpha = expf(*log_alpha);
   double a = 0.0, b = 0.0;
-  for (int64_t i = threadIdx.x; i < N; i += TPB) {
-    const float m = torch_min(q1[i], q2[i]);
-    const float lp = logp[i];
-    a += (double)(m - alpha * lp);
-    b += (double)lp;
+  // PL_U of a thread's elements per round, every load issued before the first sum (the plain
+  // loop waited out one load round trip per element); the sums keep the element order
+  constexpr int PL_U = 8;
+  for (int64_t i0 = threadIdx.x; i0 < N; i0 += PL_U * TPB) {
+    float x1[PL_U], x2[PL_U], xl[PL_U];
+#pragma unroll
+    for (int u = 0; u < PL_U; ++u) {
+      const int64_t i = i0 + (int64_t)u * TPB, ic = i < N ? i : N - 1;
+      x1[u] = q1[ic];
+      x2[u] = q2[ic];
+      xl[u] = logp[ic];
+    }
+#pragma unroll
+    for (int u = 0; u < PL_U; ++u) {
+      if (i0 + (int64_t)u * TPB < N) {
+        const float m = torch_min(x1[u], x2[u]);
+        a += (double)(m - alpha * xl[u]);
+        b += (double)xl[u];
+      }
+    }
   }
   const double ta = block_sum(a, sh);
   const double tb = block_sum(b, sh);
@@ -507,13 +522,28 @@ __global__ __launch_bounds__(TPB) void k_policy_objective_step(
   const float g1 = 1.0f;
   const float gq = -g1;
   const float gg = gq * (1.0f / (float)N);
-  for (int64_t i = threadIdx.x; i < N; i += TPB) {
-    const float a = q1[i], bq = q2[i];
-    dq1[i] = a == bq ? gg / 2.0f : (a > bq ? 0.0f : gg);
-    dq2[i] = a == bq ? gg / 2.0f : (a < bq ? 0.0f : gg);
-    dlogp[i] = (-gg) * alpha;
-    const int b = (int)i / n;  // (N = B n < 2^31)
-    dlp_new[i] = ((int)i - b * n) == 0 ? (-(g1 * d_ratio[b])) * ratio[b] : 0.0f;
+  constexpr int GU = 8;  // (loads first, as policy_loss_body)
+  for (int64_t i0 = threadIdx.x; i0 < N; i0 += GU * TPB) {
+    float x1[GU], x2[GU], dr[GU];
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      const int i = (int)(i0 + (int64_t)u * TPB), ic = i < N ? i : (int)N - 1;  // (N = B n < 2^31)
+      const int b = ic / n;
+      x1[u] = q1[ic];
+      x2[u] = q2[ic];
+      dr[u] = (ic - b * n) == 0 ? (-(g1 * d_ratio[b])) * ratio[b] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < GU; ++u) {
+      const int64_t i = i0 + (int64_t)u * TPB;
+      if (i < N) {
+        const float a = x1[u], bq = x2[u];
+        dq1[i] = a == bq ? gg / 2.0f : (a > bq ? 0.0f : gg);
+        dq2[i] = a == bq ? gg / 2.0f : (a < bq ? 0.0f : gg);
+        dlogp[i] = (-gg) * alpha;
+        dlp_new[i] = dr[u];
+      }
+    }
   }
   if (alpha_grad && threadIdx.x == 0) alpha_grad[0] = (entropy[0] - target_entropy) * expf(log_alpha[0]);
 }
