@@ -1,7 +1,7 @@
 #!/bin/bash
-# Update-graph tail A/B (MSACL_EXP_TAIL=join: the target update after the branches' join, so the
-# policy-free graph ends on the capture stream): kernel traces with the update -> next sampler gap,
-# then alternating bench lines
+# Update-graph tail A/B as run for profiles/r05_update_tail_ab.txt (then switched by a temporary
+# MSACL_EXP_TAIL=join in algorithm/msacl.py; "join" is now the only layout, so both arms below run
+# the same code): kernel traces with the update -> next sampler gap, then alternating bench lines
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
