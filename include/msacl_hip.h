@@ -276,9 +276,11 @@ int mh_gae(const float* val, const float* val2, const float* rew, const uint8_t*
            int32_t horizon, double gamma, double gae_lambda, float* adv, float* ret, void* stream);
 
 /* ---- sampler policy forward: StochaPolicy's MLP (RL/apprfunc/mlp.py:111-136, obs -> Linear ->
- * ReLU -> Linear -> ReLU -> Linear -> (mean | log_std)) as one fused f32-MFMA kernel. Supported
- * shape: hidden sizes 256 x 256 (every reference script's default), obs_dim <= 16,
- * out_dim (= 2 * act_dim) <= 32; other shapes return MH_EINVAL (the caller uses PyTorch). ---- */
+ * ReLU -> Linear -> ReLU -> Linear -> (mean | log_std)) as one fused MFMA kernel: split-f16
+ * products (three per f32 product, f32 accumulation) for obs_dim <= 15 and out_dim <= 8 (every
+ * env's policy head), f32-input MFMAs otherwise. Supported shape: hidden sizes 256 x 256 (every
+ * reference script's default), obs_dim <= 16, out_dim (= 2 * act_dim) <= 32, W2 and W3 16-byte
+ * aligned; other shapes return MH_EINVAL (the caller uses PyTorch). ---- */
 /* floats of the packed parameter buffer for a given obs_dim */
 int mh_policy_packed_size(int32_t obs_dim, int64_t* floats_out);
 /* Pack nn.Linear parameters (row-major [out][in] weights, [out] biases, device pointers) into the
