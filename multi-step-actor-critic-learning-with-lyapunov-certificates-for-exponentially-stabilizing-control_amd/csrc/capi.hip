@@ -829,6 +829,8 @@ int mh_policy_pack(const float* W1, const float* b1, const float* W2, const floa
   if (hidden1 != 256 || hidden2 != 256) return fail(MH_EINVAL, "mh_policy_pack: hidden sizes must be 256 x 256");
   if (obs_dim <= 0 || obs_dim > 16) return fail(MH_EINVAL, "mh_policy_pack: obs_dim must be in [1, 16]");
   if (out_dim <= 0 || out_dim > 32) return fail(MH_EINVAL, "mh_policy_pack: out_dim must be in [1, 32]");
+  if ((reinterpret_cast<uintptr_t>(W2) | reinterpret_cast<uintptr_t>(W3)) & 15)
+    return fail(MH_EINVAL, "mh_policy_pack: W2 and W3 must be 16-byte aligned");
   MH_HIP(mh::launch_policy_pack(W1, b1, W2, b2, W3, b3, obs_dim, out_dim, packed, (hipStream_t)stream));
   return MH_OK;
 }
