@@ -388,6 +388,7 @@ class MSACL:
         self._tb_ring = None
         self._tb_ctr = None
         self._tb_gen = 0
+        self.policy_updates = 0  # policy optimiser steps taken (host count, read by the trainer's step graph)
 
     def close(self):
         """Release the captured update graphs, their static inputs, the scratch buffers and the
@@ -557,6 +558,8 @@ class MSACL:
         return key, body, lambda outs, start: self._update_result(outs, flags, self._static, start)
 
     def _update_result(self, outs, flags, data, start):
+        if flags[1]:
+            self.policy_updates += 1  # (every update path: eager, replayed, or inside a step graph)
         tb_info = None
         if flags[1]:
             # the logged scalars (msacl.py:211-222), stacked on the device inside the update and

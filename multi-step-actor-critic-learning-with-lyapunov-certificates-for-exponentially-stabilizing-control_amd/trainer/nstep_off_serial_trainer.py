@@ -82,6 +82,7 @@ class NstepOffSerialTrainer:
         # one graph per iteration kind holding the sampling AND the update (_graph_step)
         self.graph_step = bool(kwargs.get("trainer_graph_step", os.environ.get("MSACL_GRAPH_STEP", "1") != "0"))
         self._step_graphs = {}
+        self._packed_state = None  # (sampler key, policy updates, policy version) at the last graphed pack
         self.start_time = time.time()
 
     def _sample(self):
@@ -145,9 +146,21 @@ class NstepOffSerialTrainer:
         ap = aparts(lambda out: buf.sample_batch(B, out=out), self.iteration)
         if ap is None:
             return None
+        # the policy pack (two launches, ~11 us) only when the parameters may have changed since the
+        # last graphed pack: a policy update since (the algorithm's host count, every update path)
+        # or any in-place write through torch (the parameters' version counters)
+        skey = sp[0]
+        pv = getattr(self.alg, "policy_updates", None)
+        vfn = getattr(self.sampler, "policy_version", None)
+        state = (skey, pv, vfn() if vfn is not None else None)
+        pack = not (pv is not None and vfn is not None and self._packed_state == state)
+        if not pack:
+            sp = sparts(pack=False)
         skey, pre, sbody, spost = sp
         akey, abody, apost = ap
-        key = (skey, akey)
+        key = (skey, akey, pack)
+        if pack:
+            self._packed_state = state
         pre()
         t0, start = time.perf_counter(), time.time()
         ent = self._step_graphs.get(key)
@@ -161,7 +174,7 @@ class NstepOffSerialTrainer:
             ent = self._step_graphs[key] = (g, outs)
         g, outs = ent
         self.networks.train()
-        g.replay()
+        g.replay()  # (a policy update inside advances alg.policy_updates in apost: the next step packs)
         samples, stb = spost(t0)
         self.buffer.add_batch(samples)
         self.sampler_tb_dict.add_average(stb)

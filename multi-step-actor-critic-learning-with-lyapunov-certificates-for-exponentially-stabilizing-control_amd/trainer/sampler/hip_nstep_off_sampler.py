@@ -234,8 +234,10 @@ class HipNstepOffSampler:
     def _fused_horizon_ok(self, fused):
         return fused and self.fused_horizon and self.envs.obs_dim <= 15
 
-    def _horizon(self, store, act_out=None, logp_out=None):
-        fused = self._pack_policy()
+    def _horizon(self, store, act_out=None, logp_out=None, pack=True):
+        # pack=False (a trainer step graph whose caller knows the packed copy is current): the
+        # packed parameters of the last pack are used as they are
+        fused = self._pack_policy() if (pack or self._packed is None) else self._fused_layers() is not None
         self._draw_noise()
         if self._fused_horizon_ok(fused):
             # policy -> sample -> env step -> ring push for every lockstep in ONE persistent
@@ -300,13 +302,19 @@ class HipNstepOffSampler:
             return batch
         return DeviceWindowBatch(self, store, store.cursor[2] - before)
 
-    def step_graph_parts(self):
+    def policy_version(self):
+        """Sum of the policy parameters' in-place version counters (torch bumps them on every
+        in-place write through torch: load_state_dict, optimiser steps, manual edits)."""
+        return sum(p._version for p in self.networks.policy.parameters())
+
+    def step_graph_parts(self, pack=True):
         """The pieces of one graphed sample() for a trainer-level graph that also holds the update
         after it (NstepOffSerialTrainer._graph_step): (key, pre, body, post), or None while that
         does not apply (eager horizons still due, per-kernel timing, a synchronised sampler time,
         no fused horizon, or no bound store). key: what the capture depends on (as the sampler
         graph's key); pre(): host work before the replay; body(): the horizon, exactly what the
-        sampler graph captures; post(t0) -> sample()'s return value after the replay."""
+        sampler graph captures (pack=False: without the policy pack, for a caller that knows the
+        packed copy matches the parameters); post(t0) -> sample()'s return value after the replay."""
         if (self._h is None or not self.use_graph or self._eager_calls < 1 or getattr(self, "_timing", False)
                 or self.sync_timing or self._bound is None):
             return None
@@ -325,7 +333,7 @@ class HipNstepOffSampler:
 
         def body():
             with torch.no_grad():
-                self._horizon(store)
+                self._horizon(store, pack=pack)
 
         def post(t0):
             batch = DeviceWindowBatch(self, store, None, count_fn=self._window_count)

@@ -198,9 +198,9 @@ def test_gather_into_update_inputs_equals_copy(tmp_path, monkeypatch, buffer_nam
 @pytest.mark.parametrize("env_name", ["QuadTracking", "DuctedFan"])
 def test_graphed_step_equals_separate_graphs(tmp_path, env_name):
     """trainer_graph_step (the iteration's sampling and update replayed as one graph, active with
-    an unsynchronised sampler time) gives bit-identical networks, window store, replay cursor,
-    sampler state and logged scalars to the sampler graph + update graph pair (deterministic GEMM
-    mode, as above)."""
+    an unsynchronised sampler time; the policy pack skipped after a policy-free update) gives
+    bit-identical networks, window store, replay cursor, sampler state and logged scalars to the
+    sampler graph + update graph pair (deterministic GEMM mode, as above)."""
     prev = torch.are_deterministic_algorithms_enabled()
     torch.use_deterministic_algorithms(True, warn_only=True)
 
@@ -226,7 +226,9 @@ def test_graphed_step_equals_separate_graphs(tmp_path, env_name):
         sd = {k: v.detach().cpu().clone() for k, v in alg.networks.state_dict().items()}
         store = {k: v.cpu().clone() for k, v in buffer.n_step_buf.items()}
         ring = alg._tb_ring.cpu().clone() if getattr(alg, "_tb_ring", None) is not None else None  # logged scalars
-        out = (sd, store, buffer.cursor.cpu().clone(), sampler.obs.cpu().clone(), used, ring)
+        # graphs of policy iterations that reuse the packed policy of the policy-free step before
+        skipped = any(not k[2] for k in trainer._step_graphs)
+        out = (sd, store, buffer.cursor.cpu().clone(), sampler.obs.cpu().clone(), used, ring, skipped)
         trainer.close()
         return out
 
@@ -236,6 +238,7 @@ def test_graphed_step_equals_separate_graphs(tmp_path, env_name):
     finally:
         torch.use_deterministic_algorithms(prev)
     assert any(a[4]) and not any(b[4])  # the graphed step really ran (and never in the reference run)
+    assert a[6]  # ... and skipped the redundant policy packs
     for k in a[0]:
         assert torch.equal(a[0][k], b[0][k]), k
     for k in a[1]:
