@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Per-trainer-step device timeline from a rocprofv3 --kernel-trace CSV of bench.py.
 
-A step starts at the sampler's policy pack (k_policy_scales) and ends at the next one. Prints, for
+A step starts at the sampler's first kernel (the policy pack k_policy_scales / k_policy_pack_x3
+right before the fused horizon kernel, or the fused kernel itself when the graphed step skipped
+the pack; without the fused kernel, the pack) and ends at the next one. Prints, for
 the timed steps, the step span, the sampler / update split and the number of kernels, then the
 kernel-by-kernel timeline (start offset, duration, gap before it) of one even and one odd step.
 Usage: python tools/step_timeline.py <kernel_trace.csv> [out.txt]"""
@@ -14,7 +16,15 @@ def main():
     out = open(sys.argv[2], "w") if len(sys.argv) > 2 else sys.stdout
     rows = list(csv.DictReader(open(src)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    starts = [i for i, r in enumerate(rows) if "k_policy_scales" in r["Kernel_Name"]]
+    fused = [i for i, r in enumerate(rows) if "k_sample_fused" in r["Kernel_Name"]]
+    if fused:
+        starts = []
+        for j in fused:
+            while j > 0 and any(k in rows[j - 1]["Kernel_Name"] for k in ("k_policy_scales", "k_policy_pack_x3")):
+                j -= 1
+            starts.append(j)
+    else:
+        starts = [i for i, r in enumerate(rows) if "k_policy_scales" in r["Kernel_Name"]]
     steps = []
     for a, b in zip(starts[:-1], starts[1:]):
         seg = rows[a:b]
@@ -23,6 +33,8 @@ def main():
         i_emit = max((i for i, r in enumerate(seg) if "k_emit_cells" in r["Kernel_Name"]), default=None)
         samp_end = int(seg[i_emit]["End_Timestamp"]) if i_emit is not None else t0
         busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg)
+        if fused and not any("k_gather" in r["Kernel_Name"] for r in seg):
+            continue  # a diagnostic fused-kernel launch of bench.py, not a trainer step
         steps.append((t1 - t0, samp_end - t0, t1 - samp_end, len(seg), busy, seg))
     timed = steps[-20:] if len(steps) > 20 else steps
     print(f"{len(steps)} steps; the last {len(timed)}:", file=out)
