@@ -225,13 +225,18 @@ __global__ __launch_bounds__(RTPB) void k_q_target(const float* q1, const float*
 // --------------------------------------------------- Lyapunov certificate (msacl.py:279-332)
 // cumprod of the clipped IS ratio is a wave-level inclusive product scan (n <= 64 per pass,
 // chained across passes).
+// DT: the observation width at compile time (1..16; the launcher dispatches on D), so the
+// per-lane norm loops unroll and their loads issue together instead of one round trip per
+// element (the runtime-D loop, DT = 0, waited out 2 D dependent loads per lane)
+template <int DT>
 __global__ __launch_bounds__(RTPB) void k_lyapunov(const float* logp, const float* old_logp, const float* V,
                                                    const float* V2, const float* obs, const float* obs2,
                                                    const float* c, const float* w, const float* s, float alpha1,
                                                    float alpha2, float pos_scale, float diff_scale, int B, int n,
-                                                   int D, float* is_clip, float* esl, float* lya_diff,
+                                                   int Drt, float* is_clip, float* esl, float* lya_diff,
                                                    float* loss_out, float* dV, float* dV2, double* part,
                                                    unsigned int* arrive) {
+  const int D = DT > 0 ? DT : Drt;
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * RPB + (threadIdx.x >> 6);
   const int64_t N = (int64_t)B * n;
@@ -649,10 +654,30 @@ int mh_msacl_lyapunov(const float* logp, const float* old_logp, const float* lya
   const int64_t nb = ((int64_t)B + RPB - 1) / RPB;
   RowScratch* rs = nullptr;
   if (row_scratch(1, nb, &rs) != hipSuccess) return MH_EHIP;
-  k_lyapunov<<<(unsigned)nb, RTPB, 0, (hipStream_t)stream>>>(logp, old_logp, lya_obs, lya_obs2, obs, obs2, c, w, s,
-                                                             alpha1, alpha2, pos_scale, diff_scale, B, n, D, is_clip,
-                                                             esl, lya_diff, loss_out, d_lya_obs, d_lya_obs2, rs->part,
-                                                             rs->arrive);
+#define MH_LYA(DT)                                                                                     \
+  k_lyapunov<DT><<<(unsigned)nb, RTPB, 0, (hipStream_t)stream>>>(                                      \
+      logp, old_logp, lya_obs, lya_obs2, obs, obs2, c, w, s, alpha1, alpha2, pos_scale, diff_scale, B, n, D, \
+      is_clip, esl, lya_diff, loss_out, d_lya_obs, d_lya_obs2, rs->part, rs->arrive)
+  switch (D) {
+    case 1: MH_LYA(1); break;
+    case 2: MH_LYA(2); break;
+    case 3: MH_LYA(3); break;
+    case 4: MH_LYA(4); break;
+    case 5: MH_LYA(5); break;
+    case 6: MH_LYA(6); break;
+    case 7: MH_LYA(7); break;
+    case 8: MH_LYA(8); break;
+    case 9: MH_LYA(9); break;
+    case 10: MH_LYA(10); break;
+    case 11: MH_LYA(11); break;
+    case 12: MH_LYA(12); break;
+    case 13: MH_LYA(13); break;
+    case 14: MH_LYA(14); break;
+    case 15: MH_LYA(15); break;
+    case 16: MH_LYA(16); break;
+    default: MH_LYA(0); break;
+  }
+#undef MH_LYA
   MH_CHECK_LAUNCH("lyapunov");
   return MH_OK;
 }
