@@ -115,6 +115,29 @@ struct GatherArgs {
   int64_t* idx_out = nullptr;
 };
 
+// The gather's flat grid (launch_gather): every output layout is a segment of `units` vectors of
+// vw floats, cut into GATHER_CHUNK-vector chunks, one per workgroup from wg0 on. Vector q of a
+// segment belongs to batch row q / rowlen; kind GATHER_PLAIN copies src[window * src_row + i],
+// GATHER_OBS_ACT interleaves the window's obs and act rows (aux0/1/2 = (D + A)/vw, D/vw, A/vw;
+// src_row = n store rows per window).
+#ifndef MH_GATHER_K
+#define MH_GATHER_K 4
+#endif
+constexpr int GATHER_K = MH_GATHER_K;  // vectors per thread
+constexpr int GATHER_CHUNK = 256 * GATHER_K;
+constexpr int GATHER_MAX_SEGS = 10;
+enum { GATHER_PLAIN = 0, GATHER_OBS_ACT = 1 };
+struct GatherSeg {
+  const float* src;
+  const float* src2;
+  float* dst;
+  uint32_t units, rowlen, src_row, vw, kind, aux0, aux1, aux2, wg0;
+};
+struct GatherPlan {
+  GatherSeg seg[GATHER_MAX_SEGS];
+  int nseg;
+};
+
 hipError_t launch_rollout(int env_id, const StepArgs& a, hipStream_t st);
 hipError_t launch_gae(const float* val, const float* val2, const float* rew, const uint8_t* done, int64_t E,
                       int H, double gamma, double lam, float* adv, float* ret, hipStream_t st);

@@ -9,6 +9,8 @@
 // finalize kernel scans the per-block counts (env-index-order emission, base.py:178) and
 // advances the store cursor; the emit kernel then copies each full deque into its window row,
 // staging the env's ring record block through LDS so both sides are wide/coalesced.
+#include <initializer_list>
+
 #include "rollout.h"
 #include "reset_draw.h"
 
@@ -814,27 +816,11 @@ __device__ __forceinline__ int64_t draw_index(uint64_t seed, int64_t b, uint64_t
   return size > 0 ? (int64_t)(v % (uint64_t)size) : 0;
 }
 
-// the window index of batch row b: the caller's idx, or the in-kernel draw (cached per thread: a
-// thread's grid-stride elements change row rarely)
-struct RowIndex {
-  const int64_t* idx;
-  uint64_t seed, counter;
-  int64_t size, last_b = -1, last = 0;
-  __device__ int64_t operator()(int64_t b) {
-    if (idx) return idx[b];
-    if (b != last_b) {
-      last = draw_index(seed, b, counter, size);
-      last_b = b;
-    }
-    return last;
-  }
-};
-
 // Last-workgroup arrival of an in-kernel draw: advances the counter once every workgroup has
-// READ it. Each thread's counter read was consumed (into its RowIndex) before the barrier, and
-// thread 0 arrives after the barrier; no data is handed between workgroups, so a relaxed arrival
-// suffices (the same argument as k_adam_multi's step counter, optim.hip). The next launch reads
-// the new counter across the kernel boundary.
+// READ it. Each thread's counter read was consumed (into the workgroup's drawn rows) before the
+// barrier, and thread 0 arrives after the barrier; no data is handed between workgroups, so a
+// relaxed arrival suffices (the same argument as k_adam_multi's step counter, optim.hip). The next
+// launch reads the new counter across the kernel boundary.
 __device__ __forceinline__ void draw_arrive(int64_t* draw, uint64_t counter, unsigned int total) {
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -847,116 +833,80 @@ __device__ __forceinline__ void draw_arrive(int64_t* draw, uint64_t counter, uns
   }
 }
 
-// Replay gather: blockIdx.y selects one of the 7 arrays; each thread copies 16-B vectors of
-// the sampled rows (a row of one array is n * width contiguous floats), grid-stride over
-// batch x row-vectors, so every lane moves useful bytes regardless of the field width.
-// (launch_gather bounds the batch so every per-launch element count fits 32 bits: the index
-// arithmetic is unsigned 32-bit, its divisions a few instructions instead of a 64-bit expansion)
-template <typename V>
-__device__ __forceinline__ void gather_rows(const float* src, float* dst, RowIndex& ix, int64_t batch, int64_t len) {
-  const uint32_t v = (uint32_t)(len * (int64_t)sizeof(float) / (int64_t)sizeof(V));
-  const V* s = reinterpret_cast<const V*>(src);
-  V* d = reinterpret_cast<V*>(dst);
-  const uint32_t total = (uint32_t)batch * v;
-  for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < total; q += gridDim.x * 256) {
-    const uint32_t b = q / v, i = q - b * v;
-    d[q] = s[ix(b) * (int64_t)v + i];
-  }
-}
+// Replay gather over a flat grid: launch_gather cuts every output layout into segments of
+// GATHER_CHUNK vectors per workgroup (GatherPlan), so a workgroup copies one contiguous chunk of
+// one output. The chunk spans a contiguous run of batch rows: the workgroup stages their window
+// indices in LDS once (a coalesced read of the caller's idx, or one Philox draw per row), then
+// every thread issues its GATHER_K vector loads before its first store. Sizing the grid by each
+// output's bytes (instead of one fixed-width row of workgroups per output) keeps the number of
+// workgroups — each of which draws its rows and, on the in-kernel draw, arrives on the draw
+// counter's single ticket — near what the bytes need.
+template <int VW>
+struct GVec;
+template <>
+struct GVec<1> { using T = float; };
+template <>
+struct GVec<2> { using T = float2; };
+template <>
+struct GVec<4> { using T = float4; };
 
-// the joint layouts: element-wise (D + A and D are small), rows of the windows at idx
-__device__ __forceinline__ void gather_joint(const GatherArgs& a, RowIndex& ix) {
-  const uint32_t n = (uint32_t)a.n, D = (uint32_t)a.D, A = (uint32_t)a.A, B = (uint32_t)a.batch;
-  // GJ elements per thread and round, every source address formed and loaded before the first
-  // store (a plain grid-stride loop waited out one random store-row load per element)
-  constexpr int GJ = 4;
-  const uint32_t stride = gridDim.x * 256;
-  if (blockIdx.y == 7) {
-    const uint32_t W = D + A, total = B * n * W;
-    for (uint32_t q0 = blockIdx.x * 256 + threadIdx.x; q0 < total; q0 += GJ * stride) {
-      float v[GJ];
+template <int VW>
+__device__ __forceinline__ void gather_chunk(const GatherSeg& g, const int64_t* sidx, uint32_t b_lo, uint32_t q0,
+                                             uint32_t q1) {
+  using V = typename GVec<VW>::T;
+  const V* s = reinterpret_cast<const V*>(g.src);
+  const V* s2 = reinterpret_cast<const V*>(g.src2);
+  V* d = reinterpret_cast<V*>(g.dst);
+  V x[GATHER_K];
 #pragma unroll
-      for (int u = 0; u < GJ; ++u) {
-        const uint32_t q = q0 + u * stride;
-        const uint32_t qq = q < total ? q : total - 1;
-        const uint32_t row = qq / W, c = qq - row * W, b = row / n, t = row - b * n;
-        const int64_t wr = ix(b) * (int64_t)n + t;  // the store row
-        v[u] = c < D ? a.s_obs[wr * D + c] : a.s_act[wr * A + (c - D)];
-      }
-#pragma unroll
-      for (int u = 0; u < GJ; ++u)
-        if (q0 + u * stride < total) a.o_obs_act[q0 + u * stride] = v[u];
-    }
-  } else {
-    const uint32_t total = (B + B * n) * D;
-    for (uint32_t q0 = blockIdx.x * 256 + threadIdx.x; q0 < total; q0 += GJ * stride) {
-      float v[GJ];
-#pragma unroll
-      for (int u = 0; u < GJ; ++u) {
-        const uint32_t q = q0 + u * stride;
-        const uint32_t qq = q < total ? q : total - 1;
-        const uint32_t row = qq / D, c = qq - row * D;
-        const bool first = row < B;
-        const uint32_t r = first ? row : row - B, b = first ? r : r / n, t = first ? 0 : r - b * n;
-        const float* src = first ? a.s_obs : a.s_obs2;
-        v[u] = src[(ix(b) * (int64_t)n + t) * D + c];
-      }
-#pragma unroll
-      for (int u = 0; u < GJ; ++u)
-        if (q0 + u * stride < total) a.o_v_in[q0 + u * stride] = v[u];
+  for (int u = 0; u < GATHER_K; ++u) {
+    const uint32_t q = q0 + u * 256 + threadIdx.x;
+    const uint32_t qq = q < q1 ? q : q1 - 1;
+    const uint32_t b = qq / g.rowlen, i = qq - b * g.rowlen;
+    const int64_t w = sidx[b - b_lo];  // the window
+    if (g.kind == GATHER_PLAIN) {
+      x[u] = s[w * (int64_t)g.src_row + i];
+    } else {  // [obs(t) | act(t)] rows of the window: aux0 = (D + A) / VW, aux1 = D / VW, aux2 = A / VW
+      const uint32_t t = i / g.aux0, c = i - t * g.aux0;
+      const int64_t wr = w * (int64_t)g.src_row + t;  // the store row (window w, step t)
+      x[u] = c < g.aux1 ? s[wr * g.aux1 + c] : s2[wr * g.aux2 + (c - g.aux1)];
     }
   }
+#pragma unroll
+  for (int u = 0; u < GATHER_K; ++u) {
+    const uint32_t q = q0 + u * 256 + threadIdx.x;
+    if (q < q1) d[q] = x[u];
+  }
 }
 
-__device__ __forceinline__ void gather_body(const GatherArgs& a, RowIndex& ix) {
-  if (blockIdx.y >= 7) {
-    if ((blockIdx.y == 7 && a.o_obs_act) || (blockIdx.y == 8 && a.o_v_in)) gather_joint(a, ix);
-    return;
+__global__ __launch_bounds__(256) void k_gather(GatherArgs a, GatherPlan p) {
+  __shared__ int64_t sidx[GATHER_CHUNK];
+  const uint32_t wg = blockIdx.x;
+  int y = 0;
+#pragma unroll
+  for (int k = 1; k < GATHER_MAX_SEGS; ++k) y += (k < p.nseg && wg >= p.seg[k].wg0) ? 1 : 0;
+  const GatherSeg& g = p.seg[y];
+  const uint32_t q0 = (wg - g.wg0) * GATHER_CHUNK;
+  const uint32_t q1 = g.units - q0 < GATHER_CHUNK ? g.units : q0 + GATHER_CHUNK;
+  const uint32_t b_lo = q0 / g.rowlen, b_hi = (q1 - 1) / g.rowlen;
+  const uint64_t counter = a.draw ? (uint64_t)a.draw[0] : 0u;
+  const int64_t size = a.draw ? a.cursor[1] : 0;
+  for (uint32_t r = threadIdx.x; r <= b_hi - b_lo; r += 256) {
+    const int64_t wv = a.draw ? draw_index(a.seed, b_lo + r, counter, size) : a.idx[b_lo + r];
+    sidx[r] = wv;
+    // the drawn indices, written once per row: by the workgroup holding the row's first vector
+    if (y == 0 && a.idx_out && (uint64_t)(b_lo + r) * g.rowlen >= q0) a.idx_out[b_lo + r] = wv;
   }
-  const float* src;
-  float* dst;
-  int w;
-  switch (blockIdx.y) {
-    case 0: src = a.s_obs; dst = a.o_obs; w = a.D; break;
-    case 1: src = a.s_act; dst = a.o_act; w = a.A; break;
-    case 2: src = a.s_rew; dst = a.o_rew; w = 1; break;
-    case 3: src = a.s_cost; dst = a.o_cost; w = 1; break;
-    case 4: src = a.s_obs2; dst = a.o_obs2; w = a.D; break;
-    case 5: src = a.s_done; dst = a.o_done; w = 1; break;
-    default: src = a.s_logp; dst = a.o_logp; w = 1; break;
+  __syncthreads();
+  if (g.dst) {
+    if (g.vw == 4)
+      gather_chunk<4>(g, sidx, b_lo, q0, q1);
+    else if (g.vw == 2)
+      gather_chunk<2>(g, sidx, b_lo, q0, q1);
+    else
+      gather_chunk<1>(g, sidx, b_lo, q0, q1);
   }
-  if (blockIdx.y == 0 && a.idx_out) {  // the drawn indices (one writer per row)
-    for (int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x; b < a.batch; b += (int64_t)gridDim.x * 256)
-      a.idx_out[b] = ix(b);
-  }
-  if (!dst) return;
-  const int64_t len = (int64_t)a.n * w;
-  if (len % 4 == 0)
-    gather_rows<float4>(src, dst, ix, a.batch, len);
-  else if (len % 2 == 0)
-    gather_rows<float2>(src, dst, ix, a.batch, len);
-  else
-    gather_rows<float>(src, dst, ix, a.batch, len);
-}
-
-constexpr int GATHER_LDS_ROWS = 2048;  // in-kernel draws of batches up to this size go through LDS
-
-__global__ __launch_bounds__(256) void k_gather(GatherArgs a) {
-  __shared__ int64_t sidx[GATHER_LDS_ROWS];
-  RowIndex ix;
-  ix.idx = a.draw ? nullptr : a.idx;
-  ix.seed = a.seed;
-  ix.counter = a.draw ? (uint64_t)a.draw[0] : 0u;
-  ix.size = a.draw ? a.cursor[1] : 0;
-  if (a.draw && a.batch <= GATHER_LDS_ROWS) {
-    // every workgroup draws the whole batch once (one Philox draw per row) into LDS: the copy
-    // loops then read indices like the caller-supplied path
-    for (int b = threadIdx.x; b < a.batch; b += 256) sidx[b] = draw_index(ix.seed, b, ix.counter, ix.size);
-    __syncthreads();
-    ix.idx = sidx;
-  }
-  gather_body(a, ix);
-  if (a.draw) draw_arrive(a.draw, ix.counter, gridDim.x * gridDim.y);
+  if (a.draw) draw_arrive(a.draw, counter, gridDim.x);
 }
 
 __global__ __launch_bounds__(256) void k_sample_idx(const int64_t* cursor, uint64_t seed, uint64_t counter,
@@ -1075,13 +1025,77 @@ hipError_t launch_emit_fused(int env_id, const EmitArgs& a, hipStream_t st) {
 }
 hipError_t launch_gather(const GatherArgs& a, hipStream_t st) {
   if (a.batch <= 0) return hipSuccess;
-  // the kernel's element counts are 32-bit (joint layouts: (batch + batch n) D and batch n (D + A))
+  // the kernel's vector counts are 32-bit (the largest layouts: (batch + batch n) D, batch n (D + A))
   if (a.batch * ((int64_t)a.n + 1) * ((int64_t)a.D + a.A) >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
-  const int64_t vec = (a.batch * (int64_t)a.n * (a.D > a.A ? a.D : a.A) + 1023) / 1024;  // float4s of the widest array
-  const int gx = (int)(vec < 1 ? 1 : (vec > 2048 ? 2048 : vec));
-  k_gather<<<dim3(gx, (a.o_obs_act || a.o_v_in) ? 9 : 7), 256, 0, st>>>(a);
+  const int64_t B = a.batch, n = a.n, D = a.D, A = a.A;
+  auto fits = [](const void* ptr, int vw) { return ptr == nullptr || reinterpret_cast<uintptr_t>(ptr) % (4 * vw) == 0; };
+  // the widest vector dividing every length in floats with every pointer aligned to it
+  auto width = [&](std::initializer_list<int64_t> lens, std::initializer_list<const void*> ptrs) {
+    for (int vw : {4, 2}) {
+      bool ok = true;
+      for (int64_t l : lens) ok = ok && l % vw == 0;
+      for (const void* q : ptrs) ok = ok && fits(q, vw);
+      if (ok) return vw;
+    }
+    return 1;
+  };
+  GatherPlan p{};
+  uint32_t wg = 0;
+  auto add = [&](GatherSeg g, int64_t floats) {
+    g.units = (uint32_t)(floats / g.vw);
+    g.wg0 = wg;
+    p.seg[p.nseg++] = g;
+    wg += (g.units + GATHER_CHUNK - 1) / GATHER_CHUNK;
+  };
+  // the per-row arrays [batch][n][w]: rows of n w floats; segment 0 also carries idx_out
+  const float* srcs[7] = {a.s_obs, a.s_act, a.s_rew, a.s_cost, a.s_obs2, a.s_done, a.s_logp};
+  float* dsts[7] = {a.o_obs, a.o_act, a.o_rew, a.o_cost, a.o_obs2, a.o_done, a.o_logp};
+  const int64_t ws[7] = {D, A, 1, 1, D, 1, 1};
+  for (int k = 0; k < 7; ++k) {
+    if (!dsts[k] && !(k == 0 && a.idx_out)) continue;
+    const int64_t len = n * ws[k];
+    GatherSeg g{};
+    g.vw = width({len}, {srcs[k], dsts[k]});
+    g.src = srcs[k];
+    g.dst = dsts[k];
+    g.rowlen = g.src_row = (uint32_t)(len / g.vw);
+    add(g, B * len);
+  }
+  if (a.o_obs_act) {  // [batch][n][D + A] = [obs | act] rows of the window
+    GatherSeg g{};
+    g.vw = width({D, A}, {a.s_obs, a.s_act, a.o_obs_act});
+    g.kind = GATHER_OBS_ACT;
+    g.src = a.s_obs;
+    g.src2 = a.s_act;
+    g.dst = a.o_obs_act;
+    g.aux0 = (uint32_t)((D + A) / g.vw);
+    g.aux1 = (uint32_t)(D / g.vw);
+    g.aux2 = (uint32_t)(A / g.vw);
+    g.rowlen = (uint32_t)(n * g.aux0);
+    g.src_row = (uint32_t)n;  // store rows per window
+    add(g, B * n * (D + A));
+  }
+  if (a.o_v_in) {  // [batch + batch n][D]: obs(b, 0) rows, then the obs2 windows
+    const int vw = width({D}, {a.s_obs, a.s_obs2, a.o_v_in});
+    GatherSeg h{};
+    h.vw = vw;
+    h.src = a.s_obs;
+    h.dst = a.o_v_in;
+    h.rowlen = (uint32_t)(D / vw);
+    h.src_row = (uint32_t)(n * D / vw);
+    add(h, B * D);
+    GatherSeg t{};
+    t.vw = vw;
+    t.src = a.s_obs2;
+    t.dst = a.o_v_in + B * D;
+    t.rowlen = t.src_row = (uint32_t)(n * D / vw);
+    add(t, B * n * D);
+  }
+  if (wg == 0) return hipSuccess;
+  k_gather<<<wg, 256, 0, st>>>(a, p);
   return hipGetLastError();
 }
+
 hipError_t launch_sample_idx(const int64_t* cursor, uint64_t seed, uint64_t counter, int64_t batch,
                              int64_t* idx, hipStream_t st) {
   if (batch <= 0) return hipSuccess;

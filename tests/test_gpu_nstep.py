@@ -157,6 +157,63 @@ def test_replay_gather_joint_layouts():
     assert out["v_in"].shape == (6 + 6 * n, D)
 
 
+@pytest.mark.parametrize("D,A,n", [(1, 1, 1), (2, 2, 1), (3, 1, 5), (6, 2, 3), (12, 4, 5), (7, 3, 20)])
+@pytest.mark.parametrize("shift", [0, 1, 2], ids=["aligned", "off4B", "off8B"])
+def test_replay_gather_layouts_over_chunks(D, A, n, shift):
+    """The flat chunked gather (launch_gather: one workgroup per chunk of one output, batch rows
+    straddling chunk edges) equals torch indexing of the store bit for bit, for every output, at
+    batches spanning many chunks, into destinations offset by `shift` floats (the vector width
+    falls back to what the pointers allow); the in-kernel draw writes the same indices to idx_out
+    as the host-counter draw and gathers exactly those windows."""
+    M, B = 911, 2500
+    buf = DeviceNstepReplayBuffer(obs_dim=D, act_dim=A, buffer_max_size=M, n_step=n)
+    gen = torch.Generator(device="cuda").manual_seed(D * 100 + A * 10 + n)
+    for k in KEYS:
+        buf.n_step_buf[k].copy_(torch.randn(buf.n_step_buf[k].shape, device="cuda", generator=gen))
+    buf.cursor.copy_(torch.tensor([0, M, M, 0]))
+    shapes = {"obs": (B, n, D), "act": (B, n, A), "rew": (B, n), "cost": (B, n), "obs2": (B, n, D),
+              "done": (B, n), "logp": (B, n), "obs_act": (B, n, D + A), "v_in": (B + B * n, D)}
+
+    def dests():
+        out = {}
+        for k, shp in shapes.items():
+            flat = torch.full((int(np.prod(shp)) + shift,), float("nan"), device="cuda")
+            out[k] = flat[shift:].view(shp)
+        return out
+
+    def expect(idx):
+        ref = {k: buf.n_step_buf[k][idx] for k in KEYS}
+        ref["obs_act"] = torch.cat([ref["obs"], ref["act"]], -1)
+        ref["v_in"] = torch.cat([ref["obs"][:, 0], ref["obs2"].reshape(-1, D)], 0)
+        return ref
+    st = N.stream_of(buf.device)
+    idx = torch.randint(0, M, (B,), device="cuda", generator=gen)
+    out = dests()
+    N.check(N.lib().mh_replay_gather_joint(ctypes.byref(buf.ws), n, D, A, N.ptr(idx), B,
+                                           *[N.ptr(out[k]) for k in KEYS], N.ptr(out["obs_act"]),
+                                           N.ptr(out["v_in"]), st), "gather_joint")
+    ref = expect(idx)
+    for k in shapes:
+        assert torch.equal(out[k], ref[k]), k
+    host = torch.empty(B, dtype=torch.int64, device="cuda")
+    N.check(N.lib().mh_replay_sample_indices(ctypes.byref(buf.ws), buf.seed, 0, B, N.ptr(host), st), "draw")
+    out = dests()
+    idx_out = torch.full((B,), -1, dtype=torch.int64, device="cuda")
+    N.check(N.lib().mh_replay_draw_gather(ctypes.byref(buf.ws), n, D, A, buf.seed, N.ptr(buf._draw_state), B,
+                                          N.ptr(idx_out), *[N.ptr(out[k]) for k in KEYS], N.ptr(out["obs_act"]),
+                                          N.ptr(out["v_in"]), st), "draw_gather")
+    assert torch.equal(idx_out, host)
+    assert buf.draws == 1 and int(buf._draw_state[1].item()) == 0  # advanced once; the ticket reset
+    ref = expect(host)
+    for k in shapes:
+        assert torch.equal(out[k], ref[k]), k
+    # indices only (every output null): the grid is the index segment alone
+    N.check(N.lib().mh_replay_sample_indices(ctypes.byref(buf.ws), buf.seed, 1, B, N.ptr(host), st), "draw")
+    N.check(N.lib().mh_replay_draw_gather(ctypes.byref(buf.ws), n, D, A, buf.seed, N.ptr(buf._draw_state), B,
+                                          N.ptr(idx_out), *([None] * 9), st), "draw_only")
+    assert torch.equal(idx_out, host) and buf.draws == 2
+
+
 def test_device_draw_counter_and_one_launch_draw_gather():
     """The replay draw keyed by the buffer's DEVICE counter (mh_replay_sample_indices_dev) equals
     the host-counter entry at the same counters; the one-launch draw + gather
