@@ -821,8 +821,7 @@ __device__ __forceinline__ int64_t draw_index(uint64_t seed, int64_t b, uint64_t
 // barrier, and thread 0 arrives after the barrier; no data is handed between workgroups, so a
 // relaxed arrival suffices (the same argument as k_adam_multi's step counter, optim.hip). The next
 // launch reads the new counter across the kernel boundary.
-__device__ __forceinline__ void draw_arrive(int64_t* draw, uint64_t counter, unsigned int total) {
-  __syncthreads();
+__device__ __forceinline__ void draw_arrive_synced(int64_t* draw, uint64_t counter, unsigned int total) {
   if (threadIdx.x == 0) {
     unsigned int* ticket = reinterpret_cast<unsigned int*>(draw + 1);
     const unsigned int done = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -831,6 +830,10 @@ __device__ __forceinline__ void draw_arrive(int64_t* draw, uint64_t counter, uns
       __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+__device__ __forceinline__ void draw_arrive(int64_t* draw, uint64_t counter, unsigned int total) {
+  __syncthreads();
+  draw_arrive_synced(draw, counter, total);
 }
 
 // Replay gather over a flat grid: launch_gather cuts every output layout into segments of
@@ -898,6 +901,9 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs a, GatherPlan p) {
     if (y == 0 && a.idx_out && (uint64_t)(b_lo + r) * g.rowlen >= q0) a.idx_out[b_lo + r] = wv;
   }
   __syncthreads();
+  // every thread's counter read was consumed by the draws above: arrive now, so the ticket's
+  // round trip overlaps the copy instead of trailing it
+  if (a.draw) draw_arrive_synced(a.draw, counter, gridDim.x);
   if (g.dst) {
     if (g.vw == 4)
       gather_chunk<4>(g, sidx, b_lo, q0, q1);
@@ -906,7 +912,6 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs a, GatherPlan p) {
     else
       gather_chunk<1>(g, sidx, b_lo, q0, q1);
   }
-  if (a.draw) draw_arrive(a.draw, counter, gridDim.x);
 }
 
 __global__ __launch_bounds__(256) void k_sample_idx(const int64_t* cursor, uint64_t seed, uint64_t counter,
