@@ -362,6 +362,9 @@ class MSACL:
         # forward on the one-workgroup-per-CU grid (MSACL_POLICY_ALONE_RT=0: the default grid)
         self._policy_alone_rt = os.environ.get("MSACL_POLICY_ALONE_RT", "1") == "1"
         self._pol_kept = None
+        # the policy step's stability advantage on the side stream beside the policy / critic
+        # forward chain (MSACL_POLICY_ADV_SIDE=0: on the main stream, before it)
+        self._policy_adv_side = os.environ.get("MSACL_POLICY_ADV_SIDE", "1") == "1"
         # the update's rsample noise drawn inside the policy-head kernel (Philox, a device counter);
         # MSACL_KERNEL_NOISE=0: torch's normal draw (A/B)
         self._kernel_noise = os.environ.get("MSACL_KERNEL_NOISE", "1") == "1"
@@ -963,7 +966,7 @@ class MSACL:
         s = self._buf(B, n)
         side = None
         if not reuse_adv:
-            side = self._side_stream()
+            side = self._side_stream() if self._policy_adv_side else None
             if side is not None:
                 main = torch.cuda.current_stream(self.device)
                 side.wait_stream(main)
