@@ -242,6 +242,16 @@ int mh_sample_horizon_debug_logits(mh_env_t h, float* logits_out, float* obs_out
 int mh_rollout_set_trace(mh_env_t h, float* real_next_obs, float* reward, uint8_t* terminated,
                          uint8_t* truncated);
 
+/* Step trace of the post-step env state BEFORE the autoreset overwrites it (the state
+ * SyncVectorEnv's `final_observation` is the observation of: QuadTracking.py:205-250 computes it,
+ * gymnasium resets after), for every later mh_rollout_step / mh_rollout_step_deferred of this handle:
+ * the envs that reset in a step get their pre-reset state written to DEVICE SoA [state_dim][E]
+ * floats and [xstate_dim][E] doubles (the mh_env_get_state layouts; xstate required when
+ * xstate_dim > 0); the other envs' entries are left as they were (their post-step state is the
+ * env state itself). state NULL switches it off. Parity tests only: it lets a terminal row's
+ * observation be checked against the observation map of the kernel's own state. */
+int mh_rollout_set_trace_state(mh_env_t h, float* state, double* xstate);
+
 /* On-policy trajectory store = OnSampler's mini-batch arrays (RL/trainer/sampler/
  * on_sampler.py:22-41), env-major exactly as the reference's numpy arrays:
  * obs/obs2 [E][horizon][obs_dim], act [E][horizon][act_dim], rew/cost/logp [E][horizon] float32,

@@ -98,6 +98,9 @@ struct mh_env_s {
   float* tr_reward = nullptr;
   uint8_t* tr_term = nullptr;
   uint8_t* tr_trunc = nullptr;
+  float* tr_state = nullptr;        // mh_rollout_set_trace_state: the pre-reset post-step state
+  double* tr_xstate = nullptr;      //   (caller's [S][E] / [XS][E]), copied out of tr_buf (the
+  void* tr_buf = nullptr;           //   kernel's one-pointer layout, mh::trace_xoff) after each step
 
   // optional per-kernel HIP-event timing of mh_rollout_step (bench.py's live roofline)
   bool timing = false;
@@ -151,7 +154,7 @@ static void free_handle(mh_env_s* h) {
   for (hipEvent_t e : h->ev_pending) (void)hipEventDestroy(e);
   void* ptrs[] = {h->state, h->xstate, h->steps, h->tab, h->meta, h->ctr, h->ring, h->ring_len,
                   h->ring_pos, h->emit_rank, h->block_count, h->block_offset, h->emit_list, h->h_count,
-                  h->h_list, h->h_scan, h->h_cpre};
+                  h->h_list, h->h_scan, h->h_cpre, h->tr_buf};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   delete h;
@@ -575,6 +578,7 @@ static int rollout_impl(mh_env_t h, const float* logits, const float* act_in, co
   a.reward_out = h->tr_reward;
   a.term_out = h->tr_term;
   a.trunc_out = h->tr_trunc;
+  a.trace_state = h->tr_state ? h->tr_buf : nullptr;
   a.ring = h->ring;
   a.ring_len = h->ring_len;
   a.ring_pos = h->ring_pos;
@@ -612,6 +616,13 @@ static int rollout_impl(mh_env_t h, const float* logits, const float* act_in, co
     for (int i = 0; i < 4; ++i) ev[i] = h->take_event();
   if (ev[0]) MH_HIP(hipEventRecord(ev[0], st));
   MH_HIP(mh::launch_rollout(h->env_id, a, st));
+  if (a.trace_state) {
+    const int S = h->info.state_dim, XS = h->info.xstate_dim;
+    MH_HIP(hipMemcpyAsync(h->tr_state, h->tr_buf, (size_t)S * h->E * 4, hipMemcpyDeviceToDevice, st));
+    if (XS > 0)
+      MH_HIP(hipMemcpyAsync(h->tr_xstate, (const char*)h->tr_buf + mh::trace_xoff(S, h->E), (size_t)XS * h->E * 8,
+                            hipMemcpyDeviceToDevice, st));
+  }
   if (ev[1]) MH_HIP(hipEventRecord(ev[1], st));
   if (defer) {  // the emission of this step's windows is left to the next step or the flush
     h->pending = true;
@@ -771,6 +782,18 @@ int mh_rollout_set_trace(mh_env_t h, float* real_next_obs, float* reward, uint8_
   h->tr_reward = reward;
   h->tr_term = terminated;
   h->tr_trunc = truncated;
+  return MH_OK;
+}
+
+int mh_rollout_set_trace_state(mh_env_t h, float* state, double* xstate) {
+  if (!h) return fail(MH_EINVAL, "mh_rollout_set_trace_state: null handle");
+  if (state && h->info.xstate_dim > 0 && !xstate) return fail(MH_EINVAL, "mh_rollout_set_trace_state: this env needs xstate");
+  if (state && !h->tr_buf) {
+    const int S = h->info.state_dim, XS = h->info.xstate_dim;
+    MH_HIP(hipMalloc(&h->tr_buf, (size_t)mh::trace_xoff(S, h->E) + (size_t)XS * h->E * 8 + 16));
+  }
+  h->tr_state = state;
+  h->tr_xstate = state ? xstate : nullptr;
   return MH_OK;
 }
 

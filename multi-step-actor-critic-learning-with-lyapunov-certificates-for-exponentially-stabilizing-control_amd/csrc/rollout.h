@@ -12,6 +12,8 @@ constexpr int BLK = 256;  // envs per step-kernel block (4 wavefronts)
 
 // floats of one n-step ring record: obs[D] act[A] obs2[D] rew cost done logp, padded to 16 B
 __host__ __device__ constexpr int rec_floats(int D, int A) { return ((2 * D + A + 4) + 3) / 4 * 4; }
+// byte offset of the xstate part of a state trace (StepArgs::trace_state)
+__host__ __device__ constexpr int64_t trace_xoff(int S, int64_t E) { return (S * E * 4 + 15) / 16 * 16; }
 
 struct StepArgs {
   int64_t E;
@@ -65,6 +67,10 @@ struct StepArgs {
   const int32_t* prev_list;
   float *w_obs, *w_act, *w_rew, *w_cost, *w_obs2, *w_done, *w_logp;  // window store arrays
   int64_t capacity;
+  // step trace of the post-step state of the envs that reset, BEFORE the autoreset overwrites it
+  // (parity tests only; null: not traced): SoA [S][E] floats, then (from byte trace_xoff(S, E)) [XS][E] doubles —
+  // one pointer, so the kernel's argument SGPRs do not grow
+  void* trace_state;
 };
 
 constexpr int EMIT_WAVES = 4;  // emitter waves per block in deferred mode

@@ -371,6 +371,16 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
 #else
     if (done) {
 #endif
+      if (a.trace_state) {  // parity trace: the post-step state the reset overwrites (uniform test)
+        const __amdgpu_buffer_rsrc_t rt_s = soa_rsrc(a.trace_state, (uint32_t)(trace_xoff(S, E) + XS * E * 8));
+        const int xo = (int)trace_xoff(S, E);
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, s[i]), rt_s, vo4, (int)(i * E * 4), 0);
+#pragma unroll
+        for (int i = 0; i < XS; ++i)
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, xs[i]), rt_s, vo8, xo + (int)(i * E * 8), 0);
+      }
       float rs[RS];
       if (a.reset_in) {
 #pragma unroll

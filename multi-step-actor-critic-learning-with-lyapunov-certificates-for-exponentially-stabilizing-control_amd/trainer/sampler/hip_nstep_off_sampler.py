@@ -398,13 +398,16 @@ class HipNstepOffSampler:
         N.check(N.lib().mh_env_set_timing(self._handle(), int(enable)), "mh_env_set_timing")
 
     # ------------------------------------------------------------------ parity mode
-    def step_traced(self, act_out, logp_out, trace=None):
+    def step_traced(self, act_out, logp_out, trace=None, state_trace=None):
         """One lockstep step of the sampling path itself, eagerly: exactly what one iteration of
         the sampler's horizon runs (policy forward, then the lockstep kernel with in-kernel
         TanhGauss sampling, clip, in-kernel resets and deferred emission into the bound store),
         additionally writing the sampled actions [E, A] and log-probs [E] and, when `trace` =
         (real_next_obs [E, D], reward [E], terminated u8 [E], truncated u8 [E]) device tensors is
-        given, the env step's outputs (mh_rollout_set_trace). Returns the policy logits.
+        given, the env step's outputs (mh_rollout_set_trace); `state_trace` = (state [S, E] float32,
+        xstate [XS, E] float64 or None) device tensors receive the post-step state of the envs that
+        reset, BEFORE the autoreset overwrites it (mh_rollout_set_trace_state; other columns are
+        left as they were). Returns the policy logits.
         Call flush() after the last step to emit its windows."""
         self._handle()
         N.require_device(act_out, "act_out", torch.float32, self.num_envs * self.envs.act_dim, self.device)
@@ -419,13 +422,23 @@ class HipNstepOffSampler:
             ptrs = [N.ptr(t) for t in trace]
         if self._bound is None:
             raise RuntimeError("step_traced: bind_store(buffer) first (windows go to the bound store)")
+        sptr = [None, None]
+        if state_trace is not None:
+            st, xs = state_trace
+            env = self.envs
+            N.require_device(st, "trace state", torch.float32, env.state_dim * self.num_envs, self.device)
+            if env.xstate_dim:
+                N.require_device(xs, "trace xstate", torch.float64, env.xstate_dim * self.num_envs, self.device)
+            sptr = [N.ptr(st), N.ptr(xs) if env.xstate_dim else None]
         N.check(N.lib().mh_rollout_set_trace(self._h, *ptrs), "mh_rollout_set_trace")
+        N.check(N.lib().mh_rollout_set_trace_state(self._h, *sptr), "mh_rollout_set_trace_state")
         try:
             with torch.no_grad():
                 self._draw_noise()
                 return self._policy_step(self._bound, self._pack_policy(), act_out=act_out, logp_out=logp_out)
         finally:
             N.check(N.lib().mh_rollout_set_trace(self._h, None, None, None, None), "mh_rollout_set_trace")
+            N.check(N.lib().mh_rollout_set_trace_state(self._h, None, None), "mh_rollout_set_trace_state")
 
     def flush(self):
         """Emit the windows of the last deferred lockstep step (mh_rollout_flush)."""

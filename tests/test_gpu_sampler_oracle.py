@@ -81,42 +81,27 @@ def _quad_obs_of_state(s2, xs, k):
     return Q.errors(s2[:, 6:15].reshape(n, 3, 3).copy(), s2[:, 15:18].copy(), ex, ev, Rd, Od)
 
 
-def _quad_allowance(xs, k, got, o2, st_got, done, st_pre, act):
+def _quad_allowance(xs, k, got, o2, st_post):
     """QuadTracking rows whose observation is beyond 1e-5 of the float64-polar oracle's.
 
     The observation is a function of the post-step state, and e_Omega = Omega - R^T R_d Omega_d
     (obs components 9-11) multiplies last-bit differences of that state (the rotation R leaves
     the polar factorisation rounded to float32) by |Omega_d|: a row measured on the MI355X was
     3.6e-5 / 2.3e-5 off on e_Omega x / z with |Omega| ~ 2 rad/s. Such a row passes when
-    (a) the kernel's post-step state is within 1e-5 of the oracle's (asserted for every
-        continuing row by the caller), and
+    (a) the kernel's post-step state is within 1e-5 of the oracle's (asserted for EVERY row by
+        the caller, terminal rows included: the kernel exports each env's post-step state before
+        the autoreset overwrites it, mh_rollout_set_trace_state), and
     (b) the kernel's observation is within 1e-5 of the reference's observation map applied to
         the kernel's OWN post-step state (_quad_obs_of_state),
     i.e. both halves of the step are within 1e-5 and only their composition amplifies a
-    rounding difference. A reset row's post-step state is overwritten by the reset, so (b) cannot
-    be formed for it; such a row passes only under the criterion DESIGN §4 states for the
-    reference as-is: within 1e-5 of the reference's own step (float32 SVD polar factor, st_pre /
-    act) plus that step's measured self-noise |o32 - o64| (the bound the 4,096-row slice below
-    checks for every row), with the relative part of e_Omega's three components (obs 9-11) taken
-    on the vector's magnitude: the rotation's rounding enters as R^T R_d Omega_d, an error
-    proportional to |Omega_d| spread over all three components (the row met on the MI355X:
-    |e_Omega| = 20.4 rad/s, 1.5e-5 off on a component of 0.27).
-    Returns the rows that needed it (they must be a handful: 1 in 1.77 M env-steps measured).
+    rounding difference. Terminal and continuing rows get the same check; there is no other
+    allowance. Returns the rows that needed it (a handful: 1 in 1.77 M env-steps measured).
     """
     far = ~np.isclose(got, o2, **TOL)
     rows = np.nonzero(far.any(axis=1))[0]
     if rows.size:
-        cont, rst = rows[~done[rows]], rows[done[rows]]
-        if cont.size:
-            mine = _quad_obs_of_state(st_got[cont], xs[cont], k[cont])
-            np.testing.assert_allclose(got[cont], mine, **TOL, err_msg=f"rows {cont}: obs of the kernel's own state")
-        if rst.size:
-            _, _, o32, _, _, _ = OE.env_step("QuadTracking", st_pre[rst], act[rst], xs[rst], k[rst])
-            noise = np.abs(o32.astype(np.float64) - o2[rst])
-            scale = np.abs(o32).astype(np.float64)
-            scale[:, 9:12] = scale[:, 9:12].max(axis=1, keepdims=True)  # e_Omega: the vector's magnitude
-            assert np.all(np.abs(got[rst] - o32) <= 1e-5 + 1e-5 * scale + noise), \
-                ("reset row beyond 1e-5 + the reference's own polar-factor noise", rst)
+        mine = _quad_obs_of_state(st_post[rows], xs[rows], k[rows])
+        np.testing.assert_allclose(got[rows], mine, **TOL, err_msg=f"rows {rows}: obs of the kernel's own state")
     return rows
 
 
@@ -147,6 +132,9 @@ def test_sampled_lockstep_kernel_matches_oracle(name, noise, tmp_path):
     act, logp = torch.empty(E, A, device=dev), torch.empty(E, device=dev)
     real, rew = torch.empty(E, D, device=dev), torch.empty(E, device=dev)
     term, trunc = torch.empty(E, dtype=torch.uint8, device=dev), torch.empty(E, dtype=torch.uint8, device=dev)
+    # the post-step state before the autoreset of the envs that reset (mh_rollout_set_trace_state)
+    t_st = torch.empty(env.state_dim, E, device=dev)
+    t_xs = torch.empty(max(env.xstate_dim, 1), E, dtype=torch.float64, device=dev)
     windows = OS.NStepWindows(E, NSTEP, D, A)
     expect = {k: [] for k in KEYS}
 
@@ -159,13 +147,13 @@ def test_sampled_lockstep_kernel_matches_oracle(name, noise, tmp_path):
     np.testing.assert_allclose(sampler.obs.cpu().numpy(), obs_o, **TOL)
     if quad:
         np.testing.assert_allclose(xs, xs_r, rtol=0, atol=1e-12)
-    n_reset = n_trunc = n_lp = n_quad_allow = 0
+    n_reset = n_trunc = n_lp = n_quad_allow = n_rd_allow = 0
     seed, idx = env.seed, np.arange(E)
     pol = sampler.networks.policy
     ls_lo, ls_hi = float(getattr(pol, "min_log_std", -20.0)), float(getattr(pol, "max_log_std", 1.0))
     for t in range(STEPS.get(name, 40)):
         ctr = env.get_counters().cpu().numpy()
-        logits = sampler.step_traced(act, logp, trace=(real, rew, term, trunc))
+        logits = sampler.step_traced(act, logp, trace=(real, rew, term, trunc), state_trace=(t_st, t_xs))
         a_np, lp_np, lg32 = act.cpu().numpy(), logp.cpu().numpy(), logits.cpu().numpy()
         noise_t = float(sampler._noise[0]) if noise is not None else 0.0
         got_real, got_rew = real.cpu().numpy(), rew.cpu().numpy()
@@ -174,6 +162,11 @@ def test_sampled_lockstep_kernel_matches_oracle(name, noise, tmp_path):
         st2, k2 = st2.cpu().numpy(), k2.cpu().numpy().astype(np.int64)
         xs2 = xs2.cpu().numpy() if xs2 is not None else None
         obs_next = sampler.obs.cpu().numpy()
+        # the post-step state of every env before its reset: the trace holds it for the envs that
+        # reset this lockstep, the env state itself for the others
+        rs_k = got_term | got_trunc
+        st_post = np.where(rs_k[:, None], t_st.cpu().numpy().T, st2)
+        xs_post = np.where(rs_k[:, None], t_xs.cpu().numpy().T, xs2) if quad else None
 
         # ---- the action and its log-prob: the oracle's TanhGauss of (logits, the env's eps)
         assert np.all((a_np >= cls.act_low) & (a_np <= cls.act_high))
@@ -186,8 +179,21 @@ def test_sampled_lockstep_kernel_matches_oracle(name, noise, tmp_path):
 
         # ---- the env step from the snapshot, with the kernel's own actions
         s_o, xs_o, o2, r2, te, tr = OE.env_step(name, st, a_np, xs, k, polar64=quad)
+        # ---- the post-step state of EVERY env (terminal rows too, before their reset overwrites it)
+        np.testing.assert_allclose(st_post, s_o, **TOL, err_msg="post-step state (pre-reset)")
+        if quad:
+            # Rd_last = R_d(x, v) of the post-step state (QuadTracking.py:122-149): rows beyond
+            # (1e-5, 1e-6) of the oracle's must be R_d of the kernel's OWN post-step x, v (float64
+            # arithmetic on the same float32 inputs): the two halves again, as for e_Omega below
+            far = np.nonzero(~np.isclose(xs_post, xs_o, rtol=1e-5, atol=1e-6).all(axis=1))[0]
+            if far.size:
+                _, _, rd_mine, _ = OE.QuadTracking.desired(st_post[far, 0:3].copy(), st_post[far, 3:6].copy(),
+                                                           k[far] + 1, xs[far].reshape(-1, 3, 3))
+                np.testing.assert_allclose(xs_post[far], rd_mine.reshape(-1, 9), rtol=0, atol=1e-10,
+                                           err_msg=f"rows {far}: R_d of the kernel's own state")
+            n_rd_allow += far.size
         if quad:  # rows beyond 1e-5 of the float64-polar path: see _quad_allowance
-            bad = _quad_allowance(xs, k, got_real, o2, st2, got_term | got_trunc, st, a_np)
+            bad = _quad_allowance(xs, k, got_real, o2, st_post)
             n_quad_allow += bad.size
             o2[bad] = got_real[bad]
         np.testing.assert_allclose(got_real, o2, **TOL)
@@ -204,11 +210,8 @@ def test_sampled_lockstep_kernel_matches_oracle(name, noise, tmp_path):
         n_reset += int(done.sum())
         n_trunc += int(got_trunc.sum())
 
-        # ---- continuing envs: next state, Rd_last, counter, observation
+        # ---- continuing envs: counter, observation (their next state is checked above)
         np.testing.assert_array_equal(k2, np.where(done, 0, k + 1))
-        np.testing.assert_allclose(st2[~done], s_o[~done], **TOL)
-        if quad:
-            np.testing.assert_allclose(xs2[~done], xs_o[~done], rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(obs_next[~done], o2[~done], **TOL)
         # ---- reset rows: a reset-distribution draw, and obs / Rd_last = env_reset_from(state)
         obs_new = o2.copy()
@@ -240,6 +243,8 @@ def test_sampled_lockstep_kernel_matches_oracle(name, noise, tmp_path):
     total = exp["obs"].shape[0]
     assert total > 500 and n_reset > 0 and n_trunc > 0, (total, n_reset, n_trunc)
     assert n_quad_allow <= 1e-5 * E * STEPS.get(name, 40), n_quad_allow  # a handful of 1.77 M env-steps
+    assert n_rd_allow <= 1e-5 * E * STEPS.get(name, 40), n_rd_allow
+    print(f"{name}: {n_reset} resets, rows checked against their own state: obs {n_quad_allow}, Rd_last {n_rd_allow}")
     assert n_lp > 1000
     assert int(buffer.cursor[2]) == total and total < buffer.max_size
     for key in KEYS:
