@@ -733,6 +733,14 @@ int mh_per_sample(const double* tree, int64_t pow2, const int64_t* cursor, uint6
                   uint64_t counter, int64_t batch, float beta, int64_t* idx_out,
                   float* weight_out, void* stream);
 
+/* ---- HIP-graph capture hygiene (the engine's own update capture, utils/dist.py cuda_graph) ----
+ * For a stream `origin` that is capturing, and n other streams: unjoined[i] = 1 when stream i
+ * takes part in the same capture and some of its captured work is NOT an ancestor of origin's
+ * current capture frontier (a fork that was never joined back: ending the capture then would leave
+ * a dangling branch), else 0. Host-only graph inspection (hipStreamGetCaptureInfo_v2 +
+ * hipGraphNodeGetDependencies); MH_ESTATE when origin is not capturing. */
+int mh_capture_unjoined(void* origin, void* const* streams, int32_t n, int32_t* unjoined);
+
 const char* mh_last_error(void);
 int mh_abi_version(void);
 

@@ -91,6 +91,7 @@ _PROTOS = {
     "mh_env_set_action_noise": (ctypes.c_int, [c_vp, c_vp]),
     "mh_rollout_set_trace": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp]),
     "mh_rollout_set_trace_state": (ctypes.c_int, [c_vp, c_vp, c_vp]),
+    "mh_capture_unjoined": (ctypes.c_int, [c_vp, c_vp, ctypes.c_int32, c_vp]),
     "mh_nstep_reserve": (ctypes.c_int, [c_vp, c_i32]),
     "mh_sample_horizon_windows": (ctypes.c_int, [c_vp, c_vp, c_vp]),
     "mh_sample_horizon_errors": (ctypes.c_int, [c_vp, c_vp, c_vp]),

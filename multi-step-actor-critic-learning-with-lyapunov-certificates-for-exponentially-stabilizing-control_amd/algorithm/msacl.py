@@ -587,7 +587,7 @@ class MSACL:
         if not (self.concurrent and self.device.type == "cuda" and self.twin_streams):
             return None
         if self._twin is None:
-            self._twin = torch.cuda.Stream(device=self.device)
+            self._twin = D.side_stream(self.device)
         return self._twin
 
     def _twin_pair(self, f1, f2):
@@ -605,8 +605,7 @@ class MSACL:
         if tw is None:
             return f1(), f2()
         cur = torch.cuda.current_stream(self.device)
-        tw.wait_stream(cur)
-        with torch.cuda.stream(tw):
+        with D.fork(tw):
             r2 = f2()
         r1 = f1()
         cur.wait_stream(tw)
@@ -616,7 +615,7 @@ class MSACL:
 
     def _seg_side_stream(self):
         if self._side is None:
-            self._side = torch.cuda.Stream(device=self.device)
+            self._side = D.side_stream(self.device)
         return self._side
 
     def _side_stream(self):
@@ -624,7 +623,7 @@ class MSACL:
                 and not self.force_graph_segments and not D.segment_capture_active()):
             return None
         if self._side is None:
-            self._side = torch.cuda.Stream(device=self.device)
+            self._side = D.side_stream(self.device)
         return self._side
 
     def _update_body(self, data, do_target, do_policy):
@@ -635,8 +634,7 @@ class MSACL:
         side = self._side_stream()
         if side is not None:
             main = torch.cuda.current_stream(self.device)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
+            with D.fork(side):
                 loss_lya = self._lyapunov_update(data, keep_policy=do_policy)
             loss_q, q1_mean, q2_mean = self._q_update(data, stats=do_policy)
             main.wait_stream(side)
@@ -653,8 +651,7 @@ class MSACL:
             # parameters, and each optimizer step only reads its own network's gradients.
             main = torch.cuda.current_stream(self.device)
             side = self._seg_side_stream()
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
+            with D.fork(side):
                 loss_lya = self._lyapunov_update(data, defer_step=True, keep_policy=do_policy)
             loss_q, q1_mean, q2_mean = self._q_update(data, defer_step=True, stats=do_policy)
             main.wait_stream(side)
@@ -969,8 +966,7 @@ class MSACL:
             side = self._side_stream() if self._policy_adv_side else None
             if side is not None:
                 main = torch.cuda.current_stream(self.device)
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
+                with D.fork(side):
                     self._stability_advantage(data, s)
             else:
                 self._stability_advantage(data, s)

@@ -2,6 +2,7 @@
 #include <string>
 #include <cmath>
 #include <cstring>
+#include <unordered_set>
 #include <vector>
 
 #include "msacl_hip.h"
@@ -231,6 +232,44 @@ int mh_env_create(int32_t env_id, int64_t num_envs, uint64_t seed, mh_env_t* out
                 std::string("mh_env_create: ") + hipGetErrorString(e));
   }
   *out = h;
+  return MH_OK;
+}
+
+int mh_capture_unjoined(void* origin, void* const* streams, int32_t n, int32_t* unjoined) {
+  if (n < 0 || (n > 0 && (!streams || !unjoined))) return fail(MH_EINVAL, "mh_capture_unjoined: bad arguments");
+  hipStreamCaptureStatus so = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* d = nullptr;
+  size_t nd = 0;
+  MH_HIP(hipStreamGetCaptureInfo_v2((hipStream_t)origin, &so, &id, &g, &d, &nd));
+  if (so != hipStreamCaptureStatusActive) return fail(MH_ESTATE, "mh_capture_unjoined: origin stream is not capturing");
+  // every node the origin's next captured node would depend on, transitively
+  std::vector<hipGraphNode_t> todo(d, d + nd);
+  std::unordered_set<hipGraphNode_t> anc(todo.begin(), todo.end());
+  std::vector<hipGraphNode_t> deps;
+  while (!todo.empty()) {
+    hipGraphNode_t v = todo.back();
+    todo.pop_back();
+    size_t k = 0;
+    MH_HIP(hipGraphNodeGetDependencies(v, nullptr, &k));
+    deps.assign(k, nullptr);
+    if (k) MH_HIP(hipGraphNodeGetDependencies(v, deps.data(), &k));
+    for (size_t j = 0; j < k; ++j)
+      if (deps[j] && anc.insert(deps[j]).second) todo.push_back(deps[j]);
+  }
+  for (int32_t i = 0; i < n; ++i) {
+    hipStreamCaptureStatus si = hipStreamCaptureStatusNone;
+    unsigned long long sid = 0;
+    const hipGraphNode_t* sd = nullptr;
+    size_t snd = 0;
+    unjoined[i] = 0;
+    if (streams[i] == origin) continue;
+    MH_HIP(hipStreamGetCaptureInfo_v2((hipStream_t)streams[i], &si, &sid, nullptr, &sd, &snd));
+    if (si != hipStreamCaptureStatusActive || sid != id) continue;  // not in this capture
+    for (size_t j = 0; j < snd; ++j)
+      if (sd[j] && !anc.count(sd[j])) unjoined[i] = 1;
+  }
   return MH_OK;
 }
 

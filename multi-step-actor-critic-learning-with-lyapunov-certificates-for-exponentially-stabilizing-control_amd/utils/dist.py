@@ -10,6 +10,7 @@ sizes a ring all-reduce over xGMI is latency-bound, so one call per step beats p
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import gc
 import os
 
@@ -54,21 +55,119 @@ def init_from_env(backend=None):
     return True
 
 
+# live side streams: id(stream) -> (hipStream_t handle, device index). Not weak references: a
+# weakref to a torch.cuda.Stream was seen returning an unrelated object after the stream died
+# (its referent not cleared on this image), so each stream unregisters itself when it is freed.
+_SIDE_STREAMS: "dict[int, tuple[int, int]]" = {}
+
+
+class _SideStream(torch.cuda.Stream):
+    def __del__(self):
+        _SIDE_STREAMS.pop(id(self), None)
+
+
+def side_stream(device) -> "torch.cuda.Stream":
+    """A new stream for work forked off the current stream inside an update (twin critics, the
+    critic / Lyapunov branches, the stability advantage). Registered, so that a capture ending
+    with one of them still forked is caught (cuda_graph, GraphSegments) instead of reaching
+    hipStreamEndCapture with a dangling branch."""
+    s = _SideStream(device=device)
+    _SIDE_STREAMS[id(s)] = (int(s.cuda_stream), int(s.device.index))
+    return s
+
+
+def unjoined_forks(join: bool = True):
+    """The registered side streams that take part in the current stream's capture with work the
+    current stream does not (transitively) wait for: forks never joined back
+    (mh_capture_unjoined walks the captured graph's dependencies). Returns their hipStream_t
+    handles. join=True makes the current stream wait for each of them, so the capture can still
+    end with a well-formed graph."""
+    cur = torch.cuda.current_stream()
+    handles = [h for h, d in list(_SIDE_STREAMS.values()) if d == cur.device.index]
+    if not handles:
+        return []
+    from .. import _native as N
+    arr = (ctypes.c_void_p * len(handles))(*handles)
+    out = (ctypes.c_int32 * len(handles))()
+    N.check(N.lib().mh_capture_unjoined(ctypes.c_void_p(cur.cuda_stream), arr, len(handles), out),
+            "mh_capture_unjoined")
+    bad = [h for h, u in zip(handles, out) if u]
+    if join:
+        for h in bad:
+            cur.wait_stream(torch.cuda.ExternalStream(h, device=cur.device))
+    return bad
+
+
+class UnjoinedForkError(RuntimeError):
+    pass
+
+
+class NestedForkError(RuntimeError):
+    pass
+
+
+def _unjoined_message(bad):
+    return (f"HIP graph capture ended with {len(bad)} forked stream(s) not joined back to the capture "
+            f"stream ({', '.join(hex(h) for h in bad)}): every side-stream branch must end "
+            f"with current_stream().wait_stream(side) before the capture ends (the graph was joined "
+            f"and discarded)")
+
+
+# hipStream_t of the stream each active capture began on (innermost last)
+_CAPTURE_ORIGIN: "list[int]" = []
+
+
+@contextlib.contextmanager
+def fork(side):
+    """Run the enclosed work on `side`, forked off the current stream (side waits for it); the
+    caller joins it later with current_stream().wait_stream(side). During a capture the fork must
+    come from the capture's own stream: a fork of a fork (a stream forked from a side stream, even
+    when every branch is joined back) makes hipStreamEndCapture crash on this ROCm
+    (tools/probes/capture_unjoined_probe.py, mode nested_joined: SIGSEGV), so it is
+    refused with NestedForkError before anything is enqueued."""
+    cur = torch.cuda.current_stream(side.device)
+    if _CAPTURE_ORIGIN and torch.cuda.is_current_stream_capturing() and int(cur.cuda_stream) != _CAPTURE_ORIGIN[-1]:
+        raise NestedForkError(
+            f"fork of stream {hex(int(cur.cuda_stream))} inside a HIP graph capture that began on "
+            f"{hex(_CAPTURE_ORIGIN[-1])}: forks of forks are refused (hipStreamEndCapture crashes on them); "
+            f"fork from the capture stream instead")
+    side.wait_stream(cur)
+    with torch.cuda.stream(side):
+        yield side
+
+
 @contextlib.contextmanager
 def cuda_graph(g, **kw):
-    """torch.cuda.graph with the cyclic garbage collector paused while the stream captures.
-    torch.cuda.graph collects once before the capture, but an allocation inside the capture can
-    trigger another collection, which may finalise graphs, events or streams of pipelines that
+    """torch.cuda.graph with the cyclic garbage collector paused while the stream captures, and
+    with the capture's forks checked before it ends.
+
+    gc: torch.cuda.graph collects once before the capture, but an allocation inside the capture
+    can trigger another collection, which may finalise graphs, events or streams of pipelines that
     died in reference cycles: HIP calls that are illegal during a capture (seen as aborts and a
-    host segfault in a later replay during one full test session)."""
+    host segfault in a later replay during one full test session).
+
+    forks ("capture hygiene"): a registered side stream (side_stream) whose captured work
+    the capture stream does not wait for would end the capture with a dangling branch; the check
+    joins such streams, lets the capture end, discards the graph and raises UnjoinedForkError (the
+    same join runs when the body raised, so the capture always ends on a well-formed graph).
+    Forks of forks are refused earlier, by fork()."""
     was = gc.isenabled()
     gc.disable()
+    bad = []
     try:
         with torch.cuda.graph(g, **kw):
-            yield
+            _CAPTURE_ORIGIN.append(int(torch.cuda.current_stream().cuda_stream))
+            try:
+                yield
+            finally:
+                _CAPTURE_ORIGIN.pop()
+                bad = unjoined_forks(join=True)
     finally:
         if was:
             gc.enable()
+    if bad:
+        g.reset()
+        raise UnjoinedForkError(_unjoined_message(bad))
 
 
 class GraphSegments:
@@ -88,10 +187,20 @@ class GraphSegments:
         g = torch.cuda.CUDAGraph()
         self._ctx = torch.cuda.graph(g, pool=self.pool, capture_error_mode="thread_local")
         self._ctx.__enter__()
+        _CAPTURE_ORIGIN.append(int(torch.cuda.current_stream().cuda_stream))
         self.graphs.append(g)
 
+    def _end(self):
+        _CAPTURE_ORIGIN.pop()
+        bad = unjoined_forks(join=True)
+        ctx, self._ctx = self._ctx, None
+        ctx.__exit__(None, None, None)
+        if bad:
+            self.reset()
+            raise UnjoinedForkError(_unjoined_message(bad))
+
     def _cut(self, op):
-        self._ctx.__exit__(None, None, None)
+        self._end()
         self.ops.append(op)
         self._begin()
 
@@ -139,7 +248,12 @@ class capturing:
 
     def __exit__(self, *exc):
         try:
-            self.seg._ctx.__exit__(*exc)
+            if exc[0] is None:
+                self.seg._end()
+            elif self.seg._ctx is not None:
+                _CAPTURE_ORIGIN.pop()
+                unjoined_forks(join=True)  # end the capture on a well-formed graph, then re-raise
+                self.seg._ctx.__exit__(*exc)
         finally:
             self.seg._ctx = None
             _SEG["active"] = None
