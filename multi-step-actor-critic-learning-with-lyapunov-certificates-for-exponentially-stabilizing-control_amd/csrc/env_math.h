@@ -1055,19 +1055,15 @@ struct QuadTracking {
     step_row(s, xs, rowv, a, obs, rew);
   }
 
-  // env.step on a preloaded row (load_row)
-  MH_HD static void step_row(float* s, double* xs, const double* rowv, const float* a, float* obs, float* rew) {
+  // The K Euler substeps of env.step (QuadTracking.py:205-227) with NormalizeOrientMatrix after
+  // each: FAST = every substep through the incremental polar factor P (the step's starting R is a
+  // rounded rotation, `inc`), else polar3 wherever a lane's starting R is not (externally set
+  // states). Both forms do the same arithmetic for a lane with inc; the split only keeps the
+  // general routine (a call) and its registers out of the code every sampled lockstep runs.
+  template <bool FAST>
+  MH_HD static void substeps(float* s, double* P, bool inc, float f, const float* M) {
     using Q = QuadConst;
-    const float f = a[0];
-    const float* M = a + 1;
     const float mf = (float)Q::m;
-    // NormalizeOrientMatrix of every substep through the incremental polar factor (one
-    // float64 polar factor P carried across the substeps); polar3 when the starting R is not
-    // a rounded rotation (externally set states)
-    double P[9];
-    bool inc = false;
-    float R0[9];
-    for (int i = 0; i < 9; ++i) R0[i] = s[6 + i];
 #ifdef MH_EXP_NO_SUBSTEPS  // cost-attribution experiment only
     for (int it = 0; it < 0; ++it) {
 #else
@@ -1098,17 +1094,52 @@ struct QuadTracking {
       for (int i = 0; i < 9; ++i) R[i] = R[i] + dR[i] * 0.01f;
       for (int i = 0; i < 3; ++i) W[i] = upd64(W[i], dW[i], 0.01);
       float Rn[9];
-#ifndef MH_QUAD_POLAR_NS
-      if (it == 0) inc = polar_start(R0, P);  // float64 polar factor of the step's starting R
-      if (__builtin_expect(inc, 1))
+      if (FAST || __builtin_expect(inc, 1))
         polar_step_incremental(P, R, Wf, Rn);
       else
         polar3(R, Rn);
-#else
-      (void)Wf;
-      polar3(R, Rn);
-#endif
       for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+    }
+  }
+
+  struct QuadSub {
+    float s[18];
+  };
+  // substeps<false> by value, out of line (the general polar routine's registers stay out of the
+  // caller's allocation)
+  static __host__ __device__ __noinline__ QuadSub substeps_general_call(QuadSub q, bool inc, float f, float m0, float m1, float m2) {
+    double P[9];
+    if (inc) (void)polar_start(q.s + 6, P);
+    const float M[3] = {m0, m1, m2};
+    substeps<false>(q.s, P, inc, f, M);
+    return q;
+  }
+
+  // env.step on a preloaded row (load_row)
+  MH_HD static void step_row(float* s, double* xs, const double* rowv, const float* a, float* obs, float* rew) {
+    const float f = a[0];
+    const float* M = a + 1;
+    // NormalizeOrientMatrix of every substep through the incremental polar factor (one
+    // float64 polar factor P carried across the substeps); polar3 when the starting R is not
+    // a rounded rotation (externally set states)
+    double P[9];
+#ifndef MH_QUAD_POLAR_NS
+    const bool inc = polar_start(s + 6, P);  // float64 polar factor of the step's starting R
+#if defined(__HIP_DEVICE_COMPILE__)
+    const bool fast = __all(inc);  // wave-uniform: the sampled locksteps take the FAST form
+#else
+    const bool fast = inc;
+#endif
+#else
+    const bool inc = false, fast = false;
+#endif
+    if (__builtin_expect(fast, 1)) {
+      substeps<true>(s, P, true, f, M);
+    } else {  // out of line: one call, in the branch no sampled lockstep takes
+      QuadSub q;
+      for (int i = 0; i < 18; ++i) q.s[i] = s[i];
+      q = substeps_general_call(q, inc, f, M[0], M[1], M[2]);
+      for (int i = 0; i < 18; ++i) s[i] = q.s[i];
     }
     const double* row = rowv;
 #ifdef MH_EXP_NO_DESIRED  // cost-attribution experiment only
