@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _REPO = os.path.dirname(_HERE)
@@ -205,11 +206,19 @@ def lib():
                 f"`make -C {os.path.join(_HERE, 'csrc')}` (or __graft_entry__.build()). "
                 "There is no CPU fallback.")
         L = ctypes.CDLL(LIB_PATH)
-        # A/B runs load older builds through MSACL_HIP_LIB: an entry point they lack is left
-        # unbound there (a call then raises); the in-tree library must export every one
-        ab = "MSACL_HIP_LIB" in os.environ
+        # A/B runs load older builds (MSACL_HIP_LIB plus MSACL_HIP_LIB_AB=1): an entry point they
+        # lack is left unbound there (listed on stderr; a call then raises). Every other library,
+        # an MSACL_HIP_LIB override included, must export every entry point, checked here at load.
+        ab = os.environ.get("MSACL_HIP_LIB_AB", "") == "1"
+        missing = [name for name in _PROTOS if not hasattr(L, name)]
+        if missing and not ab:
+            raise RuntimeError(f"{LIB_PATH} lacks {len(missing)} entry point(s) of include/msacl_hip.h: "
+                               f"{', '.join(missing[:8])}{' ...' if len(missing) > 8 else ''} (stale build?)")
+        if missing:
+            print(f"[msacl] A/B library {LIB_PATH}: {len(missing)} entry point(s) unbound: {', '.join(missing)}",
+                  file=sys.stderr)
         for name, (res, args) in _PROTOS.items():
-            if ab and not hasattr(L, name):
+            if name in missing:
                 continue
             fn = getattr(L, name)
             fn.restype = res

@@ -123,8 +123,16 @@ class LazyTbInfo(Mapping):
             h = self._vals.cpu()
             if self._gen is not None:  # a ring slot (MSACL._tb_pack): it must still hold this update
                 tag = int(h.view(torch.int32)[7]) & 0xFFFFFFFF
-                if tag != self._gen & 0xFFFFFFFF:
-                    raise RuntimeError(f"MSACL tb dict read after {_TB_SLOTS} later policy updates reused its slot")
+                want = self._gen & 0xFFFFFFFF
+                if tag != want:
+                    # a later generation in the slot: genuine reuse by later policy updates; an
+                    # earlier one (or a jump of more than the ring): the host mirror (_tb_gen) and the
+                    # device counter disagree, i.e. some update launch never reached _update_result
+                    d = (tag - want) & 0xFFFFFFFF
+                    kind = ("reused its slot" if d % _TB_SLOTS == 0 and 0 < d < 1 << 31 else
+                            "host/device generation desync")
+                    raise RuntimeError(f"MSACL tb dict read after {_TB_SLOTS} later policy updates {kind}: expected "
+                                       f"generation {want}, slot holds {tag}")
             v = h[:7].tolist()
             self._d = dict(zip(self.KEYS, v))
             self._d[tb_tags["alg_time"]] = (time.time() - self._start) * 1000
@@ -384,6 +392,7 @@ class MSACL:
         self.force_graph_segments = bool(kwargs.get("alg_force_graph_segments", False))
         self._static = None
         self._static_shapes = None
+        self._static_gen = 0  # bumped whenever _static is rebuilt (keys the trainer's step graphs)
         self._graphs = {}
         self._warm = set()
         # the logged scalars of each policy update land in a device ring (mh_msacl_tb_pack_ring)
@@ -402,6 +411,7 @@ class MSACL:
         for g, _outs, _prio in graphs.values():
             release_graph(g)
         self._static = self._static_shapes = None
+        self._static_gen += 1
         self._warm = set()
         self._scratch = {}
         self.last_priority = None
@@ -552,7 +562,9 @@ class MSACL:
         flags = (global_iteration % self.target_network_frequency == 0, global_iteration % self.policy_frequency == 0)
         if flags + ("drawn",) not in self._warm:
             return None
-        key = flags + (self._static["rew"].data_ptr(),)
+        # the static inputs' generation, not one tensor's address: a rebuilt static dict may reuse
+        # one old address while its other tensors moved
+        key = flags + (self._static_gen,)
 
         def body():
             draw(self._static)
@@ -746,6 +758,7 @@ class MSACL:
                 joint[1].copy_(o2)
                 self._static["obs"], self._static["obs2"] = joint[0], joint[1]
             self._static_shapes = shapes
+            self._static_gen += 1
             self._graphs = {}
             self._warm = set()
         for k, v in self._static.items():

@@ -215,9 +215,21 @@ template <int D, int A>
 MH_HD float quad_reward(const float* s, const float* Q, const float* u, const float* R) {
   float a[D], b[A];
 #pragma unroll
-  for (int i = 0; i < D; ++i) a[i] = Q[i] * (s[i] * s[i]);
+  for (int i = 0; i < D; ++i) {
+    float x = s[i];
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm("" : "+v"(x));  // one scalar per square: no v_pk_mul_f32 pairing (tests/test_build_isa.py)
+#endif
+    a[i] = Q[i] * (x * x);
+  }
 #pragma unroll
-  for (int i = 0; i < A; ++i) b[i] = R[i] * (u[i] * u[i]);
+  for (int i = 0; i < A; ++i) {
+    float x = u[i];
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm("" : "+v"(x));
+#endif
+    b[i] = R[i] * (x * x);
+  }
   float cost = np_sum<D>(a) + np_sum<A>(b);
   float r = -cost;
   bool near = true;
@@ -946,6 +958,16 @@ MH_HD bool polar_start(const float* R, double* P) {
   return true;
 }
 
+struct QuadSub {
+  float s[18];
+};
+// QuadTracking::substeps<false> by value, out of line (the general polar routine's registers stay
+// out of the caller's allocation). File-static, like polar3_general_call: every translation unit
+// keeps its own copy compiled with its own flags (an inline-linkage member would be merged by the
+// linker across units built with different options).
+static __host__ __device__ __noinline__ QuadSub quad_substeps_general_call(QuadSub q, bool inc, float f, float m0,
+                                                                           float m1, float m2);
+
 struct QuadTracking {
   // state floats: x[0:3] v[3:6] R[6:15] W[15:18]; xstate doubles: Rd_last[9]
   static constexpr int D = 12, A = 4, S = 18, XS = 9, RS = 18, K = 4;
@@ -1102,19 +1124,6 @@ struct QuadTracking {
     }
   }
 
-  struct QuadSub {
-    float s[18];
-  };
-  // substeps<false> by value, out of line (the general polar routine's registers stay out of the
-  // caller's allocation)
-  static __host__ __device__ __noinline__ QuadSub substeps_general_call(QuadSub q, bool inc, float f, float m0, float m1, float m2) {
-    double P[9];
-    if (inc) (void)polar_start(q.s + 6, P);
-    const float M[3] = {m0, m1, m2};
-    substeps<false>(q.s, P, inc, f, M);
-    return q;
-  }
-
   // env.step on a preloaded row (load_row)
   MH_HD static void step_row(float* s, double* xs, const double* rowv, const float* a, float* obs, float* rew) {
     const float f = a[0];
@@ -1138,7 +1147,7 @@ struct QuadTracking {
     } else {  // out of line: one call, in the branch no sampled lockstep takes
       QuadSub q;
       for (int i = 0; i < 18; ++i) q.s[i] = s[i];
-      q = substeps_general_call(q, inc, f, M[0], M[1], M[2]);
+      q = quad_substeps_general_call(q, inc, f, M[0], M[1], M[2]);
       for (int i = 0; i < 18; ++i) s[i] = q.s[i];
     }
     const double* row = rowv;
@@ -1203,6 +1212,15 @@ struct QuadTracking {
     for (int i = 0; i < 9; ++i) xs[i] = Rd[i];
   }
 };
+
+static __host__ __device__ __noinline__ QuadSub quad_substeps_general_call(QuadSub q, bool inc, float f, float m0,
+                                                                           float m1, float m2) {
+  double P[9];
+  if (inc) (void)polar_start(q.s + 6, P);
+  const float M[3] = {m0, m1, m2};
+  QuadTracking::substeps<false>(q.s, P, inc, f, M);
+  return q;
+}
 
 // Row 0 of a filled table equals QuadTracking::row0 bit for bit (signed zeros included).
 inline bool quad_row0_matches(const double* tab) {

@@ -33,6 +33,14 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// a + b element by element as four scalar adds: a vector `+` on f32x4 is selected as two packed
+// v_pk_add_f32, which no kernel of the library carries (tests/test_build_isa.py; csrc/Makefile)
+__device__ __forceinline__ f32x4 add4_scalar(f32x4 a, f32x4 b) {
+  float r0 = a[0] + b[0], r1 = a[1] + b[1], r2 = a[2] + b[2], r3 = a[3] + b[3];
+  asm volatile("" : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3));  // keep them scalar (no v2f32 re-pairing)
+  return f32x4{r0, r1, r2, r3};
+}
+
 constexpr int TM = 16;        // rows per workgroup
 constexpr int HID = 256;      // hidden width
 constexpr int SH = HID + 4;   // LDS row stride of a hidden tile (floats): rows 16 B apart in the banks
@@ -341,7 +349,7 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
       const int rt = wave;
       f32x4 sum = red[0][rt][lane];
 #pragma unroll
-      for (int w = 1; w < 4; ++w) sum = sum + red[w][rt][lane];
+      for (int w = 1; w < 4; ++w) sum = add4_scalar(sum, red[w][rt][lane]);
       const int n = lane & 15;
       if (n < N3) {
         const float bv = a.b3[n];
@@ -706,7 +714,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT == 1 ? 2
       for (int cb = 0; cb < 2; ++cb) {
         f32x4 sum = red[0][rt][cb][lane];
 #pragma unroll
-        for (int w = 1; w < 4; ++w) sum = sum + red[w][rt][cb][lane];
+        for (int w = 1; w < 4; ++w) sum = add4_scalar(sum, red[w][rt][cb][lane]);
         const int col = 16 * cb + c;
         if (col < K1) {
 #pragma unroll

@@ -27,6 +27,7 @@ from math import inf
 
 import torch
 
+from ..env.hip_vector_env import drain_pending_handles
 from ..utils import dist as D
 from ..utils.common_utils import ModuleOnDevice
 from ..utils.log_data import LogData
@@ -165,12 +166,14 @@ class NstepOffSerialTrainer:
         t0, start = time.perf_counter(), time.time()
         ent = self._step_graphs.get(key)
         if ent is None:
-            # graphs of an older sampler key (other policy / observation buffers) are dead
-            self._step_graphs = {k: v for k, v in self._step_graphs.items() if k[0] == skey}
+            # graphs of an older sampler key (other policy / observation buffers) or of older static
+            # update inputs (the algorithm rebuilt them: akey[2:] is their generation) are dead
+            self._step_graphs = {k: v for k, v in self._step_graphs.items() if k[0] == skey and k[1][2:] == akey[2:]}
             g = torch.cuda.CUDAGraph()
             with D.cuda_graph(g):
                 sbody()
                 outs = abody()
+            drain_pending_handles()  # env handles released by a finaliser during the capture
             ent = self._step_graphs[key] = (g, outs)
         g, outs = ent
         self.networks.train()

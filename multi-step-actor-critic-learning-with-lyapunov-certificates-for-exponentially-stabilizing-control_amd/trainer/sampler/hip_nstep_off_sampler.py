@@ -303,9 +303,19 @@ class HipNstepOffSampler:
         return DeviceWindowBatch(self, store, store.cursor[2] - before)
 
     def policy_version(self):
-        """Sum of the policy parameters' in-place version counters (torch bumps them on every
-        in-place write through torch: load_state_dict, optimiser steps, manual edits)."""
-        return sum(p._version for p in self.networks.policy.parameters())
+        """What the packed policy copy depends on besides the algorithm's policy-update count:
+        (sum of the policy parameters' version counters, the writes through .data or raw pointers
+        that those counters miss, this sampler's own invalidations). torch bumps a version counter
+        on every in-place write through torch (load_state_dict, optimiser steps, manual edits) but
+        NOT on writes through `p.data` or a kernel given the storage's pointer: such writers call
+        utils.dist.parameters_written() (broadcast_module does), or the caller invalidate_policy_pack()."""
+        return (sum(p._version for p in self.networks.policy.parameters()), D.param_epoch(),
+                getattr(self, "_pack_epoch", 0))
+
+    def invalidate_policy_pack(self):
+        """Force the next graphed sample() to re-pack the policy (after writing its parameters in
+        a way policy_version() cannot see)."""
+        self._pack_epoch = getattr(self, "_pack_epoch", 0) + 1
 
     def step_graph_parts(self, pack=True):
         """The pieces of one graphed sample() for a trainer-level graph that also holds the update

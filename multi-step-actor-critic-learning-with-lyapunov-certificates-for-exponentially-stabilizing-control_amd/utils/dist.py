@@ -306,10 +306,25 @@ def _allreduce_tensors_now(grads) -> None:
         g.copy_(f)
 
 
+# count of parameter writes that torch's version counters do not see (copies through .data,
+# kernels writing parameter storage through raw pointers outside an optimiser): every such writer
+# calls parameters_written(), and caches of parameter values (the sampler's packed policy) compare it
+_PARAM_EPOCH = [0]
+
+
+def parameters_written() -> None:
+    _PARAM_EPOCH[0] += 1
+
+
+def param_epoch() -> int:
+    return _PARAM_EPOCH[0]
+
+
 def broadcast_module(module: torch.nn.Module, src: int = 0) -> None:
     """Make every rank start from rank `src`'s parameters and buffers."""
     if world_size() <= 1:
         return
+    parameters_written()  # (written through .data below: invisible to the version counters)
     tensors = [p.data for p in module.parameters()] + [b for b in module.buffers()]
     flat = torch._utils._flatten_dense_tensors(tensors)
     dist.broadcast(flat, src)

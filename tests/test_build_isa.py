@@ -1,4 +1,4 @@
-"""CPU: static checks on the built gfx950 code object of the fused horizon sampler.
+"""CPU: static checks on the built gfx950 code object of the engine library.
 
 csrc/Makefile compiles sample_fused.hip with -fno-slp-vectorize: with the env step's scalar f32
 code SLP-vectorised into packed-FP32 instructions (v_pk_mul / v_pk_add / v_pk_fma _f32) running on
@@ -7,6 +7,12 @@ lanes 48-63 (tools/probes/variants_det.sh). The guard must not 
 alone. Since round 5 the policy pass has no packed-f32 arithmetic either (its split / rescale
 pairs are scalar: beside MFMAs a v_pk_fma_f32 costs ~22 cycles more than two v_fma_f32), so no
 k_sample_fused<Env> may contain a single packed-f32 instruction.
+
+Round 6: the same holds for EVERY kernel of libmsacl_hip.so (the flag is in the Makefile's
+CXXFLAGS for every unit). Any kernel can share a SIMD with an MFMA kernel: the update graph runs
+its critic and Lyapunov branches (MFMA MLP kernels beside row kernels, Adam, Polyak) on concurrent
+queues, and the overlapped sampler runs the env kernels beside the update. The lockstep env
+kernels had carried up to 91 packed-f32 instructions (k_rollout<QuadTracking>).
 """
 import os
 import re
@@ -18,18 +24,19 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OBJ = os.path.join(ROOT, "multi-step-actor-critic-learning-with-lyapunov-certificates-for-exponentially-stabilizing-"
                    "control_amd", "csrc", "build", "sample_fused.o")
+LIB = os.path.join(ROOT, "lib", "libmsacl_hip.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 ENVS = ("VanderPol", "Pendulum", "DuctedFan", "TwoLink", "SingleTrackCar", "QuadTracking")
 
 
-def _disassemble(tmp_path):
-    if not os.path.exists(OBJ):
-        pytest.skip("sample_fused.o not built (make -C csrc)")
+def _disassemble(tmp_path, obj=OBJ):
+    if not os.path.exists(obj):
+        pytest.skip(f"{obj} not built (make -C csrc)")
     for tool in ("llvm-objcopy", "clang-offload-bundler", "llvm-objdump"):
         if not os.path.exists(os.path.join(LLVM, tool)) and shutil.which(tool) is None:
             pytest.skip(f"{tool} not available")
     fat, co = str(tmp_path / "fatbin.bin"), str(tmp_path / "gfx950.co")
-    subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", OBJ, str(tmp_path / "o.o")], check=True)
+    subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", obj, str(tmp_path / "o.o")], check=True)
     subprocess.run([f"{LLVM}/clang-offload-bundler", "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950",
                     f"--input={fat}", f"--output={co}", "--unbundle"], check=True)
     return subprocess.run([f"{LLVM}/llvm-objdump", "-d", co], check=True, capture_output=True, text=True).stdout
@@ -52,3 +59,33 @@ def test_env_step_code_of_the_fused_kernel_is_not_packed(tmp_path):
 
 def _kernels(asm):
     return [m.group(1) for m in re.finditer(r"^[0-9a-f]+ <(.*)>:", asm, re.M)]
+
+
+def test_no_kernel_of_the_library_is_packed(tmp_path):
+    """Every unit linked into libmsacl_hip.so (csrc/build/*.o; the library's fat binary holds one
+    code object per unit), every kernel: no packed-f32 instruction."""
+    build = os.path.dirname(OBJ)
+    objs = sorted(f for f in os.listdir(build) if f.endswith(".o")) if os.path.isdir(build) else []
+    if not objs:
+        pytest.skip("csrc/build not built (make -C csrc)")
+    assert len(objs) >= 12, objs
+    counts, n_kernels = {}, 0
+    for i, o in enumerate(objs):
+        secs = subprocess.run([f"{LLVM}/llvm-readelf", "-S", os.path.join(build, o)], check=True,
+                              capture_output=True, text=True).stdout
+        if ".hip_fatbin" not in secs:  # host-only unit (no kernels)
+            continue
+        d = tmp_path / str(i)
+        d.mkdir()
+        asm = _disassemble(d, os.path.join(build, o))
+        n_kernels += len(_kernels(asm))
+        name = None
+        for line in asm.splitlines():
+            m = re.match(r"^[0-9a-f]+ <(.*)>:", line)
+            if m:
+                name = m.group(1)
+                continue
+            if name and re.search(r"\bv_pk_(mul|add|fma)_f32\b", line):
+                counts[f"{o}:{name}"] = counts.get(f"{o}:{name}", 0) + 1
+    assert n_kernels > 100, n_kernels
+    assert not counts, f"packed-f32 code in the library: {counts}"

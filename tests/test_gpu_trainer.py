@@ -245,3 +245,39 @@ def test_graphed_step_equals_separate_graphs(tmp_path, env_name):
         assert torch.equal(a[1][k], b[1][k]), k
     assert torch.equal(a[2], b[2]) and torch.equal(a[3], b[3])
     assert a[5] is not None and torch.equal(a[5], b[5])
+
+
+def test_pack_skip_sees_parameter_writes_outside_torch(tmp_path):
+    """The graphed step skips the policy pack when the parameters cannot have changed since the
+    last one; a write through `.data` (invisible to torch's version counters) followed by
+    utils.dist.parameters_written() -- what broadcast_module does -- or by the sampler's
+    invalidate_policy_pack() forces the next graphed step to pack again."""
+    import msacl_amd.utils.dist as D
+    args = default_msacl_args(env_name="QuadTracking", env_num=4096, buffer_warm_size=3000, buffer_max_size=60000,
+                              max_iteration=12, eval_interval=10 ** 6, log_save_interval=10 ** 6,
+                              apprfunc_save_interval=10 ** 6, save_folder=str(tmp_path), seed=0,
+                              num_eval_episode=1, sampler_sync_timing=False, trainer_graph_step=True)
+    args, alg, sampler, buffer, evaluator, trainer = build_pipeline(args)
+    packs = {}
+    orig = sampler.step_graph_parts
+
+    def spy(pack=True):
+        packs[trainer.iteration] = pack  # the last call of an iteration decides
+        return orig(pack=pack)
+    sampler.step_graph_parts = spy
+    writes = {8: lambda: D.parameters_written(), 10: lambda: sampler.invalidate_policy_pack()}
+    while trainer.iteration <= trainer.max_iteration:
+        if trainer.iteration in writes:
+            with torch.no_grad():
+                for p in alg.networks.policy.parameters():
+                    p.data.mul_(0.999)  # through .data: no version bump
+            writes[trainer.iteration]()
+        trainer.step()
+        trainer.iteration += 1
+    torch.cuda.synchronize()
+    trainer.close()
+    # even iterations after a policy-free step skip the pack ...
+    assert packs.get(6) is False, packs
+    # ... unless the parameters were written outside torch's view and the writer said so
+    assert packs.get(8) is True and packs.get(10) is True, packs
+    assert packs.get(12) is False, packs
