@@ -42,6 +42,12 @@ def parse():
                    help="alg_twin_streams off: q1 / q2 branches of the update on one stream (A/B)")
     p.add_argument("--overlap", action="store_true",
                    help="trainer_overlap_sampling: sampling beside the policy-free updates (A/B; off by default)")
+    p.add_argument("--dp-rehearsal", action="store_true",
+                   help="one GPU: a world-size-1 RCCL process group with the update's gradient / statistics "
+                        "all-reduces issued anyway (the data-parallel step's per-rank cost without the wire)")
+    p.add_argument("--graph-collectives", action="store_true",
+                   help="the all-reduces inside the captured update graph (MSACL_GRAPH_COLLECTIVES=1) instead of "
+                        "graph segments cut at them")
     p.add_argument("--graph-segments", action="store_true",
                    help="capture the update as graphs cut at its all-reduces (the world size > 1 path)")
     p.add_argument("--eager-update", action="store_true",
@@ -106,6 +112,19 @@ def main():
     local = D.local_device_index()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if a.graph_collectives:
+        D.set_graph_collectives(True)
+    dp_rehearsal = None
+    if a.dp_rehearsal and world == 1:
+        import socket
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        torch.distributed.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                             device_id=dev)
+        D.force_collectives(True)
+        dp_rehearsal = {"backend": torch.distributed.get_backend(), "world": 1,
+                        "collectives": "in the update graph" if D.collectives_in_graph() else "graph segments"}
     # self-check of the launch: every rank joins one all-reduce of a ones tensor over the data-path
     # backend (RCCL on the MI355X node); the count must equal --gpus, else the line is not valid
     dist_backend = torch.distributed.get_backend() if world > 1 else None
@@ -421,7 +440,7 @@ def main():
                    "env": a.env, "envs_per_gpu": a.envs, "horizon": horizon, "n_step": n, "replay_batch": 256,
                    "policy": a.policy, "parallelism": f"dp{world}"},
         "roofline": roof,
-        "dist_backend": dist_backend, "rccl_ranks": ranks_seen,
+        "dist_backend": dist_backend, "rccl_ranks": ranks_seen, "dp_rehearsal": dp_rehearsal,
         "kernels": kernels,
         "windows_per_step": round(windows_timed / a.steps, 1),
         "phases": phases,
@@ -432,6 +451,8 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+    elif dp_rehearsal is not None:
         torch.distributed.destroy_process_group()
 
 

@@ -631,7 +631,7 @@ class MSACL:
         return self._side
 
     def _side_stream(self):
-        if not (self.concurrent and D.world_size() == 1 and self.device.type == "cuda"
+        if not (self.concurrent and not D.collectives_active() and self.device.type == "cuda"
                 and not self.force_graph_segments and not D.segment_capture_active()):
             return None
         if self._side is None:
@@ -655,7 +655,7 @@ class MSACL:
             # profiles/r05_update_tail_ab.txt); the Polyak step reads only the stepped critics
             if do_target:
                 self._target_update()
-        elif self._segmented() and self.concurrent and self.device.type == "cuda":
+        elif (self._segmented() or D.collectives_active()) and self.concurrent and self.device.type == "cuda":
             # data parallel: the two backward passes still run as parallel branches, and their
             # gradients are averaged by ONE all-reduce at the join (one graph cut instead of two,
             # the branches stay concurrent inside the segment); the optimizer steps follow it.

@@ -225,8 +225,33 @@ def force_graph_segments(on: bool) -> None:
     _SEG["force"] = bool(on)
 
 
+# Collectives inside the captured update graph (RCCL supports stream capture): opt-in with
+# MSACL_GRAPH_COLLECTIVES=1 on the nccl (RCCL) backend. The update is then ONE graph at any world
+# size (no segment cuts, the trainer's graphed step applies). `force`: issue the collectives even
+# with one rank (a world-size-1 process group: the one-GPU rehearsal of the data-parallel step).
+_COLL = {"in_graph": os.environ.get("MSACL_GRAPH_COLLECTIVES", "0") == "1", "force": False}
+
+
+def set_graph_collectives(on: bool) -> None:
+    _COLL["in_graph"] = bool(on)
+
+
+def force_collectives(on: bool) -> None:
+    """Issue the gradient collectives even when the (initialised) process group has one rank."""
+    _COLL["force"] = bool(on)
+
+
+def collectives_active() -> bool:
+    """The update's gradient / statistics all-reduces are issued (world > 1, or forced)."""
+    return world_size() > 1 or (_COLL["force"] and is_initialized())
+
+
+def collectives_in_graph() -> bool:
+    return _COLL["in_graph"] and collectives_active() and is_initialized() and dist.get_backend() == "nccl"
+
+
 def graph_segments_wanted() -> bool:
-    return world_size() > 1 or _SEG["force"]
+    return _SEG["force"] or (collectives_active() and not collectives_in_graph())
 
 
 class capturing:
@@ -267,7 +292,7 @@ def segment_capture_active() -> bool:
 
 
 def _allreduce_now(t, average):
-    if world_size() > 1:
+    if collectives_active():
         dist.all_reduce(t)
         if average:
             t.div_(world_size())
@@ -295,7 +320,7 @@ def allreduce_grads(params) -> None:
 
 
 def _allreduce_tensors_now(grads) -> None:
-    if world_size() <= 1:
+    if not collectives_active():
         return
     if not grads:
         return

@@ -380,3 +380,61 @@ def test_twin_stream_update_equals_serial(monkeypatch, mode):
         states[streams] = {k: v.detach().clone() for k, v in alg.networks.state_dict().items()}
     for k, v in states[False].items():
         assert torch.equal(v, states[True][k]), k
+
+
+def test_rccl_collectives_in_the_update_graph_one_gpu(monkeypatch):
+    """The data-parallel update with REAL RCCL all-reduces on one GPU (a world-size-1 nccl process
+    group with the collectives forced, utils/dist.py force_collectives): as graph segments cut at
+    the collectives (the default for world > 1) and as ONE captured graph with the all-reduces
+    inside it (MSACL_GRAPH_COLLECTIVES=1: RCCL under stream capture). Parameters bit-identical to
+    the eager update without collectives (an all-reduce over one rank is the identity)."""
+    import socket
+    import torch.distributed as dist
+    import torch.distributions.normal as tdn
+    from msacl_amd.algorithm.msacl import MSACL
+    import msacl_amd.utils.dist as D
+    g = np.load(os.path.join(G, "msacl_update.npz"))
+    B, n = int(g["cfg_B"]), int(g["cfg_n"])
+    data = {k: torch.as_tensor(g["in_" + k], device="cuda") for k in ("obs", "act", "rew", "cost", "obs2", "done", "logp")}
+    noise = {}
+
+    def fixed(shape, dtype, device):
+        key = tuple(shape)
+        if key not in noise:
+            gen = torch.Generator(device="cuda").manual_seed(len(noise) + 1)
+            noise[key] = torch.randn(key, dtype=dtype, device=device, generator=gen)
+        return noise[key]
+
+    monkeypatch.setattr(tdn, "_standard_normal", fixed)
+
+    def run(mode):
+        alg = MSACL(**_msacl_kwargs(B, n), alg_use_graph=(mode != "eager"))
+        alg.networks.load_state_dict({k[5:]: torch.as_tensor(g[k]) for k in g.files if k.startswith("init/")})
+        for it in range(6):
+            alg.model_update(data, it)
+        kinds = {type(v[0]).__name__ for v in alg._graphs.values()}
+        st = {k: v.detach().clone() for k, v in alg.networks.state_dict().items()}
+        alg.close()
+        return st, kinds
+
+    ref, _ = run("eager")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", torch.cuda.current_device()))
+    try:
+        D.force_collectives(True)
+        D.set_graph_collectives(False)
+        seg, kinds_seg = run("graph")
+        D.set_graph_collectives(True)
+        assert D.collectives_in_graph() and not D.graph_segments_wanted()
+        one, kinds_one = run("graph")
+    finally:
+        D.force_collectives(False)
+        D.set_graph_collectives(False)
+        dist.destroy_process_group()
+    assert kinds_seg == {"GraphSegments"} and kinds_one == {"CUDAGraph"}, (kinds_seg, kinds_one)
+    for k, v in ref.items():
+        assert torch.equal(v, seg[k]), ("segments", k)
+        assert torch.equal(v, one[k]), ("in-graph", k)
