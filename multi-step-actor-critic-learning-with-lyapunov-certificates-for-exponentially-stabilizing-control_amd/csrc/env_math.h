@@ -449,22 +449,13 @@ struct SingleTrackCar {
     double f[7], g5[2] = {0.0, 0.0}, g6[2] = {0.0, 0.0}, g2 = 0.0, g3 = 0.0;
     float pb = pe + beta;
     float spb, cpb;
-#ifdef MH_EXP_CAR_FASTTRIG  // cost-attribution experiment only
-    spb = __sinf(pb);
-    cpb = __cosf(pb);
-#else
     sincos32(pb, &spb, &cpb);
-#endif
     f[0] = (double)(((v * cpb) - 1.0f) + (0.0f * sye));   // SingleTrackCar.py:165
     f[1] = (double)((v * spb) - (0.0f * sxe));            // SingleTrackCar.py:166
     f[3] = -0.0;                                               // -a_ref
     f[2] = 0.0;
     const float lsum = (float)C::lsum;
-#ifdef MH_EXP_CAR_DYNONLY  // cost-attribution experiment only: every lane in the dynamic model
-    if (true) {
-#else
     if (!(fabsf(v) < 0.1f)) {
-#endif
       // dynamic model (SingleTrackCar.py:178-196, 243-256)
       float X = div32((float)C::P1, (v * (float)C::Iz) * lsum);
       float t1 = ((-X) * (float)C::K1) * psid;
@@ -520,11 +511,7 @@ struct SingleTrackCar {
     out[6] = f[6] + (g6[0] * u0 + g6[1] * u1);
   }
   MH_HD static void step(float* s, double*, int, const float* u, const double*, float* obs, float* rew) {
-#ifdef MH_EXP_CAR_K  // cost-attribution experiment only: substeps per env step
-    for (int k = 0; k < MH_EXP_CAR_K; ++k) {
-#else
     for (int k = 0; k < K; ++k) {
-#endif
       double d[7];
       deriv(s, u, d);
 #pragma unroll
@@ -666,55 +653,6 @@ static __host__ __device__ __noinline__ F9 polar3_general_call(F9 in) {
 // general routine's iteration control, determinant and rare-branch code, converging to the same
 // float64 polar factor (the final float32 rounding differs in ~3 of 1e6 elements, by 1 ulp).
 MH_HD void polar3(const float* Rin, float* Rout) {
-#ifdef MH_EXP_NO_POLAR  // cost-attribution experiment only (tools/exp_variants.sh)
-  for (int i = 0; i < 9; ++i) Rout[i] = Rin[i];
-  return;
-#endif
-#ifdef MH_EXP_POLAR_MIXED_NOBRANCH  // diagnostic experiment only: two float64 steps + the mixed one, no branches
-  {
-    double X[9], G[9];
-    for (int i = 0; i < 9; ++i) X[i] = (double)Rin[i];
-    for (int it = 0; it < 2; ++it) {
-      (void)orth_err3<double>(X, G);
-      ns3_step3(X, G);
-    }
-    (void)orth_err3<double>(X, G);
-    ns_step3_mixed(X, G);
-    for (int i = 0; i < 9; ++i) Rout[i] = (float)X[i];
-    return;
-  }
-#endif
-#ifdef MH_EXP_POLAR_F64_NOBRANCH  // diagnostic experiment only: three branch-free float64 steps
-  {
-    double X[9], G[9];
-    for (int i = 0; i < 9; ++i) X[i] = (double)Rin[i];
-    for (int it = 0; it < 3; ++it) {
-      (void)orth_err3<double>(X, G);
-      ns3_step3(X, G);
-    }
-    for (int i = 0; i < 9; ++i) Rout[i] = (float)X[i];
-    return;
-  }
-#endif
-#ifdef MH_EXP_POLAR_F32  // diagnostic experiment only: three branch-free float32 Newton-Schulz steps
-  {
-    float X[9], G[9];
-    for (int i = 0; i < 9; ++i) X[i] = Rin[i];
-    for (int it = 0; it < 3; ++it) {
-      (void)orth_err3<float>(X, G);
-      float Y[9];
-      for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) {
-          float acc = 0.0f;
-          for (int k = 0; k < 3; ++k) acc = fmaf(X[i * 3 + k], (((k * 3 + j) % 4 == 0 ? 1.0f : 0.0f) - G[k * 3 + j]) * 0.5f, acc);
-          Y[i * 3 + j] = X[i * 3 + j] + acc;
-        }
-      for (int i = 0; i < 9; ++i) X[i] = Y[i];
-    }
-    for (int i = 0; i < 9; ++i) Rout[i] = X[i];
-    return;
-  }
-#endif
   double X[9], G[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) X[i] = (double)Rin[i];
@@ -1086,11 +1024,7 @@ struct QuadTracking {
   MH_HD static void substeps(float* s, double* P, bool inc, float f, const float* M) {
     using Q = QuadConst;
     const float mf = (float)Q::m;
-#ifdef MH_EXP_NO_SUBSTEPS  // cost-attribution experiment only
-    for (int it = 0; it < 0; ++it) {
-#else
     for (int it = 0; it < K; ++it) {
-#endif
       float* x = s;
       float* v = s + 3;
       float* R = s + 6;
@@ -1151,14 +1085,9 @@ struct QuadTracking {
       for (int i = 0; i < 18; ++i) s[i] = q.s[i];
     }
     const double* row = rowv;
-#ifdef MH_EXP_NO_DESIRED  // cost-attribution experiment only
-    for (int i = 0; i < 12; ++i) obs[i] = s[i] * 1e-3f;
-    (void)row;
-#else
     double Rd[9];
     desired_and_obs(s, row, true, xs, Rd, obs);
     for (int i = 0; i < 9; ++i) xs[i] = Rd[i];
-#endif
     // reward (QuadTracking.py:250-273), reward type 1 (linear bonus)
     float sx[3], sv[3], sr[3], sw[3], su[4];
     for (int i = 0; i < 3; ++i) {

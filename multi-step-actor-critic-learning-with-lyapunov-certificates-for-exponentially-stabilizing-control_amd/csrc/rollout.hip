@@ -261,11 +261,7 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
     if constexpr (Env::ROWN > 0) {  // Env::load_row as buffer loads (table rows 0..MAX_STEP)
       typedef double f64x2 __attribute__((ext_vector_type(2)));  // whole-vector cast: see load_row_buf
       const __amdgpu_buffer_rsrc_t rt = soa_rsrc(a.tab, (uint32_t)((MAX_STEP + 1) * Env::ROWN * 8));
-#ifdef MH_EXP_ROW_CONST  // cost-attribution experiment only: every env reads row 1
-      const int ro = (0 * k + 1) * Env::ROWN * 8;
-#else
       const int ro = (k + 1) * Env::ROWN * 8;
-#endif
       static_assert(Env::ROWN % 2 == 0, "rows are read as 16-byte pairs from column 2");
 #pragma unroll
       for (int i = 2; i < Env::ROWN; i += 2) {
@@ -285,11 +281,6 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
     float u[A];
     float logp = 0.0f;
     if constexpr (SAMPLE) {
-#ifdef MH_EXP_NO_SAMPLE  // cost-attribution experiment only
-#pragma unroll
-      for (int i = 0; i < A; ++i) u[i] = fminf(fmaxf(lgt[i], Env::act_lo(i)), Env::act_hi(i));
-      logp = 0.0f;
-#else
       float nz[4];
       rng.normal4f_fast(0, nz);
       // TanhGaussDistribution.sample (act_distribution_cls.py:45-57): z = mu + std * eps,
@@ -327,7 +318,6 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
       }
       const float ls = a.log_half_sum;
       logp = (lg - lt) - ls;
-#endif
     }
     if constexpr (!SAMPLE) {  // injected action (and its log-prob when given)
 #pragma unroll
@@ -360,17 +350,7 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
     const float rew = r * a.reward_scale;
     // ---- autoreset (gymnasium 0.28.1 SyncVectorEnv.step)
     float obsn[D];
-#ifdef MH_EXP_NO_RESET  // cost-attribution experiment only: trivial reset (state := 0, R := I)
     if (done) {
-#pragma unroll
-      for (int i = 0; i < S; ++i) s[i] = (S == 18 && (i == 6 || i == 10 || i == 14)) ? 1.0f : 0.0f;
-#pragma unroll
-      for (int i = 0; i < D; ++i) obsn[i] = 0.0f;
-      k1 = 0;
-    } else if (false) {
-#else
-    if (done) {
-#endif
       if (a.trace_state) {  // parity trace: the post-step state the reset overwrites (uniform test)
         const __amdgpu_buffer_rsrc_t rt_s = soa_rsrc(a.trace_state, (uint32_t)(trace_xoff(S, E) + XS * E * 8));
         const int xo = (int)trace_xoff(S, E);
@@ -479,7 +459,7 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
     // records transposed through LDS: in each store instruction 8 consecutive lanes write one
     // record's contiguous chunks, so an instruction touches 64 / (F / 4) records' lines instead
     // of 64 (one record per lane took 3.4 us of the 17.4 us QuadTracking step at E = 65,536:
-    // tools/exp_variants.sh, MH_EXP_NO_RING). Staged here, stored after the block barrier.
+    // a compiled-out variant, round 1). Staged here, stored after the block barrier.
     constexpr int C = RC, CP = RCP;
     __shared__ int spos[BLK / 64][64];
     if (env_thread) {
@@ -528,7 +508,6 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
       const int64_t nrec = e0 < E ? (E - e0 < 64 ? E - e0 : 64) : 0;
       const __amdgpu_buffer_rsrc_t rr = soa_rsrc(a.ring + e0 * R * F, (uint32_t)(nrec * R * F * 4));
       typedef float f32x4 __attribute__((ext_vector_type(4)));
-#ifndef MH_EXP_NO_RING  // cost-attribution experiment only: no ring record store
       float4 v[C];
       int off[C];
 #pragma unroll
@@ -540,8 +519,6 @@ __global__ __launch_bounds__(BLK + 64 * EMIT_WAVES, RolloutWaves<Env>::v) void k
       }
 #pragma unroll
       for (int j = 0; j < C; ++j) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(f32x4, v[j]), rr, off[j], 0, 0);
-#endif
-      (void)rr;
     }
   }
 }

@@ -11,7 +11,7 @@ build_dir() {  # $1 = csrc dir, $2 = include dir, $3 = out dir
   mkdir -p "$3"
   ( cd "$1" && for f in $SRCS; do
       [ -f $f.hip ] || continue
-      x=""; [ $f = sample_fused ] && x="-fno-slp-vectorize"  # as the Makefile
+      x="-fno-slp-vectorize"  # as the Makefile (every unit since round 6)
       /opt/rocm/bin/hipcc $x -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math \
         -I"$2" -I. ${EXTRA_FLAGS} -c $f.hip -o "$3/$f.o" & done; wait
     /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$3/libmsacl_hip.so" "$3"/*.o )
@@ -32,7 +32,7 @@ mkdir -p "$ROOT/gpurun_out"
 for i in 1 2; do
   for d in "$ROOT"/exp_libs/rev-* "$ROOT"/exp_libs/work*; do
     n=$(basename "$d")
-    MSACL_HIP_LIB="$d/libmsacl_hip.so" timeout -k 10 120 python "$ROOT/tools/kernel_bench.py" "$@" \
+    MSACL_HIP_LIB_AB=1 MSACL_HIP_LIB="$d/libmsacl_hip.so" timeout -k 10 120 python "$ROOT/tools/kernel_bench.py" "$@" \
       > "$ROOT/gpurun_out/ab_${n}_$i.log" 2>&1
     echo "== $n ($i)"; grep -E '"avg_us"' "$ROOT/gpurun_out/ab_${n}_$i.log" | cut -c1-160
   done
