@@ -1,8 +1,9 @@
 #!/bin/bash
 # A/B of the engine library against a git revision: `tools/ab_libs.sh build REV` compiles
 # csrc/ at REV into exp_libs/REV-<sha>/ and the working tree into exp_libs/work/;
-# `tools/ab_libs.sh run ARGS...` (GPU box) times tools/kernel_bench.py ARGS with each library,
-# alternating twice, into gpurun_out/ab_<lib>_<i>.log.
+# `tools/ab_libs.sh run ARGS...` (GPU box) times tools/kernel_bench.py ARGS (AB_TOOL=fused_ab.py:
+# the fused horizon kernel) with each library, alternating twice (AB_ROUNDS), into
+# gpurun_out/ab_<lib>_<i>.log.
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG=multi-step-actor-critic-learning-with-lyapunov-certificates-for-exponentially-stabilizing-control_amd
@@ -29,11 +30,11 @@ if [ "$1" = "build" ]; then
 fi
 shift
 mkdir -p "$ROOT/gpurun_out"
-for i in 1 2; do
+for i in $(seq 1 ${AB_ROUNDS:-2}); do
   for d in "$ROOT"/exp_libs/rev-* "$ROOT"/exp_libs/work*; do
     n=$(basename "$d")
-    MSACL_HIP_LIB_AB=1 MSACL_HIP_LIB="$d/libmsacl_hip.so" timeout -k 10 120 python "$ROOT/tools/kernel_bench.py" "$@" \
-      > "$ROOT/gpurun_out/ab_${n}_$i.log" 2>&1
-    echo "== $n ($i)"; grep -E '"avg_us"' "$ROOT/gpurun_out/ab_${n}_$i.log" | cut -c1-160
+    MSACL_HIP_LIB_AB=1 MSACL_HIP_LIB="$d/libmsacl_hip.so" timeout -k 10 120 python "$ROOT/tools/${AB_TOOL:-kernel_bench.py}" "$@" \
+      > "$ROOT/gpurun_out/ab_${n}_$i.log" 2>&1 || { tail -5 "$ROOT/gpurun_out/ab_${n}_$i.log"; exit 1; }
+    echo "== $n ($i)"; grep -E '"avg_us"|"us_per_horizon"' "$ROOT/gpurun_out/ab_${n}_$i.log" | cut -c1-200
   done
 done
