@@ -25,6 +25,7 @@
 // advanced by q x its group stride (floats; 0 = shared).
 #include <cstring>
 
+#include "policy_x3.h"
 #include "rollout.h"
 
 namespace mh {
@@ -38,6 +39,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f32x4 add4_scalar(f32x4 a, f32x4 b) {
   float r0 = a[0] + b[0], r1 = a[1] + b[1], r2 = a[2] + b[2], r3 = a[3] + b[3];
   asm volatile("" : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3));  // keep them scalar (no v2f32 re-pairing)
+  return f32x4{r0, r1, r2, r3};
+}
+__device__ __forceinline__ f32x4 mul4_scalar(f32x4 a, float k) {
+  float r0 = a[0] * k, r1 = a[1] * k, r2 = a[2] * k, r3 = a[3] * k;
+  asm volatile("" : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3));
   return f32x4{r0, r1, r2, r3};
 }
 
@@ -157,32 +163,198 @@ __device__ __forceinline__ void layer_cols(const float* in, __amdgpu_buffer_rsrc
   layer_cols_run<SIN, G, RT>(in, wr, n0, lane, acc, wb);
 }
 
+// ---- the split-f16 form of a hidden-width layer (round 6): out[16 RT][64] += in[.][K] W[n][K]^T with
+// v_mfma_f32_16x16x32_f16 on two-way f16 splits, three products per f32 product (lo.hi, hi.lo,
+// hi.hi: policy_x3.h's scheme), i.e. 16-cycle 16x16x32 MFMAs, three per 32-deep K-step, instead of
+// eight 32-cycle 16x16x4 f32 MFMAs: the f32 layer kept a wave's SIMD 16 k cycles in MFMA issue at
+// two row tiles. Operands, per lane l (16x16x32: A[row l & 15][k = 8 (l >> 4) + j], B[k][col l & 15]):
+//   A: eight consecutive floats of its row from the LDS tile, times the row tile's power of two
+//      2^e (from the tile's max |value|: every scaled value <= 2^14), then split;
+//   B: eight consecutive floats of weight row n (W [N][K] row-major: two global float4 loads per
+//      16-column block and 32-deep K-step), times the fixed WX = 2^10, then split: the f16 lo of a
+//      weight in [2^-13, 64) is a normal number, so hi + lo keeps 22 bits of it; a weight of 64 or
+//      more overflows its f16 hi, the tile's accumulators come out non-finite, and that row tile
+//      is recomputed by the f32 layer (x3_redo_nonfinite: cold, the bits of the f32 path);
+// the accumulators carry 2^e WX, undone exactly (powers of two) before the bias and activation.
+// A value is split in one rounding each way: hi = f16(v k), lo = f16(v k - hi) (v_fma_mix, the
+// product and difference exact inside the fused multiply-add).
+// The K-step's weights are loaded PF - 1 steps ahead (as layer_cols's ring), its A operand one ahead.
+constexpr int KS32 = HID / 32;  // 32-deep K-steps of a hidden-width layer
+constexpr float WX = 1024.0f, IWX = 1.0f / 1024.0f;
+typedef _Float16 f16x8m __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split2h_pair_k(float a, float b, float k, uint32_t& hi, uint32_t& lo) {
+  asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
+      "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
+      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(hi), "=&v"(lo)
+      : "v"(a), "v"(b), "v"(k));
+}
+
+// eight floats -> (hi, lo) f16x8 of the values times k
+__device__ __forceinline__ void split8(const f32x4& p, const f32x4& q, float k, f16x8m& hi, f16x8m& lo) {
+  uint32_t h[4], l[4];
+  split2h_pair_k(p[0], p[1], k, h[0], l[0]);
+  split2h_pair_k(p[2], p[3], k, h[1], l[1]);
+  split2h_pair_k(q[0], q[1], k, h[2], l[2]);
+  split2h_pair_k(q[2], q[3], k, h[3], l[3]);
+  hi = __builtin_bit_cast(f16x8m, uint4{h[0], h[1], h[2], h[3]});
+  lo = __builtin_bit_cast(f16x8m, uint4{l[0], l[1], l[2], l[3]});
+}
+
+template <int PFX>
+__device__ __forceinline__ void wring_load_x3(__amdgpu_buffer_rsrc_t wr, int n0, int lane, int ks, f32x4 (&dst)[4][2]) {
+  const int r = lane & 15, g = lane >> 4;
+  const int voff = ((n0 + r) * HID + 32 * ks + 8 * g) * 4;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      dst[j][h] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr, voff + (16 * j * HID + 4 * h) * 4, 0, 0));
+}
+
+template <int RT>
+__device__ __forceinline__ void layer_cols_pre_x3(__amdgpu_buffer_rsrc_t wr, int n0, int lane, f32x4 (&wb)[PF][4][2]) {
+#pragma unroll
+  for (int p = 0; p < PF - 1; ++p) wring_load_x3<PF>(wr, n0, lane, p, wb[p]);
+}
+
+template <int SIN, int RT>
+__device__ __forceinline__ void layer_cols_run_x3(const float* in, const float (&sc)[RT], __amdgpu_buffer_rsrc_t wr,
+                                                  int n0, int lane, f32x4 (&acc)[RT][4], f32x4 (&wb)[PF][4][2]) {
+  const int r = lane & 15, g = lane >> 4;
+  const float wx = WX;
+  const float* arow = in + r * SIN + 8 * g;
+  f32x4 a_cur[RT][2];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) a_cur[rt][h] = *reinterpret_cast<const f32x4*>(arow + 16 * rt * SIN + 4 * h);
+#pragma unroll
+  for (int ks = 0; ks < KS32; ++ks) {
+    if (ks + PF - 1 < KS32) wring_load_x3<PF>(wr, n0, lane, ks + PF - 1, wb[(ks + PF - 1) % PF]);
+    f32x4 a_nxt[RT][2];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        a_nxt[rt][h] = ks + 1 < KS32 ? *reinterpret_cast<const f32x4*>(arow + 16 * rt * SIN + 32 * (ks + 1) + 4 * h)
+                                     : a_cur[rt][h];
+    MH_SCHED_FENCE();
+    f16x8m ah[RT], al[RT], wh[4], wl[4];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) split8(a_cur[rt][0], a_cur[rt][1], sc[rt], ah[rt], al[rt]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split8(wb[ks % PF][j][0], wb[ks % PF][j][1], wx, wh[j], wl[j]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[rt], wh[j], acc[rt][j], 0, 0, 0);
+        acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], wl[j], acc[rt][j], 0, 0, 0);
+        acc[rt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[rt], wh[j], acc[rt][j], 0, 0, 0);
+      }
+    MH_SCHED_FENCE();
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) a_cur[rt][h] = a_nxt[rt][h];
+  }
+}
+
+// the largest |value| of each row tile of an epilogue's output, over the workgroup (LDS atomic max
+// on the bits: non-negative floats order as their bit patterns; NaN stays the max)
+template <int RT>
+__device__ __forceinline__ void tile_max_publish(const float (&m)[RT], uint32_t* smax) {
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    float v = m[rt];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    if ((threadIdx.x & 63) == 0) atomicMax(smax + rt, __float_as_uint(v));
+  }
+}
+// the A scale of each row tile (a power of two, every scaled value <= 2^14) and the accumulators'
+// unscale (2^-e / WX)
+template <int RT>
+__device__ __forceinline__ void tile_scales(const uint32_t* smax, float (&sc)[RT], float (&isc)[RT]) {
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const float m = __uint_as_float(smax[rt]);
+    const int e = pm_scale_exp(m);  // 0 for 0 / NaN
+    sc[rt] = pm_pow2(e);
+    isc[rt] = pm_pow2(-e) * IWX;  // exact: 2^-(e + 10) >= 2^-50
+  }
+}
+
+// The row tiles whose split-f16 accumulators came out non-finite (a weight of 64 or more, or a
+// non-finite input, which the f32 layer turns into the same non-finite values) are recomputed by
+// the f32 layer, 2^e WX-scaled so the epilogue's unscale applies unchanged. Wave-uniform and cold.
+struct Acc4 {
+  f32x4 v[4];
+};
+template <int SIN>
+__device__ __noinline__ Acc4 x3_redo_tile(const float* in, __amdgpu_buffer_rsrc_t wr, int n0, int lane, float s) {
+  f32x4 a1[1][4] = {};
+  layer_cols<SIN, HID / 16, 1>(in, wr, n0, lane, a1);
+  Acc4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r.v[j] = mul4_scalar(a1[0][j], s);
+  return r;
+}
+template <int SIN, int RT>
+__device__ __forceinline__ void x3_redo_nonfinite(const float* in, __amdgpu_buffer_rsrc_t wr, int n0, int lane,
+                                                  f32x4 (&acc)[RT][4], const float (&isc)[RT]) {
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bad |= !__builtin_isfinite(acc[rt][j][q]);
+    if (__builtin_expect(__any(bad), 0)) {
+      const Acc4 r = x3_redo_tile<SIN>(in + 16 * rt * SIN, wr, n0, lane, 1.0f / isc[rt]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[rt][j] = r.v[j];
+    }
+  }
+}
+
 // bias + activation of this wave's 64 columns into the LDS tile `out` (row stride SH), row tiles
 // 0 .. RT - 1; the MFMA's C map: column = lane & 15, rows 16 rt + 4 (lane >> 4) + q
 template <int ACT, int RT>
 __device__ __forceinline__ void epilogue_lds_t(const f32x4 (&acc)[RT][4], const float (&bias)[4], int n0, int lane,
-                                               float* out) {
+                                               float* out, const float* isc = nullptr, float* mx = nullptr) {
   const int c = lane & 15, g = lane >> 4;
 #pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
+  for (int rt = 0; rt < RT; ++rt) {
+    float m = 0.0f;
+    const float u = isc ? isc[rt] : 1.0f;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = n0 + 16 * j + c;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) out[(16 * rt + 4 * g + q) * SH + n] = act_t<ACT>(acc[rt][j][q] + bias[j]);
+      for (int q = 0; q < 4; ++q) {
+        const float v = act_t<ACT>((isc ? acc[rt][j][q] * u : acc[rt][j][q]) + bias[j]);
+        out[(16 * rt + 4 * g + q) * SH + n] = v;
+        m = fmaxf(m, fabsf(v));
+      }
     }
+    if (mx) mx[rt] = m;
+  }
 }
 
 // bias[j] = the bias of column n0 + 16 j + (lane & 15), loaded up front
 template <int RT>
 __device__ __forceinline__ void epilogue_lds(const f32x4 (&acc)[RT][4], const float (&bias)[4], int act, int n0,
-                                             int lane, float* out) {
+                                             int lane, float* out, const float* isc = nullptr, float* mx = nullptr) {
   if (act == 1)
-    epilogue_lds_t<1, RT>(acc, bias, n0, lane, out);
+    epilogue_lds_t<1, RT>(acc, bias, n0, lane, out, isc, mx);
   else if (act == 2)
-    epilogue_lds_t<2, RT>(acc, bias, n0, lane, out);
+    epilogue_lds_t<2, RT>(acc, bias, n0, lane, out, isc, mx);
   else
-    epilogue_lds_t<0, RT>(acc, bias, n0, lane, out);
+    epilogue_lds_t<0, RT>(acc, bias, n0, lane, out, isc, mx);
 }
 
 // the LDS tile (rows x HID) to global rows m0.. (ld floats), row-contiguous float4 stores
@@ -196,13 +368,16 @@ __device__ __forceinline__ void store_tile(const float* tile, float* dst, int64_
   }
 }
 
-template <int RT>
+// X3: layer 2 and a wide layer 3 in the split-f16 form (layer_cols_run_x3), layer 1 and a narrow
+// layer 3 in f32 MFMA either way
+template <int RT, bool X3>
 __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
   constexpr int TR = 16 * RT;  // rows per workgroup
   __shared__ float xs[TR * SX];
   __shared__ float hs1[TR * SH];
   __shared__ float hs2[TR * SH];
   __shared__ f32x4 red[4][RT][64];
+  __shared__ uint32_t smax[2][RT];  // X3: max |h1|, |h2| of each row tile (float bits)
   {
     int64_t q = blockIdx.y;
     if (q >= a.groups_a) {  // the second network set (its activations are not kept)
@@ -240,8 +415,13 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
   // without a round trip
   const __amdgpu_buffer_rsrc_t wr2 =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.W2), (short)0, HID * HID * 4, 0x00020000);
-  f32x4 wb2[PF][4];
-  layer_cols_pre<HID / 16>(wr2, n0, lane, wb2);
+  f32x4 wb2[PF][X3 ? 1 : 4];
+  f32x4 wx2[PF][X3 ? 4 : 1][2];
+  if constexpr (X3)
+    layer_cols_pre_x3<RT>(wr2, n0, lane, wx2);
+  else
+    layer_cols_pre<HID / 16>(wr2, n0, lane, wb2);
+  if (X3 && tid < 2 * RT) smax[tid / RT][tid % RT] = 0u;
   // ---- the hidden layers' biases and layer 1's weights (their latency overlaps the input
   // staging): W1 [H][K1], lane group g of column n reads k = 16 u + 4 g + t; k >= K1 lands past
   // the buffer's end and reads 0
@@ -302,7 +482,13 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
         }
       }
     }
-    epilogue_lds<RT>(acc, bias1, a.act1, n0, lane, hs1);
+    if constexpr (X3) {
+      float mx[RT];
+      epilogue_lds<RT>(acc, bias1, a.act1, n0, lane, hs1, nullptr, mx);
+      tile_max_publish<RT>(mx, smax[0]);
+    } else {
+      epilogue_lds<RT>(acc, bias1, a.act1, n0, lane, hs1);
+    }
   }
   __syncthreads();
   if (a.h1) store_tile(hs1, a.h1, a.ldh, m0, a.M, HID, TR);
@@ -314,7 +500,14 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
   f32x4 w3[4];  // the narrow output layer's weights (N3 <= 16), issued before layer 2's epilogue
   {
     f32x4 acc[RT][4] = {};
-    layer_cols_run<SH, HID / 16, RT>(hs1, wr2, n0, lane, acc, wb2);
+    float sc[RT], isc[RT];
+    if constexpr (X3) {
+      tile_scales<RT>(smax[0], sc, isc);
+      layer_cols_run_x3<SH, RT>(hs1, sc, wr2, n0, lane, acc, wx2);
+      x3_redo_nonfinite<SH, RT>(hs1, wr2, n0, lane, acc, isc);
+    } else {
+      layer_cols_run<SH, HID / 16, RT>(hs1, wr2, n0, lane, acc, reinterpret_cast<f32x4(&)[PF][4]>(wb2));
+    }
     if (N3 <= 16) {
 #pragma unroll
       for (int uu = 0; uu < 4; ++uu)
@@ -322,7 +515,13 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
             f32x4, __builtin_amdgcn_raw_buffer_load_b128(wr3, (r * HID + 16 * (wave * 4 + uu) + 4 * g) * 4, 0, 0));
     }
     MH_SCHED_FENCE();
-    epilogue_lds<RT>(acc, bias2, a.act2, n0, lane, hs2);
+    if constexpr (X3) {
+      float mx[RT];
+      epilogue_lds<RT>(acc, bias2, a.act2, n0, lane, hs2, isc, mx);
+      if (N3 > 16) tile_max_publish<RT>(mx, smax[1]);
+    } else {
+      epilogue_lds<RT>(acc, bias2, a.act2, n0, lane, hs2);
+    }
   }
   __syncthreads();
   if (a.h2) store_tile(hs2, a.h2, a.ldh, m0, a.M, HID, TR);
@@ -363,9 +562,22 @@ __global__ __launch_bounds__(256) void k_mlp3_fwd(Mlp3Args a) {
   } else {
     // N3 = 64 c: wave w takes output columns [N3 / 4 * w, ...) in 16-column blocks of 64-wide passes
     // (with sqsum: also into the free hs1 tile, N3 <= HID)
+    float sc3[RT], isc3[RT];
+    if constexpr (X3) tile_scales<RT>(smax[1], sc3, isc3);
     for (int nb = wave * 64; nb < N3; nb += 256) {
       f32x4 acc[RT][4] = {};
-      layer_cols<SH, HID / 16, RT>(hs2, wr3, nb, lane, acc);
+      if constexpr (X3) {
+        f32x4 wx3[PF][4][2];
+        layer_cols_pre_x3<RT>(wr3, nb, lane, wx3);
+        layer_cols_run_x3<SH, RT>(hs2, sc3, wr3, nb, lane, acc, wx3);
+        x3_redo_nonfinite<SH, RT>(hs2, wr3, nb, lane, acc, isc3);
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[rt][j] = mul4_scalar(acc[rt][j], isc3[rt]);
+      } else {
+        layer_cols<SH, HID / 16, RT>(hs2, wr3, nb, lane, acc);
+      }
       const int c = lane & 15;
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt)
@@ -810,12 +1022,27 @@ hipError_t launch_mlp3_forward(const Mlp3Args& a_in, int groups, hipStream_t st)
       if (wgs(r) <= cus) rt = r;
     if (!rt) rt = 2;
   }
+  // the split-f16 hidden layers (k_mlp3_fwd<., true>) unless MH_MLP_X3=0
+  static const bool x3 = [] {
+    const char* e = getenv("MH_MLP_X3");
+    return !(e && e[0] == '0');
+  }();
   const unsigned gy = (unsigned)groups;
-  switch (rt) {
-    case 1: k_mlp3_fwd<1><<<dim3((unsigned)((a.M + 15) / 16), gy), 256, 0, st>>>(a); break;
-    case 3: k_mlp3_fwd<3><<<dim3((unsigned)((a.M + 47) / 48), gy), 256, 0, st>>>(a); break;
-    case 4: k_mlp3_fwd<4><<<dim3((unsigned)((a.M + 63) / 64), gy), 256, 0, st>>>(a); break;
-    default: k_mlp3_fwd<2><<<dim3((unsigned)((a.M + 31) / 32), gy), 256, 0, st>>>(a); break;
+  const dim3 grid((unsigned)((a.M + 16 * rt - 1) / (16 * rt)), gy);
+  if (x3) {
+    switch (rt) {
+      case 1: k_mlp3_fwd<1, true><<<grid, 256, 0, st>>>(a); break;
+      case 3: k_mlp3_fwd<3, true><<<grid, 256, 0, st>>>(a); break;
+      case 4: k_mlp3_fwd<4, true><<<grid, 256, 0, st>>>(a); break;
+      default: k_mlp3_fwd<2, true><<<grid, 256, 0, st>>>(a); break;
+    }
+  } else {
+    switch (rt) {
+      case 1: k_mlp3_fwd<1, false><<<grid, 256, 0, st>>>(a); break;
+      case 3: k_mlp3_fwd<3, false><<<grid, 256, 0, st>>>(a); break;
+      case 4: k_mlp3_fwd<4, false><<<grid, 256, 0, st>>>(a); break;
+      default: k_mlp3_fwd<2, false><<<grid, 256, 0, st>>>(a); break;
+    }
   }
   return hipGetLastError();
 }

@@ -109,14 +109,34 @@ def test_mlp3_rejects_unsupported_shapes():
                                    N.ptr(y), 20, 1, None, N.stream_of()) == -1  # N3 = 20
 
 
+def _kink_margin_rows(x, mods, margin=1e-5):
+    """Rows whose ReLU pre-activations (float64) all keep `margin` x the layer's max |z| from 0.
+    Two correct f32 evaluations of a layer (different summation orders, or the split-f16 layer
+    against the f32 one) differ by ~1e-7 of its scale; a unit that close to the kink can take
+    either side of it, and its mask then differs between the two paths, moving every gradient of
+    its row by a whole term: a comparison of two paths' gradients is only meaningful where both
+    agree on every mask."""
+    D = lambda t: t.detach().double().cpu()  # noqa: E731
+    a, keep = D(x), torch.ones(x.shape[0], dtype=torch.bool)
+    for lin in (mods[0], mods[2]):
+        z = a @ D(lin.weight).T + D(lin.bias)
+        keep &= (z.abs() > margin * float(z.abs().max())).all(1)
+        a = z.clamp_min(0.0)
+    return keep.to(x.device)
+
+
 @pytest.mark.parametrize("acts", [(nn.ReLU, nn.ReLU, nn.Identity), (nn.Tanh, nn.Tanh, nn.Identity)])
 def test_mlp_module_fused_forward_backward_matches_per_layer(acts):
     """The MLP module (apprfunc/_fused.py) through MLP3 vs through the per-layer LinearAct launches:
-    outputs within the f32 summation-order bound, every gradient rtol 1e-4 / atol 1e-5 of its scale."""
+    outputs within the f32 summation-order bound, every gradient rtol 1e-4 / atol 1e-5 of its scale
+    (ReLU: on rows clear of the kink, _kink_margin_rows)."""
     torch.manual_seed(0)
     mods = [nn.Linear(12, 256), acts[0](), nn.Linear(256, 256), acts[1](), nn.Linear(256, 8), acts[2]()]
     net = F.MLP(*mods).cuda()
-    x = torch.randn(256, 20, 12, device="cuda", requires_grad=True)
+    x = torch.randn(256 * 21, 12, device="cuda")
+    if acts[0] is nn.ReLU:
+        x = x[_kink_margin_rows(x, mods)]
+    x = x[:256 * 20].reshape(256, 20, 12).requires_grad_(True)
     g = torch.randn(256, 20, 8, device="cuda")
     outs = []
     for on in (True, False):
@@ -239,7 +259,9 @@ def test_weight_grads_multi_matches_float64(rows):
 
 def test_twin_weight_grads_fused_equals_per_layer():
     """TwinCritic.backward_weights through the chain + mh_weight_grads vs the per-layer launches:
-    every gradient within rtol 1e-4 / atol 1e-5 of its scale."""
+    every gradient within rtol 1e-4 / atol 1e-5 of its scale. Both backward paths take the same
+    kept activations (one forward): the forward's own paths are compared above, and the ReLU
+    masks of two forwards can differ at units within rounding of the kink (_kink_margin_rows)."""
     from msacl_amd.apprfunc._twin import TwinCritic
     from msacl_amd.apprfunc.mlp import ActionValue
     torch.manual_seed(2)
@@ -250,10 +272,10 @@ def test_twin_weight_grads_fused_equals_per_layer():
     x = torch.randn(M, 16, device="cuda")
     dq = torch.randn(2, M, device="cuda")
     res = []
+    q, h1, h2 = tc.forward(x)
     for on in (True, False):
         F._MLP3["on"] = on
         try:
-            q, h1, h2 = tc.forward(x)
             tc.backward_weights(x, dq, h1, h2)
             res.append([t.clone() for t in (tc.gW1, tc.gb1, tc.gW2, tc.gb2, tc.gW3, tc.gb3)])
         finally:
@@ -347,3 +369,47 @@ def test_lyapunov_square_sum_fused_equals_separate(M):
             F._MLP3["sqsum"] = True
     for a, b in zip(*outs):
         torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+def test_mlp3_forward_weights_past_the_split_range_and_nonfinite_rows():
+    """The split-f16 hidden layers (csrc/mlp_fused.hip layer_cols_run_x3) scale weights by 2^10
+    before the f16 split: a weight of 64 or more overflows its f16 hi. Such a row tile is recomputed
+    by the f32 layer (x3_redo_nonfinite), so the results stay within the f32 bound. A non-finite
+    input row gives non-finite outputs in that row only; the other row tiles keep their bits."""
+    for K1, N3, acts in ((12, 256, (2, 2, 0)), (16, 1, (1, 1, 0))):
+        ps = _params(K1, N3, seed=7)
+        W1, b1, W2, b2, W3, b3 = ps
+        W2[3, 5] = 100.0
+        W2[200, 17] = -70.0
+        if N3 > 16:
+            W3[9, 250] = 65.0
+        M = 1000
+        x = (torch.rand(M, K1, generator=torch.Generator().manual_seed(3)) * 4 - 2).cuda()
+        y, h1, h2 = _run(x, ps, acts)
+        _check_layer(h2, h1, W2, b2, acts[1], "layer 2")
+        _check_layer(y, h2, W3, b3, acts[2], "layer 3")
+        xb = x.clone()
+        xb[40, 0] = float("nan")
+        yb, _, _ = _run(xb, ps, acts)
+        assert torch.all(torch.isnan(yb[40]))
+        tile = torch.arange(M, device="cuda") // 16 == 40 // 16
+        assert torch.equal(yb[~tile], y[~tile])
+        assert torch.all(torch.isfinite(yb[tile & (torch.arange(M, device="cuda") != 40)]))
+
+
+@pytest.mark.parametrize("name,M,K1,N3,acts", CASES[:3], ids=[c[0] for c in CASES[:3]])
+def test_mlp3_hidden_layer_error_near_f32_rounding(name, M, K1, N3, acts):
+    """The hidden layer's error against float64 on the kernel's own input, in units of the f32
+    dot-product scale 2^-24 sqrt(K) sum_k |a_k w_k|: the split-f16 form drops the lo.lo products
+    (<= 2^-22 of each product) and keeps weights to 22 bits."""
+    ps = _params(K1, N3, seed=M + K1)
+    x = (torch.rand(M, K1, generator=torch.Generator().manual_seed(1)) * 4 - 2).cuda()
+    y, h1, h2 = _run(x, ps, acts)
+    W2, b2 = ps[2], ps[3]
+    a, w = h1.double().cpu().numpy(), W2.double().cpu().numpy()
+    lin = a @ w.T + b2.double().cpu().numpy()
+    mag = np.abs(a) @ np.abs(w).T + np.abs(b2.double().cpu().numpy())
+    ref = ACT[acts[1]](lin)
+    ratio = np.abs(h2.double().cpu().numpy() - ref) / (2.0 ** -24 * 16 * mag + 1e-30)
+    print(f"{name}: layer-2 error / (2^-24 sqrt(K) mag): max {ratio.max():.3f} mean {ratio.mean():.4f}")
+    assert ratio.max() < 4.0
