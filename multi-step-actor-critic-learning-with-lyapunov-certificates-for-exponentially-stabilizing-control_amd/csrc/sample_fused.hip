@@ -928,6 +928,17 @@ void k_sample_fused(FusedArgs a) {
 // contiguous chunks: 16-byte stores when D % 4 == 0, else 4-byte, one contiguous run per
 // instruction instead of D strided stores per lane. `stage` is the wave's 64 * D floats; its next
 // writer is the same wave after these reads (a wave's LDS operations are in order).
+// The emission's replay-store writes are non-temporal (`global_store … nt`): the store rows are
+// read back only by the replay gather, 256 random windows per update, so caching them in L2 / the
+// Infinity Cache only evicts what the update that follows reads (the networks, the batch, the
+// ring). Bench 1.267-1.275 vs 1.253-1.262 B env-steps/s alternating on one box, the policy-free
+// update 0.273-0.288 vs 0.282-0.298 ms (profiles/r06_emit_nt_ab.txt).
+typedef float emit_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void emit_st(float* p, float v) { __builtin_nontemporal_store(v, p); }
+__device__ __forceinline__ void emit_st4(float* p, float4 v) {
+  __builtin_nontemporal_store(__builtin_bit_cast(emit_f4, v), reinterpret_cast<emit_f4*>(p));
+}
+
 template <int D>
 __device__ __forceinline__ void emit_rows_lds(float* dst, const float* row, float* stage, int lane) {
 #pragma unroll
@@ -940,13 +951,13 @@ __device__ __forceinline__ void emit_rows_lds(float* dst, const float* row, floa
 #pragma unroll
     for (int q = 0; q < D / 4; ++q) v[q] = s4[q * 64 + lane];
 #pragma unroll
-    for (int q = 0; q < D / 4; ++q) d4[q * 64 + lane] = v[q];
+    for (int q = 0; q < D / 4; ++q) emit_st4(reinterpret_cast<float*>(d4 + q * 64 + lane), v[q]);
   } else {
     float v[D];
 #pragma unroll
     for (int q = 0; q < D; ++q) v[q] = stage[q * 64 + lane];
 #pragma unroll
-    for (int q = 0; q < D; ++q) dst[q * 64 + lane] = v[q];
+    for (int q = 0; q < D; ++q) emit_st(dst + q * 64 + lane, v[q]);
   }
   __builtin_amdgcn_wave_barrier();
 }
@@ -1073,21 +1084,21 @@ __global__ __launch_bounds__(256) void k_emit_cells(HorizonEmitArgs a) {
       emit_rows_lds<D>(a.obs2 + o0 * D, rec + D + A, stage[wave], lane);
     } else if (valid) {
 #pragma unroll
-      for (int k = 0; k < D; ++k) a.obs[o * D + k] = rec[k];
+      for (int k = 0; k < D; ++k) emit_st(a.obs + o * D + k, rec[k]);
 #pragma unroll
-      for (int k = 0; k < D; ++k) a.obs2[o * D + k] = rec[D + A + k];
+      for (int k = 0; k < D; ++k) emit_st(a.obs2 + o * D + k, rec[D + A + k]);
     }
     if (valid) {
       if constexpr (A == 4) {  // one 16-byte row per lane: consecutive lanes, consecutive rows
-        *reinterpret_cast<float4*>(a.act + o * A) = make_float4(rec[D], rec[D + 1], rec[D + 2], rec[D + 3]);
+        emit_st4(a.act + o * A, make_float4(rec[D], rec[D + 1], rec[D + 2], rec[D + 3]));
       } else {
 #pragma unroll
-        for (int k = 0; k < A; ++k) a.act[o * A + k] = rec[D + k];
+        for (int k = 0; k < A; ++k) emit_st(a.act + o * A + k, rec[D + k]);
       }
-      a.rew[o] = rec[2 * D + A];
-      a.cost[o] = rec[2 * D + A + 1];
-      a.done[o] = rec[2 * D + A + 2];
-      a.logp[o] = rec[2 * D + A + 3];
+      emit_st(a.rew + o, rec[2 * D + A]);
+      emit_st(a.cost + o, rec[2 * D + A + 1]);
+      emit_st(a.done + o, rec[2 * D + A + 2]);
+      emit_st(a.logp + o, rec[2 * D + A + 3]);
     }
   }
 }
