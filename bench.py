@@ -23,7 +23,7 @@ sys.path.insert(0, ROOT)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PEAK_F32_MFMA_TFS = 157.3  # MI355X dense f32 matrix peak (v_mfma_f32_*_f32)
 PEAK_F16_MFMA_TFS = 2500.0  # MI355X dense f16 matrix peak (v_mfma_f32_32x32x16_f16), MI355X_MICROARCH.md
-PMC_TRAFFIC = "r06_pmc_traffic_v1.json"  # the PMC summary of the current kernels (tools/pmc.sh + tools/pmc_summary.py)
+PMC_TRAFFIC = "r06_pmc_traffic_v2.json"  # the PMC summary of the current kernels (tools/pmc.sh + tools/pmc_summary.py)
 
 
 def parse():
